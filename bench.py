@@ -1,0 +1,215 @@
+#!/usr/bin/env python
+"""Learner throughput on MI355X — BASELINE.json metric.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" is one learner update (handyrl/train.py:372-392 body) on a
+device-resident synthetic replay batch in the make_batch layout: TicTacToe
+SimpleConv2dModel forward, IS ratios, the fused HIP V-trace/UPGO target scan,
+losses, backward, SUM all-reduce of the gradients over RCCL (N > 1), grad
+clip 4.0 and Adam.  Every rank trains its own B=4096 x T=32 batch (weak
+scaling); value = N*B*T*K / max-over-ranks time of the K timed steps.
+
+Rank 0 prints ONE JSON line with, besides the metric:
+  roofline      the V-trace scan kernel (the metric's second half): algorithmic
+                bytes per launch / mean launch time from HIP events on the
+                launch stream, at the step's own size and at a cold,
+                larger-than-Infinity-Cache size;
+  cpu_baseline  the CPU learner oracle (oracle/learner.py, restating
+                train.py:218-258 + 382-385) timed on this host, 1 thread as the
+                reference ships (model.py:8), on a bounded sample (N=1 only).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from handyrl_amd import distributed as hdist          # noqa: E402
+from handyrl_amd.envs.tictactoe import SimpleConv2dModel  # noqa: E402
+from handyrl_amd.synthetic import tictactoe_batch, default_args  # noqa: E402
+from handyrl_amd.trainer import LearnerStep            # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def scan_bytes_per_launch(B, T, P=2, Pp=1, rewards=False):
+    """Algorithmic bytes of one V-trace value-head launch.
+
+    read values 4P + rho 4Pp + c 4Pp (+ rewards 4P), write targets 4P + advantages 4P
+    per env-step, plus the 4P-byte bootstrap per trajectory.
+    """
+    per_step = 12 * P + 8 * Pp + (4 * P if rewards else 0)
+    return B * T * per_step + B * 4 * P
+
+
+def time_scan(device, B, T, iters, cold=False):
+    """Mean duration of the fused value-head scan launch (VTRACE target + UPGO advantages)."""
+    from handyrl_amd.losses import compute_targets_fused
+    g = torch.Generator(device=device).manual_seed(7)
+    n_sets = 1
+    if cold:
+        # rotate through enough input sets that every launch misses the 256 MiB Infinity Cache
+        per_set = scan_bytes_per_launch(B, T)
+        n_sets = max(2, int(3 * 256 * 2 ** 20 // per_set) + 1)
+    sets = []
+    for _ in range(n_sets):
+        v = torch.tanh(torch.randn(B, T, 2, 1, device=device, generator=g))
+        ret = torch.randint(-1, 2, (B, 1, 2, 1), device=device, generator=g).float()
+        rho = torch.rand(B, T, 1, 1, device=device, generator=g)
+        sets.append((v, ret, rho))
+    for s in sets[:2]:
+        compute_targets_fused('VTRACE', 'UPGO', s[0], s[1], None, 0.7, 1, s[2], s[2])
+    stream = torch.cuda.current_stream(device)
+    start = torch.cuda.Event(enable_timing=True)
+    end = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    start.record(stream)
+    for i in range(iters):
+        s = sets[i % n_sets]
+        compute_targets_fused('VTRACE', 'UPGO', s[0], s[1], None, 0.7, 1, s[2], s[2])
+    end.record(stream)
+    end.synchronize()
+    ms = start.elapsed_time(end) / iters
+    nbytes = scan_bytes_per_launch(B, T)
+    return {'B': B, 'T': T, 'us_per_launch': ms * 1e3, 'bytes_per_launch': nbytes,
+            'GBps': nbytes / (ms * 1e-3) / 1e9, 'cold': cold}
+
+
+def cpu_baseline(B=1024, T=32, steps=3):
+    """The CPU learner oracle on this host, 1 thread (train.py as shipped: model.py:8)."""
+    from oracle.learner import CpuLearner
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        torch.manual_seed(0)
+        net = SimpleConv2dModel()
+        args = default_args(T, B)
+        batch = tictactoe_batch(B, T, torch.device('cpu'), seed=11)
+        learner = CpuLearner(net, args)
+        learner.step(batch)  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            learner.step(batch)
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(threads)
+    return {'value': B * T * steps / dt, 'unit': 'env-steps/s', 'cores': 1, 'kind': 'port',
+            'sample': 'oracle.learner.CpuLearner (restates train.py:218-258,382-385), TicTacToe net, '
+                      'synthetic B=%d T=%d, %d timed steps after 1 warm-up, torch 1 thread, %.1f s'
+                      % (B, T, steps, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=4096, help='trajectories per GPU (B)')
+    ap.add_argument('--seq', type=int, default=32, help='forward_steps (T)')
+    ap.add_argument('--graph', type=int, default=1, help='capture the 1-GPU step in a HIP graph')
+    ap.add_argument('--cpu-baseline', type=int, default=1)
+    ap.add_argument('--scan-iters', type=int, default=200)
+    opts = ap.parse_args()
+
+    rank, world, local = hdist.world_from_env()
+    if world != opts.gpus:
+        if world == 1 and opts.gpus > 1:
+            raise SystemExit('--gpus %d needs torch.distributed.run with %d processes' % (opts.gpus, opts.gpus))
+    device = torch.device('cuda', local)
+    torch.cuda.set_device(device)
+    hdist.init_process_group('cuda')
+
+    B, T = opts.batch, opts.seq
+    args = default_args(T, B)
+    torch.manual_seed(0)                       # identical initial weights on every rank
+    net = SimpleConv2dModel().to(device)
+    net.train()
+    batch = tictactoe_batch(B, T, device, seed=1000 + rank)  # each rank its own shard
+    use_graph = bool(opts.graph) and world == 1
+    learner = LearnerStep(net, args, device, graph=use_graph, world_size=world)
+
+    for _ in range(opts.warmup):
+        learner.step(batch)
+    if use_graph and opts.warmup == 0:
+        learner.step(batch)  # capture outside the timed region
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(opts.steps):
+        learner.step(batch)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    stats, nb = learner.pop_stats()
+
+    if rank == 0:
+        steps_total = world * B * T * opts.steps
+        value = steps_total / elapsed
+        hot = time_scan(device, B, T, opts.scan_iters)
+        cold = time_scan(device, 1 << 18, T, 60, cold=True)
+        roof = {
+            'kernel': 'targets_kernel<VTRACE,UPGO> value head (hrl_compute_targets_fused)',
+            'bound': 'hbm',
+            'achieved': round(hot['GBps'], 1),
+            'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s',
+            'frac': round(hot['GBps'] / HBM_PEAK_GBS, 4),
+            'traffic': None,
+            'bytes_per_launch': hot['bytes_per_launch'],
+            'us_per_launch': round(hot['us_per_launch'], 3),
+            'cold_large_B': {'B': cold['B'], 'T': T, 'achieved': round(cold['GBps'], 1),
+                             'frac': round(cold['GBps'] / HBM_PEAK_GBS, 4),
+                             'us_per_launch': round(cold['us_per_launch'], 2)},
+        }
+        cpu = cpu_baseline() if (opts.cpu_baseline and world == 1) else None
+        line = {
+            'metric': 'learner env-steps/sec at B=4096 T=32 (TicTacToe net, UPGO/VTRACE)',
+            'value': round(value, 1),
+            'unit': 'env-steps/s',
+            'n_gpus': world,
+            'steps': opts.steps,
+            'warmup': opts.warmup,
+            'ms_per_step': round(elapsed / opts.steps * 1e3, 4),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f32',
+            'data': 'synthetic (make_batch layout, SURVEY §8d D2), random-init weights',
+            'config': {'workload': 'TicTacToe SimpleConv2dModel learner step: forward + IS ratios + fused '
+                                   'HIP V-trace/UPGO scans + losses + backward + grad all-reduce + clip + Adam',
+                       'global_batch': world * B, 'per_gpu_batch': B, 'seq_len': T, 'players': 2,
+                       'parallelism': 'dp%d' % world, 'hip_graph': use_graph},
+            'roofline': roof,
+            'cpu_baseline': cpu,
+            'loss_per_dcnt': {k: v / max(stats.get('dcnt', 1.0), 1e-9) for k, v in stats.items()
+                              if k in ('p', 'v', 'ent', 'total')},
+        }
+        if cpu is not None:
+            line['speedup_vs_cpu_baseline'] = round(value / cpu['value'], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,79 @@
+"""ctypes binding of the C ABI in ``include/*.h`` (libhrl.so).
+
+The library is the ONLY compute path for the kernels it exports: if it is
+missing or fails to load, every caller gets a RuntimeError — there is no CPU
+or eager-PyTorch fallback.
+
+torch is imported first so that the HIP runtime torch ships
+(libamdhip64.so.7) is already in the process; libhrl.so's DT_NEEDED entry for
+the same soname then binds to that copy, and the hipStream_t handles torch
+hands us are valid in the library.
+"""
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede loading libhrl.so, see module doc)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libhrl.so')
+
+HRL_OK = 0
+HRL_EINVAL = -22
+
+ALG = {'MC': 0, 'TD': 1, 'UPGO': 2, 'VTRACE': 3}
+
+_f32p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_dbl = ctypes.c_double
+
+# symbol -> (restype, argtypes); mirrors include/*.h exactly
+SIGNATURES = {
+    'hrl_abi_version': (ctypes.c_int, []),
+    'hrl_strerror': (ctypes.c_char_p, [ctypes.c_int]),
+    'hrl_compute_target': (ctypes.c_int, [
+        ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _f32p,
+        _i64, _i64, _i64, _i64, _i64, _i64, _dbl, _dbl, _f32p, _f32p, ctypes.c_void_p]),
+    'hrl_compute_targets_fused': (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _f32p,
+        _i64, _i64, _i64, _i64, _i64, _i64, _dbl, _dbl, _f32p, _f32p, ctypes.c_void_p]),
+}
+
+ABI_VERSION = 1
+
+_lib = None
+
+
+def load():
+    """Load libhrl.so (once) and bind every signature; raise if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError('HIP library %s is missing: run `python -m handyrl_amd.build` '
+                           '(there is no CPU fallback for the learner kernels)' % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.hrl_abi_version() != ABI_VERSION:
+        raise RuntimeError('libhrl.so ABI %d != expected %d' % (lib.hrl_abi_version(), ABI_VERSION))
+    _lib = lib
+    return lib
+
+
+def check(code, what):
+    if code != HRL_OK:
+        msg = load().hrl_strerror(code).decode()
+        if code == HRL_EINVAL:
+            raise ValueError('%s: %s' % (what, msg))
+        raise RuntimeError('%s failed (%d): %s' % (what, code, msg))
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,450 @@
+// hrl_targets.hip — return-target scans for the HandyRL learner on MI355X (gfx950).
+//
+// Replaces handyrl/losses.py:16-74 (monte_carlo / temporal_difference / upgo /
+// vtrace / compute_target).  The reference runs each recurrence as a Python
+// loop of T-1 iterations of whole-batch torch ops (~140-344 elementwise ops
+// per call at T=32).  Here one launch does the whole backward scan of every
+// trajectory, and the fused entry point produces the value-target of one
+// algorithm and the advantages of another in the same pass
+// (train.py:248-253 issue 2-4 separate compute_target calls).
+//
+// Work decomposition (one wave64 per workgroup):
+//   * a wave owns G = 64 / C consecutive trajectories; lane = g*C + c owns one
+//     value column (trajectory g, column c) and walks it backwards in time;
+//   * time is processed in chunks of up to TCHUNK steps.  Each chunk of every
+//     input is loaded with coalesced 16-byte loads (the wave's trajectories are
+//     contiguous in the (B,T,C) layout), ALL inputs' loads are issued before
+//     any is consumed, and the values are transposed into a time-major LDS
+//     tile [t][column] whose row stride (columns+1) makes both the transposing
+//     writes and the per-lane column reads bank-conflict free;
+//   * outputs go to LDS tiles of the same shape and leave through the mirror
+//     transposition with coalesced 16-byte stores.
+// Numerics: built with -ffp-contract=off; every recurrence performs the
+// reference's float32 operations in the reference's order with the same
+// float32-rounded coefficients, so results are bit-identical to the
+// reference CPU learner (tests/test_targets_gpu.py checks max |diff|).
+// Roofline: pure HBM streaming, ~1 flop/byte, no MFMA.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hrl_targets.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kTChunk = 32;                          // time steps per LDS pass
+constexpr int kMaxTile = kTChunk * kWave;            // floats of one tensor chunk
+constexpr int kMaxVec = kMaxTile / 4 / kWave;        // float4 loads per lane (8)
+constexpr int kMaxScalar = kMaxTile / kWave;         // scalar loads per lane (32)
+constexpr int kNone = -1;
+
+struct Coef {
+    float a;   // (float)(1 - lmb)
+    float l;   // (float)lmb
+    float g;   // (float)gamma
+    float gl;  // (float)(gamma * lmb)
+};
+
+// torch.max(a, b) on two tensors propagates NaN (losses.py:36).
+__device__ __forceinline__ float max_nan(float x, float y) {
+    if (x != x) return x;
+    if (y != y) return y;
+    return x > y ? x : y;
+}
+
+// Coordinates of element e of a chunk in (g, tt, cx) order, stepped one at a time.
+struct Cursor {
+    int g, tt, cx;
+    __device__ __forceinline__ void init(int e, int L, int Cx) {
+        g = e / L;
+        const int rem = e - g * L;
+        tt = rem / Cx;
+        cx = rem - tt * Cx;
+    }
+    __device__ __forceinline__ void next(int tc, int Cx) {
+        if (++cx == Cx) {
+            cx = 0;
+            if (++tt == tc) { tt = 0; ++g; }
+        }
+    }
+    __device__ __forceinline__ int lds(int ld, int Cx) const { return tt * ld + g * Cx + cx; }
+};
+
+// One chunk of one (B, T, Cx) tensor for the wave's trajectories.
+//   global: trajectory b0+g, time t0+tt, column cx  at  (b0+g)*R + t0*Cx + tt*Cx + cx
+//   LDS   : [tt][g*Cx + cx] with row stride ld = G*Cx + 1
+struct Chunk {
+    const float *base;  // element (g=0, tt=0, cx=0)
+    int R;              // row length of one trajectory (T*Cx)
+    int L;              // span length of one trajectory in this chunk (tc*Cx)
+    int n;              // valid elements (ntraj * L)
+    int Cx, tc, ld;
+    bool shape_ok;      // spans are whole float4s (or one contiguous run)
+    bool vec;           // 16-byte loads are legal for this tensor
+
+    __device__ __forceinline__ void setup(const float *p, int64_t b0, int T, int Cx_, int t0, int tc_,
+                                          int ntraj, int ld_) {
+        Cx = Cx_; tc = tc_; ld = ld_;
+        R = T * Cx;
+        L = tc * Cx;
+        n = ntraj * L;
+        base = p + b0 * (int64_t)R + (int64_t)t0 * Cx;
+        // Contiguous spans (L == R) may straddle trajectories inside a float4;
+        // otherwise every span must be whole float4s.
+        shape_ok = (L == R) || ((L & 3) == 0 && (R & 3) == 0);
+        vec = shape_ok && ((reinterpret_cast<uintptr_t>(base) & 15) == 0);
+    }
+
+    __device__ __forceinline__ int64_t gaddr(int e) const {
+        if (L == R) return e;
+        const int g = e / L;
+        return (int64_t)g * R + (e - g * L);
+    }
+};
+
+// Registers holding one chunk between its global loads and its LDS writes.
+struct Staged {
+    float x[kMaxScalar];
+
+    __device__ __forceinline__ void load(const Chunk &c, int lane) {
+        if (c.n <= 0) return;
+        if (c.vec) {
+            const int nv = c.n >> 2;
+            if (nv == 0) return;
+#pragma unroll
+            for (int k = 0; k < kMaxVec; ++k) {
+                // clamp instead of branching so every load issues back to back
+                const int vi = min(k * kWave + (int)threadIdx.x, nv - 1);
+                const float4 q = *reinterpret_cast<const float4 *>(c.base + c.gaddr(vi * 4));
+                x[4 * k + 0] = q.x; x[4 * k + 1] = q.y; x[4 * k + 2] = q.z; x[4 * k + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kMaxScalar; ++k) {
+                const int e = min(k * kWave + (int)threadIdx.x, c.n - 1);
+                x[k] = c.base[c.gaddr(e)];
+            }
+        }
+        (void)lane;
+    }
+
+    __device__ __forceinline__ void to_lds(const Chunk &c, float *tile) const {
+        if (c.n <= 0) return;
+        const int lane = threadIdx.x;
+        if (c.vec) {
+            const int nv = c.n >> 2;
+#pragma unroll
+            for (int k = 0; k < kMaxVec; ++k) {
+                const int vi = k * kWave + lane;
+                if (vi < nv) {
+                    Cursor cur; cur.init(vi * 4, c.L, c.Cx);
+                    tile[cur.lds(c.ld, c.Cx)] = x[4 * k + 0]; cur.next(c.tc, c.Cx);
+                    tile[cur.lds(c.ld, c.Cx)] = x[4 * k + 1]; cur.next(c.tc, c.Cx);
+                    tile[cur.lds(c.ld, c.Cx)] = x[4 * k + 2]; cur.next(c.tc, c.Cx);
+                    tile[cur.lds(c.ld, c.Cx)] = x[4 * k + 3];
+                }
+            }
+            // ragged tail (< 4 elements) of a contiguous span
+            const int e = nv * 4 + lane;
+            if (e < c.n) {
+                Cursor cur; cur.init(e, c.L, c.Cx);
+                tile[cur.lds(c.ld, c.Cx)] = c.base[c.gaddr(e)];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kMaxScalar; ++k) {
+                const int e = k * kWave + lane;
+                if (e < c.n) {
+                    Cursor cur; cur.init(e, c.L, c.Cx);
+                    tile[cur.lds(c.ld, c.Cx)] = x[k];
+                }
+            }
+        }
+    }
+};
+
+// LDS tile -> global, the mirror of Staged (stores need no batching).
+__device__ __forceinline__ void store_chunk(const Chunk &c, const float *tile, float *out_base) {
+    if (c.n <= 0) return;
+    const int lane = threadIdx.x;
+    float *base = out_base;
+    const bool vec = c.shape_ok && ((reinterpret_cast<uintptr_t>(base) & 15) == 0);
+    if (vec) {
+        const int nv = c.n >> 2;
+        for (int vi = lane; vi < nv; vi += kWave) {
+            Cursor cur; cur.init(vi * 4, c.L, c.Cx);
+            float4 q;
+            q.x = tile[cur.lds(c.ld, c.Cx)]; cur.next(c.tc, c.Cx);
+            q.y = tile[cur.lds(c.ld, c.Cx)]; cur.next(c.tc, c.Cx);
+            q.z = tile[cur.lds(c.ld, c.Cx)]; cur.next(c.tc, c.Cx);
+            q.w = tile[cur.lds(c.ld, c.Cx)];
+            *reinterpret_cast<float4 *>(base + c.gaddr(vi * 4)) = q;
+        }
+        const int e = nv * 4 + lane;
+        if (e < c.n) {
+            Cursor cur; cur.init(e, c.L, c.Cx);
+            base[c.gaddr(e)] = tile[cur.lds(c.ld, c.Cx)];
+        }
+    } else {
+        for (int e = lane; e < c.n; e += kWave) {
+            Cursor cur; cur.init(e, c.L, c.Cx);
+            base[c.gaddr(e)] = tile[cur.lds(c.ld, c.Cx)];
+        }
+    }
+}
+
+struct Args {
+    const float *values, *returns, *rewards, *rhos, *cs;
+    float *targets, *advantages;
+    int64_t B;
+    int T, C, retT, rhoC, rhoDiv;
+    Coef k;
+};
+
+// Carried state of every recurrence for one column, walking t = T-1 .. 0.
+struct Carry {
+    float v_next;    // values[t+1]
+    float tv_td;     // TD target at t+1
+    float tv_up;     // UPGO target at t+1
+    float acc;       // V-trace (vs - v) at t+1
+    float vs_next;   // V-trace vs at t+1
+};
+
+// One time step of algorithm ALG for one column: reads the carry `s` of step
+// t+1, writes this algorithm's fields of the carry `nx` for step t, returns
+// the target and writes the advantage.
+template <int ALG>
+__device__ __forceinline__ float step(const Carry &s, Carry &nx, bool last, float v, float r, float rho,
+                                      float c, float ret_t, float boot, const Coef &k, float &adv) {
+    if constexpr (ALG == HRL_ALG_MC) {                       // losses.py:16-17
+        adv = ret_t - v;
+        return ret_t;
+    } else if constexpr (ALG == HRL_ALG_TD) {                // losses.py:20-28
+        const float tv = last ? boot : r + k.g * (k.a * s.v_next + k.l * s.tv_td);
+        nx.tv_td = tv;
+        adv = tv - v;
+        return tv;
+    } else if constexpr (ALG == HRL_ALG_UPGO) {              // losses.py:31-40
+        const float tv = last ? boot : r + k.g * max_nan(s.v_next, k.a * s.v_next + k.l * s.tv_up);
+        nx.tv_up = tv;
+        adv = tv - v;
+        return tv;
+    } else {                                                 // losses.py:43-58
+        const float v1 = last ? boot : s.v_next;
+        const float delta = rho * ((r + k.g * v1) - v);
+        const float acc = last ? delta : delta + (k.gl * c) * s.acc;   // vs_minus_v_xs, carried as is
+        const float vs = acc + v;
+        const float vs1 = last ? boot : s.vs_next;
+        nx.acc = acc;
+        nx.vs_next = vs;
+        adv = (r + k.g * vs1) - v;
+        return vs;
+    }
+}
+
+// TGT: algorithm whose target is written (kNone: no target output).
+// ADV: algorithm whose advantages are written.
+// REW: rewards present.  RETT: MC reads returns at every t (ret_T == T).
+template <int TGT, int ADV, bool REW, bool RETT>
+__global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
+    constexpr bool kRho = (TGT == HRL_ALG_VTRACE) || (ADV == HRL_ALG_VTRACE);
+    constexpr bool kRet = RETT && (ADV == HRL_ALG_MC);
+
+    extern __shared__ float lds[];
+    const int lane = threadIdx.x;
+    const int C = a.C;
+    const int G = kWave / C;
+    const int J = G * C;                      // value columns per wave
+    const int Jr = G * a.rhoC;                // rho columns per wave
+    const int ldv = J + 1, ldr = Jr + 1;
+    const int T = a.T;
+    const int tmax = T < kTChunk ? T : kTChunk;
+
+    const int64_t b0 = (int64_t)blockIdx.x * G;
+    const int ntraj = (int)min<int64_t>(G, a.B - b0);
+
+    // LDS carve-up (sizes fixed by tmax, see launch)
+    float *t_v = lds;
+    float *t_r = t_v + tmax * ldv;
+    float *t_ret = t_r + (REW ? tmax * ldv : 0);
+    float *t_tgt = t_ret + (kRet ? tmax * ldv : 0);
+    float *t_adv = t_tgt + (TGT != kNone ? tmax * ldv : 0);
+    float *t_rho = t_adv + tmax * ldv;
+    float *t_cs = t_rho + (kRho ? tmax * ldr : 0);
+
+    const int g = lane / C;
+    const int c = lane - g * C;
+    const bool active = (lane < J) && (g < ntraj);
+    const int rcol = g * a.rhoC + c / a.rhoDiv;
+
+    float boot = 0.f;
+    if (active) {
+        boot = a.returns[(b0 + g) * (int64_t)a.retT * C + (int64_t)(a.retT - 1) * C + c];
+    }
+
+    Carry s{0.f, 0.f, 0.f, 0.f, 0.f};
+    const int nchunks = (T + kTChunk - 1) / kTChunk;
+    for (int ch = nchunks - 1; ch >= 0; --ch) {
+        const int t0 = ch * kTChunk;
+        const int tc = min(kTChunk, T - t0);
+
+        Chunk cv, cr, cret, crho, ccs;
+        cv.setup(a.values, b0, T, C, t0, tc, ntraj, ldv);
+        if constexpr (REW) cr.setup(a.rewards, b0, T, C, t0, tc, ntraj, ldv);
+        if constexpr (kRet) cret.setup(a.returns, b0, T, C, t0, tc, ntraj, ldv);
+        if constexpr (kRho) {
+            crho.setup(a.rhos, b0, T, a.rhoC, t0, tc, ntraj, ldr);
+            ccs.setup(a.cs, b0, T, a.rhoC, t0, tc, ntraj, ldr);
+        }
+
+        // issue every input's loads before the first LDS write
+        Staged sv, sr, sret, srho, scs;
+        sv.load(cv, lane);
+        if constexpr (REW) sr.load(cr, lane);
+        if constexpr (kRet) sret.load(cret, lane);
+        if constexpr (kRho) { srho.load(crho, lane); scs.load(ccs, lane); }
+        sv.to_lds(cv, t_v);
+        if constexpr (REW) sr.to_lds(cr, t_r);
+        if constexpr (kRet) sret.to_lds(cret, t_ret);
+        if constexpr (kRho) { srho.to_lds(crho, t_rho); scs.to_lds(ccs, t_cs); }
+        __syncthreads();
+
+        if (active) {
+            for (int tt = tc - 1; tt >= 0; --tt) {
+                const bool last = (t0 + tt == T - 1);
+                const float v = t_v[tt * ldv + lane];
+                const float r = REW ? t_r[tt * ldv + lane] : 0.f;
+                const float rho = kRho ? t_rho[tt * ldr + rcol] : 0.f;
+                const float cc = kRho ? t_cs[tt * ldr + rcol] : 0.f;
+                const float ret_t = kRet ? t_ret[tt * ldv + lane] : boot;
+
+                float adv, adv_unused;
+                Carry nx = s;
+                if constexpr (TGT != kNone && TGT != ADV) {
+                    const float tgt = step<TGT>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv_unused);
+                    step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
+                    t_tgt[tt * ldv + lane] = tgt;
+                } else {
+                    const float tgt = step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
+                    if constexpr (TGT != kNone) t_tgt[tt * ldv + lane] = tgt;
+                }
+                t_adv[tt * ldv + lane] = adv;
+                nx.v_next = v;
+                s = nx;
+            }
+        }
+        __syncthreads();
+
+        const int64_t off = b0 * (int64_t)T * C + (int64_t)t0 * C;
+        if constexpr (TGT != kNone) store_chunk(cv, t_tgt, a.targets + off);
+        store_chunk(cv, t_adv, a.advantages + off);
+    }
+}
+
+template <int TGT, int ADV, bool REW, bool RETT>
+int launch_one(const Args &a, hipStream_t stream) {
+    constexpr bool kRho = (TGT == HRL_ALG_VTRACE) || (ADV == HRL_ALG_VTRACE);
+    constexpr bool kRet = RETT && (ADV == HRL_ALG_MC);
+    const int G = kWave / a.C;
+    const int J = G * a.C, Jr = G * a.rhoC;
+    const int tmax = a.T < kTChunk ? a.T : kTChunk;
+    const int vtiles = 1 + (REW ? 1 : 0) + (kRet ? 1 : 0) + (TGT != kNone ? 1 : 0) + 1;
+    const size_t lds = sizeof(float) * ((size_t)vtiles * tmax * (J + 1) + (kRho ? 2u : 0u) * tmax * (Jr + 1));
+    const int64_t blocks = (a.B + G - 1) / G;
+    if (blocks > 0x7fffffff) return HRL_EINVAL;
+    hipLaunchKernelGGL((targets_kernel<TGT, ADV, REW, RETT>), dim3((unsigned)blocks), dim3(kWave), lds,
+                       stream, a);
+    const hipError_t err = hipGetLastError();
+    return err == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)err;
+}
+
+template <int TGT, int ADV>
+int launch_flags(const Args &a, hipStream_t s) {
+    const bool rew = a.rewards != nullptr;
+    const bool rett = a.retT == a.T && a.T > 1;
+    if (rew) return rett ? launch_one<TGT, ADV, true, true>(a, s) : launch_one<TGT, ADV, true, false>(a, s);
+    return rett ? launch_one<TGT, ADV, false, true>(a, s) : launch_one<TGT, ADV, false, false>(a, s);
+}
+
+template <int TGT>
+int launch_adv(int adv, const Args &a, hipStream_t s) {
+    switch (adv) {
+        case HRL_ALG_MC: return launch_flags<TGT, HRL_ALG_MC>(a, s);
+        case HRL_ALG_TD: return launch_flags<TGT, HRL_ALG_TD>(a, s);
+        case HRL_ALG_UPGO: return launch_flags<TGT, HRL_ALG_UPGO>(a, s);
+        case HRL_ALG_VTRACE: return launch_flags<TGT, HRL_ALG_VTRACE>(a, s);
+        default: return HRL_EINVAL;
+    }
+}
+
+int dispatch(int tgt, int adv, const Args &a, hipStream_t s) {
+    switch (tgt) {
+        case kNone: return launch_adv<kNone>(adv, a, s);
+        case HRL_ALG_TD: return launch_adv<HRL_ALG_TD>(adv, a, s);
+        case HRL_ALG_UPGO: return launch_adv<HRL_ALG_UPGO>(adv, a, s);
+        case HRL_ALG_VTRACE: return launch_adv<HRL_ALG_VTRACE>(adv, a, s);
+        default: return HRL_EINVAL;
+    }
+}
+
+bool valid_alg(int alg) { return alg >= HRL_ALG_MC && alg <= HRL_ALG_VTRACE; }
+
+int prepare(int target_alg, int adv_alg, const float *values, const float *returns, const float *rewards,
+            const float *rhos, const float *cs, int64_t B, int64_t T, int64_t C, int64_t ret_T,
+            int64_t rho_C, int64_t rho_div, double lmb, double gamma, float *targets, float *advantages,
+            void *stream) {
+    if (!valid_alg(target_alg) || !valid_alg(adv_alg)) return HRL_EINVAL;
+    if (B < 0 || T < 1 || C < 1 || C > kWave || T > (1 << 24)) return HRL_EINVAL;
+    if (ret_T != 1 && ret_T != T) return HRL_EINVAL;
+    if (rho_C < 1 || rho_div < 1 || rho_C * rho_div != C) {
+        // rho columns must tile the value columns: rho_C == 1 (rho_div == C) or rho_C == P (rho_div == K)
+        return HRL_EINVAL;
+    }
+    if (target_alg == HRL_ALG_MC && targets != nullptr) return HRL_EINVAL;
+    if (B == 0) return HRL_OK;  // empty batch: nothing to read or write (data pointers may be NULL)
+    const bool need_rho = target_alg == HRL_ALG_VTRACE || adv_alg == HRL_ALG_VTRACE;
+    if (!values || !returns || !advantages || (need_rho && (!rhos || !cs))) return HRL_EINVAL;
+    if (B * T * C > (int64_t)1 << 40) return HRL_EINVAL;
+    Args a;
+    a.values = values; a.returns = returns; a.rewards = rewards; a.rhos = rhos; a.cs = cs;
+    a.targets = targets; a.advantages = advantages;
+    a.B = B; a.T = (int)T; a.C = (int)C; a.retT = (int)ret_T; a.rhoC = (int)rho_C; a.rhoDiv = (int)rho_div;
+    a.k.a = (float)(1.0 - lmb);
+    a.k.l = (float)lmb;
+    a.k.g = (float)gamma;
+    a.k.gl = (float)(gamma * lmb);
+    const int tgt = (targets == nullptr || target_alg == HRL_ALG_MC) ? kNone : target_alg;
+    return dispatch(tgt, adv_alg, a, static_cast<hipStream_t>(stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+int hrl_abi_version(void) { return 1; }
+
+const char *hrl_strerror(int code) {
+    if (code == HRL_OK) return "success";
+    if (code == HRL_EINVAL) return "invalid argument (algorithm, shape or pointer)";
+    if (code <= HRL_ELAUNCH_BASE) return hipGetErrorString(static_cast<hipError_t>(HRL_ELAUNCH_BASE - code));
+    return "unknown error";
+}
+
+int hrl_compute_target(int alg, const float *values, const float *returns, const float *rewards,
+                       const float *rhos, const float *cs, int64_t B, int64_t T, int64_t C, int64_t ret_T,
+                       int64_t rho_C, int64_t rho_div, double lmb, double gamma, float *targets,
+                       float *advantages, void *stream) {
+    return prepare(alg, alg, values, returns, rewards, rhos, cs, B, T, C, ret_T, rho_C, rho_div, lmb, gamma,
+                   targets, advantages, stream);
+}
+
+int hrl_compute_targets_fused(int target_alg, int adv_alg, const float *values, const float *returns,
+                              const float *rewards, const float *rhos, const float *cs, int64_t B, int64_t T,
+                              int64_t C, int64_t ret_T, int64_t rho_C, int64_t rho_div, double lmb,
+                              double gamma, float *targets, float *advantages, void *stream) {
+    return prepare(target_alg, adv_alg, values, returns, rewards, rhos, cs, B, T, C, ret_T, rho_C, rho_div, lmb,
+                   gamma, targets, advantages, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,197 @@
+"""The learner update on MI355X (handyrl/train.py:312-414, Trainer).
+
+``LearnerStep`` is one iteration of the reference's training loop body
+(train.py:372-392) on a device-resident batch:
+
+    forward_prediction -> IS ratios -> fused HIP target scans -> losses
+    -> backward (+ bucketed RCCL SUM all-reduce, overlapped) -> clip 4.0
+    -> Adam(lr = 3e-8 * data_cnt_ema, weight_decay = 1e-5)
+
+differences from the reference that do not change the arithmetic:
+* no ``.item()`` in the step: loss sums and ``dcnt`` accumulate on the device
+  and are read once per epoch (train.py:199, :390 sync every step);
+* gradients sit in one flat buffer (zeroed by one kernel, clipped by one
+  norm, all-reduced in a few buckets);
+* optionally the whole step is captured once in a HIP graph and replayed
+  (``graph=True``): the batch tensors are then static buffers that the caller
+  refills (``load_batch``), exactly like a graph's input slots.
+
+``Trainer`` keeps the reference class's epoch API (``train()`` returns a CPU
+copy of the model, lr schedule at epoch end, train.py:357-401) over any batch
+source with a ``batch()`` method.
+"""
+
+import copy
+
+import torch
+import torch.nn as nn
+
+from . import distributed as hdist
+from .train import forward_prediction, loss_terms
+
+DEFAULT_LR = 3e-8  # train.py:318
+
+
+class LearnerStep:
+    def __init__(self, net, args, device, lr=None, graph=False, reduce_group=None, world_size=1,
+                 bucket_bytes=256 * 1024):
+        self.net = net.to(device)
+        self.args = args
+        self.device = device
+        self.graph = graph and device.type == 'cuda'
+        self.params = [p for p in self.net.parameters() if p.requires_grad]
+        self.grads = hdist.FlatGrads(self.params)
+        self.reducer = None
+        if world_size > 1:
+            self.reducer = hdist.GradAllReduce(self.grads, group=reduce_group, bucket_bytes=bucket_bytes)
+        if lr is None:
+            lr = DEFAULT_LR * args['batch_size'] * args['forward_steps']
+        if self.graph:
+            self.optimizer = torch.optim.Adam(self.params, lr=torch.tensor(lr, device=device),
+                                              weight_decay=1e-5, capturable=True, foreach=True)
+        else:
+            self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=1e-5, foreach=True)
+        self._graph = None
+        self._static = None
+        self._static_out = None
+        self.stats = None
+
+    # -- learning rate (train.py:396-398) ---------------------------------
+    def set_lr(self, lr):
+        for group in self.optimizer.param_groups:
+            if isinstance(group['lr'], torch.Tensor):
+                group['lr'].fill_(lr)
+            else:
+                group['lr'] = lr
+
+    # -- one update ----------------------------------------------------------
+    def _body(self, batch, hidden):
+        self.grads.zero()
+        outputs = forward_prediction(self.net, hidden, batch, self.args)
+        losses, dcnt = loss_terms(outputs, batch, self.args)
+        losses['total'].backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        gnorm = self.grads.clip_(4.0)
+        self.optimizer.step()
+        out = {k: v.detach() for k, v in losses.items()}
+        out['dcnt'] = dcnt
+        out['grad_norm'] = gnorm
+        return out
+
+    def _accumulate(self, out):
+        vec = torch.stack([out[k].reshape(()) for k in sorted(out)])
+        if self.stats is None:
+            self.stats_keys = sorted(out)
+            self.stats = torch.zeros_like(vec)
+            self.batches = 0
+        self.stats += vec
+        self.batches += 1
+
+    def step(self, batch, hidden=None):
+        """Run one update; returns the step's losses / dcnt as device tensors (no sync)."""
+        if self.graph:
+            if self._graph is None:
+                self._capture(batch, hidden)
+            elif batch is not self._static:
+                self.load_batch(batch)
+            self._graph.replay()
+            out = self._static_out
+        else:
+            out = self._body(batch, hidden)
+        self._accumulate(out)
+        return out
+
+    def _capture(self, batch, hidden):
+        if self.reducer is not None:
+            raise RuntimeError('HIP-graph capture of the multi-GPU step is not supported; use graph=False')
+        self._static = batch
+        # warm up on a side stream (allocator pools, MIOpen kernel selection, lazy state)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                self._body(batch, hidden)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self._graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._graph):
+            self._static_out = self._body(batch, hidden)
+
+    def load_batch(self, batch):
+        """Copy a new batch into the captured graph's static input tensors."""
+        for k, v in batch.items():
+            dst = self._static[k]
+            if isinstance(v, dict):
+                for kk, vv in v.items():
+                    dst[kk].copy_(vv, non_blocking=True)
+            else:
+                dst.copy_(v, non_blocking=True)
+
+    def pop_stats(self):
+        """Sum of the per-step losses since the last call (one host sync), as a dict."""
+        if self.stats is None:
+            return {}, 0
+        vals = self.stats
+        if self.reducer is not None:
+            vals = hdist.all_reduce_sum_([vals.clone()], self.reducer.group)[0]
+        vals = vals.tolist()
+        res = dict(zip(self.stats_keys, vals))
+        n = self.batches
+        self.stats = None
+        return res, n
+
+
+class Trainer:
+    """Reference-API trainer (train.py:312-414) driving LearnerStep on one GPU rank.
+
+    ``batcher`` is any object with ``batch()`` returning a make_batch-layout
+    dict (host or device tensors); ``model`` is the env's network.
+    """
+
+    def __init__(self, args, model, batcher, device=None, graph=False, world_size=1, group=None):
+        self.args = args
+        self.model = model
+        self.batcher = batcher
+        self.device = device or torch.device('cuda', torch.cuda.current_device())
+        self.default_lr = DEFAULT_LR
+        self.data_cnt_ema = args['batch_size'] * args['forward_steps']
+        self.steps = 0
+        self.update_flag = False
+        self.shutdown_flag = False
+        self.learner = LearnerStep(model, args, self.device, lr=self.default_lr * self.data_cnt_ema,
+                                   graph=graph, reduce_group=group, world_size=world_size)
+
+    def _to_device(self, batch):
+        def mv(x):
+            if isinstance(x, dict):
+                return {k: mv(v) for k, v in x.items()}
+            return x.to(self.device, non_blocking=True) if x is not None else None
+        return mv(batch)
+
+    def train(self, max_steps=None):
+        """One epoch: step until update_flag / shutdown (or max_steps); returns a CPU model copy."""
+        self.model.train()
+        n = 0
+        while (n == 0 or not (self.update_flag or self.shutdown_flag)) and (max_steps is None or n < max_steps):
+            batch = self._to_device(self.batcher.batch())
+            B, P = batch['value'].size(0), batch['value'].size(2)
+            hidden = self.model.init_hidden([B, P]) if hasattr(self.model, 'init_hidden') else None
+            if hidden is not None:
+                hidden = self._to_device(hidden)
+            self.learner.step(batch, hidden)
+            n += 1
+            self.steps += 1
+        sums, batch_cnt = self.learner.pop_stats()
+        data_cnt = sums.pop('dcnt', 0.0)
+        sums.pop('grad_norm', None)
+        print('loss = %s' % ' '.join('%s:%.3f' % (k, v / max(data_cnt, 1e-9)) for k, v in sums.items()))
+        self.data_cnt_ema = self.data_cnt_ema * 0.8 + data_cnt / (1e-2 + batch_cnt) * 0.2
+        self.learner.set_lr(self.default_lr * self.data_cnt_ema / (1 + self.steps * 1e-5))
+        model = copy.deepcopy(self.model).cpu()
+        model.eval()
+        return model
+
+
+def clip_grad_norm_reference(params, max_norm=4.0):
+    """The reference's clip (train.py:384), kept for tests that compare both forms."""
+    return nn.utils.clip_grad_norm_(params, max_norm)

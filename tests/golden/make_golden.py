@@ -1,0 +1,317 @@
+"""Golden-vector generator for the learner hot path.
+
+Runs ONLY in the build container, where the reference HandyRL tree is mounted
+read-only at ``$HANDYRL_REF`` (default ``/root/reference``).  It imports the
+reference's own learner math and writes small ``.npz`` fixtures (inputs and
+expected outputs, nothing else) next to this file.  The reference itself never
+enters this repository and never travels to the GPU box: the tests only read
+the fixtures.
+
+Fixtures written
+----------------
+``targets.npz`` + ``targets.json``
+    ``handyrl.losses.compute_target`` (losses.py:61-74) for MC / TD / UPGO /
+    VTRACE on the value-head convention (returns = outcome (B,1,P,1),
+    rewards=None, gamma=1; train.py:245) and the return-head convention
+    (returns (B,T,P,1), rewards present, gamma=0.8; train.py:246), over
+    T in {1,2,9,32}, P in {1,2}, rho P-extent in {1,P}, plus a trailing-dim
+    K=2 case.
+``loss.npz`` + ``loss.json``
+    ``handyrl.train.compute_loss`` (train.py:218-258) on real ``make_batch``
+    batches (train.py:33-133) built from seeded self-play episodes
+    (generation.py:20-88) of TicTacToe and Geister, with fixed network
+    outputs, recording every ``compute_target`` call, the composed advantages,
+    the losses, ``dcnt`` and the gradients w.r.t. the network outputs.
+``learner.npz`` + ``learner.json``
+    Three learner steps of the TicTacToe ``SimpleConv2dModel`` exactly as
+    ``Trainer.train`` runs them (train.py:375-385): loss, backward,
+    ``clip_grad_norm_(4.0)``, ``Adam(lr=3e-8*B*T, weight_decay=1e-5)``.
+
+Usage:  python tests/golden/make_golden.py
+"""
+
+import json
+import os
+import random
+import sys
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+REF = os.environ.get('HANDYRL_REF', '/root/reference')
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF)
+
+from handyrl import losses as ref_losses            # noqa: E402
+from handyrl import train as ref_train              # noqa: E402
+from handyrl.model import ModelWrapper, RandomModel  # noqa: E402
+from handyrl.generation import Generator            # noqa: E402
+from handyrl.environment import make_env            # noqa: E402
+
+torch.set_num_threads(1)
+
+
+def _np(x):
+    return None if x is None else x.detach().cpu().numpy().copy()
+
+
+# ---------------------------------------------------------------------------
+# 1. compute_target cases
+# ---------------------------------------------------------------------------
+
+def target_cases():
+    g = torch.Generator().manual_seed(1234)
+    arrays, manifest = {}, []
+    shapes = []
+    for T in (1, 2, 9, 32):
+        for P, Pr in ((1, 1), (2, 1), (2, 2)):
+            shapes.append((5, T, P, Pr, 1))
+    shapes.append((3, 9, 2, 1, 2))   # trailing value dim K=2, rho broadcast over P and K
+    shapes.append((4, 16, 4, 4, 1))  # four-player, per-player rho
+    cid = 0
+    for (B, T, P, Pr, K) in shapes:
+        for head in ('value', 'return'):
+            values = torch.tanh(torch.randn(B, T, P, K, generator=g))
+            rhos = torch.clamp(torch.exp(0.5 * torch.randn(B, T, Pr, 1, generator=g)), 0, 1)
+            cs = torch.clamp(torch.exp(0.5 * torch.randn(B, T, Pr, 1, generator=g)), 0, 1)
+            if head == 'value':
+                returns = torch.randint(-1, 2, (B, 1, P, K), generator=g).float()
+                rewards, gamma = None, 1
+            else:
+                returns = torch.randn(B, T, P, K, generator=g)
+                rewards = 0.1 * torch.randn(B, T, P, K, generator=g)
+                gamma = 0.8
+            lmb = 0.7
+            for alg in ('MC', 'TD', 'UPGO', 'VTRACE'):
+                tgt, adv = ref_losses.compute_target(alg, values, returns, rewards, lmb, gamma, rhos, cs)
+                pre = '%d:' % cid
+                arrays[pre + 'values'] = _np(values)
+                arrays[pre + 'returns'] = _np(returns)
+                if rewards is not None:
+                    arrays[pre + 'rewards'] = _np(rewards)
+                arrays[pre + 'rhos'] = _np(rhos)
+                arrays[pre + 'cs'] = _np(cs)
+                arrays[pre + 'target'] = _np(tgt)
+                arrays[pre + 'adv'] = _np(adv)
+                manifest.append({'id': cid, 'alg': alg, 'head': head, 'B': B, 'T': T, 'P': P,
+                                 'Pr': Pr, 'K': K, 'gamma': gamma, 'lmb': lmb,
+                                 'has_rewards': rewards is not None})
+                cid += 1
+    # values is None convention (losses.py:62-63)
+    none_out = ref_losses.compute_target('VTRACE', None, None, None, 0.7, 1, None, None)
+    assert none_out == (None, 0)
+    return arrays, manifest
+
+
+# ---------------------------------------------------------------------------
+# 2. compute_loss cases on real make_batch batches
+# ---------------------------------------------------------------------------
+
+def gen_episodes(env_name, n, obs_flag, seed, net_cls=None):
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    env = make_env({'env': env_name})
+    if net_cls is not None:
+        model = ModelWrapper(net_cls())
+    else:
+        model = ModelWrapper(RandomModel(env))
+    gargs = {'observation': obs_flag, 'gamma': 0.8, 'compress_steps': 4}
+    gen = Generator(env, gargs)
+    eps = []
+    while len(eps) < n:
+        ep = gen.generate({p: model for p in env.players()}, {'player': env.players()})
+        if ep is not None:
+            eps.append(ep)
+    return eps
+
+
+def select_windows(episodes, B, T, compress_steps, seed):
+    """Window choice as Batcher.select_episode (train.py:284-302), uniform over episodes."""
+    rnd = random.Random(seed)
+    out = []
+    for _ in range(B):
+        ep = episodes[rnd.randrange(len(episodes))]
+        turn_candidates = 1 + max(0, ep['steps'] - T)
+        st = rnd.randrange(turn_candidates)
+        ed = min(st + T, ep['steps'])
+        st_block = st // compress_steps
+        ed_block = (ed - 1) // compress_steps + 1
+        out.append({'args': ep['args'], 'outcome': ep['outcome'], 'moment': ep['moment'][st_block:ed_block],
+                    'base': st_block * compress_steps, 'start': st, 'end': ed, 'total': ep['steps']})
+    return out
+
+
+class FixedOutputs(nn.Module):
+    """A 'network' whose outputs are its parameters, so d(loss)/d(output) is a param grad."""
+
+    def __init__(self, N, A, has_return, seed):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed)
+        self.p = nn.Parameter(torch.randn(N, A, generator=g))
+        self.v = nn.Parameter(torch.tanh(torch.randn(N, 1, generator=g)))
+        self.r = nn.Parameter(torch.randn(N, 1, generator=g)) if has_return else None
+
+    def forward(self, x, hidden=None):
+        out = {'policy': self.p, 'value': self.v}
+        if self.r is not None:
+            out['return'] = self.r
+        return out
+
+
+def loss_cases():
+    arrays, manifest = {}, []
+    specs = [
+        # name, env, tbt, obs, B, T, policy_target, value_target, has_return
+        ('ttt_tbt', 'TicTacToe', True, False, 6, 16, 'UPGO', 'VTRACE', False),
+        ('ttt_tbt_T9', 'TicTacToe', True, False, 8, 9, 'VTRACE', 'VTRACE', False),
+        ('ttt_tbt_td', 'TicTacToe', True, False, 6, 5, 'TD', 'MC', False),
+        ('ttt_obs', 'TicTacToe', True, True, 5, 4, 'UPGO', 'VTRACE', False),
+        ('ttt_solo', 'TicTacToe', False, False, 6, 9, 'MC', 'TD', False),
+        ('geister_ret', 'Geister', True, False, 4, 16, 'UPGO', 'VTRACE', True),
+        ('geister_ret_td', 'Geister', True, False, 3, 8, 'TD', 'UPGO', True),
+    ]
+    from handyrl.envs.tictactoe import SimpleConv2dModel
+    ep_cache = {}
+    for ci, (name, env_name, tbt, obs, B, T, ptgt, vtgt, has_ret) in enumerate(specs):
+        key = (env_name, obs)
+        if key not in ep_cache:
+            if env_name == 'TicTacToe':
+                ep_cache[key] = gen_episodes(env_name, 24, obs, seed=7 + ci, net_cls=SimpleConv2dModel)
+            else:
+                ep_cache[key] = gen_episodes(env_name, 3, obs, seed=7 + ci)
+        eps = select_windows(ep_cache[key], B, T, 4, seed=100 + ci)
+        args = {'turn_based_training': tbt, 'observation': obs, 'forward_steps': T, 'compress_steps': 4,
+                'lambda': 0.7, 'gamma': 0.8, 'policy_target': ptgt, 'value_target': vtgt,
+                'entropy_regularization': 0.1, 'entropy_regularization_decay': 0.1}
+        random.seed(500 + ci)  # make_batch draws a random player in solo mode (train.py:58)
+        batch = ref_train.make_batch(eps, args)
+        Pp = batch['action'].size(2)
+        A = batch['policy'].size(-1)
+        N = B * T * Pp
+        net = FixedOutputs(N, A, has_ret, seed=900 + ci)
+
+        calls = []
+        orig_ct = ref_train.compute_target
+
+        def spy_ct(alg, *a):
+            out = orig_ct(alg, *a)
+            calls.append((alg, a, out))
+            return out
+
+        captured = {}
+        orig_cl = ref_train.compose_losses
+
+        def spy_cl(outputs, log_sel, total_adv, targets, batch_, args_):
+            captured['log_sel'] = log_sel.detach().clone()
+            captured['total_adv'] = total_adv.detach().clone()
+            return orig_cl(outputs, log_sel, total_adv, targets, batch_, args_)
+
+        ref_train.compute_target = spy_ct
+        ref_train.compose_losses = spy_cl
+        try:
+            losses, dcnt = ref_train.compute_loss(batch, net, None, args)
+        finally:
+            ref_train.compute_target = orig_ct
+            ref_train.compose_losses = orig_cl
+        losses['total'].backward()
+
+        pre = '%d:' % ci
+        for k, v in batch.items():
+            if k == 'observation':
+                continue
+            arrays[pre + 'batch.' + k] = _np(v)
+        arrays[pre + 'out.policy'] = _np(net.p)
+        arrays[pre + 'out.value'] = _np(net.v)
+        arrays[pre + 'grad.policy'] = _np(net.p.grad)
+        arrays[pre + 'grad.value'] = _np(net.v.grad)
+        if has_ret:
+            arrays[pre + 'out.return'] = _np(net.r)
+            arrays[pre + 'grad.return'] = _np(net.r.grad)
+        arrays[pre + 'log_sel'] = _np(captured['log_sel'])
+        arrays[pre + 'total_adv'] = _np(captured['total_adv'])
+        call_meta = []
+        for j, (alg, a, out) in enumerate(calls):
+            values, returns, rewards, lmb, gamma, rhos, cs = a
+            cpre = pre + 'call%d.' % j
+            if values is not None:
+                arrays[cpre + 'values'] = _np(values)
+                arrays[cpre + 'target'] = _np(out[0])
+                arrays[cpre + 'adv'] = _np(out[1])
+            arrays[cpre + 'rhos'] = _np(rhos)
+            call_meta.append({'alg': alg, 'values_none': values is None, 'gamma': gamma, 'lmb': lmb,
+                              'has_rewards': rewards is not None})
+        manifest.append({'id': ci, 'name': name, 'env': env_name, 'B': B, 'T': T, 'Pp': Pp, 'A': A,
+                         'has_return': has_ret, 'args': args, 'dcnt': dcnt,
+                         'losses': {k: float(v.item()) for k, v in losses.items()}, 'calls': call_meta})
+    return arrays, manifest
+
+
+# ---------------------------------------------------------------------------
+# 3. learner steps with the TicTacToe net
+# ---------------------------------------------------------------------------
+
+def learner_case():
+    from handyrl.envs.tictactoe import SimpleConv2dModel
+    B, T = 16, 9
+    eps = gen_episodes('TicTacToe', 32, False, seed=31, net_cls=SimpleConv2dModel)
+    args = {'turn_based_training': True, 'observation': False, 'forward_steps': T, 'compress_steps': 4,
+            'lambda': 0.7, 'gamma': 0.8, 'policy_target': 'UPGO', 'value_target': 'VTRACE',
+            'entropy_regularization': 0.1, 'entropy_regularization_decay': 0.1}
+    batch = ref_train.make_batch(select_windows(eps, B, T, 4, seed=77), args)
+
+    torch.manual_seed(2024)
+    net = SimpleConv2dModel()
+    arrays = {}
+    names = []
+    for k, v in net.state_dict().items():
+        arrays['init.' + k] = _np(v)
+        names.append(k)
+    for k, v in batch.items():
+        arrays['batch.' + k] = _np(v)
+
+    model = ModelWrapper(net)
+    params = list(model.parameters())
+    opt = torch.optim.Adam(params, lr=3e-8 * B * T, weight_decay=1e-5)
+    model.train()
+    step_losses = []
+    for s in range(3):
+        losses, dcnt = ref_train.compute_loss(batch, model, None, args)
+        opt.zero_grad()
+        losses['total'].backward()
+        gn = nn.utils.clip_grad_norm_(params, 4.0)
+        opt.step()
+        step_losses.append({k: float(v.item()) for k, v in losses.items()})
+        step_losses[-1]['grad_norm'] = float(gn)
+        step_losses[-1]['dcnt'] = dcnt
+    for k, v in net.state_dict().items():
+        arrays['final.' + k] = _np(v)
+    meta = {'B': B, 'T': T, 'args': args, 'lr': 3e-8 * B * T, 'steps': step_losses, 'state_names': names}
+    return arrays, meta
+
+
+def main():
+    arr, man = target_cases()
+    np.savez_compressed(os.path.join(OUT, 'targets.npz'), **arr)
+    with open(os.path.join(OUT, 'targets.json'), 'w') as f:
+        json.dump(man, f, indent=0)
+    print('targets: %d cases' % len(man))
+
+    arr, man = loss_cases()
+    np.savez_compressed(os.path.join(OUT, 'loss.npz'), **arr)
+    with open(os.path.join(OUT, 'loss.json'), 'w') as f:
+        json.dump(man, f, indent=1)
+    print('loss: %d cases' % len(man))
+
+    arr, meta = learner_case()
+    np.savez_compressed(os.path.join(OUT, 'learner.npz'), **arr)
+    with open(os.path.join(OUT, 'learner.json'), 'w') as f:
+        json.dump(meta, f, indent=1)
+    print('learner: %d steps' % len(meta['steps']))
+
+
+if __name__ == '__main__':
+    main()

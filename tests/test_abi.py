@@ -1,0 +1,76 @@
+"""libhrl.so loads on a CPU-only host and exports exactly the C ABI of include/*.h.
+
+No compute call is made here (no GPU): only the argument-validation paths,
+which return before any HIP call.
+"""
+
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+from handyrl_amd import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    syms = set()
+    for h in glob.glob(os.path.join(ROOT, 'include', '*.h')):
+        text = open(h).read()
+        text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+        syms |= set(re.findall(r'\b(hrl_[a-z0-9_]+)\s*\(', text))
+    return syms
+
+
+def test_header_symbols_bound():
+    syms = declared_symbols()
+    assert 'hrl_compute_target' in syms and 'hrl_compute_targets_fused' in syms
+    assert syms == set(_native.SIGNATURES), 'ctypes signatures out of sync with include/*.h'
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.load()
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+    out = subprocess.run(['nm', '-D', '--defined-only', _native.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r' T (hrl_[a-z0-9_]+)', out))
+    assert declared_symbols() <= exported
+
+
+def test_abi_version_and_errors():
+    lib = _native.load()
+    assert lib.hrl_abi_version() == _native.ABI_VERSION
+    assert b'invalid' in lib.hrl_strerror(_native.HRL_EINVAL)
+    assert lib.hrl_strerror(0) == b'success'
+
+
+@pytest.mark.parametrize('alg,kw', [
+    (7, {}),                                  # unknown algorithm
+    (1, {'T': 0}),                            # empty time axis
+    (1, {'C': 65}),                           # more columns than a wave
+    (1, {'ret_T': 3}),                        # returns time extent not in {1, T}
+    (3, {'rho_C': 2, 'rho_div': 2, 'C': 2}),  # rho columns do not tile value columns
+    (3, {'null_rho': True}),                  # V-trace without rhos
+    (0, {'targets': True}),                   # MC writes no targets
+])
+def test_invalid_arguments_rejected_without_gpu(alg, kw):
+    lib = _native.load()
+    dummy = ctypes.c_void_p(16)
+    B, T, C = 4, kw.get('T', 8), kw.get('C', 2)
+    rho_C, rho_div = kw.get('rho_C', 1), kw.get('rho_div', C)
+    rho = None if kw.get('null_rho') else dummy
+    tgt = dummy if kw.get('targets') else None
+    code = lib.hrl_compute_target(alg, dummy, dummy, None, rho, rho, B, T, C, kw.get('ret_T', 1),
+                                  rho_C, rho_div, 0.7, 1.0, tgt, dummy, None)
+    assert code == _native.HRL_EINVAL
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_native, '_lib', None)
+    monkeypatch.setattr(_native, 'LIB_PATH', str(tmp_path / 'nope.so'))
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        _native.load()

@@ -1,0 +1,111 @@
+"""Learner parity on the GPU: handyrl_amd.train / trainer vs the reference.
+
+* compute_loss (HIP fused target scans + PyTorch-ROCm) on the reference's
+  make_batch batches with fixed network outputs: losses to rel 1e-5, dcnt
+  exact, gradients w.r.t. the outputs;
+* three learner steps of the TicTacToe net from the reference's initial
+  weights: per-step losses and final weights vs the reference's;
+* the HIP-graph-captured step equals the eager step;
+* the BASELINE-size synthetic batch (B=4096, T=32) against the CPU oracle.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import learner as ol
+
+from tests.test_oracle_learner import FixedOutputs, loss_case, learner_setup
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def _to(batch, dev):
+    return {k: (v.to(dev) if isinstance(v, torch.Tensor) else {kk: vv.to(dev) for kk, vv in v.items()})
+            for k, v in batch.items()}
+
+
+def _close(a, b, rtol=RTOL, what=''):
+    assert abs(a - b) <= rtol * max(1.0, abs(b)), (what, a, b)
+
+
+def test_compute_loss_golden(cuda, golden_loss):
+    from handyrl_amd.train import compute_loss
+    meta, arrays = golden_loss
+    for c in meta:
+        batch, net = loss_case(arrays, c)
+        net = net.to(cuda)
+        losses, dcnt = compute_loss(_to(batch, cuda), net, None, c['args'])
+        assert dcnt == c['dcnt']
+        for k, v in c['losses'].items():
+            _close(losses[k].item(), v, what=(c['name'], k))
+        losses['total'].backward()
+        pre = '%d:' % c['id']
+        np.testing.assert_allclose(net.p.grad.cpu().numpy(), arrays[pre + 'grad.policy'], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(net.v.grad.cpu().numpy(), arrays[pre + 'grad.value'], rtol=1e-5, atol=1e-6)
+        if c['has_return']:
+            np.testing.assert_allclose(net.r.grad.cpu().numpy(), arrays[pre + 'grad.return'], rtol=1e-5, atol=1e-6)
+
+
+def test_learner_steps_golden(cuda, golden_learner):
+    from handyrl_amd.trainer import LearnerStep
+    meta, arrays, net, batch = learner_setup(golden_learner)
+    step = LearnerStep(net, meta['args'], cuda, lr=meta['lr'], graph=False)
+    net.train()
+    b = _to(batch, cuda)
+    for s, ref in enumerate(meta['steps']):
+        out = step.step(b)
+        for k in ('p', 'v', 'ent', 'total', 'grad_norm'):
+            _close(out[k].item(), ref[k], what=(s, k))
+        assert out['dcnt'].item() == ref['dcnt']
+    for k, v in net.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), arrays['final.' + k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_graph_step_equals_eager(cuda):
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.synthetic import tictactoe_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    B, T = 256, 9
+    args = default_args(T, B)
+    batch = tictactoe_batch(B, T, cuda, seed=3)
+    torch.manual_seed(0)
+    ref_net = SimpleConv2dModel()
+    g_net = SimpleConv2dModel()
+    g_net.load_state_dict(ref_net.state_dict())
+    eager = LearnerStep(ref_net, args, cuda, graph=False)
+    graph = LearnerStep(g_net, args, cuda, graph=True)
+    for _ in range(5):
+        e_out = eager.step(batch)
+    graph.step(batch)          # capture: 3 warm-up updates + 1 replay
+    g_out = graph.step(batch)  # 5th update
+    torch.cuda.synchronize()
+    for k in ('p', 'v', 'ent', 'total'):
+        _close(g_out[k].item(), e_out[k].item(), rtol=1e-5, what=k)
+    for (k, a), b in zip(ref_net.state_dict().items(), g_net.state_dict().values()):
+        np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize('B,T', [(4096, 32), (4096, 9)])
+def test_baseline_batch_losses_vs_oracle(cuda, B, T):
+    from handyrl_amd.synthetic import tictactoe_batch, default_args
+    from handyrl_amd.train import loss_terms, forward_prediction
+    args = default_args(T, B)
+    batch = tictactoe_batch(B, T, cuda, seed=B + T)
+    g = torch.Generator().manual_seed(5)
+    p = torch.randn(B * T, 9, generator=g)
+    v = torch.tanh(torch.randn(B * T, 1, generator=g))
+    net_gpu = FixedOutputs(p.numpy(), v.numpy()).to(cuda)
+    net_cpu = FixedOutputs(p.numpy(), v.numpy())
+    losses, dcnt = loss_terms(forward_prediction(net_gpu, None, batch, args), batch, args)
+    cpu_batch = {k: t.cpu() for k, t in batch.items()}
+    ref, ref_dcnt = ol.compute_loss(cpu_batch, net_cpu, None, args)
+    assert dcnt.item() == ref_dcnt
+    for k in ref:
+        _close(losses[k].item(), ref[k].item(), what=k)
+    losses['total'].backward()
+    ref['total'].backward()
+    np.testing.assert_allclose(net_gpu.p.grad.cpu().numpy(), net_cpu.p.grad.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(net_gpu.v.grad.cpu().numpy(), net_cpu.v.grad.numpy(), rtol=1e-5, atol=1e-6)
