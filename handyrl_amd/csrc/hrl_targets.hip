@@ -33,7 +33,7 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kTChunk = 32;                          // time steps per LDS pass
+constexpr int kTChunk = 16;                          // time steps per LDS pass
 constexpr int kMaxTile = kTChunk * kWave;            // floats of one tensor chunk
 constexpr int kMaxVec = kMaxTile / 4 / kWave;        // float4 loads per lane (8)
 constexpr int kMaxScalar = kMaxTile / kWave;         // scalar loads per lane (32)
@@ -53,42 +53,42 @@ __device__ __forceinline__ float max_nan(float x, float y) {
     return x > y ? x : y;
 }
 
-// Coordinates of element e of a chunk in (g, tt, cx) order, stepped one at a time.
-struct Cursor {
-    int g, tt, cx;
-    __device__ __forceinline__ void init(int e, int L, int Cx) {
-        g = e / L;
-        const int rem = e - g * L;
-        tt = rem / Cx;
-        cx = rem - tt * Cx;
-    }
-    __device__ __forceinline__ void next(int tc, int Cx) {
-        if (++cx == Cx) {
-            cx = 0;
-            if (++tt == tc) { tt = 0; ++g; }
-        }
-    }
-    __device__ __forceinline__ int lds(int ld, int Cx) const { return tt * ld + g * Cx + cx; }
-};
+// floor(e / d) for 0 <= e < 2^20 and d >= 1, given inv = 1.0f / d: the exact
+// quotient of (e + 0.5) / d sits at least 0.5/d away from an integer, far more
+// than the float32 rounding error at these magnitudes, so no integer divide.
+__device__ __forceinline__ int fdiv(int e, float inv) {
+    return (int)(((float)e + 0.5f) * inv);
+}
+
+// LDS row stride for rows of L floats read column-wise by lanes (g, c), c < Cx:
+// the smallest Lp >= L with Lp == Cx (mod 32) makes g*Lp + c distinct modulo
+// 32 over each 32-lane half when Cx divides 32 (conflict-free ds_read_b32).
+__host__ __device__ __forceinline__ int padded_row(int L, int Cx) {
+    const int m = 32;
+    const int want = Cx % m;
+    return L + ((want - L % m) % m + m) % m;
+}
 
 // One chunk of one (B, T, Cx) tensor for the wave's trajectories.
-//   global: trajectory b0+g, time t0+tt, column cx  at  (b0+g)*R + t0*Cx + tt*Cx + cx
-//   LDS   : [tt][g*Cx + cx] with row stride ld = G*Cx + 1
+//   global: trajectory b0+g, time t0+tt, column cx at (b0+g)*R + t0*Cx + tt*Cx + cx
+//   LDS   : trajectory-major rows, [g][tt*Cx + cx], row stride Lp
 struct Chunk {
     const float *base;  // element (g=0, tt=0, cx=0)
     int R;              // row length of one trajectory (T*Cx)
     int L;              // span length of one trajectory in this chunk (tc*Cx)
+    int Lp;             // padded LDS row stride
     int n;              // valid elements (ntraj * L)
-    int Cx, tc, ld;
+    float invL;
     bool shape_ok;      // spans are whole float4s (or one contiguous run)
     bool vec;           // 16-byte loads are legal for this tensor
 
-    __device__ __forceinline__ void setup(const float *p, int64_t b0, int T, int Cx_, int t0, int tc_,
-                                          int ntraj, int ld_) {
-        Cx = Cx_; tc = tc_; ld = ld_;
+    __device__ __forceinline__ void setup(const float *p, int64_t b0, int T, int Cx, int t0, int tc,
+                                          int ntraj, int Lp_) {
         R = T * Cx;
         L = tc * Cx;
+        Lp = Lp_;
         n = ntraj * L;
+        invL = 1.0f / (float)L;
         base = p + b0 * (int64_t)R + (int64_t)t0 * Cx;
         // Contiguous spans (L == R) may straddle trajectories inside a float4;
         // otherwise every span must be whole float4s.
@@ -96,68 +96,82 @@ struct Chunk {
         vec = shape_ok && ((reinterpret_cast<uintptr_t>(base) & 15) == 0);
     }
 
-    __device__ __forceinline__ int64_t gaddr(int e) const {
-        if (L == R) return e;
-        const int g = e / L;
-        return (int64_t)g * R + (e - g * L);
+    // global offset (from base; < 2^31 by the host's size check) and LDS slot of element e
+    __device__ __forceinline__ void locate(int e, int &gofs, int &slot) const {
+        const int g = fdiv(e, invL);
+        const int rem = e - g * L;
+        gofs = (L == R) ? e : g * R + rem;
+        slot = g * Lp + rem;
+    }
+    // LDS slots of elements e..e+3 given element e's trajectory g and offset rem
+    __device__ __forceinline__ int slot_after(int g, int rem, int j) const {
+        const int r = rem + j;
+        const bool wrap = r >= L;   // only when a float4 straddles two trajectories
+        return (wrap ? g + 1 : g) * Lp + (wrap ? r - L : r);
     }
 };
 
 // Registers holding one chunk between its global loads and its LDS writes.
+template <bool VEC>
 struct Staged {
-    float x[kMaxScalar];
+    float x[VEC ? 4 * kMaxVec : kMaxScalar];
 
-    __device__ __forceinline__ void load(const Chunk &c, int lane) {
+    __device__ __forceinline__ void load(const Chunk &c) {
         if (c.n <= 0) return;
-        if (c.vec) {
+        const int lane = threadIdx.x;
+        if constexpr (VEC) {
             const int nv = c.n >> 2;
             if (nv == 0) return;
 #pragma unroll
             for (int k = 0; k < kMaxVec; ++k) {
                 // clamp instead of branching so every load issues back to back
-                const int vi = min(k * kWave + (int)threadIdx.x, nv - 1);
-                const float4 q = *reinterpret_cast<const float4 *>(c.base + c.gaddr(vi * 4));
+                const int vi = min(k * kWave + lane, nv - 1);
+                int go; int slot;
+                c.locate(vi * 4, go, slot);
+                const float4 q = *reinterpret_cast<const float4 *>(c.base + go);
                 x[4 * k + 0] = q.x; x[4 * k + 1] = q.y; x[4 * k + 2] = q.z; x[4 * k + 3] = q.w;
             }
         } else {
 #pragma unroll
             for (int k = 0; k < kMaxScalar; ++k) {
-                const int e = min(k * kWave + (int)threadIdx.x, c.n - 1);
-                x[k] = c.base[c.gaddr(e)];
+                const int e = min(k * kWave + lane, c.n - 1);
+                int go; int slot;
+                c.locate(e, go, slot);
+                x[k] = c.base[go];
             }
         }
-        (void)lane;
     }
 
     __device__ __forceinline__ void to_lds(const Chunk &c, float *tile) const {
         if (c.n <= 0) return;
         const int lane = threadIdx.x;
-        if (c.vec) {
+        if constexpr (VEC) {
             const int nv = c.n >> 2;
 #pragma unroll
             for (int k = 0; k < kMaxVec; ++k) {
-                const int vi = k * kWave + lane;
-                if (vi < nv) {
-                    Cursor cur; cur.init(vi * 4, c.L, c.Cx);
-                    tile[cur.lds(c.ld, c.Cx)] = x[4 * k + 0]; cur.next(c.tc, c.Cx);
-                    tile[cur.lds(c.ld, c.Cx)] = x[4 * k + 1]; cur.next(c.tc, c.Cx);
-                    tile[cur.lds(c.ld, c.Cx)] = x[4 * k + 2]; cur.next(c.tc, c.Cx);
-                    tile[cur.lds(c.ld, c.Cx)] = x[4 * k + 3];
+                const int e = (k * kWave + lane) * 4;
+                if (e < 4 * nv) {
+                    const int g = fdiv(e, c.invL);
+                    const int rem = e - g * c.L;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) tile[c.slot_after(g, rem, j)] = x[4 * k + j];
                 }
             }
             // ragged tail (< 4 elements) of a contiguous span
             const int e = nv * 4 + lane;
             if (e < c.n) {
-                Cursor cur; cur.init(e, c.L, c.Cx);
-                tile[cur.lds(c.ld, c.Cx)] = c.base[c.gaddr(e)];
+                int go; int slot;
+                c.locate(e, go, slot);
+                tile[slot] = c.base[go];
             }
         } else {
 #pragma unroll
             for (int k = 0; k < kMaxScalar; ++k) {
                 const int e = k * kWave + lane;
                 if (e < c.n) {
-                    Cursor cur; cur.init(e, c.L, c.Cx);
-                    tile[cur.lds(c.ld, c.Cx)] = x[k];
+                    int go; int slot;
+                    c.locate(e, go, slot);
+                    tile[slot] = x[k];
                 }
             }
         }
@@ -165,31 +179,36 @@ struct Staged {
 };
 
 // LDS tile -> global, the mirror of Staged (stores need no batching).
+template <bool VEC>
 __device__ __forceinline__ void store_chunk(const Chunk &c, const float *tile, float *out_base) {
     if (c.n <= 0) return;
     const int lane = threadIdx.x;
     float *base = out_base;
-    const bool vec = c.shape_ok && ((reinterpret_cast<uintptr_t>(base) & 15) == 0);
-    if (vec) {
+    if constexpr (VEC) {
         const int nv = c.n >> 2;
         for (int vi = lane; vi < nv; vi += kWave) {
-            Cursor cur; cur.init(vi * 4, c.L, c.Cx);
+            const int e = vi * 4;
+            const int g = fdiv(e, c.invL);
+            const int rem = e - g * c.L;
             float4 q;
-            q.x = tile[cur.lds(c.ld, c.Cx)]; cur.next(c.tc, c.Cx);
-            q.y = tile[cur.lds(c.ld, c.Cx)]; cur.next(c.tc, c.Cx);
-            q.z = tile[cur.lds(c.ld, c.Cx)]; cur.next(c.tc, c.Cx);
-            q.w = tile[cur.lds(c.ld, c.Cx)];
-            *reinterpret_cast<float4 *>(base + c.gaddr(vi * 4)) = q;
+            q.x = tile[c.slot_after(g, rem, 0)];
+            q.y = tile[c.slot_after(g, rem, 1)];
+            q.z = tile[c.slot_after(g, rem, 2)];
+            q.w = tile[c.slot_after(g, rem, 3)];
+            const int go = (c.L == c.R) ? e : g * c.R + rem;
+            *reinterpret_cast<float4 *>(base + go) = q;
         }
         const int e = nv * 4 + lane;
         if (e < c.n) {
-            Cursor cur; cur.init(e, c.L, c.Cx);
-            base[c.gaddr(e)] = tile[cur.lds(c.ld, c.Cx)];
+            int go; int slot;
+            c.locate(e, go, slot);
+            base[go] = tile[slot];
         }
     } else {
         for (int e = lane; e < c.n; e += kWave) {
-            Cursor cur; cur.init(e, c.L, c.Cx);
-            base[c.gaddr(e)] = tile[cur.lds(c.ld, c.Cx)];
+            int go; int slot;
+            c.locate(e, go, slot);
+            base[go] = tile[slot];
         }
     }
 }
@@ -246,7 +265,7 @@ __device__ __forceinline__ float step(const Carry &s, Carry &nx, bool last, floa
 // TGT: algorithm whose target is written (kNone: no target output).
 // ADV: algorithm whose advantages are written.
 // REW: rewards present.  RETT: MC reads returns at every t (ret_T == T).
-template <int TGT, int ADV, bool REW, bool RETT>
+template <int TGT, int ADV, bool REW, bool RETT, bool VEC>
 __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
     constexpr bool kRho = (TGT == HRL_ALG_VTRACE) || (ADV == HRL_ALG_VTRACE);
     constexpr bool kRet = RETT && (ADV == HRL_ALG_MC);
@@ -256,27 +275,29 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
     const int C = a.C;
     const int G = kWave / C;
     const int J = G * C;                      // value columns per wave
-    const int Jr = G * a.rhoC;                // rho columns per wave
-    const int ldv = J + 1, ldr = Jr + 1;
     const int T = a.T;
     const int tmax = T < kTChunk ? T : kTChunk;
+    const int Lpv = padded_row(tmax * C, C);         // value-shaped rows
+    const int Lpr = padded_row(tmax * a.rhoC, 1);    // rho rows (lanes of one g share a slot)
 
     const int64_t b0 = (int64_t)blockIdx.x * G;
     const int ntraj = (int)min<int64_t>(G, a.B - b0);
 
     // LDS carve-up (sizes fixed by tmax, see launch)
+    const int vt = G * Lpv, rt = G * Lpr;
     float *t_v = lds;
-    float *t_r = t_v + tmax * ldv;
-    float *t_ret = t_r + (REW ? tmax * ldv : 0);
-    float *t_tgt = t_ret + (kRet ? tmax * ldv : 0);
-    float *t_adv = t_tgt + (TGT != kNone ? tmax * ldv : 0);
-    float *t_rho = t_adv + tmax * ldv;
-    float *t_cs = t_rho + (kRho ? tmax * ldr : 0);
+    float *t_r = t_v + vt;
+    float *t_ret = t_r + (REW ? vt : 0);
+    float *t_tgt = t_ret + (kRet ? vt : 0);
+    float *t_adv = t_tgt + (TGT != kNone ? vt : 0);
+    float *t_rho = t_adv + vt;
+    float *t_cs = t_rho + (kRho ? rt : 0);
 
     const int g = lane / C;
     const int c = lane - g * C;
     const bool active = (lane < J) && (g < ntraj);
-    const int rcol = g * a.rhoC + c / a.rhoDiv;
+    const int vbase = g * Lpv + c;                     // + tt*C
+    const int rbase = g * Lpr + c / a.rhoDiv;          // + tt*rhoC
 
     float boot = 0.f;
     if (active) {
@@ -290,20 +311,20 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
         const int tc = min(kTChunk, T - t0);
 
         Chunk cv, cr, cret, crho, ccs;
-        cv.setup(a.values, b0, T, C, t0, tc, ntraj, ldv);
-        if constexpr (REW) cr.setup(a.rewards, b0, T, C, t0, tc, ntraj, ldv);
-        if constexpr (kRet) cret.setup(a.returns, b0, T, C, t0, tc, ntraj, ldv);
+        cv.setup(a.values, b0, T, C, t0, tc, ntraj, Lpv);
+        if constexpr (REW) cr.setup(a.rewards, b0, T, C, t0, tc, ntraj, Lpv);
+        if constexpr (kRet) cret.setup(a.returns, b0, T, C, t0, tc, ntraj, Lpv);
         if constexpr (kRho) {
-            crho.setup(a.rhos, b0, T, a.rhoC, t0, tc, ntraj, ldr);
-            ccs.setup(a.cs, b0, T, a.rhoC, t0, tc, ntraj, ldr);
+            crho.setup(a.rhos, b0, T, a.rhoC, t0, tc, ntraj, Lpr);
+            ccs.setup(a.cs, b0, T, a.rhoC, t0, tc, ntraj, Lpr);
         }
 
         // issue every input's loads before the first LDS write
-        Staged sv, sr, sret, srho, scs;
-        sv.load(cv, lane);
-        if constexpr (REW) sr.load(cr, lane);
-        if constexpr (kRet) sret.load(cret, lane);
-        if constexpr (kRho) { srho.load(crho, lane); scs.load(ccs, lane); }
+        Staged<VEC> sv, sr, sret, srho, scs;
+        sv.load(cv);
+        if constexpr (REW) sr.load(cr);
+        if constexpr (kRet) sret.load(cret);
+        if constexpr (kRho) { srho.load(crho); scs.load(ccs); }
         sv.to_lds(cv, t_v);
         if constexpr (REW) sr.to_lds(cr, t_r);
         if constexpr (kRet) sret.to_lds(cret, t_ret);
@@ -313,23 +334,25 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
         if (active) {
             for (int tt = tc - 1; tt >= 0; --tt) {
                 const bool last = (t0 + tt == T - 1);
-                const float v = t_v[tt * ldv + lane];
-                const float r = REW ? t_r[tt * ldv + lane] : 0.f;
-                const float rho = kRho ? t_rho[tt * ldr + rcol] : 0.f;
-                const float cc = kRho ? t_cs[tt * ldr + rcol] : 0.f;
-                const float ret_t = kRet ? t_ret[tt * ldv + lane] : boot;
+                const int iv = vbase + tt * C;
+                const int ir = rbase + tt * a.rhoC;
+                const float v = t_v[iv];
+                const float r = REW ? t_r[iv] : 0.f;
+                const float rho = kRho ? t_rho[ir] : 0.f;
+                const float cc = kRho ? t_cs[ir] : 0.f;
+                const float ret_t = kRet ? t_ret[iv] : boot;
 
                 float adv, adv_unused;
                 Carry nx = s;
                 if constexpr (TGT != kNone && TGT != ADV) {
                     const float tgt = step<TGT>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv_unused);
                     step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
-                    t_tgt[tt * ldv + lane] = tgt;
+                    t_tgt[iv] = tgt;
                 } else {
                     const float tgt = step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
-                    if constexpr (TGT != kNone) t_tgt[tt * ldv + lane] = tgt;
+                    if constexpr (TGT != kNone) t_tgt[iv] = tgt;
                 }
-                t_adv[tt * ldv + lane] = adv;
+                t_adv[iv] = adv;
                 nx.v_next = v;
                 s = nx;
             }
@@ -337,34 +360,51 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
         __syncthreads();
 
         const int64_t off = b0 * (int64_t)T * C + (int64_t)t0 * C;
-        if constexpr (TGT != kNone) store_chunk(cv, t_tgt, a.targets + off);
-        store_chunk(cv, t_adv, a.advantages + off);
+        if constexpr (TGT != kNone) store_chunk<VEC>(cv, t_tgt, a.targets + off);
+        store_chunk<VEC>(cv, t_adv, a.advantages + off);
     }
 }
 
-template <int TGT, int ADV, bool REW, bool RETT>
+template <int TGT, int ADV, bool REW, bool RETT, bool VEC>
 int launch_one(const Args &a, hipStream_t stream) {
     constexpr bool kRho = (TGT == HRL_ALG_VTRACE) || (ADV == HRL_ALG_VTRACE);
     constexpr bool kRet = RETT && (ADV == HRL_ALG_MC);
     const int G = kWave / a.C;
-    const int J = G * a.C, Jr = G * a.rhoC;
     const int tmax = a.T < kTChunk ? a.T : kTChunk;
     const int vtiles = 1 + (REW ? 1 : 0) + (kRet ? 1 : 0) + (TGT != kNone ? 1 : 0) + 1;
-    const size_t lds = sizeof(float) * ((size_t)vtiles * tmax * (J + 1) + (kRho ? 2u : 0u) * tmax * (Jr + 1));
+    const size_t vt = (size_t)G * padded_row(tmax * a.C, a.C);
+    const size_t rt = (size_t)G * padded_row(tmax * a.rhoC, 1);
+    const size_t lds = sizeof(float) * (vtiles * vt + (kRho ? 2 : 0) * rt);
     const int64_t blocks = (a.B + G - 1) / G;
     if (blocks > 0x7fffffff) return HRL_EINVAL;
-    hipLaunchKernelGGL((targets_kernel<TGT, ADV, REW, RETT>), dim3((unsigned)blocks), dim3(kWave), lds,
+    hipLaunchKernelGGL((targets_kernel<TGT, ADV, REW, RETT, VEC>), dim3((unsigned)blocks), dim3(kWave), lds,
                        stream, a);
     const hipError_t err = hipGetLastError();
     return err == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)err;
 }
 
+// 16-byte loads/stores need every tensor 16-byte aligned and every per-
+// trajectory span a whole number of float4s (or one contiguous run, T <= chunk).
+bool vector_ok(const Args &a) {
+    auto aligned = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (!aligned(a.values) || !aligned(a.returns) || !aligned(a.rewards) || !aligned(a.rhos) || !aligned(a.cs) ||
+        !aligned(a.targets) || !aligned(a.advantages))
+        return false;
+    if (a.T <= kTChunk) return true;
+    // full chunks are kTChunk*Cx floats (a multiple of 4); rows and the tail chunk must be too
+    return ((a.T * a.C) & 3) == 0 && ((a.T * a.rhoC) & 3) == 0;
+}
+
+template <int TGT, int ADV, bool REW>
+int launch_vec(const Args &a, hipStream_t s) {
+    const bool rett = (ADV == HRL_ALG_MC) && a.retT == a.T && a.T > 1;
+    if (vector_ok(a)) return rett ? launch_one<TGT, ADV, REW, true, true>(a, s) : launch_one<TGT, ADV, REW, false, true>(a, s);
+    return rett ? launch_one<TGT, ADV, REW, true, false>(a, s) : launch_one<TGT, ADV, REW, false, false>(a, s);
+}
+
 template <int TGT, int ADV>
 int launch_flags(const Args &a, hipStream_t s) {
-    const bool rew = a.rewards != nullptr;
-    const bool rett = a.retT == a.T && a.T > 1;
-    if (rew) return rett ? launch_one<TGT, ADV, true, true>(a, s) : launch_one<TGT, ADV, true, false>(a, s);
-    return rett ? launch_one<TGT, ADV, false, true>(a, s) : launch_one<TGT, ADV, false, false>(a, s);
+    return a.rewards != nullptr ? launch_vec<TGT, ADV, true>(a, s) : launch_vec<TGT, ADV, false>(a, s);
 }
 
 template <int TGT>
@@ -405,7 +445,7 @@ int prepare(int target_alg, int adv_alg, const float *values, const float *retur
     if (B == 0) return HRL_OK;  // empty batch: nothing to read or write (data pointers may be NULL)
     const bool need_rho = target_alg == HRL_ALG_VTRACE || adv_alg == HRL_ALG_VTRACE;
     if (!values || !returns || !advantages || (need_rho && (!rhos || !cs))) return HRL_EINVAL;
-    if (B * T * C > (int64_t)1 << 40) return HRL_EINVAL;
+    if (B * T * C > (int64_t)1 << 40 || T * C * kWave >= ((int64_t)1 << 31)) return HRL_EINVAL;
     Args a;
     a.values = values; a.returns = returns; a.rewards = rewards; a.rhos = rhos; a.cs = cs;
     a.targets = targets; a.advantages = advantages;
