@@ -36,6 +36,13 @@ SIGNATURES = {
     'hrl_compute_targets_fused': (ctypes.c_int, [
         ctypes.c_int, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _f32p,
         _i64, _i64, _i64, _i64, _i64, _i64, _dbl, _dbl, _f32p, _f32p, ctypes.c_void_p]),
+    'hrl_bn_workspace_bytes': (ctypes.c_int64, [_i64, _i64, _i64]),
+    'hrl_bn_forward_train': (ctypes.c_int, [
+        _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, _dbl, _dbl, _f32p, _f32p, _f32p,
+        ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_bn_backward': (ctypes.c_int, [
+        _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
+        ctypes.c_void_p, _i64, ctypes.c_void_p]),
 }
 
 ABI_VERSION = 1

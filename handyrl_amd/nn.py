@@ -1,0 +1,111 @@
+"""HIP-backed layers for the learner's env networks, and the pass that installs them.
+
+Env networks stay exactly as their plugins define them (Environment.net(),
+handyrl/environment.py); ``accelerate(model)`` swaps, in place, the modules
+whose training-mode kernels are the learner step's bottleneck on MI355X for
+subclasses with identical parameters, buffers and state_dict keys:
+
+* ``nn.BatchNorm2d`` -> ``BatchNorm2d`` (csrc/hrl_bn.hip): training-mode
+  forward/backward as coalesced streaming passes with fp64 statistics.  In
+  eval mode, on CPU tensors, or for shapes the kernels do not take (rows
+  wider than 3072 floats, or than 1024 when not a multiple of 4) the module is the plain torch layer.
+
+The HIP path is taken whenever the input is a CUDA tensor in training mode;
+if libhrl.so is missing that raises (no silent fallback).
+"""
+
+import torch
+import torch.nn as nn
+
+from . import _native
+
+__all__ = ['BatchNorm2d', 'accelerate', 'batch_norm_train']
+
+_MAX_ROW = 3072        # float4 path (row width a multiple of 4)
+_MAX_ROW_SCALAR = 1024  # scalar path
+
+
+class _BatchNormTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
+        N, C = x.shape[0], x.shape[1]
+        HW = x[0, 0].numel()
+        x = x.contiguous()
+        lib = _native.load()
+        ws_bytes = lib.hrl_bn_workspace_bytes(N, C, HW)
+        if ws_bytes < 0:
+            raise ValueError('hrl_bn: unsupported shape %s' % (tuple(x.shape),))
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+        y = torch.empty_like(x)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+        code = lib.hrl_bn_forward_train(
+            _native.ptr(x), N, C, HW, _native.ptr(weight), _native.ptr(bias),
+            _native.ptr(running_mean), _native.ptr(running_var), float(momentum), float(eps),
+            _native.ptr(y), _native.ptr(mean), _native.ptr(invstd), _native.ptr(ws), ws_bytes,
+            _native.stream_of(x.device))
+        _native.check(code, 'hrl_bn_forward_train')
+        ctx.save_for_backward(x, weight, mean, invstd)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, mean, invstd = ctx.saved_tensors
+        N, C = x.shape[0], x.shape[1]
+        HW = x[0, 0].numel()
+        dy = dy.contiguous()
+        lib = _native.load()
+        ws_bytes = lib.hrl_bn_workspace_bytes(N, C, HW)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+        dx = torch.empty_like(x)
+        dw = torch.empty(C, dtype=torch.float32, device=x.device) if weight is not None else None
+        db = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_bias else None
+        code = lib.hrl_bn_backward(
+            _native.ptr(x), _native.ptr(dy), N, C, HW, _native.ptr(weight), _native.ptr(mean), _native.ptr(invstd),
+            _native.ptr(dx), _native.ptr(dw), _native.ptr(db), _native.ptr(ws), ws_bytes,
+            _native.stream_of(x.device))
+        _native.check(code, 'hrl_bn_backward')
+        return dx, dw, db, None, None, None, None
+
+
+def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps):
+    """F.batch_norm(..., training=True) on the HIP kernels (x: (N, C, *spatial) fp32 CUDA)."""
+    return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps)
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d whose training-mode CUDA path runs csrc/hrl_bn.hip."""
+
+    def forward(self, x):
+        row = x.shape[1] * x.shape[2] * x.shape[3] if x.dim() == 4 else 0
+        use_hip = (self.training and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+                   and x.shape[0] > 0 and (row <= _MAX_ROW_SCALAR or (row % 4 == 0 and row <= _MAX_ROW)))
+        if not use_hip:
+            return super().forward(x)
+        self._check_input_dim(x)
+        momentum = 0.0 if self.momentum is None else self.momentum
+        if self.track_running_stats and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(1)
+            if self.momentum is None:  # cumulative moving average
+                momentum = 1.0 / float(self.num_batches_tracked.item())
+        rm = self.running_mean if self.track_running_stats else None
+        rv = self.running_var if self.track_running_stats else None
+        return batch_norm_train(x, self.weight, self.bias, rm, rv, momentum, self.eps)
+
+
+def accelerate(model):
+    """Swap HIP-backed layers into ``model`` in place (same parameters and state_dict); returns it."""
+    for name, child in list(model.named_children()):
+        if type(child) is nn.BatchNorm2d:
+            new = BatchNorm2d(child.num_features, eps=child.eps, momentum=child.momentum,
+                              affine=child.affine, track_running_stats=child.track_running_stats)
+            new.weight, new.bias = child.weight, child.bias
+            if child.track_running_stats:
+                new.running_mean, new.running_var = child.running_mean, child.running_var
+                new.num_batches_tracked = child.num_batches_tracked
+            new.train(child.training)
+            setattr(model, name, new)
+        else:
+            accelerate(child)
+    return model

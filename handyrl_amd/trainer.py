@@ -27,6 +27,7 @@ import torch
 import torch.nn as nn
 
 from . import distributed as hdist
+from .nn import accelerate
 from .train import forward_prediction, loss_terms
 
 DEFAULT_LR = 3e-8  # train.py:318
@@ -34,8 +35,10 @@ DEFAULT_LR = 3e-8  # train.py:318
 
 class LearnerStep:
     def __init__(self, net, args, device, lr=None, graph=False, reduce_group=None, world_size=1,
-                 bucket_bytes=256 * 1024):
+                 bucket_bytes=256 * 1024, hip_layers=True):
         self.net = net.to(device)
+        if hip_layers and device.type == 'cuda':
+            accelerate(self.net)  # HIP BatchNorm etc.; same parameters and state_dict
         self.args = args
         self.device = device
         self.graph = graph and device.type == 'cuda'

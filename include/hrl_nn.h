@@ -1,0 +1,55 @@
+/*
+ * hrl_nn.h — C ABI of the MI355X kernels for the learner's network hot ops
+ * (libhrl.so).
+ *
+ * Training-mode BatchNorm over (N, C, HW) NCHW activations, the op that
+ * dominates the learner step of the board-game nets (TicTacToe
+ * SimpleConv2dModel handyrl/envs/tictactoe.py:17-69, GeisterNet
+ * handyrl/envs/geister.py:100-167, GeeseNet handyrl/envs/kaggle/
+ * hungry_geese.py:23-57): their BatchNorm2d layers see N = B*T*P samples of a
+ * tiny board (HW = 9 .. 77), a shape the vendor spatial BatchNorm handles at
+ * ~3% of HBM bandwidth.  Replaces torch.nn.BatchNorm2d.forward/backward in
+ * training mode (the reference calls it through nn.Module, train.py:380-383).
+ *
+ * Semantics follow torch.nn.functional.batch_norm(training=True):
+ *   mean_c, var_c = biased statistics over (N, HW);  invstd = 1/sqrt(var+eps)
+ *   y = x * alpha_c + beta_c,  alpha = invstd*weight, beta = bias - mean*alpha
+ *   running_mean = (1-m)*running_mean + m*mean
+ *   running_var  = (1-m)*running_var  + m*var*M/(M-1),  M = N*HW
+ * Statistics accumulate in fp64; all reductions are in a fixed order
+ * (deterministic).  All pointers are device pointers, fp32, contiguous;
+ * weight/bias and running_* may be NULL.  Asynchronous on `stream`; no
+ * allocation, no synchronisation (graph-capturable).
+ * `workspace` is caller-allocated scratch of hrl_bn_workspace_bytes() bytes.
+ * Returns 0, HRL_EINVAL or HRL_ELAUNCH_BASE - hipError_t (hrl_targets.h).
+ */
+#ifndef HRL_NN_H
+#define HRL_NN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Scratch bytes needed by hrl_bn_forward_train / hrl_bn_backward for this shape. */
+int64_t hrl_bn_workspace_bytes(int64_t N, int64_t C, int64_t HW);
+
+/* Training forward: y, save_mean, save_invstd (C floats each), running stats updated in place. */
+int hrl_bn_forward_train(const float *x, int64_t N, int64_t C, int64_t HW,
+                         const float *weight, const float *bias,
+                         float *running_mean, float *running_var, double momentum, double eps,
+                         float *y, float *save_mean, float *save_invstd,
+                         void *workspace, int64_t workspace_bytes, void *stream);
+
+/* Backward of the training forward: dx (may not alias dy), dweight/dbias (C floats, may be NULL). */
+int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW,
+                    const float *weight, const float *save_mean, const float *save_invstd,
+                    float *dx, float *dweight, float *dbias,
+                    void *workspace, int64_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HRL_NN_H */

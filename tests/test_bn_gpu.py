@@ -1,0 +1,98 @@
+"""HIP BatchNorm2d (csrc/hrl_bn.hip) vs torch's CPU BatchNorm2d — the reference
+learner's BatchNorm (it trains on the CPU, train.py:364-385).
+
+Forward output, running statistics, num_batches_tracked and the gradients
+w.r.t. input, weight and bias, over the board shapes of the reference nets
+(TicTacToe 3x3, Geister 6x6, Geese 7x11), odd row widths (scalar path) and
+the BASELINE size.
+"""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(C, momentum=0.1, affine=True, track=True):
+    from handyrl_amd.nn import BatchNorm2d
+    ref = nn.BatchNorm2d(C, momentum=momentum, affine=affine, track_running_stats=track)
+    if affine:
+        with torch.no_grad():
+            ref.weight.uniform_(0.5, 1.5)
+            ref.bias.uniform_(-0.5, 0.5)
+    hip = BatchNorm2d(C, momentum=momentum, affine=affine, track_running_stats=track)
+    hip.load_state_dict(ref.state_dict())
+    return ref, hip
+
+
+@pytest.mark.parametrize('N,C,H,W', [
+    (1000, 32, 3, 3),    # TicTacToe block (float4 path, 3 rows per pass)
+    (37, 32, 6, 6),      # Geister board
+    (13, 32, 7, 11),     # Geese board: rows wider than a workgroup (3 column slots)
+    (9, 3, 3, 3),        # odd row width: scalar path
+    (1, 32, 3, 3),       # single sample
+    (4099, 8, 1, 1),     # 1x1 "board", many rows per pass
+])
+@pytest.mark.parametrize('affine', [True, False])
+def test_bn_matches_torch_cpu(cuda, N, C, H, W, affine):
+    torch.manual_seed(N + C)
+    ref, hip = _pair(C, affine=affine)
+    hip = hip.to(cuda)
+    x = torch.randn(N, C, H, W) * 2 + 0.5
+    dy = torch.randn(N, C, H, W)
+    xr = x.clone().requires_grad_(True)
+    xh = x.to(cuda).requires_grad_(True)
+    for _ in range(2):  # two steps: running stats accumulate
+        yr = ref(xr)
+        yh = hip(xh)
+    np.testing.assert_allclose(yh.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-5, atol=2e-5)
+    yr.backward(dy)
+    yh.backward(dy.to(cuda))
+    np.testing.assert_allclose(xh.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-4, atol=1e-5)
+    if affine:
+        np.testing.assert_allclose(hip.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(hip.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-4, atol=1e-4)
+    for k in ('running_mean', 'running_var'):
+        np.testing.assert_allclose(getattr(hip, k).cpu().numpy(), getattr(ref, k).numpy(), rtol=1e-5, atol=1e-6)
+    assert hip.num_batches_tracked.item() == ref.num_batches_tracked.item() == 2
+
+
+def test_bn_cumulative_momentum_and_eval(cuda):
+    ref, hip = _pair(16, momentum=None)
+    hip = hip.to(cuda)
+    for i in range(3):
+        x = torch.randn(50, 16, 3, 3) + i
+        ref(x)
+        hip(x.to(cuda))
+    np.testing.assert_allclose(hip.running_var.cpu().numpy(), ref.running_var.numpy(), rtol=1e-5, atol=1e-6)
+    ref.eval(); hip.eval()
+    x = torch.randn(20, 16, 3, 3)
+    np.testing.assert_allclose(hip(x.to(cuda)).detach().cpu().numpy(), ref(x).detach().numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_bn_baseline_size_deterministic(cuda):
+    """N = B*T = 131072 TicTacToe activations: two runs bit-identical, close to torch fp64."""
+    from handyrl_amd.nn import batch_norm_train
+    g = torch.Generator(device=cuda).manual_seed(0)
+    x = torch.randn(131072, 32, 3, 3, device=cuda, generator=g) * 3 + 1
+    w = torch.rand(32, device=cuda, generator=g) + 0.5
+    b = torch.randn(32, device=cuda, generator=g)
+    y1 = batch_norm_train(x, w, b, None, None, 0.1, 1e-5)
+    y2 = batch_norm_train(x, w, b, None, None, 0.1, 1e-5)
+    assert torch.equal(y1, y2)
+    ref = torch.nn.functional.batch_norm(x.double(), None, None, w.double(), b.double(), True, 0.1, 1e-5)
+    assert (y1.double() - ref).abs().max().item() < 2e-5
+
+
+def test_accelerate_keeps_state_dict(cuda):
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.nn import accelerate, BatchNorm2d
+    net = SimpleConv2dModel()
+    sd = {k: v.clone() for k, v in net.state_dict().items()}
+    accelerate(net)
+    assert sum(isinstance(m, BatchNorm2d) for m in net.modules()) == 3
+    assert list(net.state_dict()) == list(sd)
+    for k, v in net.state_dict().items():
+        assert torch.equal(v, sd[k])

@@ -8,11 +8,14 @@ dev = torch.device('cuda', 0)
 N = 4096 * 32
 
 
-def run(name, cl=False, bench=False, cudnn=True, iters=10):
+def run(name, cl=False, bench=False, cudnn=True, iters=10, hip=False):
     torch.backends.cudnn.benchmark = bench
     torch.backends.cudnn.enabled = cudnn
     torch.manual_seed(0)
     net = SimpleConv2dModel().to(dev)
+    if hip:
+        from handyrl_amd.nn import accelerate
+        accelerate(net)
     x = (torch.rand(N, 3, 3, 3, device=dev) < 0.5).float()
     if cl:
         net = net.to(memory_format=torch.channels_last)
@@ -36,6 +39,7 @@ if __name__ == '__main__':
     t0 = time.perf_counter()
     {'nchw': lambda: run('nchw'),
      'cl': lambda: run('channels_last', cl=True),
+     'hip': lambda: run('nchw + HIP BatchNorm', hip=True),
      'nchw_bench': lambda: run('nchw benchmark', bench=True),
      'cl_bench': lambda: run('channels_last benchmark', cl=True, bench=True)}[which]()
     print('  (%s total %.1f s incl. warm-up)' % (which, time.perf_counter() - t0), flush=True)
