@@ -8,7 +8,16 @@ subclasses with identical parameters, buffers and state_dict keys:
 * ``nn.BatchNorm2d`` -> ``BatchNorm2d`` (csrc/hrl_bn.hip): training-mode
   forward/backward as coalesced streaming passes with fp64 statistics.  In
   eval mode, on CPU tensors, or for shapes the kernels do not take (rows
-  wider than 3072 floats, or than 1024 when not a multiple of 4) the module is the plain torch layer.
+  wider than 3072 floats, or than 1024 when not a multiple of 4) the module
+  is the plain torch layer.
+* ``nn.Conv2d`` (stride 1, 'same' zero padding, no dilation/groups) ->
+  ``BoardConv2d`` on boards of at most ``BOARD_MAX_CELLS`` cells: on a tiny
+  board a convolution IS a dense matrix, Y[N, Cout*HW] = X[N, Cin*HW] @ W_board
+  with W_board[(ci,p),(co,q)] = W[co, ci, p-q+k//2] (zero off the board), so
+  the layer runs as one fp32 hipBLASLt GEMM on the NCHW rows (MFMA f32, exact
+  fp32 products) with the bias in the epilogue, instead of an implicit-GEMM
+  convolution wrapped in NCHW<->NHWC transposes.  The backward is the two
+  GEMMs of that matmul plus a scatter-add folding dW_board back onto W.
 
 The HIP path is taken whenever the input is a CUDA tensor in training mode;
 if libhrl.so is missing that raises (no silent fallback).
@@ -19,7 +28,7 @@ import torch.nn as nn
 
 from . import _native
 
-__all__ = ['BatchNorm2d', 'accelerate', 'batch_norm_train']
+__all__ = ['BatchNorm2d', 'BoardConv2d', 'accelerate', 'batch_norm_train']
 
 _MAX_ROW = 3072        # float4 path (row width a multiple of 4)
 _MAX_ROW_SCALAR = 1024  # scalar path
@@ -74,6 +83,89 @@ def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps):
     return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps)
 
 
+BOARD_MAX_CELLS = 16
+
+
+class BoardConv2d(nn.Conv2d):
+    """nn.Conv2d computed as one dense GEMM over the flattened board (see module doc)."""
+
+    def _board_tables(self, H, W, device):
+        """(gather, fold) index tables for an HxW board, cached per (H, W, device).
+
+        gather[(ci,p),(co,q)] : flat index into cat([weight.flatten(), 0])
+        fold[w, j]            : the j-th W_board entry that weight element w feeds
+                                (padded with the index of an appended zero)
+        """
+        key = (H, W, device)
+        cache = self.__dict__.setdefault('_board_cache', {})
+        if key not in cache:
+            Cout, Cin, kh, kw = self.weight.shape
+            ph, pw = self.padding
+            HW = H * W
+            nw = Cout * Cin * kh * kw
+            gather = torch.full((Cin, HW, Cout, HW), nw, dtype=torch.long)
+            co = torch.arange(Cout).view(1, Cout)
+            ci = torch.arange(Cin).view(Cin, 1)
+            for q in range(HW):
+                qy, qx = divmod(q, W)
+                for dy in range(kh):
+                    for dx in range(kw):
+                        py, px = qy + dy - ph, qx + dx - pw
+                        if 0 <= py < H and 0 <= px < W:
+                            gather[:, py * W + px, :, q] = ((co * Cin + ci) * kh + dy) * kw + dx
+            gather = gather.view(-1)
+            # invert: every weight element appears once per valid (p, q) pair of its tap
+            order = torch.argsort(gather, stable=True)
+            counts = torch.bincount(gather, minlength=nw + 1)[:nw]
+            width = int(counts.max().item()) if nw else 0
+            fold = torch.full((nw, max(width, 1)), gather.numel(), dtype=torch.long)
+            starts = torch.cumsum(counts, 0) - counts
+            for w in range(nw):
+                c = int(counts[w])
+                fold[w, :c] = order[starts[w]:starts[w] + c]
+            cache[key] = (gather.view(Cin * HW, Cout * HW).to(device), fold.to(device))
+        return cache[key]
+
+    def forward(self, x):
+        if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
+                and x.shape[2] * x.shape[3] <= BOARD_MAX_CELLS):
+            return super().forward(x)
+        N, Cin, H, W = x.shape
+        gather, fold = self._board_tables(H, W, x.device)
+        w_board = _BoardWeight.apply(self.weight, gather, fold)   # (Cin*HW, Cout*HW)
+        x2 = x.reshape(N, Cin * H * W)
+        if self.bias is not None:
+            y = torch.addmm(self.bias.repeat_interleave(H * W), x2, w_board)
+        else:
+            y = x2 @ w_board
+        return y.view(N, self.out_channels, H, W)
+
+
+class _BoardWeight(torch.autograd.Function):
+    """W -> W_board by a fixed gather; backward folds dW_board onto W by a fixed
+    gather-and-sum (deterministic, no atomics or sort)."""
+
+    @staticmethod
+    def forward(ctx, weight, gather, fold):
+        ctx.save_for_backward(fold)
+        ctx.wshape = weight.shape
+        wz = torch.cat([weight.reshape(-1), weight.new_zeros(1)])
+        return wz[gather]
+
+    @staticmethod
+    def backward(ctx, grad):
+        (fold,) = ctx.saved_tensors
+        gz = torch.cat([grad.reshape(-1), grad.new_zeros(1)])
+        return gz[fold].sum(1).view(ctx.wshape), None, None
+
+
+def _board_conv_ok(m):
+    k = m.kernel_size
+    return (m.stride == (1, 1) and m.dilation == (1, 1) and m.groups == 1 and m.padding_mode == 'zeros'
+            and isinstance(m.padding, tuple) and m.padding == (k[0] // 2, k[1] // 2) and k[0] % 2 == 1
+            and k[1] % 2 == 1)
+
+
 class BatchNorm2d(nn.BatchNorm2d):
     """nn.BatchNorm2d whose training-mode CUDA path runs csrc/hrl_bn.hip."""
 
@@ -95,9 +187,22 @@ class BatchNorm2d(nn.BatchNorm2d):
 
 
 def accelerate(model):
-    """Swap HIP-backed layers into ``model`` in place (same parameters and state_dict); returns it."""
+    """Swap HIP-backed layers into ``model`` in place (same parameters and state_dict); returns it.
+
+    BoardConv2d checks the board size of every input and runs the plain
+    convolution on boards larger than BOARD_MAX_CELLS cells.
+    """
     for name, child in list(model.named_children()):
-        if type(child) is nn.BatchNorm2d:
+        if type(child) is nn.Conv2d and _board_conv_ok(child):
+            new = BoardConv2d(child.in_channels, child.out_channels, child.kernel_size, stride=1,
+                              padding=child.padding, bias=child.bias is not None,
+                              device=child.weight.device, dtype=child.weight.dtype)
+            new.weight = child.weight
+            if child.bias is not None:
+                new.bias = child.bias
+            new.train(child.training)
+            setattr(model, name, new)
+        elif type(child) is nn.BatchNorm2d:
             new = BatchNorm2d(child.num_features, eps=child.eps, momentum=child.momentum,
                               affine=child.affine, track_running_stats=child.track_running_stats)
             new.weight, new.bias = child.weight, child.bias

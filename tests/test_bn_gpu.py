@@ -88,11 +88,49 @@ def test_bn_baseline_size_deterministic(cuda):
 
 def test_accelerate_keeps_state_dict(cuda):
     from handyrl_amd.envs.tictactoe import SimpleConv2dModel
-    from handyrl_amd.nn import accelerate, BatchNorm2d
+    from handyrl_amd.nn import accelerate, BatchNorm2d, BoardConv2d
     net = SimpleConv2dModel()
     sd = {k: v.clone() for k, v in net.state_dict().items()}
     accelerate(net)
     assert sum(isinstance(m, BatchNorm2d) for m in net.modules()) == 3
+    assert sum(isinstance(m, BoardConv2d) for m in net.modules()) == 6  # stem, 3 blocks, 2 heads
     assert list(net.state_dict()) == list(sd)
     for k, v in net.state_dict().items():
         assert torch.equal(v, sd[k])
+
+
+@pytest.mark.parametrize('cin,cout,k,H,W,bias', [
+    (3, 32, 3, 3, 3, True),    # TicTacToe stem
+    (32, 32, 3, 3, 3, False),  # TicTacToe block (BN follows, no bias)
+    (32, 2, 1, 3, 3, True),    # TicTacToe policy head 1x1
+    (5, 7, 3, 4, 4, True),     # 16-cell board
+    (4, 3, 5, 3, 3, True),     # 5x5 kernel on a 3x3 board
+])
+def test_board_conv_matches_torch_cpu(cuda, cin, cout, k, H, W, bias):
+    from handyrl_amd.nn import BoardConv2d
+    torch.manual_seed(cin * cout)
+    ref = nn.Conv2d(cin, cout, k, padding=k // 2, bias=bias)
+    hip = BoardConv2d(cin, cout, k, padding=k // 2, bias=bias)
+    hip.load_state_dict(ref.state_dict())
+    hip = hip.to(cuda)
+    x = torch.randn(777, cin, H, W)
+    dy = torch.randn(777, cout, H, W)
+    xr = x.clone().requires_grad_(True)
+    xh = x.to(cuda).requires_grad_(True)
+    yr, yh = ref(xr), hip(xh)
+    np.testing.assert_allclose(yh.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-5, atol=1e-5)
+    yr.backward(dy)
+    yh.backward(dy.to(cuda))
+    np.testing.assert_allclose(xh.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(hip.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-4, atol=1e-3)
+    if bias:
+        np.testing.assert_allclose(hip.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-4, atol=1e-3)
+
+
+def test_board_conv_large_board_uses_plain_conv(cuda):
+    from handyrl_amd.nn import BoardConv2d
+    m = BoardConv2d(4, 4, 3, padding=1).to(cuda)
+    x = torch.randn(3, 4, 6, 6, device=cuda)   # 36 cells > BOARD_MAX_CELLS
+    ref = torch.nn.functional.conv2d(x, m.weight, m.bias, padding=1)
+    assert torch.allclose(m(x), ref, atol=1e-5)
+    assert '_board_cache' not in m.__dict__ or not m.__dict__['_board_cache']

@@ -84,8 +84,11 @@ def test_graph_step_equals_eager(cuda):
     torch.cuda.synchronize()
     for k in ('p', 'v', 'ent', 'total'):
         _close(g_out[k].item(), e_out[k].item(), rtol=1e-5, what=k)
+    # hipBLASLt may pick a different (split-K) GEMM schedule under capture, so the
+    # two runs differ by fp32 summation order; Adam's m/sqrt(v) amplifies that on
+    # near-zero gradients to ~1e-6 absolute after five updates.
     for (k, a), b in zip(ref_net.state_dict().items(), g_net.state_dict().values()):
-        np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-5, atol=1e-6, err_msg=k)
+        np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-5, atol=5e-6, err_msg=k)
 
 
 @pytest.mark.parametrize('B,T', [(4096, 32), (4096, 9)])
