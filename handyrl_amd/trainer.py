@@ -35,12 +35,14 @@ DEFAULT_LR = 3e-8  # train.py:318
 
 class LearnerStep:
     def __init__(self, net, args, device, lr=None, graph=False, reduce_group=None, world_size=1,
-                 bucket_bytes=256 * 1024, hip_layers=True):
+                 bucket_bytes=256 * 1024, hip_layers=True, loss_fn=None):
         self.net = net.to(device)
         if hip_layers and device.type == 'cuda':
             accelerate(self.net)  # HIP BatchNorm etc.; same parameters and state_dict
         self.args = args
         self.device = device
+        # loss_fn(outputs, batch, args) -> (losses, dcnt tensor); the HIP path by default
+        self.loss_fn = loss_fn or loss_terms
         self.graph = graph and device.type == 'cuda'
         self.params = [p for p in self.net.parameters() if p.requires_grad]
         self.grads = hdist.FlatGrads(self.params)
@@ -71,7 +73,7 @@ class LearnerStep:
     def _body(self, batch, hidden):
         self.grads.zero()
         outputs = forward_prediction(self.net, hidden, batch, self.args)
-        losses, dcnt = loss_terms(outputs, batch, self.args)
+        losses, dcnt = self.loss_fn(outputs, batch, self.args)
         losses['total'].backward()
         if self.reducer is not None:
             self.reducer.finish()

@@ -1,0 +1,120 @@
+"""Data-parallel learner step on CPU with gloo, world_size 2.
+
+Two ranks each train half of a batch; the bucketed, hook-launched SUM
+all-reduce (handyrl_amd/distributed.py) must reproduce the single-process
+full-batch update exactly as the reference defines it (losses are sums over
+the batch, train.py:202-213, so gradients add).  The loss here is the CPU
+oracle's (the HIP scans need a GPU); the distributed machinery is the
+product's.
+"""
+
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class SmallNet(nn.Module):
+    """BatchNorm-free TicTacToe-shaped net (BN statistics are per replica, so excluded)."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(3, 8, 3, padding=1)
+        self.conv2 = nn.Conv2d(8, 8, 3, padding=1)
+        self.fc_p = nn.Linear(72, 9)
+        self.fc_v = nn.Linear(72, 1)
+
+    def forward(self, x, hidden=None):
+        h = F.relu(self.conv2(F.relu(self.conv(x)))).flatten(1)
+        return {'policy': self.fc_p(h), 'value': torch.tanh(self.fc_v(h))}
+
+
+def oracle_loss(outputs, batch, args):
+    from oracle.learner import loss_from_outputs
+    losses, dcnt = loss_from_outputs(outputs, batch, args)
+    return losses, torch.tensor(dcnt)
+
+
+def make_batch_and_args(B=8, T=9):
+    from handyrl_amd.synthetic import tictactoe_batch, default_args
+    return tictactoe_batch(B, T, torch.device('cpu'), seed=42), default_args(T, B)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, out_path, steps, bucket_bytes):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from handyrl_amd import distributed as hdist
+    from handyrl_amd.trainer import LearnerStep
+    hdist.init_process_group('cpu')
+    batch, args = make_batch_and_args()
+    B = batch['value'].size(0)
+    shard = {k: v[rank * B // world:(rank + 1) * B // world] for k, v in batch.items()}
+    torch.manual_seed(0)
+    net = SmallNet()
+    step = LearnerStep(net, args, torch.device('cpu'), world_size=world, loss_fn=oracle_loss,
+                       bucket_bytes=bucket_bytes)
+    assert len(step.reducer.buckets) >= 1
+    for _ in range(steps):
+        step.step(shard)
+    sums, n = step.pop_stats()           # all-reduced loss sums
+    flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()])
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    if rank == 0:
+        torch.save({'params': [g.clone() for g in gathered], 'sums': sums, 'buckets': len(step.reducer.buckets)},
+                   out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _single_process(steps):
+    from handyrl_amd.trainer import LearnerStep
+    batch, args = make_batch_and_args()
+    torch.manual_seed(0)
+    net = SmallNet()
+    step = LearnerStep(net, args, torch.device('cpu'), loss_fn=oracle_loss)
+    for _ in range(steps):
+        step.step(batch)
+    sums, _ = step.pop_stats()
+    return torch.cat([p.detach().reshape(-1) for p in net.parameters()]).numpy(), sums
+
+
+@pytest.mark.parametrize('bucket_bytes', [256 * 1024, 1024])   # one bucket / several hook-launched buckets
+def test_two_rank_sum_allreduce_matches_full_batch(bucket_bytes):
+    steps = 3
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, 'r0.pt')
+        mp.spawn(_rank_main, args=(2, _free_port(), out, steps, bucket_bytes), nprocs=2, join=True)
+        res = torch.load(out, weights_only=True)
+    ref_params, ref_sums = _single_process(steps)
+    p0, p1 = (p.numpy() for p in res['params'])
+    np.testing.assert_array_equal(p0, p1)                        # replicas stay identical
+    np.testing.assert_allclose(p0, ref_params, rtol=1e-5, atol=1e-7)
+    for k in ('p', 'v', 'ent', 'total', 'dcnt'):
+        assert abs(res['sums'][k] - ref_sums[k]) <= 1e-4 * max(1.0, abs(ref_sums[k])), k
+    if bucket_bytes == 1024:
+        assert res['buckets'] > 1
+
+
+def test_bucket_layout_covers_flat_buffer():
+    from handyrl_amd.distributed import FlatGrads
+    net = SmallNet()
+    fg = FlatGrads(list(net.parameters()))
+    for p in net.parameters():
+        assert p.grad.data_ptr() >= fg.flat.data_ptr()
+        assert p.grad.shape == p.shape
+    assert fg.flat.numel() == sum(p.numel() for p in net.parameters())
