@@ -67,10 +67,12 @@ def time_scan(device, B, T, iters, cold=False):
         v = torch.tanh(torch.randn(B, T, 2, 1, device=device, generator=g))
         ret = torch.randint(-1, 2, (B, 1, 2, 1), device=device, generator=g).float()
         rho = torch.rand(B, T, 1, 1, device=device, generator=g)
-        sets.append((v, ret, rho))
+        cs = torch.rand(B, T, 1, 1, device=device, generator=g)   # a separate tensor, as in the learner
+        sets.append((v, ret, rho, cs))
+
     def launch(i):
         st = sets[i % n_sets]
-        compute_targets_fused('VTRACE', 'UPGO', st[0], st[1], None, 0.7, 1, st[2], st[2])
+        compute_targets_fused('VTRACE', 'UPGO', st[0], st[1], None, 0.7, 1, st[2], st[3])
     for i in range(2):
         launch(i)
     # capture the launches back to back in one HIP graph so the timing is the

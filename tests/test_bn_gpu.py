@@ -94,6 +94,8 @@ def test_accelerate_keeps_state_dict(cuda):
     accelerate(net)
     assert sum(isinstance(m, BatchNorm2d) for m in net.modules()) == 3
     assert sum(isinstance(m, BoardConv2d) for m in net.modules()) == 6  # stem, 3 blocks, 2 heads
+    from handyrl_amd.nn import Linear
+    assert sum(isinstance(m, Linear) for m in net.modules()) == 2
     assert list(net.state_dict()) == list(sd)
     for k, v in net.state_dict().items():
         assert torch.equal(v, sd[k])
@@ -134,3 +136,22 @@ def test_board_conv_large_board_uses_plain_conv(cuda):
     ref = torch.nn.functional.conv2d(x, m.weight, m.bias, padding=1)
     assert torch.allclose(m(x), ref, atol=1e-5)
     assert '_board_cache' not in m.__dict__ or not m.__dict__['_board_cache']
+
+
+def test_linear_chunked_weight_grad(cuda):
+    from handyrl_amd.nn import Linear
+    torch.manual_seed(0)
+    ref = nn.Linear(18, 9)
+    hip = Linear(18, 9)
+    hip.load_state_dict(ref.state_dict())
+    hip = hip.to(cuda)
+    x = torch.randn(8192, 18)
+    dy = torch.randn(8192, 9)
+    xr, xh = x.clone().requires_grad_(True), x.to(cuda).requires_grad_(True)
+    yr, yh = ref(xr), hip(xh)
+    np.testing.assert_allclose(yh.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-5, atol=1e-5)
+    yr.backward(dy)
+    yh.backward(dy.to(cuda))
+    np.testing.assert_allclose(xh.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(hip.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(hip.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-4, atol=1e-3)
