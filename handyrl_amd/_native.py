@@ -43,6 +43,16 @@ SIGNATURES = {
     'hrl_bn_backward': (ctypes.c_int, [
         _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
         ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_loss_workspace_bytes': (ctypes.c_int64, [_i64, _i64, _i64, _i64]),
+    'hrl_loss_forward': (ctypes.c_int, [
+        _f32p, _f32p, ctypes.c_void_p, _i64, _i64, _i64, _i64, _i64,
+        _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
+        ctypes.c_int, ctypes.c_int, ctypes.c_int, _dbl, _dbl, _dbl, _dbl,
+        ctypes.c_void_p, _i64, _f32p, ctypes.c_void_p]),
+    'hrl_loss_backward': (ctypes.c_int, [
+        _f32p, ctypes.c_void_p, _i64, _i64, _i64, _i64, _i64,
+        _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _dbl, _dbl,
+        ctypes.c_void_p, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_void_p]),
 }
 
 ABI_VERSION = 1

@@ -8,22 +8,28 @@ Public functions keep the reference signatures:
 * ``compute_loss(batch, model, hidden, args) -> (losses, dcnt)``
                                                        train.py:218-258
 
-The env network runs on PyTorch-ROCm.  The return-target scans run in the HIP
-library: the 2-4 ``compute_target`` calls of train.py:248-253 become ONE
-fused launch per value head (``compute_targets_fused``: value_target's
-targets + policy_target's advantages).  ``loss_terms`` is the sync-free core:
-it returns ``dcnt`` as a device tensor so the learner step never waits on the
-host (the reference calls ``.item()`` at train.py:199 and :390).
+The env network runs on PyTorch-ROCm.  Everything after it runs in the HIP
+library (csrc/hrl_loss.hip): importance ratios, value preparation, the
+return-target scans (the 2-4 ``compute_target`` calls of train.py:248-253
+become one fused scan per value head), the advantages and the five loss sums
+are one autograd Function whose backward is a single closed-form kernel.
+``loss_terms`` is the sync-free core: it returns ``dcnt`` as a device tensor
+so the learner step never waits on the host (the reference calls ``.item()``
+at train.py:199 and :390).  ``compose_losses`` keeps the reference's
+PyTorch formulation as a public function, and ``loss_terms_composed`` uses it
+(with the HIP scans) for outputs the fused kernel does not take (value heads
+wider than one scalar).
 """
 
 import torch
 import torch.distributions as dist
 import torch.nn.functional as F
 
+from . import _native
 from .losses import compute_targets_fused
 from .util import map_r, bimap_r, trimap_r
 
-__all__ = ['forward_prediction', 'compose_losses', 'compute_loss', 'loss_terms']
+__all__ = ['forward_prediction', 'compose_losses', 'compute_loss', 'loss_terms', 'loss_terms_composed']
 
 
 def forward_prediction(model, hidden, batch, args):
@@ -106,10 +112,97 @@ def compose_losses(outputs, log_selected_policies, total_advantages, targets, ba
     return losses, dcnt
 
 
-def loss_terms(outputs, batch, args):
-    """IS ratios, value symmetrisation, fused HIP target scans, composed losses.
+class _FusedLoss(torch.autograd.Function):
+    """train.py:220-258 + compose_losses as csrc/hrl_loss.hip (forward 5 launches, backward 1)."""
 
-    train.py:220-258 without host synchronisation.
+    @staticmethod
+    def forward(ctx, tpol, value, ret_out, bpol, action, emask, tmask, omask, progress, outcome, ret, reward,
+                cfg):
+        B, T, Pp, A = tpol.shape
+        P = tmask.shape[2]
+        lib = _native.load()
+        ws_bytes = lib.hrl_loss_workspace_bytes(B, T, P, Pp)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=tpol.device)
+        losses = torch.empty(6, dtype=torch.float32, device=tpol.device)
+        p = _native.ptr
+        code = lib.hrl_loss_forward(
+            p(tpol), p(bpol), p(action), B, T, P, Pp, A, p(emask), p(tmask), p(omask), p(progress),
+            p(value), p(outcome), p(ret_out), p(ret), p(reward),
+            cfg['value_target'], cfg['policy_target'], cfg['symmetrize'], cfg['lambda'], cfg['gamma'],
+            cfg['ent_coef'], cfg['ent_decay'], p(ws), ws_bytes, p(losses), _native.stream_of(tpol.device))
+        _native.check(code, 'hrl_loss_forward')
+        ctx.cfg = cfg
+        ctx.has_value, ctx.has_ret = value is not None, ret_out is not None
+        ctx.save_for_backward(tpol, value, ret_out, action, emask, tmask, omask, progress, ws)
+        return losses
+
+    @staticmethod
+    def backward(ctx, dlosses):
+        tpol, value, ret_out, action, emask, tmask, omask, progress, ws = ctx.saved_tensors
+        B, T, Pp, A = tpol.shape
+        P = tmask.shape[2]
+        dl = dlosses[:5].contiguous()
+        g_tpol = torch.empty_like(tpol)
+        g_value = torch.empty_like(value) if ctx.has_value else None
+        g_ret = torch.empty_like(ret_out) if ctx.has_ret else None
+        p = _native.ptr
+        lib = _native.load()
+        code = lib.hrl_loss_backward(
+            p(tpol), p(action), B, T, P, Pp, A, p(emask), p(tmask), p(omask), p(progress),
+            p(value), p(ret_out), ctx.cfg['ent_coef'], ctx.cfg['ent_decay'], p(ws), ws.numel(), p(dl),
+            p(g_tpol), p(g_value), p(g_ret), _native.stream_of(tpol.device))
+        _native.check(code, 'hrl_loss_backward')
+        return (g_tpol, g_value, g_ret) + (None,) * 10
+
+
+def _fusable(outputs, batch):
+    pol = outputs.get('policy')
+    if pol is None or not pol.is_cuda or pol.dtype != torch.float32 or pol.dim() != 4:
+        return False
+    for k in ('value', 'return'):
+        o = outputs.get(k)
+        if o is not None and (o.dim() != 4 or o.shape[-1] != 1 or o.dtype != torch.float32):
+            return False
+    P = batch['turn_mask'].shape[2]
+    return pol.shape[2] in (1, P) and batch['turn_mask'].shape[-1] == 1
+
+
+def loss_terms(outputs, batch, args):
+    """train.py:220-258 and compose_losses on the HIP kernels; (losses, dcnt tensor), no host sync."""
+    if not _fusable(outputs, batch):
+        return loss_terms_composed(outputs, batch, args)
+    alg = _native.ALG
+    for k in ('value_target', 'policy_target'):
+        if args[k] not in alg:
+            raise ValueError('No algorithm named %s' % args[k])
+    value, ret_out = outputs.get('value'), outputs.get('return')
+    P = batch['turn_mask'].shape[2]
+    cfg = {'value_target': alg[args['value_target']], 'policy_target': alg[args['policy_target']],
+           'symmetrize': int(bool(args['turn_based_training']) and value is not None and P == 2),
+           'lambda': float(args['lambda']), 'gamma': float(args['gamma']),
+           'ent_coef': float(args['entropy_regularization']),
+           'ent_decay': float(args['entropy_regularization_decay'])}
+    c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+    with_ret = ret_out is not None
+    vec = _FusedLoss.apply(c(outputs['policy']), c(value), c(ret_out), c(batch['policy'].detach()),
+                           c(batch['action']), c(batch['episode_mask']), c(batch['turn_mask']),
+                           c(batch['observation_mask']), c(batch['progress']),
+                           c(batch['outcome']) if value is not None else None,
+                           c(batch['return']) if with_ret else None, c(batch['reward']) if with_ret else None, cfg)
+    losses = {'p': vec[0]}
+    if value is not None:
+        losses['v'] = vec[1]
+    if with_ret:
+        losses['r'] = vec[2]
+    losses['ent'] = vec[3]
+    losses['total'] = vec[4]
+    return losses, vec[5].detach()
+
+
+def loss_terms_composed(outputs, batch, args):
+    """IS ratios, value symmetrisation, fused HIP target scans, PyTorch-composed losses.
+
+    train.py:220-258 without host synchronisation, for any output shapes.
     """
     actions = batch['action']
     emasks = batch['episode_mask']

@@ -112,3 +112,65 @@ def test_baseline_batch_losses_vs_oracle(cuda, B, T):
     ref['total'].backward()
     np.testing.assert_allclose(net_gpu.p.grad.cpu().numpy(), net_cpu.p.grad.numpy(), rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(net_gpu.v.grad.cpu().numpy(), net_cpu.v.grad.numpy(), rtol=1e-5, atol=1e-6)
+
+
+ALGS = ('MC', 'TD', 'UPGO', 'VTRACE')
+
+
+@pytest.mark.parametrize('vt', ALGS)
+@pytest.mark.parametrize('pt', ALGS)
+def test_fused_loss_all_target_pairs(cuda, golden_loss, vt, pt):
+    """Fused HIP loss vs the CPU oracle for every (value_target, policy_target),
+    on the Geister batch with a return head (A = 214, rewards, gamma = 0.8)."""
+    from handyrl_amd.train import compute_loss
+    meta, arrays = golden_loss
+    c = next(m for m in meta if m['name'] == 'geister_ret')
+    args = dict(c['args'], value_target=vt, policy_target=pt)
+    batch, net_cpu = loss_case(arrays, c)
+    _, net_gpu = loss_case(arrays, c)
+    net_gpu = net_gpu.to(cuda)
+    ref, ref_dcnt = ol.compute_loss(batch, net_cpu, None, args)
+    out, dcnt = compute_loss(_to(batch, cuda), net_gpu, None, args)
+    assert dcnt == ref_dcnt
+    for k in ref:
+        _close(out[k].item(), ref[k].item(), what=(vt, pt, k))
+    ref['total'].backward()
+    out['total'].backward()
+    for a, b in ((net_gpu.p, net_cpu.p), (net_gpu.v, net_cpu.v), (net_gpu.r, net_cpu.r)):
+        np.testing.assert_allclose(a.grad.cpu().numpy(), b.grad.numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize('weights', [(1, 0, 0, 0, 0), (0, 0, 0, 1, 0), (0.5, 2.0, -1.0, 0.25, 1.0)])
+def test_fused_loss_arbitrary_upstream_grads(cuda, golden_loss, weights):
+    """Backward from any combination of the five losses (not only 'total')."""
+    from handyrl_amd.train import compute_loss
+    meta, arrays = golden_loss
+    c = next(m for m in meta if m['name'] == 'geister_ret')
+    batch, net_cpu = loss_case(arrays, c)
+    _, net_gpu = loss_case(arrays, c)
+    net_gpu = net_gpu.to(cuda)
+    ref, _ = ol.compute_loss(batch, net_cpu, None, c['args'])
+    out, _ = compute_loss(_to(batch, cuda), net_gpu, None, c['args'])
+    keys = ('p', 'v', 'r', 'ent', 'total')
+    sum(w * ref[k] for w, k in zip(weights, keys)).backward()
+    sum(w * out[k] for w, k in zip(weights, keys)).backward()
+    for a, b in ((net_gpu.p, net_cpu.p), (net_gpu.v, net_cpu.v), (net_gpu.r, net_cpu.r)):
+        np.testing.assert_allclose(a.grad.cpu().numpy(), b.grad.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_fused_loss_deterministic(cuda):
+    from handyrl_amd.synthetic import tictactoe_batch, default_args
+    from handyrl_amd.train import loss_terms, forward_prediction
+    B, T = 4096, 32
+    args = default_args(T, B)
+    batch = tictactoe_batch(B, T, cuda, seed=9)
+    g = torch.Generator().manual_seed(1)
+    net = FixedOutputs(torch.randn(B * T, 9, generator=g).numpy(),
+                       torch.tanh(torch.randn(B * T, 1, generator=g)).numpy()).to(cuda)
+    runs = []
+    for _ in range(2):
+        net.zero_grad()
+        losses, dcnt = loss_terms(forward_prediction(net, None, batch, args), batch, args)
+        losses['total'].backward()
+        runs.append((torch.stack([losses[k] for k in ('p', 'v', 'ent', 'total')]).cpu(), net.p.grad.clone()))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
