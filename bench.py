@@ -101,6 +101,18 @@ def time_scan(device, B, T, iters, cold=False):
             'GBps': nbytes / (ms * 1e-3) / 1e9, 'cold': cold}
 
 
+def pmc_traffic(B, T):
+    """HBM bytes per launch of the scan from the committed rocprofv3 PMC passes (profiles/), or None."""
+    path = os.path.join(ROOT, 'profiles', 'r01_scan_pmc.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        for c in json.load(f)['configs']:
+            if c['B'] == B and c['T'] == T:
+                return c['traffic_bytes']
+    return None
+
+
 def cpu_baseline(B=1024, T=32, steps=3):
     """The CPU learner oracle on this host, 1 thread (train.py as shipped: model.py:8)."""
     from oracle.learner import CpuLearner
@@ -188,12 +200,14 @@ def main():
             'peak': HBM_PEAK_GBS,
             'unit': 'GB/s',
             'frac': round(hot['GBps'] / HBM_PEAK_GBS, 4),
-            'traffic': None,
+            'traffic': pmc_traffic(B, T),
+            'traffic_source': 'profiles/r01_scan_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected)',
             'bytes_per_launch': hot['bytes_per_launch'],
             'us_per_launch': round(hot['us_per_launch'], 3),
             'cold_large_B': {'B': cold['B'], 'T': T, 'achieved': round(cold['GBps'], 1),
                              'frac': round(cold['GBps'] / HBM_PEAK_GBS, 4),
-                             'us_per_launch': round(cold['us_per_launch'], 2)},
+                             'us_per_launch': round(cold['us_per_launch'], 2),
+                             'traffic': pmc_traffic(cold['B'], T)},
         }
         cpu = cpu_baseline() if (opts.cpu_baseline and world == 1) else None
         line = {
