@@ -22,6 +22,11 @@ Fixtures written
     (generation.py:20-88) of TicTacToe and Geister, with fixed network
     outputs, recording every ``compute_target`` call, the composed advantages,
     the losses, ``dcnt`` and the gradients w.r.t. the network outputs.
+``make_batch.npz`` + ``make_batch.json``
+    ``handyrl.train.make_batch`` (train.py:33-133) on windows of seeded
+    TicTacToe / Geister self-play episodes in the four training modes; the
+    episodes are stored decompressed and pickle-free (JSON structure + npz
+    arrays, ``encode_episode``), the outputs as arrays.
 ``learner.npz`` + ``learner.json``
     Three learner steps of the TicTacToe ``SimpleConv2dModel`` exactly as
     ``Trainer.train`` runs them (train.py:375-385): loss, backward,
@@ -293,6 +298,65 @@ def learner_case():
     return arrays, meta
 
 
+# ---------------------------------------------------------------------------
+# 4. make_batch on real episode windows
+# ---------------------------------------------------------------------------
+
+def encode(obj, arrays, prefix):
+    """Pickle-free encoding: JSON structure, ndarrays into `arrays` (tests/golden/episodes.py decodes)."""
+    if isinstance(obj, np.ndarray):
+        key = '%s#%d' % (prefix, len(arrays))
+        arrays[key] = obj
+        return {'__nd__': key}
+    if isinstance(obj, dict):
+        return {'__dict__': [[k, encode(v, arrays, prefix)] for k, v in obj.items()]}
+    if isinstance(obj, (list, tuple)):
+        return [encode(v, arrays, prefix) for v in obj]
+    if isinstance(obj, (np.floating, np.integer)):
+        return obj.item()
+    return obj
+
+
+def make_batch_cases():
+    import bz2
+    import pickle
+    from handyrl.envs.tictactoe import SimpleConv2dModel
+    arrays, manifest = {}, []
+    specs = [
+        ('ttt_tbt', 'TicTacToe', True, False, 6, 16),
+        ('ttt_tbt_short', 'TicTacToe', True, False, 5, 4),
+        ('ttt_obs', 'TicTacToe', True, True, 5, 7),
+        ('ttt_solo', 'TicTacToe', False, False, 6, 9),
+        ('geister_tbt', 'Geister', True, False, 3, 12),
+    ]
+    for ci, (name, env_name, tbt, obs, B, T) in enumerate(specs):
+        net = SimpleConv2dModel if env_name == 'TicTacToe' else None
+        eps = gen_episodes(env_name, 6 if env_name == 'TicTacToe' else 2, obs, seed=60 + ci, net_cls=net)
+        windows = select_windows(eps, B, T, 4, seed=200 + ci)
+        args = {'turn_based_training': tbt, 'observation': obs, 'forward_steps': T, 'compress_steps': 4}
+        random.seed(300 + ci)
+        batch = ref_train.make_batch(windows, args)
+        enc_windows = []
+        for w in windows:
+            moments = sum([pickle.loads(bz2.decompress(ms)) for ms in w['moment']], [])
+            ew = {k: v for k, v in w.items() if k not in ('moment', 'args')}
+            ew['moments'] = encode(moments, arrays, '%d:in' % ci)
+            ew['outcome'] = encode(w['outcome'], arrays, '%d:in' % ci)
+            enc_windows.append(ew)
+        out_keys = []
+        for k, v in batch.items():
+            if isinstance(v, dict):
+                for kk, vv in v.items():
+                    arrays['%d:out.%s.%s' % (ci, k, kk)] = _np(vv)
+                    out_keys.append('%s.%s' % (k, kk))
+            else:
+                arrays['%d:out.%s' % (ci, k)] = _np(v)
+                out_keys.append(k)
+        manifest.append({'id': ci, 'name': name, 'env': env_name, 'args': args, 'seed': 300 + ci,
+                         'windows': enc_windows, 'out_keys': out_keys})
+    return arrays, manifest
+
+
 def main():
     arr, man = target_cases()
     np.savez_compressed(os.path.join(OUT, 'targets.npz'), **arr)
@@ -305,6 +369,12 @@ def main():
     with open(os.path.join(OUT, 'loss.json'), 'w') as f:
         json.dump(man, f, indent=1)
     print('loss: %d cases' % len(man))
+
+    arr, man = make_batch_cases()
+    np.savez_compressed(os.path.join(OUT, 'make_batch.npz'), **arr)
+    with open(os.path.join(OUT, 'make_batch.json'), 'w') as f:
+        json.dump(man, f)
+    print('make_batch: %d cases' % len(man))
 
     arr, meta = learner_case()
     np.savez_compressed(os.path.join(OUT, 'learner.npz'), **arr)
