@@ -137,6 +137,54 @@ def cpu_baseline(B=1024, T=32, steps=3):
                       % (B, T, steps, dt)}
 
 
+def secondary_t9(device, steps=10, warmup=3, B=4096, T=9):
+    """BASELINE.json configs[1]: TicTacToe B=4096 T=9, the north star's >=50x point."""
+    args = default_args(T, B)
+    torch.manual_seed(0)
+    net = SimpleConv2dModel().to(device)
+    batch = tictactoe_batch(B, T, device, seed=77)
+    learner = LearnerStep(net, args, device, graph=True)
+    for _ in range(max(warmup, 1)):
+        learner.step(batch)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        learner.step(batch)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    value = B * T * steps / dt
+    ref_cpu = 18.7e3   # BASELINE.md: reference train.py, 1 thread, B=4096 T=9 (survey container CPU)
+    return {'config': 'TicTacToe B=4096 T=9 (BASELINE.json configs[1])', 'value': round(value, 1),
+            'unit': 'env-steps/s', 'ms_per_step': round(dt / steps * 1e3, 4),
+            'vs_reference_cpu_1thread': round(value / ref_cpu, 1),
+            'reference_cpu_source': 'BASELINE.md, 18.7k env-steps/s measured in the survey container'}
+
+
+def secondary_rollout(device, E=16384, reps=5):
+    """Device self-play throughput: E concurrent TicTacToe games, one batched forward per ply."""
+    from handyrl_amd.rollout import TicTacToeBatch, DeviceGenerator, DeviceReplay
+    torch.manual_seed(0)
+    net = SimpleConv2dModel().to(device)
+    gen = DeviceGenerator(TicTacToeBatch(E, device), net)
+    rep = DeviceReplay(4 * E, 9, (3, 3, 3), 9, 2, device)
+    g = torch.Generator(device=device).manual_seed(0)
+    rep.add(gen.generate(generator=g))   # warm-up
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    plies = 0
+    for _ in range(reps):
+        ep = gen.generate(generator=g)
+        rep.add(ep)
+        plies += ep['length'].sum()
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    plies = int(plies)
+    return {'config': 'TicTacToe device self-play, %d concurrent games, SimpleConv2dModel inference' % E,
+            'value': round(plies / dt, 1), 'unit': 'env-steps/s', 'games_per_s': round(E * reps / dt, 1),
+            'reference_cpu_worker': 1840.0,
+            'reference_cpu_source': 'SURVEY §6: generation.py per worker process, measured in the survey container'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -147,6 +195,7 @@ def main():
     ap.add_argument('--graph', type=int, default=1, help='capture the 1-GPU step in a HIP graph')
     ap.add_argument('--cpu-baseline', type=int, default=1)
     ap.add_argument('--scan-iters', type=int, default=200)
+    ap.add_argument('--secondary', type=int, default=1, help='also time the B=4096 T=9 config (N=1)')
     opts = ap.parse_args()
 
     rank, world, local = hdist.world_from_env()
@@ -210,6 +259,8 @@ def main():
                              'traffic': pmc_traffic(cold['B'], T)},
         }
         cpu = cpu_baseline() if (opts.cpu_baseline and world == 1) else None
+        t9 = secondary_t9(device) if (opts.secondary and world == 1) else None
+        ro = secondary_rollout(device) if (opts.secondary and world == 1) else None
         line = {
             'metric': 'learner env-steps/sec at B=4096 T=32 (TicTacToe net, UPGO/VTRACE)',
             'value': round(value, 1),
@@ -234,6 +285,10 @@ def main():
         }
         if cpu is not None:
             line['speedup_vs_cpu_baseline'] = round(value / cpu['value'], 1)
+        if t9 is not None:
+            line['secondary'] = t9
+        if ro is not None:
+            line['rollout'] = ro
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

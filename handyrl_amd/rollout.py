@@ -1,0 +1,256 @@
+"""Device-resident batched self-play and replay for the learner.
+
+The reference plays one game per worker process, one batch-1 CPU inference
+per player per ply (generation.py:20-88, model.py:43-53), ships each episode
+as bz2(pickle) blocks over TCP/pipes (generation.py:79-86, worker.py), and a
+batcher process rebuilds padded training windows on the CPU (train.py:33-133,
+284-302).  Here thousands of games advance together on the GPU:
+
+* ``TicTacToeBatch``  E concurrent games as tensors, rules of
+  handyrl/envs/tictactoe.py:103-172 (black moves first, 8 winning lines,
+  outcome +-1 / 0, 3-plane observation relative to the viewing player);
+* ``DeviceGenerator`` one batched forward of the env network per ply for
+  every live game, the reference's legal-action masking (-1e32,
+  generation.py:49-52) and categorical sampling over the legal actions by
+  Gumbel-max (the same distribution as ``random.choices(legal,
+  weights=softmax(p[legal]))``, generation.py:53), episode returns as the
+  reference's discounted sum (generation.py:73-77);
+* ``DeviceReplay``    a ring buffer of episodes in HBM; ``sample`` draws
+  windows with the reference Batcher's recency-weighted episode choice and
+  uniform window start (train.py:284-293) and gathers them straight into the
+  make_batch layout (train.py:109-133) the learner consumes -- no host copy,
+  no pickling.
+
+Scope: turn-based two-player training without opponent observation
+(turn_based_training=True, observation=False), the TicTacToe configuration.
+"""
+
+import numpy as np
+import torch
+
+__all__ = ['TicTacToeBatch', 'DeviceGenerator', 'DeviceReplay', 'episodes_to_wire']
+
+
+class TicTacToeBatch:
+    """E TicTacToe games on one device (handyrl/envs/tictactoe.py:72-172)."""
+
+    A = 9
+    P = 2
+    MAX_PLIES = 9
+    OBS_SHAPE = (3, 3, 3)
+    LINES = ((0, 1, 2), (3, 4, 5), (6, 7, 8), (0, 3, 6), (1, 4, 7), (2, 5, 8), (0, 4, 8), (2, 4, 6))
+
+    def __init__(self, E, device):
+        self.E, self.device = E, device
+        self.lines = torch.tensor(self.LINES, device=device)
+        self.reset()
+
+    def reset(self):
+        E, dev = self.E, self.device
+        self.board = torch.zeros(E, 9, dtype=torch.int8, device=dev)     # +1 black, -1 white
+        self.color = torch.ones(E, dtype=torch.int8, device=dev)          # side to move
+        self.nmoves = torch.zeros(E, dtype=torch.int32, device=dev)
+        self.winner = torch.zeros(E, dtype=torch.int8, device=dev)
+
+    def turn(self):
+        """Index of the player to move: 0 (black) on even plies."""
+        return (self.nmoves % 2).long()
+
+    def terminal(self):
+        return (self.winner != 0) | (self.nmoves >= 9)
+
+    def legal(self):
+        return self.board == 0
+
+    def observation(self, player):
+        """(E,3,3,3): [turn-view indicator, own stones, opponent stones] for `player` (E,) (tictactoe.py:157-168)."""
+        turn_view = player == self.turn()
+        me = torch.where(turn_view, self.color, -self.color).view(-1, 1)
+        b = self.board
+        planes = torch.stack([turn_view.view(-1, 1).expand(-1, 9), b == me, b == -me], dim=1)
+        return planes.float().view(-1, 3, 3, 3)
+
+    def step(self, action, active):
+        """Play `action` (E,) for the side to move in every `active` game (tictactoe.py:103-118)."""
+        rows = torch.arange(self.E, device=self.device)
+        act = torch.where(active, action, torch.zeros_like(action))
+        new = torch.where(active, self.color, self.board[rows, act])
+        self.board[rows, act] = new
+        sums = self.board.long()[:, self.lines].sum(-1)                   # (E, 8)
+        won = active & (sums == 3 * self.color.long().view(-1, 1)).any(-1)
+        self.winner = torch.where(won, self.color, self.winner)
+        self.color = torch.where(active, -self.color, self.color)
+        self.nmoves = self.nmoves + active.int()
+
+    def outcome(self):
+        """(E, 2) float: +1/-1 for the winner/loser, 0/0 for a draw (tictactoe.py:140-147)."""
+        w = self.winner.float()
+        return torch.stack([w, -w], dim=1)
+
+
+class DeviceGenerator:
+    """Batched self-play of E games with one env-network forward per ply (generation.py:20-88)."""
+
+    def __init__(self, env_batch, net, gamma=0.8):
+        self.env = env_batch
+        self.net = net
+        self.gamma = gamma
+
+    @torch.no_grad()
+    def generate(self, generator=None):
+        env, E, dev = self.env, self.env.E, self.env.device
+        Tm, A, P = env.MAX_PLIES, env.A, env.P
+        env.reset()
+        obs = torch.zeros(E, Tm, *env.OBS_SHAPE, device=dev)
+        policy = torch.zeros(E, Tm, A, device=dev)
+        amask = torch.full((E, Tm, A), 1e32, device=dev)
+        action = torch.zeros(E, Tm, dtype=torch.long, device=dev)
+        value = torch.zeros(E, Tm, device=dev)
+        turn = torch.zeros(E, Tm, dtype=torch.long, device=dev)
+        was_training = self.net.training
+        self.net.eval()
+        for t in range(Tm):
+            active = ~env.terminal()
+            player = env.turn()
+            o = env.observation(player)
+            out = self.net(o, None)
+            m = torch.where(env.legal(), 0.0, 1e32)                        # generation.py:50-51
+            p = out['policy'] - m
+            u = torch.rand(E, A, device=dev, generator=generator).clamp_(1e-20, 1.0)
+            a = torch.argmax(p - torch.log(-torch.log(u)), dim=-1)          # Gumbel-max = softmax over legal
+            act = active.view(-1, 1)
+            obs[:, t] = torch.where(act.view(-1, 1, 1, 1), o, obs[:, t])
+            policy[:, t] = torch.where(act, p, policy[:, t])
+            amask[:, t] = torch.where(act, m, amask[:, t])
+            action[:, t] = torch.where(active, a, action[:, t])
+            value[:, t] = torch.where(active, out['value'].view(-1), value[:, t])
+            turn[:, t] = torch.where(active, player, turn[:, t])
+            env.step(a, active)
+        self.net.train(was_training)
+        length = env.nmoves.long()
+        # rewards are None in TicTacToe, so the discounted returns are 0 (generation.py:73-77)
+        zeros = torch.zeros(E, Tm, P, device=dev)
+        return {'observation': obs, 'policy': policy, 'action_mask': amask, 'action': action, 'value': value,
+                'turn': turn, 'length': length, 'outcome': env.outcome(), 'reward': zeros, 'return': zeros.clone()}
+
+
+class DeviceReplay:
+    """Ring buffer of episodes in HBM; windows gathered into the make_batch layout."""
+
+    def __init__(self, capacity, max_plies, obs_shape, A, P, device, maximum_episodes=None):
+        self.N, self.Tm, self.P, self.device = capacity, max_plies, P, device
+        self.maximum_episodes = maximum_episodes or capacity
+        f = dict(device=device)
+        self.obs = torch.zeros(capacity, max_plies, *obs_shape, **f)
+        self.policy = torch.zeros(capacity, max_plies, A, **f)
+        self.amask = torch.full((capacity, max_plies, A), 1e32, **f)
+        self.action = torch.zeros(capacity, max_plies, dtype=torch.long, **f)
+        self.value = torch.zeros(capacity, max_plies, **f)
+        self.turn = torch.zeros(capacity, max_plies, dtype=torch.long, **f)
+        self.reward = torch.zeros(capacity, max_plies, P, **f)
+        self.ret = torch.zeros(capacity, max_plies, P, **f)
+        self.length = torch.ones(capacity, dtype=torch.long, **f)
+        self.outcome = torch.zeros(capacity, P, **f)
+        self.ptr = 0      # next slot
+        self.count = 0    # stored episodes (<= capacity)
+
+    def add(self, ep):
+        E = ep['length'].shape[0]
+        slots = (self.ptr + torch.arange(E, device=self.device)) % self.N
+        for dst, key in ((self.obs, 'observation'), (self.policy, 'policy'), (self.amask, 'action_mask'),
+                         (self.action, 'action'), (self.value, 'value'), (self.turn, 'turn'),
+                         (self.reward, 'reward'), (self.ret, 'return'), (self.length, 'length'),
+                         (self.outcome, 'outcome')):
+            dst.index_copy_(0, slots, ep[key])
+        self.ptr = (self.ptr + E) % self.N
+        self.count = min(self.count + E, self.N)
+
+    def _age_order(self):
+        """Slot of the i-th oldest stored episode (i = 0 oldest)."""
+        start = (self.ptr - self.count) % self.N
+        return (start + torch.arange(self.count, device=self.device)) % self.N
+
+    def sample_windows(self, B, T, generator=None):
+        """(slot, start) of B windows, as Batcher.select_episode draws them (train.py:284-293).
+
+        Episode i of the n newest (i = n-1 newest) is accepted with probability
+        1 - (n-1-i)/maximum_episodes; drawing from that weighting directly is
+        the distribution of the reference's rejection loop.
+        """
+        n = min(self.count, self.maximum_episodes)
+        i = torch.arange(n, device=self.device, dtype=torch.float64)
+        w = 1.0 - (n - 1 - i) / self.maximum_episodes
+        pick = torch.multinomial(w.float(), B, replacement=True, generator=generator)
+        slots = self._age_order()[self.count - n:][pick]
+        steps = self.length[slots]
+        cand = 1 + torch.clamp(steps - T, min=0)
+        u = torch.rand(B, device=self.device, generator=generator)
+        start = torch.minimum((u * cand).long(), cand - 1)
+        return slots, start
+
+    def gather(self, slots, start, T):
+        """make_batch-layout batch of the windows [start, start+T) of episodes `slots` (train.py:33-133)."""
+        B, P, dev = slots.shape[0], self.P, self.device
+        t = start.view(-1, 1) + torch.arange(T, device=dev).view(1, -1)      # (B, T)
+        length = self.length[slots].view(-1, 1)
+        valid = t < length
+        tc = torch.minimum(t, length - 1)
+        e = slots.view(-1, 1)
+        vf = valid.float()
+        obs = self.obs[e, tc] * vf.view(B, T, *([1] * (self.obs.dim() - 2)))
+        pol = self.policy[e, tc] * vf.unsqueeze(-1)
+        amask = torch.where(valid.unsqueeze(-1), self.amask[e, tc], torch.full_like(pol, 1e32))
+        act = self.action[e, tc] * valid.long()
+        onehot = torch.nn.functional.one_hot(self.turn[e, tc], P).float() * vf.unsqueeze(-1)   # (B,T,P)
+        oc = self.outcome[slots].view(B, 1, P, 1)
+        val = (onehot * self.value[e, tc].unsqueeze(-1)).unsqueeze(-1)
+        val = torch.where(valid.view(B, T, 1, 1), val, oc.expand(B, T, P, 1))
+        rew = self.reward[e, tc] * vf.unsqueeze(-1)
+        ret = self.ret[e, tc] * vf.unsqueeze(-1)
+        progress = torch.where(valid, t.float() / length.float(), torch.ones_like(vf))
+        return {
+            'observation': obs.unsqueeze(2).contiguous(),
+            'policy': pol.unsqueeze(2).contiguous(),
+            'value': val.contiguous(),
+            'action': act.view(B, T, 1, 1).contiguous(),
+            'outcome': oc.contiguous(),
+            'reward': rew.unsqueeze(-1).contiguous(),
+            'return': ret.unsqueeze(-1).contiguous(),
+            'episode_mask': vf.view(B, T, 1, 1).contiguous(),
+            'turn_mask': onehot.unsqueeze(-1).contiguous(),
+            'observation_mask': onehot.unsqueeze(-1).clone(),
+            'action_mask': amask.unsqueeze(2).contiguous(),
+            'progress': progress.unsqueeze(-1).contiguous(),
+        }
+
+    def sample(self, B, T, generator=None):
+        slots, start = self.sample_windows(B, T, generator)
+        return self.gather(slots, start, T)
+
+
+def episodes_to_wire(ep, compress_steps=4):
+    """Device episodes -> the reference episode format (generation.py:79-86), for parity checks."""
+    import bz2
+    import pickle
+    cpu = {k: v.cpu().numpy() for k, v in ep.items()}
+    out = []
+    for e in range(cpu['length'].shape[0]):
+        L = int(cpu['length'][e])
+        moments = []
+        for t in range(L):
+            p = int(cpu['turn'][e, t])
+            m = {k: {0: None, 1: None} for k in ('observation', 'policy', 'action_mask', 'action', 'value',
+                                                    'reward', 'return')}
+            m['observation'][p] = cpu['observation'][e, t].astype(np.float32)
+            m['policy'][p] = cpu['policy'][e, t].astype(np.float32)
+            m['action_mask'][p] = cpu['action_mask'][e, t].astype(np.float32)
+            m['action'][p] = int(cpu['action'][e, t])
+            m['value'][p] = np.array([cpu['value'][e, t]], dtype=np.float32)
+            for q in (0, 1):
+                m['return'][q] = float(cpu['return'][e, t, q])
+            m['turn'] = [p]
+            moments.append(m)
+        out.append({'args': {}, 'steps': L, 'outcome': {0: float(cpu['outcome'][e, 0]), 1: float(cpu['outcome'][e, 1])},
+                    'moment': [bz2.compress(pickle.dumps(moments[i:i + compress_steps]))
+                               for i in range(0, L, compress_steps)]})
+    return out

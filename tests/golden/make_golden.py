@@ -357,6 +357,30 @@ def make_batch_cases():
     return arrays, manifest
 
 
+# ---------------------------------------------------------------------------
+# 5. TicTacToe rules (handyrl/envs/tictactoe.py:72-172) on random games
+# ---------------------------------------------------------------------------
+
+def tictactoe_rules():
+    env = make_env({'env': 'TicTacToe'})
+    rnd = random.Random(2025)
+    games = []
+    arrays = {}
+    for g in range(60):
+        env.reset()
+        plies = []
+        while not env.terminal():
+            legal = env.legal_actions(env.turn())
+            a = rnd.choice(legal)
+            key = '%d:%d' % (g, len(plies))
+            arrays[key + ':obs0'] = env.observation(0)
+            arrays[key + ':obs1'] = env.observation(1)
+            plies.append({'turn': env.turn(), 'legal': legal, 'action': a})
+            env.play(a)
+        games.append({'plies': plies, 'outcome': [env.outcome()[0], env.outcome()[1]]})
+    return arrays, games
+
+
 def main():
     arr, man = target_cases()
     np.savez_compressed(os.path.join(OUT, 'targets.npz'), **arr)
@@ -375,6 +399,12 @@ def main():
     with open(os.path.join(OUT, 'make_batch.json'), 'w') as f:
         json.dump(man, f)
     print('make_batch: %d cases' % len(man))
+
+    arr, games = tictactoe_rules()
+    np.savez_compressed(os.path.join(OUT, 'tictactoe_rules.npz'), **arr)
+    with open(os.path.join(OUT, 'tictactoe_rules.json'), 'w') as f:
+        json.dump(games, f)
+    print('tictactoe rules: %d games' % len(games))
 
     arr, meta = learner_case()
     np.savez_compressed(os.path.join(OUT, 'learner.npz'), **arr)

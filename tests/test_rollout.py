@@ -1,0 +1,164 @@
+"""Device rollout and replay (handyrl_amd/rollout.py) vs the reference.
+
+* TicTacToe rules: the batched env and the CPU plugin replay 60 random games
+  recorded from the reference env (tests/golden/tictactoe_rules.*): legal
+  actions, both players' observations, terminal plies and outcomes;
+* the replay's window gather equals make_batch (bit-exact to the reference,
+  tests/test_make_batch.py) on the same episodes converted to the
+  reference's wire format;
+* sampling: actions follow softmax over the legal actions; window choice
+  follows the Batcher's recency weighting.
+"""
+
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import load_golden
+
+
+@pytest.fixture(scope='module')
+def rules():
+    return load_golden('tictactoe_rules')
+
+
+def test_cpu_env_matches_reference_rules(rules):
+    from handyrl_amd.envs.tictactoe import Environment
+    games, arrays = rules
+    env = Environment()
+    for g, game in enumerate(games):
+        env.reset()
+        for i, ply in enumerate(game['plies']):
+            assert not env.terminal()
+            assert env.turn() == ply['turn']
+            assert env.legal_actions(env.turn()) == ply['legal']
+            for p in (0, 1):
+                np.testing.assert_array_equal(env.observation(p), arrays['%d:%d:obs%d' % (g, i, p)])
+            env.play(ply['action'])
+        assert env.terminal()
+        assert [env.outcome()[0], env.outcome()[1]] == game['outcome']
+
+
+def _replay_games(games, device):
+    """Drive all games in parallel through TicTacToeBatch with the recorded actions."""
+    from handyrl_amd.rollout import TicTacToeBatch
+    E = len(games)
+    env = TicTacToeBatch(E, device)
+    T = max(len(g['plies']) for g in games)
+    return env, T
+
+
+@pytest.mark.parametrize('device', ['cpu', pytest.param('cuda', marks=pytest.mark.gpu)])
+def test_batched_env_matches_reference_rules(rules, device):
+    if device == 'cuda' and not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    games, arrays = rules
+    dev = torch.device(device)
+    env, T = _replay_games(games, dev)
+    for t in range(T):
+        live = torch.tensor([t < len(g['plies']) for g in games], device=dev)
+        assert torch.equal(~env.terminal(), live)
+        acts = torch.zeros(len(games), dtype=torch.long, device=dev)
+        for g, game in enumerate(games):
+            if t < len(game['plies']):
+                ply = game['plies'][t]
+                assert int(env.turn()[g]) == ply['turn']
+                assert torch.nonzero(env.legal()[g]).view(-1).tolist() == ply['legal']
+                acts[g] = ply['action']
+        for p in (0, 1):
+            o = env.observation(torch.full((len(games),), p, dtype=torch.long, device=dev)).cpu().numpy()
+            for g, game in enumerate(games):
+                if t < len(game['plies']):
+                    np.testing.assert_array_equal(o[g], arrays['%d:%d:obs%d' % (g, t, p)])
+        env.step(acts, live)
+    assert bool(env.terminal().all())
+    assert env.outcome().cpu().tolist() == [[float(x) for x in g['outcome']] for g in games]
+
+
+def _generate(device, E=64, seed=0):
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.rollout import TicTacToeBatch, DeviceGenerator
+    torch.manual_seed(seed)
+    net = SimpleConv2dModel().to(device)
+    gen = DeviceGenerator(TicTacToeBatch(E, device), net)
+    g = torch.Generator(device=device).manual_seed(seed)
+    return gen.generate(generator=g)
+
+
+@pytest.mark.parametrize('device', ['cpu', pytest.param('cuda', marks=pytest.mark.gpu)])
+@pytest.mark.parametrize('T', [9, 4, 12])
+def test_replay_gather_equals_make_batch(device, T):
+    if device == 'cuda' and not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from handyrl_amd.batch import make_batch
+    from handyrl_amd.rollout import DeviceReplay, episodes_to_wire
+    dev = torch.device(device)
+    ep = _generate(dev, E=48, seed=T)
+    rep = DeviceReplay(64, 9, (3, 3, 3), 9, 2, dev)
+    rep.add(ep)
+    g = torch.Generator(device=dev).manual_seed(1)
+    slots, start = rep.sample_windows(40, T, generator=g)
+    batch = rep.gather(slots, start, T)
+    wire = episodes_to_wire(ep)
+    windows = []
+    for s, st in zip(slots.tolist(), start.tolist()):
+        e = wire[s]
+        L = e['steps']
+        ed = min(st + T, L)
+        # the whole episode is stored from base 0 (compress blocks cover every ply)
+        windows.append({'args': {}, 'outcome': e['outcome'], 'moment': e['moment'], 'base': 0,
+                        'start': st, 'end': ed, 'total': L})
+    ref = make_batch(windows, {'turn_based_training': True, 'observation': False, 'forward_steps': T})
+    for k, v in ref.items():
+        got = batch[k].cpu()
+        assert got.shape == v.shape and got.dtype == v.dtype, (k, got.shape, v.shape)
+        np.testing.assert_array_equal(got.numpy(), v.numpy(), err_msg=k)
+
+
+def test_generated_games_are_legal_and_complete():
+    ep = _generate(torch.device('cpu'), E=200, seed=3)
+    L = ep['length']
+    assert int(L.min()) >= 5 and int(L.max()) <= 9
+    act, amask = ep['action'], ep['action_mask']
+    t = torch.arange(9).view(1, -1)
+    live = t < L.view(-1, 1)
+    chosen = amask.gather(-1, act.unsqueeze(-1)).squeeze(-1)
+    assert bool((chosen[live] == 0).all())             # every played action was legal
+    # each square is played at most once per game
+    for e in range(20):
+        a = act[e, :int(L[e])].tolist()
+        assert len(set(a)) == len(a)
+    # turns alternate starting with player 0
+    assert torch.equal(ep['turn'][live], (t.expand_as(live) % 2)[live])
+
+
+def test_gumbel_sampling_matches_softmax_over_legal():
+    """generation.py:53 samples random.choices(legal, weights=softmax(p[legal]))."""
+    torch.manual_seed(0)
+    logits = torch.tensor([0.5, -1.0, 2.0, 0.0, 0.3, -0.2, 1.0, 0.1, -2.0])
+    legal = torch.tensor([1, 0, 1, 1, 0, 1, 1, 1, 0], dtype=torch.bool)
+    m = torch.where(legal, 0.0, 1e32)
+    p = logits - m
+    n = 200000
+    u = torch.rand(n, 9).clamp_(1e-20, 1.0)
+    a = torch.argmax(p - torch.log(-torch.log(u)), dim=-1)
+    freq = torch.bincount(a, minlength=9).float() / n
+    expect = torch.softmax(logits.masked_fill(~legal, -float('inf')), 0)
+    assert float(freq[~legal].sum()) == 0.0
+    assert torch.allclose(freq, expect, atol=4e-3)
+
+
+def test_window_choice_recency_weighting():
+    """P(episode i of n) proportional to 1 - (n-1-i)/maximum_episodes (train.py:286-289)."""
+    from handyrl_amd.rollout import DeviceReplay
+    rep = DeviceReplay(10, 9, (3, 3, 3), 9, 2, torch.device('cpu'), maximum_episodes=20)
+    rep.count, rep.ptr = 10, 0
+    rep.length.fill_(9)
+    g = torch.Generator().manual_seed(0)
+    slots, start = rep.sample_windows(200000, 9, generator=g)
+    freq = torch.bincount(slots, minlength=10).double() / slots.numel()
+    w = 1 - (9 - torch.arange(10, dtype=torch.float64)) / 20
+    assert torch.allclose(freq, w / w.sum(), atol=4e-3)
+    assert int(start.max()) == 0     # 9-ply episodes, T=9: one window per episode
