@@ -38,10 +38,10 @@ SIGNATURES = {
         _i64, _i64, _i64, _i64, _i64, _i64, _dbl, _dbl, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_bn_workspace_bytes': (ctypes.c_int64, [_i64, _i64, _i64]),
     'hrl_bn_forward_train': (ctypes.c_int, [
-        _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, _dbl, _dbl, _f32p, _f32p, _f32p,
+        _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, _dbl, _dbl, ctypes.c_int, _f32p, _f32p, _f32p,
         ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_bn_backward': (ctypes.c_int, [
-        _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
+        _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_int, _f32p, _f32p, _f32p,
         ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_loss_workspace_bytes': (ctypes.c_int64, [_i64, _i64, _i64, _i64]),
     'hrl_loss_forward': (ctypes.c_int, [
@@ -55,7 +55,7 @@ SIGNATURES = {
         ctypes.c_void_p, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib = None
 

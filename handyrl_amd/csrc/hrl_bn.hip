@@ -216,7 +216,10 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
 }
 
 // ---- forward apply: y = x*alpha[c] + beta[c] ----
-template <int VW>
+// relu(v) as torch.relu: negatives to 0, NaN stays NaN
+__device__ __forceinline__ float relu(float v) { return v < 0.f ? 0.f : v; }
+
+template <int VW, bool RELU>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float *__restrict__ x, Geo g,
                                                             const float *__restrict__ alpha,
                                                             const float *__restrict__ beta, float *__restrict__ y) {
@@ -242,7 +245,10 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float *__restr
                 float v[VW];
                 load_vec<VW>(x + off, v);
 #pragma unroll
-                for (int j = 0; j < VW; ++j) v[j] = v[j] * al[k][j] + be[k][j];
+                for (int j = 0; j < VW; ++j) {
+                    v[j] = v[j] * al[k][j] + be[k][j];
+                    if constexpr (RELU) v[j] = relu(v[j]);
+                }
                 store_vec<VW>(y + off, v);
             }
         }
@@ -250,22 +256,32 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float *__restr
 }
 
 // ---- backward reduce: per-block sum(dy) and sum(dy*(x-mean)) per channel ----
-template <int VW>
+// With RELU the forward output was relu(x*alpha + beta): the incoming gradient
+// is masked where that pre-activation is <= 0 (threshold_backward), recomputed
+// here from x with the forward's own per-channel alpha/beta.
+template <int VW, bool RELU>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const float *__restrict__ x,
                                                                  const float *__restrict__ dy, Geo g,
                                                                  const float *__restrict__ mean,
+                                                                 const float *__restrict__ invstd,
+                                                                 const float *__restrict__ weight,
+                                                                 const float *__restrict__ bias,
                                                                  double *__restrict__ part) {
     extern __shared__ double sh[];
     Lane ln;
     ln.init(g);
-    float mu[kMaxSlots][VW];
+    float mu[kMaxSlots][VW], al[kMaxSlots][VW], be[kMaxSlots][VW];
     double a[kMaxSlots][VW], b[kMaxSlots][VW];
 #pragma unroll
     for (int k = 0; k < kMaxSlots; ++k)
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
             a[k][j] = b[k][j] = 0.0;
-            mu[k][j] = mean[ln.col[k] >= 0 ? (ln.col[k] * VW + j) / g.HW : 0];
+            const int ch = ln.col[k] >= 0 ? (ln.col[k] * VW + j) / g.HW : 0;
+            mu[k][j] = mean[ch];
+            // the forward's alpha/beta, recomputed with the same float operations (bn_finalize_kernel)
+            al[k][j] = RELU ? invstd[ch] * (weight ? weight[ch] : 1.0f) : 0.f;
+            be[k][j] = RELU ? (bias ? bias[ch] : 0.0f) - mean[ch] * al[k][j] : 0.f;
         }
     const int64_t r0 = (int64_t)blockIdx.x * g.rows_per_block;
     const int64_t r1 = min(g.N, r0 + g.rows_per_block);
@@ -280,6 +296,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const float *__
                 load_vec<VW>(dy + off, gv);
 #pragma unroll
                 for (int j = 0; j < VW; ++j) {
+                    if constexpr (RELU) {
+                        if (!(xv[j] * al[k][j] + be[k][j] > 0.f)) gv[j] = 0.f;
+                    }
                     a[k][j] += (double)gv[j];
                     b[k][j] += (double)gv[j] * (double)(xv[j] - mu[k][j]);
                 }
@@ -290,7 +309,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const float *__
 }
 
 // ---- backward apply: dx = ((dy - mean(dy)) - (x-mean)*k) * invstd * w ----
-template <int VW>
+template <int VW, bool RELU>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float *__restrict__ x,
                                                                 const float *__restrict__ dy, Geo g,
                                                                 const float *__restrict__ mean,
@@ -298,10 +317,12 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float *__r
                                                                 const float *__restrict__ weight,
                                                                 const float *__restrict__ kcoef,
                                                                 const float *__restrict__ gmean,
+                                                                const float *__restrict__ bias,
                                                                 float *__restrict__ dx) {
     Lane ln;
     ln.init(g);
     float mu[kMaxSlots][VW], kk[kMaxSlots][VW], gm[kMaxSlots][VW], is[kMaxSlots][VW], ww[kMaxSlots][VW];
+    float al[kMaxSlots][VW], be[kMaxSlots][VW];
 #pragma unroll
     for (int k = 0; k < kMaxSlots; ++k)
 #pragma unroll
@@ -312,6 +333,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float *__r
             gm[k][j] = gmean[ch];
             is[k][j] = invstd[ch];
             ww[k][j] = weight ? weight[ch] : 1.0f;
+            al[k][j] = RELU ? is[k][j] * ww[k][j] : 0.f;
+            be[k][j] = RELU ? (bias ? bias[ch] : 0.0f) - mu[k][j] * al[k][j] : 0.f;
         }
     const int64_t r0 = (int64_t)blockIdx.x * g.rows_per_block;
     const int64_t r1 = min(g.N, r0 + g.rows_per_block);
@@ -326,6 +349,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float *__r
                 load_vec<VW>(dy + off, gv);
 #pragma unroll
                 for (int j = 0; j < VW; ++j) {
+                    if constexpr (RELU) {
+                        if (!(xv[j] * al[k][j] + be[k][j] > 0.f)) gv[j] = 0.f;
+                    }
                     const float t = (xv[j] - mu[k][j]) * kk[k][j];
                     xv[j] = (((gv[j] - gm[k][j]) - t) * is[k][j]) * ww[k][j];
                 }
@@ -373,6 +399,30 @@ int launch_status() {
 
 }  // namespace
 
+namespace {
+
+template <int VW, bool RELU>
+void launch_apply(const Geo &g, hipStream_t s, const float *x, const float *ca, const float *cb, float *y) {
+    hipLaunchKernelGGL((bn_apply_kernel<VW, RELU>), dim3(g.nblocks), dim3(kThreads), 0, s, x, g, ca, cb, y);
+}
+
+template <int VW, bool RELU>
+void launch_bwd(const Geo &g, hipStream_t s, size_t lds, const float *x, const float *dy, const float *mean,
+                const float *invstd, const float *weight, const float *bias, double *part) {
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<VW, RELU>), dim3(g.nblocks), dim3(kThreads), lds, s, x, dy, g, mean,
+                       invstd, weight, bias, part);
+}
+
+template <int VW, bool RELU>
+void launch_bwd_apply(const Geo &g, hipStream_t s, const float *x, const float *dy, const float *mean,
+                      const float *invstd, const float *weight, const float *kcoef, const float *gmean,
+                      const float *bias, float *dx) {
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<VW, RELU>), dim3(g.nblocks), dim3(kThreads), 0, s, x, dy, g, mean, invstd,
+                       weight, kcoef, gmean, bias, dx);
+}
+
+}  // namespace
+
 extern "C" {
 
 int64_t hrl_bn_workspace_bytes(int64_t N, int64_t C, int64_t HW) {
@@ -383,7 +433,7 @@ int64_t hrl_bn_workspace_bytes(int64_t N, int64_t C, int64_t HW) {
 }
 
 int hrl_bn_forward_train(const float *x, int64_t N, int64_t C, int64_t HW, const float *weight, const float *bias,
-                         float *running_mean, float *running_var, double momentum, double eps, float *y,
+                         float *running_mean, float *running_var, double momentum, double eps, int relu, float *y,
                          float *save_mean, float *save_invstd, void *workspace, int64_t workspace_bytes,
                          void *stream) {
     if (!x || !y || !save_mean || !save_invstd || !workspace) return HRL_EINVAL;
@@ -405,14 +455,14 @@ int hrl_bn_forward_train(const float *x, int64_t N, int64_t C, int64_t HW, const
                        save_mean, save_invstd, coef_a, coef_b, (float *)nullptr, (float *)nullptr);
     rc = launch_status();
     if (rc) return rc;
-    if (vec) hipLaunchKernelGGL(bn_apply_kernel<4>, dim3(g.nblocks), dim3(kThreads), 0, s, x, g, coef_a, coef_b, y);
-    else hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(g.nblocks), dim3(kThreads), 0, s, x, g, coef_a, coef_b, y);
+    if (vec) relu ? launch_apply<4, true>(g, s, x, coef_a, coef_b, y) : launch_apply<4, false>(g, s, x, coef_a, coef_b, y);
+    else relu ? launch_apply<1, true>(g, s, x, coef_a, coef_b, y) : launch_apply<1, false>(g, s, x, coef_a, coef_b, y);
     return launch_status();
 }
 
 int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW, const float *weight,
-                    const float *save_mean, const float *save_invstd, float *dx, float *dweight, float *dbias,
-                    void *workspace, int64_t workspace_bytes, void *stream) {
+                    const float *bias, const float *save_mean, const float *save_invstd, int relu, float *dx,
+                    float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream) {
     if (!x || !dy || !dx || !save_mean || !save_invstd || !workspace || dx == dy) return HRL_EINVAL;
     const bool vec = (C * HW) % 4 == 0 && aligned16(x) && aligned16(dy) && aligned16(dx);
     Geo g;
@@ -423,8 +473,10 @@ int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64
     float *kcoef = reinterpret_cast<float *>(part + (int64_t)g.nblocks * g.C * 2);
     float *gmean = kcoef + g.C;
     const size_t lds = sizeof(double) * 2 * g.S;
-    if (vec) hipLaunchKernelGGL(bn_bwd_reduce_kernel<4>, dim3(g.nblocks), dim3(kThreads), lds, s, x, dy, g, save_mean, part);
-    else hipLaunchKernelGGL(bn_bwd_reduce_kernel<1>, dim3(g.nblocks), dim3(kThreads), lds, s, x, dy, g, save_mean, part);
+    if (vec) relu ? launch_bwd<4, true>(g, s, lds, x, dy, save_mean, save_invstd, weight, bias, part)
+                  : launch_bwd<4, false>(g, s, lds, x, dy, save_mean, save_invstd, weight, bias, part);
+    else relu ? launch_bwd<1, true>(g, s, lds, x, dy, save_mean, save_invstd, weight, bias, part)
+              : launch_bwd<1, false>(g, s, lds, x, dy, save_mean, save_invstd, weight, bias, part);
     int rc = launch_status();
     if (rc) return rc;
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(g.C), dim3(kThreads), 0, s, 1, part, g.nblocks, g.C,
@@ -432,12 +484,10 @@ int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64
                        0.0f, 0.0, (float *)nullptr, const_cast<float *>(save_invstd), kcoef, gmean, dweight, dbias);
     rc = launch_status();
     if (rc) return rc;
-    if (vec)
-        hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, dim3(g.nblocks), dim3(kThreads), 0, s, x, dy, g, save_mean,
-                           save_invstd, weight, kcoef, gmean, dx);
-    else
-        hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(g.nblocks), dim3(kThreads), 0, s, x, dy, g, save_mean,
-                           save_invstd, weight, kcoef, gmean, dx);
+    if (vec) relu ? launch_bwd_apply<4, true>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx)
+                  : launch_bwd_apply<4, false>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx);
+    else relu ? launch_bwd_apply<1, true>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx)
+              : launch_bwd_apply<1, false>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx);
     return launch_status();
 }
 

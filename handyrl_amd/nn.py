@@ -26,11 +26,12 @@ if libhrl.so is missing that raises (no silent fallback).
 """
 
 import torch
+import torch.fx
 import torch.nn as nn
 
 from . import _native
 
-__all__ = ['BatchNorm2d', 'BoardConv2d', 'Linear', 'accelerate', 'batch_norm_train']
+__all__ = ['BatchNorm2d', 'BoardConv2d', 'Linear', 'accelerate', 'batch_norm_train', 'fuse_bn_relu', 'unfuse']
 
 _MAX_ROW = 3072        # float4 path (row width a multiple of 4)
 _MAX_ROW_SCALAR = 1024  # scalar path
@@ -38,7 +39,7 @@ _MAX_ROW_SCALAR = 1024  # scalar path
 
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu=False):
         N, C = x.shape[0], x.shape[1]
         HW = x[0, 0].numel()
         x = x.contiguous()
@@ -52,17 +53,18 @@ class _BatchNormTrain(torch.autograd.Function):
         invstd = torch.empty(C, dtype=torch.float32, device=x.device)
         code = lib.hrl_bn_forward_train(
             _native.ptr(x), N, C, HW, _native.ptr(weight), _native.ptr(bias),
-            _native.ptr(running_mean), _native.ptr(running_var), float(momentum), float(eps),
+            _native.ptr(running_mean), _native.ptr(running_var), float(momentum), float(eps), int(relu),
             _native.ptr(y), _native.ptr(mean), _native.ptr(invstd), _native.ptr(ws), ws_bytes,
             _native.stream_of(x.device))
         _native.check(code, 'hrl_bn_forward_train')
-        ctx.save_for_backward(x, weight, mean, invstd)
+        ctx.save_for_backward(x, weight, bias, mean, invstd)
         ctx.has_bias = bias is not None
+        ctx.relu = bool(relu)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, mean, invstd = ctx.saved_tensors
+        x, weight, bias, mean, invstd = ctx.saved_tensors
         N, C = x.shape[0], x.shape[1]
         HW = x[0, 0].numel()
         dy = dy.contiguous()
@@ -73,16 +75,16 @@ class _BatchNormTrain(torch.autograd.Function):
         dw = torch.empty(C, dtype=torch.float32, device=x.device) if weight is not None else None
         db = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_bias else None
         code = lib.hrl_bn_backward(
-            _native.ptr(x), _native.ptr(dy), N, C, HW, _native.ptr(weight), _native.ptr(mean), _native.ptr(invstd),
-            _native.ptr(dx), _native.ptr(dw), _native.ptr(db), _native.ptr(ws), ws_bytes,
-            _native.stream_of(x.device))
+            _native.ptr(x), _native.ptr(dy), N, C, HW, _native.ptr(weight), _native.ptr(bias), _native.ptr(mean),
+            _native.ptr(invstd), int(ctx.relu), _native.ptr(dx), _native.ptr(dw), _native.ptr(db),
+            _native.ptr(ws), ws_bytes, _native.stream_of(x.device))
         _native.check(code, 'hrl_bn_backward')
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
-def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps):
-    """F.batch_norm(..., training=True) on the HIP kernels (x: (N, C, *spatial) fp32 CUDA)."""
-    return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps)
+def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps, relu=False):
+    """F.batch_norm(..., training=True) [+ ReLU] on the HIP kernels (x: (N, C, *spatial) fp32 CUDA)."""
+    return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu)
 
 
 BOARD_MAX_CELLS = 16
@@ -209,14 +211,22 @@ def _board_conv_ok(m):
 
 
 class BatchNorm2d(nn.BatchNorm2d):
-    """nn.BatchNorm2d whose training-mode CUDA path runs csrc/hrl_bn.hip."""
+    """nn.BatchNorm2d whose training-mode CUDA path runs csrc/hrl_bn.hip.
+
+    ``fused_relu`` (set by ``fuse_bn_relu``) makes the module apply the ReLU
+    that followed it in the net's forward: inside the kernels on the HIP path,
+    as ``F.relu`` otherwise.
+    """
+
+    fused_relu = False
 
     def forward(self, x):
         row = x.shape[1] * x.shape[2] * x.shape[3] if x.dim() == 4 else 0
         use_hip = (self.training and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
                    and x.shape[0] > 0 and (row <= _MAX_ROW_SCALAR or (row % 4 == 0 and row <= _MAX_ROW)))
         if not use_hip:
-            return super().forward(x)
+            y = super().forward(x)
+            return torch.relu(y) if self.fused_relu else y
         self._check_input_dim(x)
         momentum = 0.0 if self.momentum is None else self.momentum
         if self.track_running_stats and self.num_batches_tracked is not None:
@@ -225,7 +235,7 @@ class BatchNorm2d(nn.BatchNorm2d):
                 momentum = 1.0 / float(self.num_batches_tracked.item())
         rm = self.running_mean if self.track_running_stats else None
         rv = self.running_var if self.track_running_stats else None
-        return batch_norm_train(x, self.weight, self.bias, rm, rv, momentum, self.eps)
+        return batch_norm_train(x, self.weight, self.bias, rm, rv, momentum, self.eps, self.fused_relu)
 
 
 def accelerate(model):
@@ -263,4 +273,82 @@ def accelerate(model):
             setattr(model, name, new)
         else:
             accelerate(child)
+    return model
+
+
+class _LeafTracer(torch.fx.Tracer):
+    """Trace the env net, keeping the HIP-backed modules as opaque calls."""
+
+    def is_leaf_module(self, m, qualname):
+        return isinstance(m, (BatchNorm2d, BoardConv2d, Linear)) or super().is_leaf_module(m, qualname)
+
+
+def _is_relu(gm, node):
+    if node.op == 'call_function' and node.target in (torch.relu, torch.nn.functional.relu):
+        return len(node.args) == 1
+    if node.op == 'call_method' and node.target == 'relu':
+        return len(node.args) == 1
+    if node.op == 'call_module':
+        return isinstance(gm.get_submodule(node.target), nn.ReLU)
+    return False
+
+
+def fuse_bn_relu(model, example=None):
+    """Fold every BatchNorm2d -> ReLU pair of ``model.forward`` into the BatchNorm (torch.fx).
+
+    The model keeps its class, parameters and state_dict; only its forward is
+    replaced by the rewritten graph.  Recurrent nets (``init_hidden``) and nets
+    that do not trace are left as they are.  With ``example`` (an observation
+    batch), the rewritten forward is checked against the original (eval mode)
+    and dropped on any mismatch.  Returns the number of fused pairs.
+    """
+    if hasattr(model, 'init_hidden') or 'forward' in model.__dict__:
+        return 0
+    try:
+        graph = _LeafTracer().trace(model)
+    except Exception:
+        return 0
+    gm = torch.fx.GraphModule(model, graph)
+    pairs = []
+    for node in gm.graph.nodes:
+        if node.op == 'call_module' and isinstance(gm.get_submodule(node.target), BatchNorm2d):
+            users = list(node.users)
+            if len(users) == 1 and _is_relu(gm, users[0]) and users[0].args[0] is node:
+                pairs.append((node, users[0]))
+    if not pairs:
+        return 0
+    for bn_node, relu_node in pairs:
+        relu_node.replace_all_uses_with(bn_node)
+        gm.graph.erase_node(relu_node)
+    gm.graph.lint()
+    gm.recompile()
+    bns = [gm.get_submodule(n.target) for n, _ in pairs]
+    if example is not None:
+        was = model.training
+        model.eval()
+        with torch.no_grad():
+            ref = model(example, None)
+            for bn in bns:
+                bn.fused_relu = True
+            new = gm(example, None)
+        model.train(was)
+        same = set(ref) == set(new) and all(
+            torch.allclose(ref[k], new[k], rtol=1e-5, atol=1e-6) for k in ref if ref[k] is not None)
+        if not same:
+            for bn in bns:
+                bn.fused_relu = False
+            return 0
+    for bn in bns:
+        bn.fused_relu = True
+    model.forward = gm.forward
+    return len(pairs)
+
+
+def unfuse(model):
+    """Undo fuse_bn_relu (e.g. before pickling the model for CPU workers)."""
+    if 'forward' in model.__dict__:
+        del model.forward
+    for m in model.modules():
+        if isinstance(m, BatchNorm2d):
+            m.fused_relu = False
     return model

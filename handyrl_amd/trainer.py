@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from . import distributed as hdist
-from .nn import accelerate
+from .nn import accelerate, fuse_bn_relu
 from .train import forward_prediction, loss_terms
 
 DEFAULT_LR = 3e-8  # train.py:318
@@ -37,8 +37,10 @@ class LearnerStep:
     def __init__(self, net, args, device, lr=None, graph=False, reduce_group=None, world_size=1,
                  bucket_bytes=256 * 1024, hip_layers=True, loss_fn=None):
         self.net = net.to(device)
+        self._fuse_pending = False
         if hip_layers and device.type == 'cuda':
             accelerate(self.net)  # HIP BatchNorm etc.; same parameters and state_dict
+            self._fuse_pending = True  # BN->ReLU fusion, checked on the first batch
         self.args = args
         self.device = device
         # loss_fn(outputs, batch, args) -> (losses, dcnt tensor); the HIP path by default
@@ -71,6 +73,11 @@ class LearnerStep:
 
     # -- one update ----------------------------------------------------------
     def _body(self, batch, hidden):
+        if self._fuse_pending:
+            self._fuse_pending = False
+            obs = batch['observation']
+            if hidden is None and isinstance(obs, torch.Tensor):
+                self.fused_pairs = fuse_bn_relu(self.net, obs[:2].reshape(-1, *obs.shape[3:]))
         self.grads.zero()
         outputs = forward_prediction(self.net, hidden, batch, self.args)
         losses, dcnt = self.loss_fn(outputs, batch, self.args)

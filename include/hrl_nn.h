@@ -35,17 +35,21 @@ extern "C" {
 /* Scratch bytes needed by hrl_bn_forward_train / hrl_bn_backward for this shape. */
 int64_t hrl_bn_workspace_bytes(int64_t N, int64_t C, int64_t HW);
 
-/* Training forward: y, save_mean, save_invstd (C floats each), running stats updated in place. */
+/* Training forward: y, save_mean, save_invstd (C floats each), running stats updated in place.
+ * relu != 0 fuses the ReLU that follows the BatchNorm in the env nets
+ * (F.relu(bn(conv(h))), tictactoe.py:62-65): y = relu(x*alpha + beta). */
 int hrl_bn_forward_train(const float *x, int64_t N, int64_t C, int64_t HW,
                          const float *weight, const float *bias,
-                         float *running_mean, float *running_var, double momentum, double eps,
+                         float *running_mean, float *running_var, double momentum, double eps, int relu,
                          float *y, float *save_mean, float *save_invstd,
                          void *workspace, int64_t workspace_bytes, void *stream);
 
-/* Backward of the training forward: dx (may not alias dy), dweight/dbias (C floats, may be NULL). */
+/* Backward of the training forward: dx (may not alias dy), dweight/dbias (C floats, may be NULL).
+ * With relu != 0 the ReLU mask is recomputed from x (no saved output needed);
+ * bias is then required to rebuild the forward's per-channel shift. */
 int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW,
-                    const float *weight, const float *save_mean, const float *save_invstd,
-                    float *dx, float *dweight, float *dbias,
+                    const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
+                    int relu, float *dx, float *dweight, float *dbias,
                     void *workspace, int64_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus

@@ -155,3 +155,37 @@ def test_linear_chunked_weight_grad(cuda):
     np.testing.assert_allclose(xh.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(hip.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-4, atol=1e-3)
     np.testing.assert_allclose(hip.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize('N,C,H,W', [(1000, 32, 3, 3), (9, 3, 3, 3), (13, 32, 7, 11)])
+def test_bn_relu_fused_matches_torch_cpu(cuda, N, C, H, W):
+    torch.manual_seed(N)
+    ref, hip = _pair(C)
+    hip.fused_relu = True
+    hip = hip.to(cuda)
+    x = torch.randn(N, C, H, W) * 2 + 0.3
+    dy = torch.randn(N, C, H, W)
+    xr, xh = x.clone().requires_grad_(True), x.to(cuda).requires_grad_(True)
+    yr = torch.relu(ref(xr))
+    yh = hip(xh)
+    np.testing.assert_allclose(yh.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-5, atol=2e-5)
+    yr.backward(dy)
+    yh.backward(dy.to(cuda))
+    np.testing.assert_allclose(xh.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(hip.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(hip.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_fx_fusion_in_learner(cuda):
+    """LearnerStep fuses the TicTacToe net's three BN->ReLU pairs and keeps the state_dict keys."""
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.nn import BatchNorm2d
+    from handyrl_amd.synthetic import tictactoe_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    net = SimpleConv2dModel()
+    keys = list(net.state_dict())
+    step = LearnerStep(net, default_args(9, 64), cuda)
+    step.step(tictactoe_batch(64, 9, cuda, seed=0))
+    assert step.fused_pairs == 3
+    assert all(m.fused_relu for m in net.modules() if isinstance(m, BatchNorm2d))
+    assert list(net.state_dict()) == keys
