@@ -25,6 +25,8 @@ The HIP path is taken whenever the input is a CUDA tensor in training mode;
 if libhrl.so is missing that raises (no silent fallback).
 """
 
+import operator
+
 import torch
 import torch.fx
 import torch.nn as nn
@@ -136,71 +138,58 @@ class Linear(nn.Linear):
 class BoardConv2d(nn.Conv2d):
     """nn.Conv2d computed as one dense GEMM over the flattened board (see module doc)."""
 
-    def _board_tables(self, H, W, device):
-        """(gather, fold) index tables for an HxW board, cached per (H, W, device).
-
-        gather[(ci,p),(co,q)] : flat index into cat([weight.flatten(), 0])
-        fold[w, j]            : the j-th W_board entry that weight element w feeds
-                                (padded with the index of an appended zero)
-        """
-        key = (H, W, device)
-        cache = self.__dict__.setdefault('_board_cache', {})
-        if key not in cache:
-            Cout, Cin, kh, kw = self.weight.shape
-            ph, pw = self.padding
-            HW = H * W
-            nw = Cout * Cin * kh * kw
-            gather = torch.full((Cin, HW, Cout, HW), nw, dtype=torch.long)
-            co = torch.arange(Cout).view(1, Cout)
-            ci = torch.arange(Cin).view(Cin, 1)
-            for q in range(HW):
-                qy, qx = divmod(q, W)
-                for dy in range(kh):
-                    for dx in range(kw):
-                        py, px = qy + dy - ph, qx + dx - pw
-                        if 0 <= py < H and 0 <= px < W:
-                            gather[:, py * W + px, :, q] = ((co * Cin + ci) * kh + dy) * kw + dx
-            gather = gather.view(-1)
-            # invert: every weight element appears once per valid (p, q) pair of its tap
-            order = torch.argsort(gather, stable=True)
-            counts = torch.bincount(gather, minlength=nw + 1)[:nw]
-            width = int(counts.max().item()) if nw else 0
-            fold = torch.full((nw, max(width, 1)), gather.numel(), dtype=torch.long)
-            starts = torch.cumsum(counts, 0) - counts
-            for w in range(nw):
-                c = int(counts[w])
-                fold[w, :c] = order[starts[w]:starts[w] + c]
-            cache[key] = (gather.view(Cin * HW, Cout * HW).to(device), fold.to(device))
-        return cache[key]
-
     def forward(self, x):
         if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
                 and x.shape[2] * x.shape[3] <= BOARD_MAX_CELLS):
             return super().forward(x)
         N, Cin, H, W = x.shape
-        gather, fold = self._board_tables(H, W, x.device)
-        w_board = _BoardWeight.apply(self.weight, gather, fold)   # (Cin*HW, Cout*HW)
-        x2 = x.reshape(N, Cin * H * W)
-        bias = self.bias.repeat_interleave(H * W) if self.bias is not None else None
-        return _RowMatmul.apply(x2, w_board, bias).view(N, self.out_channels, H, W)
+        w_board = _BoardWeight.apply(self.weight, H, W)              # (Cin*HW, Cout*HW)
+        bias = _BoardBias.apply(self.bias, H * W) if self.bias is not None else None
+        return _RowMatmul.apply(x.reshape(N, Cin * H * W), w_board, bias).view(N, self.out_channels, H, W)
 
 
 class _BoardWeight(torch.autograd.Function):
-    """W -> W_board by a fixed gather; backward folds dW_board onto W by a fixed
-    gather-and-sum (deterministic, no atomics or sort)."""
+    """W -> W_board (csrc/hrl_board.hip); backward folds dW_board onto W (deterministic)."""
 
     @staticmethod
-    def forward(ctx, weight, gather, fold):
-        ctx.save_for_backward(fold)
-        ctx.wshape = weight.shape
-        wz = torch.cat([weight.reshape(-1), weight.new_zeros(1)])
-        return wz[gather]
+    def forward(ctx, weight, H, W):
+        Cout, Cin, kh, kw = weight.shape
+        w = weight.contiguous()
+        out = torch.empty(Cin * H * W, Cout * H * W, dtype=w.dtype, device=w.device)
+        _native.check(_native.load().hrl_board_weight(_native.ptr(w), Cout, Cin, kh, kw, H, W, _native.ptr(out),
+                                                       _native.stream_of(w.device)), 'hrl_board_weight')
+        ctx.geom = (Cout, Cin, kh, kw, H, W)
+        return out
 
     @staticmethod
     def backward(ctx, grad):
-        (fold,) = ctx.saved_tensors
-        gz = torch.cat([grad.reshape(-1), grad.new_zeros(1)])
-        return gz[fold].sum(1).view(ctx.wshape), None, None
+        Cout, Cin, kh, kw, H, W = ctx.geom
+        g = grad.contiguous()
+        out = torch.empty(Cout, Cin, kh, kw, dtype=g.dtype, device=g.device)
+        _native.check(_native.load().hrl_board_fold(_native.ptr(g), Cout, Cin, kh, kw, H, W, _native.ptr(out),
+                                                     _native.stream_of(g.device)), 'hrl_board_fold')
+        return out, None, None
+
+
+class _BoardBias(torch.autograd.Function):
+    """b -> b_board[co*HW + q] = b[co]; backward sums over the board cells."""
+
+    @staticmethod
+    def forward(ctx, bias, HW):
+        out = torch.empty(bias.shape[0] * HW, dtype=bias.dtype, device=bias.device)
+        _native.check(_native.load().hrl_board_bias(_native.ptr(bias.contiguous()), bias.shape[0], HW,
+                                                     _native.ptr(out), _native.stream_of(bias.device)), 'hrl_board_bias')
+        ctx.shape = (bias.shape[0], HW)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        Cout, HW = ctx.shape
+        g = grad.contiguous()
+        out = torch.empty(Cout, dtype=g.dtype, device=g.device)
+        _native.check(_native.load().hrl_board_bias_fold(_native.ptr(g), Cout, HW, _native.ptr(out),
+                                                          _native.stream_of(g.device)), 'hrl_board_bias_fold')
+        return out, None
 
 
 def _board_conv_ok(m):
@@ -276,11 +265,45 @@ def accelerate(model):
     return model
 
 
+class _MultiBoardConv(nn.Module):
+    """Sibling BoardConv2d layers reading the same activation, as ONE GEMM.
+
+    The env nets' heads (tictactoe.py:35-49, e.g. head_p / head_v) each start
+    with a 1x1 conv of the same body output; concatenating their board
+    matrices reads the activation once and, in backward, produces the summed
+    input gradient in one GEMM instead of two GEMMs and an add.  The convs are
+    referenced, not registered, so parameters and state_dict are unchanged.
+    """
+
+    def __init__(self, convs):
+        super().__init__()
+        object.__setattr__(self, 'convs', list(convs))
+
+    def forward(self, x):
+        convs = self.convs
+        if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
+                and x.shape[2] * x.shape[3] <= BOARD_MAX_CELLS):
+            return tuple(c(x) for c in convs)
+        N, Cin, H, W = x.shape
+        HW = H * W
+        wb = torch.cat([_BoardWeight.apply(c.weight, H, W) for c in convs], dim=1)
+        parts = [_BoardBias.apply(c.bias, HW) if c.bias is not None else c.weight.new_zeros(c.out_channels * HW)
+                 for c in convs]
+        y = _RowMatmul.apply(x.reshape(N, Cin * HW), wb, torch.cat(parts))
+        outs, off = [], 0
+        for c in convs:
+            n = c.out_channels * HW
+            outs.append(y[:, off:off + n].reshape(N, c.out_channels, H, W))
+            off += n
+        return tuple(outs)
+
+
 class _LeafTracer(torch.fx.Tracer):
     """Trace the env net, keeping the HIP-backed modules as opaque calls."""
 
     def is_leaf_module(self, m, qualname):
-        return isinstance(m, (BatchNorm2d, BoardConv2d, Linear)) or super().is_leaf_module(m, qualname)
+        return isinstance(m, (BatchNorm2d, BoardConv2d, Linear, _MultiBoardConv)) or \
+            super().is_leaf_module(m, qualname)
 
 
 def _is_relu(gm, node):
@@ -294,13 +317,15 @@ def _is_relu(gm, node):
 
 
 def fuse_bn_relu(model, example=None):
-    """Fold every BatchNorm2d -> ReLU pair of ``model.forward`` into the BatchNorm (torch.fx).
+    """Rewrite ``model.forward`` with torch.fx: every BatchNorm2d -> ReLU pair is
+    folded into the BatchNorm, and sibling BoardConv2d layers reading the same
+    activation become one _MultiBoardConv GEMM.
 
     The model keeps its class, parameters and state_dict; only its forward is
     replaced by the rewritten graph.  Recurrent nets (``init_hidden``) and nets
     that do not trace are left as they are.  With ``example`` (an observation
     batch), the rewritten forward is checked against the original (eval mode)
-    and dropped on any mismatch.  Returns the number of fused pairs.
+    and dropped on any mismatch.  Returns the number of rewrites.
     """
     if hasattr(model, 'init_hidden') or 'forward' in model.__dict__:
         return 0
@@ -315,11 +340,29 @@ def fuse_bn_relu(model, example=None):
             users = list(node.users)
             if len(users) == 1 and _is_relu(gm, users[0]) and users[0].args[0] is node:
                 pairs.append((node, users[0]))
-    if not pairs:
-        return 0
     for bn_node, relu_node in pairs:
         relu_node.replace_all_uses_with(bn_node)
         gm.graph.erase_node(relu_node)
+    merged = 0
+    for node in list(gm.graph.nodes):
+        sibs = [u for u in node.users if u.op == 'call_module' and type(gm.get_submodule(u.target)) is BoardConv2d
+                and u.args == (node,) and not u.kwargs]
+        if len(sibs) < 2:
+            continue
+        name = '_hrl_multiconv%d' % merged
+        gm.add_submodule(name, _MultiBoardConv([gm.get_submodule(u.target) for u in sibs]))
+        with gm.graph.inserting_after(node):
+            multi = gm.graph.call_module(name, (node,))
+        anchor = multi
+        for i, u in enumerate(sibs):
+            with gm.graph.inserting_after(anchor):
+                item = gm.graph.call_function(operator.getitem, (multi, i))
+            u.replace_all_uses_with(item)
+            gm.graph.erase_node(u)
+            anchor = item
+        merged += 1
+    if not pairs and not merged:
+        return 0
     gm.graph.lint()
     gm.recompile()
     bns = [gm.get_submodule(n.target) for n, _ in pairs]
@@ -341,7 +384,7 @@ def fuse_bn_relu(model, example=None):
     for bn in bns:
         bn.fused_relu = True
     model.forward = gm.forward
-    return len(pairs)
+    return len(pairs) + merged
 
 
 def unfuse(model):

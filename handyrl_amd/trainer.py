@@ -53,11 +53,14 @@ class LearnerStep:
             self.reducer = hdist.GradAllReduce(self.grads, group=reduce_group, bucket_bytes=bucket_bytes)
         if lr is None:
             lr = DEFAULT_LR * args['batch_size'] * args['forward_steps']
+        # one fused multi-tensor Adam kernel on the GPU (train.py:322: Adam, weight_decay 1e-5)
+        fused = device.type == 'cuda'
         if self.graph:
             self.optimizer = torch.optim.Adam(self.params, lr=torch.tensor(lr, device=device),
-                                              weight_decay=1e-5, capturable=True, foreach=True)
+                                              weight_decay=1e-5, capturable=True, fused=True)
         else:
-            self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=1e-5, foreach=True)
+            self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=1e-5, fused=fused,
+                                              foreach=None if fused else True)
         self._graph = None
         self._static = None
         self._static_out = None

@@ -52,6 +52,21 @@ int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64
                     int relu, float *dx, float *dweight, float *dbias,
                     void *workspace, int64_t workspace_bytes, void *stream);
 
+/*
+ * Tiny-board convolution as one dense matrix (handyrl_amd/nn.py BoardConv2d):
+ * W_board[(ci*H*W + p), (co*H*W + q)] = W[co, ci, dy, dx] where input cell p
+ * is output cell q shifted by (dy - kh/2, dx - kw/2), zero off the board.
+ * hrl_board_weight builds W_board (Cin*HW x Cout*HW); hrl_board_fold sums a
+ * W_board-shaped gradient back onto W (deterministic, one thread per weight).
+ * hrl_board_bias / hrl_board_bias_fold do the same for the bias: b_board[co*HW+q] = b[co].
+ */
+int hrl_board_weight(const float *w, int64_t Cout, int64_t Cin, int64_t kh, int64_t kw, int64_t H, int64_t W,
+                     float *w_board, void *stream);
+int hrl_board_fold(const float *g_board, int64_t Cout, int64_t Cin, int64_t kh, int64_t kw, int64_t H, int64_t W,
+                   float *g_w, void *stream);
+int hrl_board_bias(const float *b, int64_t Cout, int64_t HW, float *b_board, void *stream);
+int hrl_board_bias_fold(const float *g_board, int64_t Cout, int64_t HW, float *g_b, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

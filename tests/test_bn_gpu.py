@@ -186,6 +186,6 @@ def test_fx_fusion_in_learner(cuda):
     keys = list(net.state_dict())
     step = LearnerStep(net, default_args(9, 64), cuda)
     step.step(tictactoe_batch(64, 9, cuda, seed=0))
-    assert step.fused_pairs == 3
+    assert step.fused_pairs == 4   # three BN->ReLU folds + the two head convs merged
     assert all(m.fused_relu for m in net.modules() if isinstance(m, BatchNorm2d))
     assert list(net.state_dict()) == keys
