@@ -57,6 +57,11 @@ SIGNATURES = {
     'hrl_board_fold': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _i64, _i64, _i64, _f32p, ctypes.c_void_p]),
     'hrl_board_bias': (ctypes.c_int, [_f32p, _i64, _i64, _f32p, ctypes.c_void_p]),
     'hrl_board_bias_fold': (ctypes.c_int, [_f32p, _i64, _i64, _f32p, ctypes.c_void_p]),
+    'hrl_conv3x3_workspace_bytes': (ctypes.c_int64, [_i64]),
+    'hrl_conv3x3_forward': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _f32p, _f32p, ctypes.c_int, _f32p,
+                                           ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_conv3x3_wgrad': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, _f32p, ctypes.c_void_p, _i64,
+                                         ctypes.c_void_p]),
 }
 
 ABI_VERSION = 2

@@ -1,0 +1,361 @@
+// hrl_conv.hip — 3x3 'same' convolution on a 3x3 board with fp32 MFMA (gfx950).
+//
+// The TicTacToe body (tictactoe.py:52-69) is three 32->32 3x3 convs on a 3x3
+// board over N = B*T*P samples.  As a dense matrix the layer is the GEMM
+// Y[N, 288] = X[N, 288] @ W_board[288, 288], but only 49 of the 81
+// (input cell p, output cell q) 32x32 blocks of W_board are real taps: the
+// others fall off the board.  These kernels skip them:
+//
+//   out[n, co, q] = sum_{p in nbhd(q)} sum_ci in[n, ci, p] * W[co, ci, tap(p, q)]
+//
+// with v_mfma_f32_16x16x4_f32 (exact fp32 products, k-ordered accumulation).
+//
+// conv3x3_kernel (forward; also the input gradient, run on dY with the
+// kernel flipped and transposed — a 'same' conv's adjoint):
+//   * a workgroup = 4 waves; each wave owns a 16-row tile of the (N, C*9)
+//     NCHW rows per iteration and walks row tiles grid-stride;
+//   * the packed weights [tap][co-tile][ci][16] (36 KB) are staged in LDS once
+//     per workgroup; the B fragment of lane l (k = l>>4, j = l&15) is then a
+//     bank-conflict-free ds_read_b32;
+//   * each wave's A tile is 16 rows x 288 floats in LDS with a row stride of
+//     290 (== 2 mod 32), conflict-free for the A fragment reads;
+//   * the next row tile's global loads are issued before the MFMA loop and
+//     land in registers while the MFMAs run;
+//   * 9 output cells x 2 column tiles = 18 accumulators (72 AGPRs); the
+//     epilogue stages the 16x288 output tile through the A buffer and leaves
+//     with coalesced 16-byte stores.
+// conv3x3_wgrad_kernel (weight gradient): dW[tap][ci][co] accumulates
+//   X^T dY over (row, (p,q) pairs with that tap) per wave (36 accumulators);
+//   the 4 waves fold through LDS, and a wide reduce folds the per-workgroup
+//   partials, both in a fixed order (deterministic).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hrl_nn.h"
+#include "../../include/hrl_targets.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBoard = 3;                 // 3x3 board
+constexpr int kCells = kBoard * kBoard;   // 9
+constexpr int kTaps = 9;                  // 3x3 kernel
+constexpr int kC = 32;                    // channels (in and out) per launch
+constexpr int kRow = kC * kCells;         // 288 floats per sample
+constexpr int kStride = kRow + 2;         // LDS row stride, == 2 (mod 32)
+constexpr int kTile = 16;                 // rows per wave tile
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kVec = kTile * kRow / 4 / 64;   // float4 per lane per tile (18)
+
+// tap index of input cell p feeding output cell q (dy, dx in 0..2), or -1
+__host__ __device__ constexpr int tap_of(int p, int q) {
+    const int dy = p / kBoard - q / kBoard + 1;
+    const int dx = p % kBoard - q % kBoard + 1;
+    return (dy < 0 || dy > 2 || dx < 0 || dx > 2) ? -1 : dy * 3 + dx;
+}
+
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------ forward / input gradient
+// x: (M, 288) rows; wpk: packed [tap][ct][ci][16] = W'[tap][ci][ct*16+j]; y: (M, 288)
+__global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restrict__ x, int64_t M,
+                                                           const float *__restrict__ wpk,
+                                                           const float *__restrict__ bias,
+                                                           float *__restrict__ y) {
+    __shared__ float w_lds[kTaps * 2 * kC * 16];           // 36 KB
+    __shared__ float a_lds[kWaves][kTile * kStride];       // 4 x 18.1 KB
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < kTaps * 2 * kC * 16; i += kThreads) w_lds[i] = wpk[i];
+
+    const int64_t ntiles = (M + kTile - 1) / kTile;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
+    float *as = a_lds[wave];
+
+    // per-lane column/bias for the epilogue: lane owns output column j = lane&15 of each tile
+    float bias_v[2] = {0.f, 0.f};
+    if (bias) {
+        bias_v[0] = bias[lane & 15];
+        bias_v[1] = bias[16 + (lane & 15)];
+    }
+
+    float4 stage[kVec];
+    auto issue = [&](int64_t t) {
+        // rows t*16 .. t*16+15 are contiguous: 16*288 floats = 1152 float4
+        const int64_t base = t * kTile * kRow;
+        const int64_t lim = M * kRow;
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int64_t e = base + (int64_t)(k * 64 + lane) * 4;
+            const int64_t ec = e < lim ? e : lim - 4;          // clamp (ragged last tile), no branch
+            stage[k] = *reinterpret_cast<const float4 *>(x + ec);
+        }
+    };
+    if (tile < ntiles) issue(tile);
+    __syncthreads();   // weights in LDS
+
+    for (; tile < ntiles; tile += stride) {
+        // staged tile -> LDS (padded rows)
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int e = (k * 64 + lane) * 4;                 // element within the tile
+            const int r = e / kRow, c = e - r * kRow;          // kRow % 4 == 0: one row per float4
+            float *d = as + r * kStride + c;
+            d[0] = stage[k].x; d[1] = stage[k].y; d[2] = stage[k].z; d[3] = stage[k].w;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes done
+        __builtin_amdgcn_wave_barrier();
+        const int64_t next = tile + stride;
+        if (next < ntiles) issue(next);       // in flight during the MFMAs
+
+        f32x4 acc[kCells][2];
+#pragma unroll
+        for (int q = 0; q < kCells; ++q) acc[q][0] = acc[q][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        const int ar = lane & 15;          // A row (sample within the tile)
+        const int ak = lane >> 4;          // A/B k within the 4-wide step
+        const float *arow = as + ar * kStride;
+#pragma unroll
+        for (int q = 0; q < kCells; ++q) {
+#pragma unroll
+            for (int p = 0; p < kCells; ++p) {
+                const int tap = tap_of(p, q);
+                if (tap < 0) continue;
+                const float *wt0 = w_lds + ((tap * 2 + 0) * kC) * 16 + ak * 16 + (lane & 15);
+                const float *wt1 = w_lds + ((tap * 2 + 1) * kC) * 16 + ak * 16 + (lane & 15);
+#pragma unroll
+                for (int s = 0; s < kC / 4; ++s) {
+                    const float a = arow[(4 * s + ak) * kCells + p];
+                    acc[q][0] = mfma(a, wt0[s * 64], acc[q][0]);
+                    acc[q][1] = mfma(a, wt1[s * 64], acc[q][1]);
+                }
+            }
+        }
+
+        // epilogue: accumulators -> LDS tile [row][co*9 + q] -> coalesced stores
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < kCells; ++q)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = (lane >> 4) * 4 + r;       // C/D: row = (lane>>4)*4 + reg
+                    const int co = ct * 16 + (lane & 15);      //      col = lane & 15
+                    as[row * kStride + co * kCells + q] = acc[q][ct][r] + bias_v[ct];
+                }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int64_t obase = tile * kTile * kRow;
+        const int64_t lim = M * kRow;
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int e = (k * 64 + lane) * 4;
+            const int r = e / kRow, c = e - r * kRow;
+            const float *sp = as + r * kStride + c;
+            if (obase + e < lim) *reinterpret_cast<float4 *>(y + obase + e) = make_float4(sp[0], sp[1], sp[2], sp[3]);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ------------------------------------------------------------------ weight gradient
+// dW[tap][ci][co] = sum_rows sum_{(p,q): tap(p,q) = tap} x[row, ci, p] * dy[row, co, q]
+// MFMA C tile = 16 ci x 16 co; A[i = ci][k = row], B[k = row][j = co]
+__global__ __launch_bounds__(kThreads) void conv3x3_wgrad_kernel(const float *__restrict__ x,
+                                                                 const float *__restrict__ dy, int64_t M,
+                                                                 float *__restrict__ partial) {
+    // one LDS array: per-wave x and dy tiles during the loop, the 4 wave partials after it
+    __shared__ float lds[2 * kWaves * kTile * kStride];    // 148 KB >= 4 x 9216 floats
+    static_assert(2 * kWaves * kTile * kStride >= kWaves * kTaps * kC * kC, "fold buffer");
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    float *xs = lds + wave * kTile * kStride;
+    float *gs = lds + (kWaves + wave) * kTile * kStride;
+    const int64_t ntiles = (M + kTile - 1) / kTile;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+
+    f32x4 acc[kTaps][2][2];
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < ntiles; tile += stride) {
+        const int64_t base = tile * kTile * kRow;
+        const int64_t lim = M * kRow;
+        float4 sx[kVec], sg[kVec];
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int64_t e = base + (int64_t)(k * 64 + lane) * 4;
+            const bool ok = e < lim;
+            const int64_t ec = ok ? e : lim - 4;
+            sx[k] = *reinterpret_cast<const float4 *>(x + ec);
+            sg[k] = *reinterpret_cast<const float4 *>(dy + ec);
+            if (!ok) sg[k] = make_float4(0.f, 0.f, 0.f, 0.f);   // ragged tile: zero gradient rows
+        }
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int e = (k * 64 + lane) * 4;
+            const int r = e / kRow, c = e - r * kRow;
+            float *d = xs + r * kStride + c;
+            d[0] = sx[k].x; d[1] = sx[k].y; d[2] = sx[k].z; d[3] = sx[k].w;
+            float *h = gs + r * kStride + c;
+            h[0] = sg[k].x; h[1] = sg[k].y; h[2] = sg[k].z; h[3] = sg[k].w;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int i16 = lane & 15;   // A row = ci within the tile / B col = co within the tile
+        const int kk = lane >> 4;    // k = row within the 4-row step
+#pragma unroll
+        for (int q = 0; q < kCells; ++q) {
+#pragma unroll
+            for (int p = 0; p < kCells; ++p) {
+                const int tap = tap_of(p, q);
+                if (tap < 0) continue;
+#pragma unroll
+                for (int s = 0; s < kTile / 4; ++s) {
+                    const int row = 4 * s + kk;
+                    const float a0 = xs[row * kStride + (0 * 16 + i16) * kCells + p];
+                    const float a1 = xs[row * kStride + (1 * 16 + i16) * kCells + p];
+                    const float b0 = gs[row * kStride + (0 * 16 + i16) * kCells + q];
+                    const float b1 = gs[row * kStride + (1 * 16 + i16) * kCells + q];
+                    acc[tap][0][0] = mfma(a0, b0, acc[tap][0][0]);
+                    acc[tap][0][1] = mfma(a0, b1, acc[tap][0][1]);
+                    acc[tap][1][0] = mfma(a1, b0, acc[tap][1][0]);
+                    acc[tap][1][1] = mfma(a1, b1, acc[tap][1][1]);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    // fold the block's 4 wave partials in a fixed order through the (now free) tile LDS,
+    // then write one partial per workgroup: partial[block][tap][ci][co]
+    __syncthreads();
+    float *red = lds;
+    constexpr int kW = kTaps * kC * kC;
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int ci = it * 16 + (lane >> 4) * 4 + r;
+                    const int co = jt * 16 + (lane & 15);
+                    red[wave * kW + (t * kC + ci) * kC + co] = acc[t][it][jt][r];
+                }
+    __syncthreads();
+    float *out = partial + (int64_t)blockIdx.x * kW;
+    for (int i = threadIdx.x; i < kW; i += kThreads)
+        out[i] = ((red[i] + red[kW + i]) + red[2 * kW + i]) + red[3 * kW + i];
+}
+
+// fold per-workgroup partials into dW[co][ci][3][3]: a workgroup owns 64 consecutive
+// outputs; its 4 waves take every 4th partial (4 independent sums in flight per
+// thread) and combine in a fixed order -> deterministic.
+__global__ __launch_bounds__(256) void conv3x3_wgrad_reduce_kernel(const float *__restrict__ partial, int nparts,
+                                                                   float *__restrict__ dw) {
+    __shared__ float red[4][64];
+    constexpr int kW = kTaps * kC * kC;
+    const int col = threadIdx.x & 63, sub = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + col;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int w = sub;
+    for (; w + 12 < nparts; w += 16) {
+        s0 += partial[(int64_t)w * kW + i];
+        s1 += partial[(int64_t)(w + 4) * kW + i];
+        s2 += partial[(int64_t)(w + 8) * kW + i];
+        s3 += partial[(int64_t)(w + 12) * kW + i];
+    }
+    for (; w < nparts; w += 4) s0 += partial[(int64_t)w * kW + i];
+    red[sub][col] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (sub == 0) {
+        const float s = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
+        const int co = i % kC, ci = (i / kC) % kC, tap = i / (kC * kC);
+        dw[(co * kC + ci) * kTaps + tap] = s;
+    }
+}
+
+// W[co][ci][tap] -> packed [tap][ct][ci'][16] for the conv kernel.
+// flip = 0: forward (ci' = ci, output co);  flip = 1: input gradient (ci' = co, output ci, tap mirrored)
+__global__ void conv3x3_pack_kernel(const float *__restrict__ w, int flip, float *__restrict__ wpk) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // packed index
+    if (i >= kTaps * 2 * kC * 16) return;
+    const int j = i % 16, k = (i / 16) % kC, ct = (i / (16 * kC)) % 2, tap = i / (16 * kC * 2);
+    const int out_c = ct * 16 + j;   // output channel of this conv
+    const int in_c = k;              // input channel of this conv (the MFMA k)
+    float v;
+    if (!flip) v = w[(out_c * kC + in_c) * kTaps + tap];
+    else v = w[(in_c * kC + out_c) * kTaps + (kTaps - 1 - tap)];
+    wpk[i] = v;
+}
+
+// One 4-wave workgroup per CU (LDS: 111 KB forward, 148 KB weight gradient);
+// the waves walk row tiles grid-stride so the next tile's loads overlap MFMAs.
+constexpr int kGrid = 256;
+
+int status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
+}
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int grid_for(int64_t M) {
+    const int64_t tiles = (M + kTile - 1) / kTile;
+    const int64_t blocks = (tiles + kWaves - 1) / kWaves;
+    return (int)(blocks < kGrid ? blocks : kGrid);
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t hrl_conv3x3_workspace_bytes(int64_t M) {
+    if (M < 1) return -1;
+    return (int64_t)grid_for(M) * kTaps * kC * kC * 4 + (int64_t)kTaps * 2 * kC * 16 * 4 * 2;
+}
+
+int hrl_conv3x3_forward(const float *x, int64_t M, int64_t C_in, int64_t C_out, const float *weight,
+                        const float *bias, int flip, float *y, void *workspace, int64_t workspace_bytes,
+                        void *stream) {
+    if (C_in != kC || C_out != kC || M < 1 || !x || !weight || !y || !workspace) return HRL_EINVAL;
+    if (!aligned16(x) || !aligned16(y) || workspace_bytes < hrl_conv3x3_workspace_bytes(M)) return HRL_EINVAL;
+    if (flip && bias) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    float *wpk = static_cast<float *>(workspace);
+    hipLaunchKernelGGL(conv3x3_pack_kernel, dim3((kTaps * 2 * kC * 16 + 255) / 256), dim3(256), 0, s, weight, flip,
+                       wpk);
+    int rc = status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(conv3x3_kernel, dim3(grid_for(M)), dim3(kThreads), 0, s, x, M, wpk, bias, y);
+    return status();
+}
+
+int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, int64_t C_out, float *dweight,
+                      void *workspace, int64_t workspace_bytes, void *stream) {
+    if (C_in != kC || C_out != kC || M < 1 || !x || !dy || !dweight || !workspace) return HRL_EINVAL;
+    if (!aligned16(x) || !aligned16(dy) || workspace_bytes < hrl_conv3x3_workspace_bytes(M)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int grid = grid_for(M);
+    float *partial = static_cast<float *>(workspace) + kTaps * 2 * kC * 16 * 2;
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(grid), dim3(kThreads), 0, s, x, dy, M, partial);
+    int rc = status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, partial, grid,
+                       dweight);
+    return status();
+}
+
+}  // extern "C"

@@ -143,9 +143,61 @@ class BoardConv2d(nn.Conv2d):
                 and x.shape[2] * x.shape[3] <= BOARD_MAX_CELLS):
             return super().forward(x)
         N, Cin, H, W = x.shape
+        if (H, W) == (3, 3) and self.kernel_size == (3, 3) and Cin == 32 and self.out_channels == 32 and N > 0:
+            return _Conv3x3.apply(x.contiguous(), self.weight, self.bias)   # block-sparse MFMA kernels
         w_board = _BoardWeight.apply(self.weight, H, W)              # (Cin*HW, Cout*HW)
         bias = _BoardBias.apply(self.bias, H * W) if self.bias is not None else None
-        return _RowMatmul.apply(x.reshape(N, Cin * H * W), w_board, bias).view(N, self.out_channels, H, W)
+        x2 = x.reshape(N, Cin * H * W)
+        if bias is not None and Cin * H * W < 64:
+            # narrow input (the stem: 3 planes x 9 cells): carry the bias as an extra all-ones
+            # input column, so its gradient comes out of the weight-gradient GEMM instead of a
+            # separate column reduction over all N rows
+            x2 = torch.cat([x2, x2.new_ones(N, 1)], dim=1)
+            w_board = torch.cat([w_board, bias.view(1, -1)], dim=0)
+            bias = None
+        return _RowMatmul.apply(x2, w_board, bias).view(N, self.out_channels, H, W)
+
+
+class _Conv3x3(torch.autograd.Function):
+    """32->32 3x3 conv on a 3x3 board: csrc/hrl_conv.hip (fp32 MFMA, off-board taps skipped)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        N = x.shape[0]
+        lib = _native.load()
+        ws_bytes = lib.hrl_conv3x3_workspace_bytes(N)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+        y = torch.empty_like(x)
+        w = weight.contiguous()
+        _native.check(lib.hrl_conv3x3_forward(_native.ptr(x), N, 32, 32, _native.ptr(w), _native.ptr(bias), 0,
+                                              _native.ptr(y), _native.ptr(ws), ws_bytes,
+                                              _native.stream_of(x.device)), 'hrl_conv3x3_forward')
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        N = x.shape[0]
+        lib = _native.load()
+        ws_bytes = lib.hrl_conv3x3_workspace_bytes(N)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+        stream = _native.stream_of(x.device)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _native.check(lib.hrl_conv3x3_forward(_native.ptr(dy), N, 32, 32, _native.ptr(w), None, 1,
+                                                  _native.ptr(dx), _native.ptr(ws), ws_bytes, stream),
+                          'hrl_conv3x3_forward(flip)')
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w)
+            _native.check(lib.hrl_conv3x3_wgrad(_native.ptr(x), _native.ptr(dy), N, 32, 32, _native.ptr(dw),
+                                                _native.ptr(ws), ws_bytes, stream), 'hrl_conv3x3_wgrad')
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum((0, 2, 3))
+        return dx, dw, db
 
 
 class _BoardWeight(torch.autograd.Function):

@@ -67,6 +67,22 @@ int hrl_board_fold(const float *g_board, int64_t Cout, int64_t Cin, int64_t kh, 
 int hrl_board_bias(const float *b, int64_t Cout, int64_t HW, float *b_board, void *stream);
 int hrl_board_bias_fold(const float *g_board, int64_t Cout, int64_t HW, float *g_b, void *stream);
 
+/*
+ * 3x3 'same' convolution of 32 -> 32 channels on a 3x3 board (TicTacToe body,
+ * tictactoe.py:57-58) with fp32 MFMA, skipping the off-board taps
+ * (csrc/hrl_conv.hip).  x, y: (M, 32*9) NCHW rows; weight (32, 32, 3, 3).
+ * flip = 0: y = conv(x, W) + bias.  flip = 1: y = conv^T(x, W), the input
+ * gradient of the forward (bias must be NULL).
+ * hrl_conv3x3_wgrad: dweight (32, 32, 3, 3) = d conv / dW for input x and output gradient dy.
+ * workspace: hrl_conv3x3_workspace_bytes(M) bytes.
+ */
+int64_t hrl_conv3x3_workspace_bytes(int64_t M);
+int hrl_conv3x3_forward(const float *x, int64_t M, int64_t C_in, int64_t C_out, const float *weight,
+                        const float *bias, int flip, float *y, void *workspace, int64_t workspace_bytes,
+                        void *stream);
+int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, int64_t C_out, float *dweight,
+                      void *workspace, int64_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -189,3 +189,28 @@ def test_fx_fusion_in_learner(cuda):
     assert step.fused_pairs == 4   # three BN->ReLU folds + the two head convs merged
     assert all(m.fused_relu for m in net.modules() if isinstance(m, BatchNorm2d))
     assert list(net.state_dict()) == keys
+
+
+@pytest.mark.parametrize('N', [1, 15, 16, 17, 1000, 4099])
+@pytest.mark.parametrize('bias', [False, True])
+def test_conv3x3_mfma_matches_torch_cpu(cuda, N, bias):
+    """csrc/hrl_conv.hip (block-sparse fp32 MFMA): forward, input and weight gradients."""
+    from handyrl_amd.nn import BoardConv2d
+    torch.manual_seed(N)
+    ref = nn.Conv2d(32, 32, 3, padding=1, bias=bias)
+    hip = BoardConv2d(32, 32, 3, padding=1, bias=bias)
+    hip.load_state_dict(ref.state_dict())
+    hip = hip.to(cuda)
+    x = torch.randn(N, 32, 3, 3)
+    dy = torch.randn(N, 32, 3, 3)
+    xr, xh = x.clone().requires_grad_(True), x.to(cuda).requires_grad_(True)
+    yr, yh = ref(xr), hip(xh)
+    np.testing.assert_allclose(yh.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-5, atol=2e-5)
+    yr.backward(dy)
+    yh.backward(dy.to(cuda))
+    np.testing.assert_allclose(xh.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-5, atol=2e-5)
+    scale = max(1.0, float(ref.weight.grad.abs().max()))
+    np.testing.assert_allclose(hip.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-4, atol=1e-5 * scale)
+    if bias:   # sums of 9N terms: tolerance relative to the largest channel sum
+        bscale = max(1.0, float(ref.bias.grad.abs().max()))
+        np.testing.assert_allclose(hip.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-4, atol=1e-5 * bscale)
