@@ -69,6 +69,36 @@ __global__ void board_bias_fold_kernel(const float *__restrict__ gb, int Cout, i
     g[co] = s;
 }
 
+// ---- column sums of a row-major (M, N) matrix (bias gradients over M = B*T*P rows) ----
+// stage 1: workgroup g folds rows [g*rpb, (g+1)*rpb) per column; each thread owns one
+// column (N <= 256: 256/N rows at a time) and accumulates in fp64.
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float *__restrict__ x, int64_t M, int N,
+                                                             int64_t rows_per_block, double *__restrict__ part) {
+    __shared__ double red[256];
+    const int per = 256 / N;                  // rows handled side by side
+    const int c = threadIdx.x % N, ro = threadIdx.x / N;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(M, r0 + rows_per_block);
+    double s = 0.0;
+    if (ro < per)
+        for (int64_t r = r0 + ro; r < r1; r += per) s += (double)x[r * N + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x < N) {
+        double t = 0.0;
+        for (int k = 0; k < per; ++k) t += red[k * N + threadIdx.x];
+        part[(int64_t)blockIdx.x * N + threadIdx.x] = t;
+    }
+}
+
+__global__ void colsum_final_kernel(const double *__restrict__ part, int nblocks, int N, float *__restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= N) return;
+    double t = 0.0;
+    for (int b = 0; b < nblocks; ++b) t += part[(int64_t)b * N + c];
+    out[c] = (float)t;
+}
+
 bool geo(int64_t Cout, int64_t Cin, int64_t kh, int64_t kw, int64_t H, int64_t W, BoardGeo &g) {
     if (Cout < 1 || Cin < 1 || kh < 1 || kw < 1 || H < 1 || W < 1 || kh % 2 == 0 || kw % 2 == 0) return false;
     if (H * W > 64 || Cout * H * W > 65536 || Cin * H * W > 65536) return false;
@@ -119,6 +149,29 @@ int hrl_board_bias_fold(const float *g_board, int64_t Cout, int64_t HW, float *g
     if (!g_board || !g_b || Cout < 1 || HW < 1 || Cout * HW > 65536) return HRL_EINVAL;
     hipLaunchKernelGGL(board_bias_fold_kernel, dim3((int)((Cout + 63) / 64)), dim3(64), 0,
                        static_cast<hipStream_t>(stream), g_board, (int)Cout, (int)HW, g_b);
+    return status();
+}
+
+int64_t hrl_colsum_workspace_bytes(int64_t M, int64_t N) {
+    if (M < 1 || N < 1 || N > 256) return -1;
+    return 1024 * N * 8;
+}
+
+int hrl_colsum(const float *x, int64_t M, int64_t N, float *out, void *workspace, int64_t workspace_bytes,
+               void *stream) {
+    if (!x || !out || !workspace || M < 1 || N < 1 || N > 256) return HRL_EINVAL;
+    if (workspace_bytes < hrl_colsum_workspace_bytes(M, N)) return HRL_EINVAL;
+    int64_t nb = (M + 127) / 128;
+    nb = nb > 1024 ? 1024 : nb;
+    const int64_t rpb = (M + nb - 1) / nb;
+    nb = (M + rpb - 1) / rpb;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    double *part = static_cast<double *>(workspace);
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)nb), dim3(256), 0, s, x, M, (int)N, rpb, part);
+    int rc = status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, part, (int)nb, (int)N,
+                       out);
     return status();
 }
 

@@ -108,6 +108,21 @@ def _xt_dy(x, dy):
     return torch.bmm(x.view(S, M // S, K).transpose(1, 2), dy.view(S, M // S, N)).sum(0)
 
 
+def _colsum(dy):
+    """dy.sum(0) for a (M, N) CUDA fp32 matrix: csrc/hrl_board.hip (framework column sums run ~20x slower)."""
+    M, N = dy.shape
+    if not (dy.is_cuda and dy.dtype == torch.float32 and N <= 256 and M >= ROWS_MIN_CHUNKED):
+        return dy.sum(0)
+    dy = dy.contiguous()
+    lib = _native.load()
+    ws_bytes = lib.hrl_colsum_workspace_bytes(M, N)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dy.device)
+    out = torch.empty(N, dtype=dy.dtype, device=dy.device)
+    _native.check(lib.hrl_colsum(_native.ptr(dy), M, N, _native.ptr(out), _native.ptr(ws), ws_bytes,
+                                 _native.stream_of(dy.device)), 'hrl_colsum')
+    return out
+
+
 class _RowMatmul(torch.autograd.Function):
     """y = x @ w (+ bias) over many rows, with the chunked weight-gradient GEMM."""
 
@@ -122,7 +137,7 @@ class _RowMatmul(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dx = dy @ w.t() if ctx.needs_input_grad[0] else None
         dw = _xt_dy(x, dy) if ctx.needs_input_grad[1] else None
-        db = dy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        db = _colsum(dy) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db
 
 

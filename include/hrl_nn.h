@@ -67,6 +67,12 @@ int hrl_board_fold(const float *g_board, int64_t Cout, int64_t Cin, int64_t kh, 
 int hrl_board_bias(const float *b, int64_t Cout, int64_t HW, float *b_board, void *stream);
 int hrl_board_bias_fold(const float *g_board, int64_t Cout, int64_t HW, float *g_b, void *stream);
 
+/* out[c] = sum_r x[r, c] for a row-major (M, N) matrix, N <= 256 (bias gradients over
+ * M = B*T*P rows); fp64 accumulation, fixed-order folds (deterministic). */
+int64_t hrl_colsum_workspace_bytes(int64_t M, int64_t N);
+int hrl_colsum(const float *x, int64_t M, int64_t N, float *out, void *workspace, int64_t workspace_bytes,
+               void *stream);
+
 /*
  * 3x3 'same' convolution of 32 -> 32 channels on a 3x3 board (TicTacToe body,
  * tictactoe.py:57-58) with fp32 MFMA, skipping the off-board taps

@@ -214,3 +214,14 @@ def test_conv3x3_mfma_matches_torch_cpu(cuda, N, bias):
     if bias:   # sums of 9N terms: tolerance relative to the largest channel sum
         bscale = max(1.0, float(ref.bias.grad.abs().max()))
         np.testing.assert_allclose(hip.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-4, atol=1e-5 * bscale)
+
+
+@pytest.mark.parametrize('M,N', [(4096, 27), (131072, 27), (5000, 1), (70001, 256)])
+def test_colsum_matches_fp64(cuda, M, N):
+    from handyrl_amd.nn import _colsum
+    g = torch.Generator(device=cuda).manual_seed(M)
+    x = torch.randn(M, N, device=cuda, generator=g)
+    got = _colsum(x)
+    ref = x.double().sum(0)
+    assert torch.allclose(got.double(), ref, rtol=1e-6, atol=1e-4)
+    assert torch.equal(_colsum(x), got)      # deterministic
