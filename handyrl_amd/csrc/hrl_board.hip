@@ -91,12 +91,20 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float *__rest
     }
 }
 
-__global__ void colsum_final_kernel(const double *__restrict__ part, int nblocks, int N, float *__restrict__ out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= N) return;
+// stage 2: one workgroup per column folds the block partials with a fixed-shape tree
+__global__ __launch_bounds__(256) void colsum_final_kernel(const double *__restrict__ part, int nblocks, int N,
+                                                           float *__restrict__ out) {
+    __shared__ double red[256];
+    const int c = blockIdx.x;
     double t = 0.0;
-    for (int b = 0; b < nblocks; ++b) t += part[(int64_t)b * N + c];
-    out[c] = (float)t;
+    for (int b = threadIdx.x; b < nblocks; b += 256) t += part[(int64_t)b * N + c];
+    red[threadIdx.x] = t;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[c] = (float)red[0];
 }
 
 bool geo(int64_t Cout, int64_t Cin, int64_t kh, int64_t kw, int64_t H, int64_t W, BoardGeo &g) {
@@ -170,8 +178,7 @@ int hrl_colsum(const float *x, int64_t M, int64_t N, float *out, void *workspace
     hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)nb), dim3(256), 0, s, x, M, (int)N, rpb, part);
     int rc = status();
     if (rc) return rc;
-    hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, part, (int)nb, (int)N,
-                       out);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)N), dim3(256), 0, s, part, (int)nb, (int)N, out);
     return status();
 }
 
