@@ -47,6 +47,9 @@ def make_batch_and_args(B=8, T=9):
     return tictactoe_batch(B, T, torch.device('cpu'), seed=42), default_args(T, B)
 
 
+pytestmark = []
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
@@ -118,3 +121,55 @@ def test_bucket_layout_covers_flat_buffer():
         assert p.grad.data_ptr() >= fg.flat.data_ptr()
         assert p.grad.shape == p.shape
     assert fg.flat.numel() == sum(p.numel() for p in net.parameters())
+
+
+def _gpu_rank_main(rank, world, port, out_path, steps):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK='0')
+    from handyrl_amd.trainer import LearnerStep
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    # gloo over device tensors: exercises the product's bucketed hook-launched all-reduce and the HIP
+    # learner step with two ranks on one GPU (RCCL itself needs one GPU per rank)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    batch, args = make_batch_and_args(B=64, T=9)
+    batch = {k: v.to(dev) for k, v in batch.items()}
+    B = batch['value'].size(0)
+    shard = {k: v[rank * B // world:(rank + 1) * B // world].contiguous() for k, v in batch.items()}
+    torch.manual_seed(0)
+    net = SmallNet()
+    step = LearnerStep(net, args, dev, world_size=world, bucket_bytes=1024)
+    for _ in range(steps):
+        step.step(shard)
+    sums, _ = step.pop_stats()
+    flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).cpu()
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    if rank == 0:
+        torch.save({'params': gathered, 'sums': sums}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_gpu_step_matches_full_batch(cuda):
+    from handyrl_amd.trainer import LearnerStep
+    steps = 2
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, 'r0.pt')
+        mp.spawn(_gpu_rank_main, args=(2, _free_port(), out, steps), nprocs=2, join=True)
+        res = torch.load(out, weights_only=True)
+    batch, args = make_batch_and_args(B=64, T=9)
+    batch = {k: v.to(cuda) for k, v in batch.items()}
+    torch.manual_seed(0)
+    net = SmallNet()
+    step = LearnerStep(net, args, cuda)
+    for _ in range(steps):
+        step.step(batch)
+    ref_sums, _ = step.pop_stats()
+    ref = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).cpu()
+    p0, p1 = res['params']
+    assert torch.equal(p0, p1)
+    assert torch.allclose(p0, ref, rtol=1e-5, atol=1e-6), (p0 - ref).abs().max()
+    for k in ('p', 'v', 'ent', 'total', 'dcnt'):
+        assert abs(res['sums'][k] - ref_sums[k]) <= 1e-4 * max(1.0, abs(ref_sums[k])), k
