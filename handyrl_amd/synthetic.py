@@ -70,6 +70,20 @@ def tictactoe_batch(B, T, device, seed=0, obs_shape=(3, 3, 3), A=9, P=2, min_len
     }
 
 
+def geister_batch(B, T, device, seed=0, P=2, min_len=5):
+    """C3 Geister batch: observation {'board': (B,T,1,7,6,6), 'scalar': (B,T,1,18)}, A = 214.
+
+    Same generator as tictactoe_batch (the Bernoulli board planes come from
+    it); the scalar features are Bernoulli(0.5) too, zero on padded steps.
+    """
+    batch = tictactoe_batch(B, T, device, seed=seed, obs_shape=(7, 6, 6), A=214, P=P, min_len=min_len)
+    g = torch.Generator(device=device).manual_seed(seed + 1)
+    valid = batch['episode_mask'].view(B, T, 1, 1)
+    scalar = (torch.rand(B, T, 1, 18, device=device, generator=g) < 0.5).float() * valid
+    batch['observation'] = {'board': batch['observation'], 'scalar': scalar.contiguous()}
+    return batch
+
+
 def default_args(T, batch_size=None):
     """config.yaml train_args for the learner (config.yaml:9-31), TicTacToe-style."""
     return {

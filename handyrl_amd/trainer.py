@@ -29,6 +29,7 @@ import torch.nn as nn
 from . import distributed as hdist
 from .nn import accelerate, fuse_bn_relu
 from .train import forward_prediction, loss_terms
+from .util import bimap_r
 
 DEFAULT_LR = 3e-8  # train.py:318
 
@@ -108,8 +109,11 @@ class LearnerStep:
         if self.graph:
             if self._graph is None:
                 self._capture(batch, hidden)
-            elif batch is not self._static:
-                self.load_batch(batch)
+            else:
+                if batch is not self._static:
+                    self.load_batch(batch)
+                if hidden is not None and hidden is not self._static_hidden:
+                    bimap_r(self._static_hidden, hidden, lambda dst, src: dst.copy_(src, non_blocking=True))
             self._graph.replay()
             out = self._static_out
         else:
@@ -121,6 +125,7 @@ class LearnerStep:
         if self.reducer is not None:
             raise RuntimeError('HIP-graph capture of the multi-GPU step is not supported; use graph=False')
         self._static = batch
+        self._static_hidden = hidden  # recurrent nets: the window's initial state (zeros, train.py:375)
         # warm up on a side stream (allocator pools, MIOpen kernel selection, lazy state)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))

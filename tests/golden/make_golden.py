@@ -381,6 +381,60 @@ def tictactoe_rules():
     return arrays, games
 
 
+# ---------------------------------------------------------------------------
+# 6. GeisterNet (recurrent DRC ConvLSTM, geister.py:17-167): init, forward, RNN compute_loss
+# ---------------------------------------------------------------------------
+
+def geister_net_case():
+    from handyrl.envs.geister import GeisterNet
+    arrays = {}
+    torch.manual_seed(11)
+    net = GeisterNet()
+    meta = {'state': {}}
+    for k, v in net.state_dict().items():
+        vv = v.double()
+        meta['state'][k] = [list(v.shape), float(vv.sum()), float((vv * vv).sum())]
+    # forward on a fixed observation batch with a non-zero hidden state (train mode)
+    g = torch.Generator().manual_seed(12)
+    N = 6
+    obs = {'board': (torch.rand(N, 7, 6, 6, generator=g) < 0.4).float(),
+           'scalar': (torch.rand(N, 18, generator=g) < 0.5).float()}
+    hs = [torch.randn(N, 32, 6, 6, generator=g) * 0.1 for _ in range(3)]
+    cs = [torch.randn(N, 32, 6, 6, generator=g) * 0.1 for _ in range(3)]
+    arrays['fwd.board'] = _np(obs['board'])
+    arrays['fwd.scalar'] = _np(obs['scalar'])
+    for i in range(3):  # saved before the call: the reference DRC rebinds the list entries in place
+        arrays['fwd.h%d' % i] = _np(hs[i])
+        arrays['fwd.c%d' % i] = _np(cs[i])
+    out = net(obs, (hs, cs))
+    for i in range(3):
+        arrays['fwd.out_h%d' % i] = _np(out['hidden'][0][i])
+        arrays['fwd.out_c%d' % i] = _np(out['hidden'][1][i])
+    for k in ('policy', 'value', 'return'):
+        arrays['fwd.out_' + k] = _np(out[k])
+    # compute_loss through the RNN branch on real Geister windows (train.py:155-174)
+    eps = gen_episodes('Geister', 2, False, seed=13)
+    B, T = 3, 6
+    args = {'turn_based_training': True, 'observation': False, 'forward_steps': T, 'compress_steps': 4,
+            'lambda': 0.7, 'gamma': 0.8, 'policy_target': 'UPGO', 'value_target': 'VTRACE',
+            'entropy_regularization': 0.1, 'entropy_regularization_decay': 0.1}
+    batch = ref_train.make_batch(select_windows(eps, B, T, 4, seed=14), args)
+    model = ModelWrapper(net)
+    hidden = model.init_hidden([B, batch['value'].size(2)])
+    losses, dcnt = ref_train.compute_loss(batch, model, hidden, args)
+    losses['total'].backward()
+    for k, v in batch.items():
+        if isinstance(v, dict):
+            for kk, vv in v.items():
+                arrays['batch.%s.%s' % (k, kk)] = _np(vv)
+        else:
+            arrays['batch.' + k] = _np(v)
+    meta['loss'] = {'args': args, 'dcnt': dcnt, 'losses': {k: float(v.item()) for k, v in losses.items()},
+                    'grad_sq': {n: float((p.grad.double() ** 2).sum()) for n, p in net.named_parameters()
+                                if p.grad is not None}}
+    return arrays, meta
+
+
 def main():
     arr, man = target_cases()
     np.savez_compressed(os.path.join(OUT, 'targets.npz'), **arr)
@@ -405,6 +459,12 @@ def main():
     with open(os.path.join(OUT, 'tictactoe_rules.json'), 'w') as f:
         json.dump(games, f)
     print('tictactoe rules: %d games' % len(games))
+
+    arr, meta = geister_net_case()
+    np.savez_compressed(os.path.join(OUT, 'geister_net.npz'), **arr)
+    with open(os.path.join(OUT, 'geister_net.json'), 'w') as f:
+        json.dump(meta, f, indent=1)
+    print('geister net: %d tensors' % len(meta['state']))
 
     arr, meta = learner_case()
     np.savez_compressed(os.path.join(OUT, 'learner.npz'), **arr)

@@ -1,0 +1,136 @@
+"""GeisterNet (config C3, recurrent DRC ConvLSTM) against the reference.
+
+Golden data (tests/golden/geister_net.*, made by make_golden.py from
+handyrl/envs/geister.py:17-167 and train.py:136-258):
+* per-tensor sum / sum of squares of the seeded initial state_dict
+  (torch.manual_seed(11); GeisterNet()): same keys, shapes, values;
+* one training-mode forward with a non-zero hidden state;
+* compute_loss through the recurrent branch of forward_prediction on a
+  reference make_batch batch of real Geister windows, with the per-parameter
+  squared gradient norms of the summed loss.
+CPU tests pin handyrl_amd.envs.geister.GeisterNet and the oracle; the GPU test
+runs the product path (HIP BatchNorm, HIP target scans, fused HIP loss) on it.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import load_golden
+from oracle import learner as ol
+from handyrl_amd.envs.geister import GeisterNet
+
+
+@pytest.fixture(scope='module')
+def golden():
+    return load_golden('geister_net')
+
+
+def seeded_net():
+    torch.manual_seed(11)
+    return GeisterNet()
+
+
+def test_init_matches_reference(golden):
+    meta, _ = golden
+    sd = seeded_net().state_dict()
+    assert list(sd) == list(meta['state'])
+    for k, (shape, s, sq) in meta['state'].items():
+        v = sd[k].double()
+        assert list(v.shape) == shape, k
+        # fp64 sums of fp32 weights: identical weights agree to reduction-order rounding
+        assert abs(float(v.sum()) - s) <= 1e-12 * max(1.0, abs(s)), k
+        assert abs(float((v * v).sum()) - sq) <= 1e-12 * max(1.0, sq), k
+    assert sum(p.numel() for p in seeded_net().parameters()) == 233832
+
+
+def fwd_inputs(arrays):
+    obs = {'board': torch.from_numpy(arrays['fwd.board'].copy()),
+           'scalar': torch.from_numpy(arrays['fwd.scalar'].copy())}
+    hs = [torch.from_numpy(arrays['fwd.h%d' % i].copy()) for i in range(3)]
+    cs = [torch.from_numpy(arrays['fwd.c%d' % i].copy()) for i in range(3)]
+    return obs, (hs, cs)
+
+
+def check_forward(out, arrays, atol):
+    for k in ('policy', 'value', 'return'):
+        np.testing.assert_allclose(out[k].detach().cpu().numpy(), arrays['fwd.out_' + k], rtol=0, atol=atol)
+    for i in range(3):
+        np.testing.assert_allclose(out['hidden'][0][i].detach().cpu().numpy(), arrays['fwd.out_h%d' % i],
+                                   rtol=0, atol=atol)
+        np.testing.assert_allclose(out['hidden'][1][i].detach().cpu().numpy(), arrays['fwd.out_c%d' % i],
+                                   rtol=0, atol=atol)
+
+
+def test_forward_matches_reference(golden):
+    _, arrays = golden
+    obs, hidden = fwd_inputs(arrays)
+    hs_in = list(hidden[0])
+    out = seeded_net()(obs, hidden)
+    check_forward(out, arrays, atol=1e-6)
+    assert all(a is b for a, b in zip(hidden[0], hs_in))  # caller's hidden lists left untouched
+
+
+def golden_batch(arrays):
+    batch = {}
+    for k in arrays.files:
+        if not k.startswith('batch.'):
+            continue
+        parts = k.split('.')[1:]
+        v = torch.from_numpy(arrays[k].copy())
+        if len(parts) == 2:
+            batch.setdefault(parts[0], {})[parts[1]] = v
+        else:
+            batch[parts[0]] = v
+    return batch
+
+
+def check_loss(losses, dcnt, grads, meta, rtol):
+    ref = meta['loss']
+    assert dcnt == ref['dcnt']
+    for k, v in ref['losses'].items():
+        assert abs(float(losses[k].detach()) - v) <= rtol * max(1.0, abs(v)), (k, float(losses[k].detach()), v)
+    for n, sq in ref['grad_sq'].items():
+        assert abs(grads[n] - sq) <= rtol * max(1e-6, sq) + 1e-9, (n, grads[n], sq)
+
+
+def test_oracle_rnn_compute_loss_matches_reference(golden):
+    meta, arrays = golden
+    batch = golden_batch(arrays)
+    net = seeded_net()
+    B, P = batch['value'].shape[0], batch['value'].shape[2]
+    losses, dcnt = ol.compute_loss(batch, net, net.init_hidden([B, P]), meta['loss']['args'])
+    losses['total'].backward()
+    grads = {n: float((p.grad.double() ** 2).sum()) for n, p in net.named_parameters() if p.grad is not None}
+    check_loss(losses, dcnt, grads, meta, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_forward_matches_reference(golden, cuda):
+    from handyrl_amd.nn import accelerate
+    _, arrays = golden
+    net = seeded_net().to(cuda)
+    accelerate(net)
+    obs, hidden = fwd_inputs(arrays)
+    obs = {k: v.to(cuda) for k, v in obs.items()}
+    hidden = ([h.to(cuda) for h in hidden[0]], [c.to(cuda) for c in hidden[1]])
+    check_forward(net(obs, hidden), arrays, atol=2e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_rnn_compute_loss_matches_reference(golden, cuda):
+    """Product compute_loss (HIP BN / scans / fused loss) through the recurrent branch."""
+    from handyrl_amd.nn import accelerate
+    from handyrl_amd.train import compute_loss
+    meta, arrays = golden
+    batch = {k: ({kk: vv.to(cuda) for kk, vv in v.items()} if isinstance(v, dict) else v.to(cuda))
+             for k, v in golden_batch(arrays).items()}
+    net = seeded_net().to(cuda)
+    accelerate(net)
+    B, P = batch['value'].shape[0], batch['value'].shape[2]
+    hidden = net.init_hidden([B, P])
+    hidden = ([h.to(cuda) for h in hidden[0]], [c.to(cuda) for c in hidden[1]])
+    losses, dcnt = compute_loss(batch, net, hidden, meta['loss']['args'])
+    losses['total'].backward()
+    grads = {n: float((p.grad.double() ** 2).sum()) for n, p in net.named_parameters() if p.grad is not None}
+    check_loss(losses, dcnt, grads, meta, rtol=1e-4)
