@@ -185,6 +185,64 @@ def secondary_rollout(device, E=16384, reps=5):
             'reference_cpu_source': 'SURVEY §6: generation.py per worker process, measured in the survey container'}
 
 
+def secondary_geister_learner(device, B=256, T=16, steps=10, warmup=3):
+    """recurrent learner step (GeisterNet unrolled over T, config.yaml batch 256)."""
+    from handyrl_amd.envs.geister import GeisterNet
+    from handyrl_amd.synthetic import geister_batch
+    args = default_args(T, B)
+    torch.manual_seed(0)
+    net = GeisterNet().to(device)
+    batch = geister_batch(B, T, device, seed=5)
+    hidden = tuple([h.to(device) for h in hs] for hs in net.init_hidden([B, 2]))
+    learner = LearnerStep(net, args, device, graph=True)
+    for _ in range(max(warmup, 1)):
+        learner.step(batch, hidden)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        learner.step(batch, hidden)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    value = B * T * steps / dt
+    ref_cpu = 929.0
+    return {'config': 'Geister recurrent learner B=%d T=%d (GeisterNet, UPGO/VTRACE)' % (B, T),
+            'value': round(value, 1), 'unit': 'env-steps/s', 'ms_per_step': round(dt / steps * 1e3, 3),
+            'vs_reference_cpu_1thread': round(value / ref_cpu, 1),
+            'reference_cpu_source': 'tools/ref_geister_cpu.py: reference compute_loss+backward+Adam, '
+                                    'B=64 T=16, 1 thread, 929 env-steps/s (build container)'}
+
+
+def secondary_geister_rollout(device, E=2048, reps=2):
+    """BASELINE.json configs[2]: Geister device self-play, E concurrent games, recurrent GeisterNet inference."""
+    from handyrl_amd.envs.geister import GeisterNet, GeisterBatch
+    from handyrl_amd.rollout import DeviceGenerator, DeviceReplay
+    from handyrl_amd.nn import accelerate
+    torch.manual_seed(0)
+    net = accelerate(GeisterNet().to(device))
+    gen = DeviceGenerator(GeisterBatch(E, device), net)
+    rep = DeviceReplay(4 * E, GeisterBatch.MAX_PLIES, GeisterBatch.OBS_SHAPE, GeisterBatch.A, 2, device,
+                       obs_dtype=torch.uint8)
+    g = torch.Generator(device=device).manual_seed(0)
+    rep.add(gen.generate(generator=g))   # warm-up
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    plies = 0
+    for _ in range(reps):
+        ep = gen.generate(generator=g)
+        rep.add(ep)
+        plies += ep['length'].sum()
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    plies = int(plies)
+    return {'config': 'Geister device self-play, %d concurrent games, GeisterNet (DRC ConvLSTM) inference '
+                      '(BASELINE.json configs[2])' % E,
+            'value': round(plies / dt, 1), 'unit': 'env-steps/s', 'games_per_s': round(E * reps / dt, 1),
+            'mean_plies': round(plies / (E * reps), 1),
+            'reference_cpu_worker': 349.0,
+            'reference_cpu_source': 'tools/ref_geister_gen_cpu.py: reference Generator + GeisterNet, 1 thread, '
+                                    'build container'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -261,6 +319,8 @@ def main():
         cpu = cpu_baseline() if (opts.cpu_baseline and world == 1) else None
         t9 = secondary_t9(device) if (opts.secondary and world == 1) else None
         ro = secondary_rollout(device) if (opts.secondary and world == 1) else None
+        gro = secondary_geister_rollout(device) if (opts.secondary and world == 1) else None
+        gle = secondary_geister_learner(device) if (opts.secondary and world == 1) else None
         line = {
             'metric': 'learner env-steps/sec at B=4096 T=32 (TicTacToe net, UPGO/VTRACE)',
             'value': round(value, 1),
@@ -289,6 +349,10 @@ def main():
             line['secondary'] = t9
         if ro is not None:
             line['rollout'] = ro
+        if gro is not None:
+            line['geister_rollout'] = gro
+        if gle is not None:
+            line['geister_learner'] = gle
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -16,9 +16,10 @@ bit for bit (pinned by tests/golden/geister_net.json):
   colour (scalar[0]); value / return 1x1 conv 64->1 -> BN -> ReLU -> Linear(36, 1);
   value through tanh.  233,832 parameters.
 
-The rules stay in the reference plugin (handyrl.envs.geister.Environment,
-geister.py:170-541): the learner only needs the net and the observation
-format {'board': (7, 6, 6), 'scalar': (18,)}, 214 actions.
+``GeisterBatch`` restates the rules (geister.py:170-541) as tensor ops over
+E concurrent games for device self-play (rollout.DeviceGenerator); the
+per-game CPU plugin stays the reference's Environment.  Observation format
+{'board': (7, 6, 6), 'scalar': (18,)}, 214 actions.
 """
 
 import numpy as np
@@ -135,3 +136,160 @@ class GeisterNet(nn.Module):
         policy = torch.cat([self.head_p_move(h), self.head_p_set(scalar[:, :1])], dim=-1)
         return {'policy': policy, 'value': torch.tanh(self.head_v(h)), 'return': self.head_r(h),
                 'hidden': hidden}
+
+
+class GeisterBatch:
+    """E Geister games advanced together on one device (rules of geister.py:170-541).
+
+    State per game: ``board`` (E, 36) int8 piece codes in the reference's
+    absolute frame (cell = x*6 + y; -1 empty, piece = colour*2 + type, type 0
+    blue / 1 red), ``color`` to move, ``turn_count`` (-2, -1: setting the
+    layouts; 200 moves end in a draw), ``win`` (-1 none, 0 black, 1 white,
+    2 draw) and the piece counts ``cnt`` (E, 4).  Actions are the reference's
+    labels: 0..143 = direction*36 + cell in the mover's frame (white's frame
+    is the board rotated 180 degrees, so white's label is 143 minus the
+    absolute one), 144 + k = initial layout k of C(8, 4).
+    """
+
+    A = 214
+    P = 2
+    MAX_PLIES = 202
+    OBS_SHAPE = {'board': (BOARD_PLANES, *BOARD), 'scalar': (SCALARS,)}
+    MOVES = 144
+    # initial squares of the 8 pieces of each colour (geister.py:179-182); 'B2' = x 1, y 1
+    OPOS_NAMES = (('B2', 'C2', 'D2', 'E2', 'B1', 'C1', 'D1', 'E1'), ('E5', 'D5', 'C5', 'B5', 'E6', 'D6', 'C6', 'B6'))
+    OPOS = tuple(tuple('ABCDEF'.index(s[0]) * 6 + '123456'.index(s[1]) for s in names) for names in OPOS_NAMES)
+    DIRS = ((-1, 0), (0, -1), (0, 1), (1, 0))
+    GOALS = (((-1, 5), (6, 5)), ((-1, 0), (6, 0)))
+    MAX_MOVES = 200
+
+    def __init__(self, E, device):
+        import itertools
+        self.E, self.device = E, device
+        dev = device
+        # target cell of (direction, cell), -1 off the board; off-board goal flags per colour
+        tgt = torch.full((4, 36), -1, dtype=torch.long)
+        goal = torch.zeros(2, 4, 36, dtype=torch.bool)
+        for d, (dx, dy) in enumerate(self.DIRS):
+            for x in range(6):
+                for y in range(6):
+                    nx, ny = x + dx, y + dy
+                    if 0 <= nx < 6 and 0 <= ny < 6:
+                        tgt[d, x * 6 + y] = nx * 6 + ny
+                    else:
+                        for c in range(2):
+                            goal[c, d, x * 6 + y] = (nx, ny) in self.GOALS[c]
+        self.tgt = tgt.to(dev)
+        self.tgt_safe = tgt.clamp(min=0).to(dev)
+        self.goal = goal.view(2, 144).to(dev)
+        # layout k: blue flags of the 8 pieces (geister.py:189, 227-234; OSEQ = combinations(range(8), 4))
+        blue = torch.zeros(70, 8, dtype=torch.bool)
+        for k, seq in enumerate(itertools.combinations(range(8), 4)):
+            blue[k, list(seq)] = True
+        self.layout_type = (~blue).to(torch.int8).to(dev)      # piece type per slot: 0 blue, 1 red
+        self.opos = torch.tensor(self.OPOS, dtype=torch.long, device=dev)
+        self.reset()
+
+    def reset(self):
+        E, dev = self.E, self.device
+        self.board = torch.full((E, 36), -1, dtype=torch.int8, device=dev)
+        self.color = torch.zeros(E, dtype=torch.long, device=dev)
+        self.turn_count = torch.full((E,), -2, dtype=torch.long, device=dev)
+        self.win = torch.full((E,), -1, dtype=torch.long, device=dev)
+        self.cnt = torch.zeros(E, 4, dtype=torch.long, device=dev)
+
+    def turn(self):
+        return self.color
+
+    def plies(self):
+        return self.turn_count + 2
+
+    def terminal(self):
+        return self.win >= 0
+
+    def legal(self):
+        """(E, 214) bool legal-action mask of the side to move (geister.py:460-487)."""
+        b = self.board.long()
+        own = (b >= 0) & (b // 2 == self.color.view(-1, 1))                     # (E, 36)
+        own_blue = own & (b % 2 == 0)
+        own_t = torch.gather(own, 1, self.tgt_safe.view(1, -1).expand(self.E, -1)).view(-1, 4, 36)
+        on = (self.tgt >= 0).view(1, 4, 36)
+        to_goal = own_blue.view(-1, 1, 36) & self.goal[self.color].view(-1, 4, 36)
+        moves = own.view(-1, 1, 36) & torch.where(on, ~own_t, to_goal)          # absolute frame (E, 4, 36)
+        moves = moves.view(-1, 144)
+        moves = torch.where((self.color == 1).view(-1, 1), moves.flip(-1), moves)
+        setting = (self.turn_count < 0).view(-1, 1)
+        lay = setting.expand(-1, 70)
+        return torch.cat([moves & ~setting, lay], dim=1)
+
+    def step(self, action, active):
+        """Play `action` (E,) for the side to move in every `active` game (geister.py:359-394)."""
+        E, dev = self.E, self.device
+        rows = torch.arange(E, device=dev)
+        c = self.color
+        setting = active & (self.turn_count < 0)
+        moving = active & (self.turn_count >= 0)
+        # -- layout actions: place the mover's 8 pieces
+        lay = (action - self.MOVES).clamp(0, 69)
+        pieces = (c.view(-1, 1) * 2 + self.layout_type[lay].long())             # (E, 8)
+        cells = self.opos[c]                                                   # (E, 8)
+        cur = torch.gather(self.board, 1, cells)
+        self.board.scatter_(1, cells, torch.where(setting.view(-1, 1), pieces.to(torch.int8), cur))
+        add = torch.zeros(E, 4, dtype=torch.long, device=dev)
+        add.scatter_(1, torch.stack([c * 2, c * 2 + 1], 1), torch.full((E, 2), 4, dtype=torch.long, device=dev))
+        self.cnt += add * setting.long().view(-1, 1)
+        # -- moves
+        a_abs = torch.where(c == 1, self.MOVES - 1 - action, action).clamp(0, self.MOVES - 1)
+        d, src = a_abs // 36, a_abs % 36
+        dst = self.tgt[d, src]
+        piece = self.board[rows, src].long()
+        off = moving & (dst < 0)
+        on = moving & (dst >= 0)
+        dst_s = dst.clamp(min=0)
+        cap = self.board[rows, dst_s].long()
+        captured = on & (cap >= 0)
+        cnt_dec = torch.zeros(E, 4, dtype=torch.long, device=dev)
+        cnt_dec[rows, cap.clamp(min=0)] += captured.long()
+        cnt_dec[rows, piece.clamp(min=0)] += off.long()                          # piece leaves by the goal
+        self.cnt -= cnt_dec
+        gone = captured & (self.cnt[rows, cap.clamp(min=0)] == 0)
+        win = torch.where(off, c, self.win)
+        win = torch.where(gone, torch.where(cap % 2 == 0, c, 1 - c), win)
+        # board: source emptied, piece lands on an on-board target
+        src_val = torch.where(moving, torch.full_like(piece, -1), self.board[rows, src].long())
+        self.board[rows, src] = src_val.to(torch.int8)
+        dst_val = torch.where(on, piece, self.board[rows, dst_s].long())
+        self.board[rows, dst_s] = dst_val.to(torch.int8)
+        self.color = torch.where(active, 1 - c, c)
+        self.turn_count = self.turn_count + active.long()
+        draw = moving & (self.turn_count >= self.MAX_MOVES) & (win < 0)
+        self.win = torch.where(draw, torch.full_like(win, 2), win)
+
+    def observation(self, player):
+        """{'board': (E,7,6,6), 'scalar': (E,18)} seen by `player` (E,) (geister.py:495-535, player given)."""
+        turn_view = player == self.color
+        me = torch.where(turn_view, self.color, 1 - self.color)
+        opp = 1 - me
+        b = self.board.long()
+        cnt = self.cnt
+        rows = torch.arange(self.E, device=self.device)
+        counts = torch.stack([cnt[rows, me * 2], cnt[rows, me * 2 + 1], cnt[rows, opp * 2], cnt[rows, opp * 2 + 1]], 1)
+        onehot = (counts.view(-1, 4, 1) == torch.arange(1, 5, device=self.device).view(1, 1, 4)).view(-1, 16)
+        scalar = torch.cat([(me == 0).view(-1, 1), turn_view.view(-1, 1), onehot], 1).float()
+        blue_c = b == (me * 2).view(-1, 1)
+        red_c = b == (me * 2 + 1).view(-1, 1)
+        own_all = blue_c | red_c
+        opp_all = (b >= 0) & ~own_all
+        zero = torch.zeros_like(own_all)
+        planes = torch.stack([torch.ones_like(own_all), own_all, opp_all, blue_c, red_c, zero, zero], 1).float()
+        planes = torch.where((me == 1).view(-1, 1, 1), planes.flip(-1), planes)   # white: rotate 180 degrees
+        return {'board': planes.view(-1, BOARD_PLANES, *BOARD), 'scalar': scalar}
+
+    def reward(self):
+        """(E, 2) fp64: -0.01 per ply for both players (geister.py:427-429; a Python float there)."""
+        return torch.full((self.E, 2), -0.01, dtype=torch.float64, device=self.device)
+
+    def outcome(self):
+        """(E, 2): +1/-1 for the winning colour, 0/0 for a draw (geister.py:431-438)."""
+        w = torch.where(self.win == 0, 1.0, torch.where(self.win == 1, -1.0, 0.0))
+        return torch.stack([w, -w], dim=1)

@@ -19,19 +19,27 @@ import torch
 
 from .rollout import DeviceGenerator, DeviceReplay, TicTacToeBatch
 from .trainer import LearnerStep
+from .util import map_r
 
 __all__ = ['SelfPlayTrainer', 'evaluate_vs_random']
 
 
 class SelfPlayTrainer:
-    def __init__(self, net, args, device, games_per_round=4096, capacity=65536, graph=False, seed=0):
+    """``env_cls``: a batched env (TicTacToeBatch, envs.geister.GeisterBatch); recurrent nets
+    train from a zero hidden state at every window start (train.py:375)."""
+
+    def __init__(self, net, args, device, games_per_round=4096, capacity=65536, graph=False, seed=0,
+                 env_cls=TicTacToeBatch, obs_dtype=torch.uint8):
         self.args = args
         self.device = device
-        self.env = TicTacToeBatch(games_per_round, device)
+        self.env = env_cls(games_per_round, device)
         self.gen = DeviceGenerator(self.env, net, gamma=args['gamma'])
-        self.replay = DeviceReplay(capacity, TicTacToeBatch.MAX_PLIES, TicTacToeBatch.OBS_SHAPE, TicTacToeBatch.A,
-                                   TicTacToeBatch.P, device, maximum_episodes=args.get('maximum_episodes', capacity))
+        self.replay = DeviceReplay(capacity, env_cls.MAX_PLIES, env_cls.OBS_SHAPE, env_cls.A, env_cls.P, device,
+                                   maximum_episodes=args.get('maximum_episodes', capacity), obs_dtype=obs_dtype)
         self.learner = LearnerStep(net, args, device, graph=graph)
+        self.hidden = None
+        if hasattr(net, 'init_hidden'):
+            self.hidden = map_r(net.init_hidden([args['batch_size'], env_cls.P]), lambda h: h.to(device))
         self.rng = torch.Generator(device=device).manual_seed(seed)
         self.episodes = 0
         self.steps = 0
@@ -46,7 +54,7 @@ class SelfPlayTrainer:
         B, T = self.args['batch_size'], self.args['forward_steps']
         for _ in range(n):
             batch = self.replay.sample(B, T, generator=self.rng)
-            self.learner.step(batch)
+            self.learner.step(batch, self.hidden)
             self.steps += 1
 
     def run(self, rounds, steps_per_round, log=None):

@@ -28,6 +28,8 @@ Scope: turn-based two-player training without opponent observation
 import numpy as np
 import torch
 
+from .util import map_r, bimap_r
+
 __all__ = ['TicTacToeBatch', 'DeviceGenerator', 'DeviceReplay', 'episodes_to_wire']
 
 
@@ -55,6 +57,9 @@ class TicTacToeBatch:
     def turn(self):
         """Index of the player to move: 0 (black) on even plies."""
         return (self.nmoves % 2).long()
+
+    def plies(self):
+        return self.nmoves
 
     def terminal(self):
         return (self.winner != 0) | (self.nmoves >= 9)
@@ -88,60 +93,104 @@ class TicTacToeBatch:
         return torch.stack([w, -w], dim=1)
 
 
-class DeviceGenerator:
-    """Batched self-play of E games with one env-network forward per ply (generation.py:20-88)."""
+def _alloc(spec, lead, device, dtype=torch.float32):
+    """Zero tensors (*lead, *shape) for an observation spec: a shape tuple or {name: shape}."""
+    if isinstance(spec, dict):
+        return {k: torch.zeros(*lead, *v, device=device, dtype=dtype) for k, v in spec.items()}
+    return torch.zeros(*lead, *spec, device=device, dtype=dtype)
 
-    def __init__(self, env_batch, net, gamma=0.8):
+
+class DeviceGenerator:
+    """Batched self-play of E games with one env-network forward per ply (generation.py:20-88).
+
+    Recurrent nets (``init_hidden``, e.g. GeisterNet) keep one hidden state
+    per game and player in HBM, starting from ``init_hidden`` zeros; each ply
+    only the mover's state advances (generation.py:23-25, 38-41).  Rewards
+    (``env.reward()``, e.g. Geister's -0.01 per ply) are recorded for both
+    players every ply and turned into discounted returns in fp64 exactly as
+    the reference's Python-float loop (generation.py:73-77).
+    """
+
+    def __init__(self, env_batch, net, gamma=0.8, check_every=16):
         self.env = env_batch
         self.net = net
         self.gamma = gamma
+        self.check_every = check_every
 
     @torch.no_grad()
     def generate(self, generator=None):
         env, E, dev = self.env, self.env.E, self.env.device
         Tm, A, P = env.MAX_PLIES, env.A, env.P
         env.reset()
-        obs = torch.zeros(E, Tm, *env.OBS_SHAPE, device=dev)
+        rows = torch.arange(E, device=dev)
+        obs = _alloc(env.OBS_SHAPE, (E, Tm), dev)
         policy = torch.zeros(E, Tm, A, device=dev)
         amask = torch.full((E, Tm, A), 1e32, device=dev)
         action = torch.zeros(E, Tm, dtype=torch.long, device=dev)
         value = torch.zeros(E, Tm, device=dev)
         turn = torch.zeros(E, Tm, dtype=torch.long, device=dev)
+        reward = torch.zeros(E, Tm, P, device=dev, dtype=torch.float64)   # Python floats in the reference
+        has_reward = hasattr(env, 'reward')
+        hidden = None
+        if hasattr(self.net, 'init_hidden'):
+            hidden = map_r(self.net.init_hidden([E, P]), lambda h: h.to(dev))
         was_training = self.net.training
         self.net.eval()
         for t in range(Tm):
+            if t and self.check_every and t % self.check_every == 0 and bool(env.terminal().all()):
+                break
             active = ~env.terminal()
             player = env.turn()
             o = env.observation(player)
-            out = self.net(o, None)
+            h_in = None if hidden is None else map_r(hidden, lambda h: h[rows, player])
+            out = self.net(o, h_in)
             m = torch.where(env.legal(), 0.0, 1e32)                        # generation.py:50-51
             p = out['policy'] - m
             u = torch.rand(E, A, device=dev, generator=generator).clamp_(1e-20, 1.0)
             a = torch.argmax(p - torch.log(-torch.log(u)), dim=-1)          # Gumbel-max = softmax over legal
             act = active.view(-1, 1)
-            obs[:, t] = torch.where(act.view(-1, 1, 1, 1), o, obs[:, t])
+            bimap_r(obs, o, lambda buf, x: buf[:, t].copy_(
+                torch.where(active.view(-1, *([1] * (x.dim() - 1))), x, buf[:, t])))
             policy[:, t] = torch.where(act, p, policy[:, t])
             amask[:, t] = torch.where(act, m, amask[:, t])
             action[:, t] = torch.where(active, a, action[:, t])
             value[:, t] = torch.where(active, out['value'].view(-1), value[:, t])
             turn[:, t] = torch.where(active, player, turn[:, t])
+            if has_reward:
+                reward[:, t] = torch.where(act, env.reward(), reward[:, t])
+            if hidden is not None:
+                def advance(h, nh):
+                    cur = h[rows, player]
+                    h[rows, player] = torch.where(active.view(-1, *([1] * (nh.dim() - 1))), nh, cur)
+                bimap_r(hidden, out['hidden'], advance)
             env.step(a, active)
         self.net.train(was_training)
-        length = env.nmoves.long()
-        # rewards are None in TicTacToe, so the discounted returns are 0 (generation.py:73-77)
-        zeros = torch.zeros(E, Tm, P, device=dev)
+        length = env.plies().long()
+        # discounted returns per player, fp64 like the reference's Python floats (generation.py:73-77)
+        ret = torch.zeros(E, Tm, P, device=dev)
+        acc = torch.zeros(E, P, dtype=torch.float64, device=dev)
+        if has_reward:
+            for t in range(Tm - 1, -1, -1):
+                acc = reward[:, t] + self.gamma * acc
+                ret[:, t] = acc.float()
         return {'observation': obs, 'policy': policy, 'action_mask': amask, 'action': action, 'value': value,
-                'turn': turn, 'length': length, 'outcome': env.outcome(), 'reward': zeros, 'return': zeros.clone()}
+                'turn': turn, 'length': length, 'outcome': env.outcome(), 'reward': reward.float(), 'return': ret}
 
 
 class DeviceReplay:
-    """Ring buffer of episodes in HBM; windows gathered into the make_batch layout."""
+    """Ring buffer of episodes in HBM; windows gathered into the make_batch layout.
 
-    def __init__(self, capacity, max_plies, obs_shape, A, P, device, maximum_episodes=None):
+    ``obs_shape`` is a shape or {name: shape}; ``obs_dtype`` lets binary
+    observation planes (TicTacToe, Geister) live in HBM as uint8, a quarter
+    of the bytes, widened to fp32 by the gather.
+    """
+
+    def __init__(self, capacity, max_plies, obs_shape, A, P, device, maximum_episodes=None,
+                 obs_dtype=torch.float32):
         self.N, self.Tm, self.P, self.device = capacity, max_plies, P, device
         self.maximum_episodes = maximum_episodes or capacity
         f = dict(device=device)
-        self.obs = torch.zeros(capacity, max_plies, *obs_shape, **f)
+        self.obs = _alloc(obs_shape, (capacity, max_plies), device, obs_dtype)
         self.policy = torch.zeros(capacity, max_plies, A, **f)
         self.amask = torch.full((capacity, max_plies, A), 1e32, **f)
         self.action = torch.zeros(capacity, max_plies, dtype=torch.long, **f)
@@ -157,7 +206,8 @@ class DeviceReplay:
     def add(self, ep):
         E = ep['length'].shape[0]
         slots = (self.ptr + torch.arange(E, device=self.device)) % self.N
-        for dst, key in ((self.obs, 'observation'), (self.policy, 'policy'), (self.amask, 'action_mask'),
+        bimap_r(self.obs, ep['observation'], lambda dst, src: dst.index_copy_(0, slots, src.to(dst.dtype)))
+        for dst, key in ((self.policy, 'policy'), (self.amask, 'action_mask'),
                          (self.action, 'action'), (self.value, 'value'), (self.turn, 'turn'),
                          (self.reward, 'reward'), (self.ret, 'return'), (self.length, 'length'),
                          (self.outcome, 'outcome')):
@@ -197,7 +247,7 @@ class DeviceReplay:
         tc = torch.minimum(t, length - 1)
         e = slots.view(-1, 1)
         vf = valid.float()
-        obs = self.obs[e, tc] * vf.view(B, T, *([1] * (self.obs.dim() - 2)))
+        obs = map_r(self.obs, lambda o: (o[e, tc].float() * vf.view(B, T, *([1] * (o.dim() - 2)))).unsqueeze(2))
         pol = self.policy[e, tc] * vf.unsqueeze(-1)
         amask = torch.where(valid.unsqueeze(-1), self.amask[e, tc], torch.full_like(pol, 1e32))
         act = self.action[e, tc] * valid.long()
@@ -209,7 +259,7 @@ class DeviceReplay:
         ret = self.ret[e, tc] * vf.unsqueeze(-1)
         progress = torch.where(valid, t.float() / length.float(), torch.ones_like(vf))
         return {
-            'observation': obs.unsqueeze(2).contiguous(),
+            'observation': obs,
             'policy': pol.unsqueeze(2).contiguous(),
             'value': val.contiguous(),
             'action': act.view(B, T, 1, 1).contiguous(),
@@ -232,7 +282,8 @@ def episodes_to_wire(ep, compress_steps=4):
     """Device episodes -> the reference episode format (generation.py:79-86), for parity checks."""
     import bz2
     import pickle
-    cpu = {k: v.cpu().numpy() for k, v in ep.items()}
+    cpu = map_r(ep, lambda v: v.cpu().numpy())
+    has_reward = bool((cpu['reward'] != 0).any())
     out = []
     for e in range(cpu['length'].shape[0]):
         L = int(cpu['length'][e])
@@ -241,12 +292,14 @@ def episodes_to_wire(ep, compress_steps=4):
             p = int(cpu['turn'][e, t])
             m = {k: {0: None, 1: None} for k in ('observation', 'policy', 'action_mask', 'action', 'value',
                                                     'reward', 'return')}
-            m['observation'][p] = cpu['observation'][e, t].astype(np.float32)
+            m['observation'][p] = map_r(cpu['observation'], lambda o: o[e, t].astype(np.float32))
             m['policy'][p] = cpu['policy'][e, t].astype(np.float32)
             m['action_mask'][p] = cpu['action_mask'][e, t].astype(np.float32)
             m['action'][p] = int(cpu['action'][e, t])
             m['value'][p] = np.array([cpu['value'][e, t]], dtype=np.float32)
             for q in (0, 1):
+                if has_reward:
+                    m['reward'][q] = float(cpu['reward'][e, t, q])
                 m['return'][q] = float(cpu['return'][e, t, q])
             m['turn'] = [p]
             moments.append(m)

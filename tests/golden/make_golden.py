@@ -381,6 +381,41 @@ def tictactoe_rules():
     return arrays, games
 
 
+def geister_rules(n_games=24, seed=2026):
+    """Random Geister games (geister.py:170-541): per ply the turn player, legal-action
+    mask, both players' observations (player given: opponent colours hidden), action;
+    per game the outcome, the ply count and the reward."""
+    env = make_env({'env': 'Geister'})
+    rnd = random.Random(seed)
+    arrays, games = {}, []
+    for g in range(n_games):
+        env.reset()
+        turn, legal, acts, boards, scalars = [], [], [], [], []
+        while not env.terminal():
+            p = env.turn()
+            la = env.legal_actions(p)
+            m = np.zeros(env.action_length(), np.uint8)
+            m[la] = 1
+            o = [env.observation(q) for q in (0, 1)]
+            a = rnd.choice(la)
+            turn.append(p)
+            legal.append(m)
+            acts.append(a)
+            boards.append(np.stack([o[0]['board'], o[1]['board']]).astype(np.uint8))
+            scalars.append(np.stack([o[0]['scalar'], o[1]['scalar']]).astype(np.uint8))
+            env.play(a)
+        pre = '%d:' % g
+        arrays[pre + 'turn'] = np.array(turn, np.int8)
+        arrays[pre + 'legal'] = np.packbits(np.stack(legal), axis=-1)
+        arrays[pre + 'action'] = np.array(acts, np.int16)
+        arrays[pre + 'board'] = np.packbits(np.stack(boards), axis=-1)   # (L, 2, 7, 6, 1) bits of the last axis
+        arrays[pre + 'scalar'] = np.stack(scalars)
+        oc = env.outcome()
+        games.append({'plies': len(acts), 'outcome': [oc[0], oc[1]], 'win_color': env.win_color,
+                      'reward': env.reward()[0]})
+    return arrays, games
+
+
 # ---------------------------------------------------------------------------
 # 6. GeisterNet (recurrent DRC ConvLSTM, geister.py:17-167): init, forward, RNN compute_loss
 # ---------------------------------------------------------------------------
@@ -459,6 +494,13 @@ def main():
     with open(os.path.join(OUT, 'tictactoe_rules.json'), 'w') as f:
         json.dump(games, f)
     print('tictactoe rules: %d games' % len(games))
+
+    arr, games = geister_rules()
+    np.savez_compressed(os.path.join(OUT, 'geister_rules.npz'), **arr)
+    with open(os.path.join(OUT, 'geister_rules.json'), 'w') as f:
+        json.dump(games, f)
+    print('geister rules: %d games, %d plies, win colours %s' % (
+        len(games), sum(g['plies'] for g in games), sorted(g['win_color'] for g in games)))
 
     arr, meta = geister_net_case()
     np.savez_compressed(os.path.join(OUT, 'geister_net.npz'), **arr)

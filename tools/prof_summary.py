@@ -1,6 +1,8 @@
 """Summarise a rocprofv3 kernel trace (CSV) per learner step.
 
     python tools/prof_summary.py <run_kernel_trace.csv> <steps> [--match NAME]
+<steps> may be 'per:SUBSTR': the number of launches of the (once-per-step)
+kernel whose name contains SUBSTR, e.g. per:fused_adam.
 Prints kernel-name groups with total time per step and mean duration per call.
 """
 import collections
@@ -9,9 +11,12 @@ import sys
 
 
 def main():
-    path, steps = sys.argv[1], int(sys.argv[2])
+    path, steps = sys.argv[1], sys.argv[2]
     match = sys.argv[sys.argv.index('--match') + 1] if '--match' in sys.argv else None
     rows = list(csv.DictReader(open(path)))
+    if steps.startswith('per:'):
+        steps = sum(1 for r in rows if steps[4:] in r['Kernel_Name'])
+    steps = int(steps)
     tot, cnt = collections.Counter(), collections.Counter()
     for r in rows:
         n = r['Kernel_Name']
