@@ -64,9 +64,13 @@ SIGNATURES = {
                                          ctypes.c_void_p]),
     'hrl_colsum_workspace_bytes': (ctypes.c_int64, [_i64, _i64]),
     'hrl_colsum': (ctypes.c_int, [_f32p, _i64, _i64, _f32p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_lstm_gates_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p,
+                                              ctypes.c_void_p]),
+    'hrl_lstm_gates_backward': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p,
+                                               ctypes.c_void_p]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lib = None
 

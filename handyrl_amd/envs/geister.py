@@ -71,13 +71,41 @@ class DRC(nn.Module):
         states = [blk.init_hidden(input_size, batch_size) for blk in self.blocks]
         return [s[0] for s in states], [s[1] for s in states]
 
+    use_hip = False   # set by handyrl_amd.nn.accelerate
+
     def forward(self, x, hidden, num_repeats):
         if hidden is None:
-            hidden = self.init_hidden(x.shape[-2:], x.shape[:-3])
+            hidden = tuple([t.to(x.device) for t in ts] for ts in self.init_hidden(x.shape[-2:], x.shape[:-3]))
         hs, cs = list(hidden[0]), list(hidden[1])
+        if self.use_hip and x.is_cuda:
+            return self._forward_hip(x, hs, cs, num_repeats)
         for _ in range(num_repeats):
             for i, blk in enumerate(self.blocks):
                 hs[i], cs[i] = blk(x, (hs[i], cs[i]))
+        return hs[-1], (hs, cs)
+
+    def _forward_hip(self, x, hs, cs, num_repeats):
+        """Same cells, regrouped: conv([x, h]) = conv_x(x) + conv_h(h).
+
+        Every repeat of every layer sees the same x, so the x halves of the
+        three layers run once, as one 32 -> 3*128 convolution (bias folded in);
+        each cell then convolves only its h (32 -> 128) and the fused HIP gate
+        kernel adds the two (nn.lstm_gates).  A third fewer cell FLOPs, no
+        concatenation, one gate launch per cell and direction.
+        """
+        from ..nn import lstm_gates
+        cin = x.shape[-3]
+        ws = [blk.conv.weight for blk in self.blocks]
+        bias = [blk.conv.bias for blk in self.blocks]
+        pad = self.blocks[0].conv.padding
+        w_x = torch.cat([w[:, :cin] for w in ws])
+        b_x = None if bias[0] is None else torch.cat(bias)
+        zx = F.conv2d(x, w_x, b_x, padding=pad).chunk(len(self.blocks), dim=-3)
+        w_h = [w[:, cin:].contiguous() for w in ws]
+        for _ in range(num_repeats):
+            for i in range(len(self.blocks)):
+                zh = F.conv2d(hs[i], w_h[i], None, padding=pad)
+                hs[i], cs[i] = lstm_gates(zx[i], zh, cs[i])
         return hs[-1], (hs, cs)
 
 

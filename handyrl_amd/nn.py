@@ -259,6 +259,55 @@ class _BoardBias(torch.autograd.Function):
         return out, None
 
 
+class _LSTMGates(torch.autograd.Function):
+    """ConvLSTM cell gates (csrc/hrl_lstm.hip): z = zx + zh -> (h', c'), saved gate activations."""
+
+    @staticmethod
+    def forward(ctx, zx, zh, c):
+        N, G, Hh, Ww = zh.shape
+        H, HW = G // 4, Hh * Ww
+        zh = zh.contiguous()
+        c = c.contiguous()
+        if zx is not None and (zx.shape != zh.shape or zx.stride()[1:] != zh.stride()[1:]):
+            zx = zx.contiguous()
+        h_out = torch.empty_like(c)
+        c_out = torch.empty_like(c)
+        gates = torch.empty_like(zh)
+        lib = _native.load()
+        _native.check(lib.hrl_lstm_gates_forward(_native.ptr(zx), 0 if zx is None else zx.stride(0), _native.ptr(zh),
+                                                 _native.ptr(c), N, H, HW, _native.ptr(h_out), _native.ptr(c_out),
+                                                 _native.ptr(gates), _native.stream_of(zh.device)),
+                      'hrl_lstm_gates_forward')
+        ctx.save_for_backward(gates, c, c_out)
+        ctx.has_zx = zx is not None
+        return h_out, c_out
+
+    @staticmethod
+    def backward(ctx, dh, dc_out):
+        gates, c, c_out = ctx.saved_tensors
+        N, G, Hh, Ww = gates.shape
+        dz = torch.empty_like(gates)
+        dc = torch.empty_like(c)
+        dh = None if dh is None else dh.contiguous()
+        dc_out = None if dc_out is None else dc_out.contiguous()
+        _native.check(_native.load().hrl_lstm_gates_backward(
+            _native.ptr(gates), _native.ptr(c), _native.ptr(c_out), _native.ptr(dh), _native.ptr(dc_out),
+            N, G // 4, Hh * Ww, _native.ptr(dz), _native.ptr(dc), _native.stream_of(gates.device)),
+            'hrl_lstm_gates_backward')
+        return (dz if ctx.has_zx else None), dz, dc
+
+
+def lstm_gates(zx, zh, c):
+    """(h', c') of a ConvLSTM cell from its gate pre-activations zx + zh (i, f, o, g order).
+
+    ``zx`` (may be None) can be a channel slice of a wider tensor; the HIP
+    kernels run forward and backward in one launch each.
+    """
+    if not zh.is_cuda:
+        raise RuntimeError('lstm_gates runs on the HIP device only (no CPU fallback)')
+    return _LSTMGates.apply(zx, zh, c)
+
+
 def _board_conv_ok(m):
     k = m.kernel_size
     return (m.stride == (1, 1) and m.dilation == (1, 1) and m.groups == 1 and m.padding_mode == 'zeros'
@@ -329,6 +378,8 @@ def accelerate(model):
             setattr(model, name, new)
         else:
             accelerate(child)
+    if hasattr(model, 'use_hip'):   # modules with their own HIP fast path (e.g. envs.geister.DRC)
+        model.use_hip = True
     return model
 
 

@@ -89,6 +89,22 @@ int hrl_conv3x3_forward(const float *x, int64_t M, int64_t C_in, int64_t C_out, 
 int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, int64_t C_out, float *dweight,
                       void *workspace, int64_t workspace_bytes, void *stream);
 
+/*
+ * Fused ConvLSTM cell gates (GeisterNet DRC, handyrl/envs/geister.py:48-63;
+ * replaces the split/sigmoid/tanh/mul/add chain of ConvLSTMCell.forward and
+ * its autograd backward).  Gate pre-activations z = zx + zh in channel order
+ * i, f, o, g: zh (N, 4H, HW) contiguous; zx the same shape with per-sample
+ * stride zx_stride floats (a channel slice of a wider tensor) or NULL.
+ * Forward: gates (N, 4H, HW) = (sigmoid i, sigmoid f, sigmoid o, tanh g);
+ *          c_out = f*c + i*g; h_out = o*tanh(c_out).
+ * Backward: dz (N, 4H, HW) and dc (N, H, HW) from dh / dc_out (either may be NULL = zero).
+ */
+int hrl_lstm_gates_forward(const float *zx, int64_t zx_stride, const float *zh, const float *c, int64_t N, int64_t H,
+                           int64_t HW, float *h_out, float *c_out, float *gates, void *stream);
+int hrl_lstm_gates_backward(const float *gates, const float *c, const float *c_out, const float *dh,
+                            const float *dc_out, int64_t N, int64_t H, int64_t HW, float *dz, float *dc,
+                            void *stream);
+
 #ifdef __cplusplus
 }
 #endif

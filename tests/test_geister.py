@@ -134,3 +134,66 @@ def test_gpu_rnn_compute_loss_matches_reference(golden, cuda):
     losses['total'].backward()
     grads = {n: float((p.grad.double() ** 2).sum()) for n, p in net.named_parameters() if p.grad is not None}
     check_loss(losses, dcnt, grads, meta, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('hw', [(6, 6), (3, 5)])
+def test_lstm_gates_kernel_vs_torch(cuda, hw):
+    """csrc/hrl_lstm.hip vs the fp32 torch ConvLSTM cell tail (geister.py:52-63), forward and backward.
+
+    zx is a channel slice of a wider tensor (the fused x-half convolution); (3, 5)
+    boards take the scalar (non-float4) path.  Tolerance: 2e-6 abs (transcendental ulps).
+    """
+    from handyrl_amd.nn import lstm_gates
+    g = torch.Generator(device=cuda).manual_seed(0)
+    N, H = 37, 32
+    wide = torch.randn(N, 3 * 4 * H, *hw, device=cuda, generator=g).requires_grad_()
+    zh = torch.randn(N, 4 * H, *hw, device=cuda, generator=g).requires_grad_()
+    c = torch.randn(N, H, *hw, device=cuda, generator=g).requires_grad_()
+    dh = torch.randn(N, H, *hw, device=cuda, generator=g)
+    dc = torch.randn(N, H, *hw, device=cuda, generator=g)
+
+    def ref(zx, zh, c):
+        i, f, o, gg = (zx + zh).chunk(4, 1)
+        c2 = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        return torch.sigmoid(o) * torch.tanh(c2), c2
+
+    for use_dc in (True, False):
+        outs, grads = [], []
+        for fn in (lstm_gates, ref):
+            for t in (wide, zh, c):
+                t.grad = None
+            h2, c2 = fn(wide[:, 4 * H:8 * H], zh, c)
+            loss = (h2 * dh).sum() + ((c2 * dc).sum() if use_dc else 0)
+            loss.backward()
+            outs.append((h2.detach(), c2.detach()))
+            grads.append((wide.grad.clone(), zh.grad.clone(), c.grad.clone()))
+        for a, b in zip(outs[0], outs[1]):
+            torch.testing.assert_close(a, b, rtol=0, atol=2e-6)
+        for a, b in zip(grads[0], grads[1]):
+            torch.testing.assert_close(a, b, rtol=0, atol=2e-6)
+        assert float(grads[0][0][:, :4 * H].abs().sum()) == 0.0
+
+
+@pytest.mark.gpu
+def test_drc_hip_path_matches_reference_cells(golden, cuda):
+    """accelerate(GeisterNet) regroups the DRC (x half once, fused gates); same outputs and gradients."""
+    from handyrl_amd.nn import accelerate
+    _, arrays = golden
+    plain = seeded_net().to(cuda)
+    fast = accelerate(seeded_net().to(cuda))
+    assert fast.body.use_hip and not plain.body.use_hip
+    obs, hidden = fwd_inputs(arrays)
+    obs = {k: v.to(cuda) for k, v in obs.items()}
+    res = []
+    for net in (plain, fast):
+        h = ([t.to(cuda) for t in hidden[0]], [t.to(cuda) for t in hidden[1]])
+        out = net(obs, h)
+        loss = out['policy'].square().sum() + out['value'].sum() + sum(t.square().sum() for t in out['hidden'][1])
+        loss.backward()
+        res.append((out, {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None}))
+    check_forward(res[1][0], arrays, atol=2e-5)
+    assert set(res[0][1]) == set(res[1][1])
+    # fp32 reassociation (x/h halves summed in the gate kernel, HIP BN): norm-relative 1e-4
+    errs = {n: float((res[1][1][n] - gp).norm() / gp.norm().clamp(min=1e-12)) for n, gp in res[0][1].items()}
+    assert max(errs.values()) < 1e-4, sorted(errs.items(), key=lambda kv: -kv[1])[:5]
