@@ -101,6 +101,52 @@ def time_scan(device, B, T, iters, cold=False):
             'GBps': nbytes / (ms * 1e-3) / 1e9, 'cold': cold}
 
 
+MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+
+
+def time_conv(device, M, iters=20):
+    """The step's dominant net kernel: the 32->32 3x3-board MFMA conv (csrc/hrl_conv.hip) at M = B*T rows.
+
+    Algorithmic FLOPs per launch: 49 on-board 32x32 tap blocks x 2 per sample
+    (the 32 off-board blocks of the dense 9x9 board matrix are not work).
+    Timed with HIP events on the launch stream over `iters` back-to-back launches.
+    """
+    from handyrl_amd import _native
+    lib = _native.load()
+    g = torch.Generator(device=device).manual_seed(3)
+    x = torch.randn(M, 288, device=device, generator=g)
+    w = torch.randn(32, 32, 3, 3, device=device, generator=g) * 0.1
+    b = torch.randn(32, device=device, generator=g)
+    y = torch.empty_like(x)
+    ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
+    stream = torch.cuda.current_stream(device)
+    P = _native.ptr
+
+    def launch():
+        _native.check(lib.hrl_conv3x3_forward(P(x), M, 32, 32, P(w), P(b), 0, P(y), P(ws), ws_bytes,
+                                              _native.stream_of(device)), 'hrl_conv3x3_forward')
+    for _ in range(3):
+        launch()
+    start = torch.cuda.Event(enable_timing=True)
+    end = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    start.record(stream)
+    for _ in range(iters):
+        launch()
+    end.record(stream)
+    end.synchronize()
+    us = start.elapsed_time(end) * 1e3 / iters
+    flops = 2.0 * M * 49 * 32 * 32
+    tf = flops / (us * 1e-6) / 1e12
+    return {'kernel': 'conv3x3_reg_kernel (+ 2 us weight pack)', 'bound': 'mfma', 'achieved': round(tf, 1),
+            'peak': MFMA_F32_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': round(tf / MFMA_F32_PEAK_TFLOPS, 4),
+            'flops_per_launch': flops, 'us_per_launch': round(us, 2), 'M': M,
+            'launches_per_step': '3 forward + 3 input-gradient (same kernel) + 3 weight-gradient',
+            'note': 'fp32 MFMA at the clock the chip holds under this load (DVFS); SURVEY D3: reported '
+                    'beside, not instead of, the scan roofline'}
+
+
 def pmc_traffic(B, T):
     """HBM bytes per launch of the scan from the committed rocprofv3 PMC passes (profiles/), or None."""
     path = os.path.join(ROOT, 'profiles', 'r01_scan_pmc.json')
@@ -316,6 +362,7 @@ def main():
                              'us_per_launch': round(cold['us_per_launch'], 2),
                              'traffic': pmc_traffic(cold['B'], T)},
         }
+        net_roof = time_conv(device, B * T)
         cpu = cpu_baseline() if (opts.cpu_baseline and world == 1) else None
         t9 = secondary_t9(device) if (opts.secondary and world == 1) else None
         ro = secondary_rollout(device) if (opts.secondary and world == 1) else None
@@ -339,6 +386,7 @@ def main():
                        'global_batch': world * B, 'per_gpu_batch': B, 'seq_len': T, 'players': 2,
                        'parallelism': 'dp%d' % world, 'hip_graph': use_graph},
             'roofline': roof,
+            'net_roofline': net_roof,
             'cpu_baseline': cpu,
             'loss_per_dcnt': {k: v / max(stats.get('dcnt', 1.0), 1e-9) for k, v in stats.items()
                               if k in ('p', 'v', 'ent', 'total')},

@@ -10,20 +10,21 @@
 //
 // with v_mfma_f32_16x16x4_f32 (exact fp32 products, k-ordered accumulation).
 //
-// conv3x3_kernel (forward; also the input gradient, run on dY with the
+// conv3x3_reg_kernel (forward; also the input gradient, run on dY with the
 // kernel flipped and transposed — a 'same' conv's adjoint):
 //   * a workgroup = 4 waves; each wave owns a 16-row tile of the (N, C*9)
 //     NCHW rows per iteration and walks row tiles grid-stride;
-//   * the packed weights [tap][co-tile][ci][16] (36 KB) are staged in LDS once
-//     per workgroup; the B fragment of lane l (k = l>>4, j = l&15) is then a
-//     bank-conflict-free ds_read_b32;
+//   * the packed weights [tap][co-tile][ci][16] live in VGPRs (144 per lane);
 //   * each wave's A tile is 16 rows x 288 floats in LDS with a row stride of
 //     290 (== 2 mod 32), conflict-free for the A fragment reads;
 //   * the next row tile's global loads are issued before the MFMA loop and
 //     land in registers while the MFMAs run;
-//   * 9 output cells x 2 column tiles = 18 accumulators (72 AGPRs); the
-//     epilogue stages the 16x288 output tile through the A buffer and leaves
-//     with coalesced 16-byte stores.
+//   * 9 output cells x 2 column tiles = 18 accumulators; the epilogue stages
+//     the 16x288 output tile through LDS and leaves with coalesced 16-byte
+//     stores, issued one iteration later (see the kernel).
+//   Measured (tools/conv_bench.py, M = 131072): 125-138 us per launch, the
+//   784 MFMAs per tile at ~1.7 GHz, the clock the chip holds under this
+//   MFMA+LDS load on random data (MI355X_MICROARCH.md, DVFS give-back).
 // conv3x3_wgrad_kernel (weight gradient): dW[tap][ci][co] accumulates
 //   X^T dY over (row, (p,q) pairs with that tap) per wave (36 accumulators);
 //   the 4 waves fold through LDS, and a wide reduce folds the per-workgroup
@@ -63,106 +64,117 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 
 // ------------------------------------------------------------------ forward / input gradient
 // x: (M, 288) rows; wpk: packed [tap][ct][ci][16] = W'[tap][ci][ct*16+j]; y: (M, 288)
-__global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restrict__ x, int64_t M,
-                                                           const float *__restrict__ wpk,
-                                                           const float *__restrict__ bias,
-                                                           float *__restrict__ y) {
-    __shared__ float w_lds[kTaps * 2 * kC * 16];           // 36 KB
-    __shared__ float a_lds[kWaves][kTile * kStride];       // 4 x 18.1 KB
+// Forward / input gradient, the production kernel.
+//  * each wave keeps ALL packed weight fragments in VGPRs (144 floats per lane:
+//    9 taps x 2 column tiles x 8 k-steps); the MFMA loop reads only the A
+//    fragment from LDS, one ds_read per up to 18 MFMAs;
+//  * p-major MFMA order: one A fragment feeds every output cell q it reaches
+//    (up to 18 independent accumulators), hiding the 40-cycle dependent-MFMA
+//    latency; each accumulator still sums in (p, s) order;
+//  * software-pipelined epilogue: tile i's outputs go to a second LDS buffer
+//    and are stored to HBM during iteration i+1, BEFORE tile i+2's loads are
+//    issued.  Loads and stores share one in-order vmcnt counter, so storing at
+//    the end of an iteration made the next iteration's wait for its staged
+//    loads also drain every store (an HBM write latency per tile).
+__global__ __launch_bounds__(kThreads) void conv3x3_reg_kernel(const float *__restrict__ x, int64_t M,
+                                                               const float *__restrict__ wpk,
+                                                               const float *__restrict__ bias,
+                                                               float *__restrict__ y) {
+    __shared__ float a_lds[kWaves][kTile * kStride];       // 4 x 18.1 KB: staged inputs
+    __shared__ float o_lds[kWaves][kTile * kStride];       // 4 x 18.1 KB: outputs awaiting their store
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < kTaps * 2 * kC * 16; i += kThreads) w_lds[i] = wpk[i];
+    float wreg[kTaps][2][kC / 4];
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int s = 0; s < kC / 4; ++s) wreg[t][ct][s] = wpk[((t * 2 + ct) * kC + 4 * s) * 16 + lane];
 
     const int64_t ntiles = (M + kTile - 1) / kTile;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
     float *as = a_lds[wave];
-
-    // per-lane column/bias for the epilogue: lane owns output column j = lane&15 of each tile
+    float *os = o_lds[wave];
+    const int64_t lim = M * kRow;
     float bias_v[2] = {0.f, 0.f};
     if (bias) {
         bias_v[0] = bias[lane & 15];
         bias_v[1] = bias[16 + (lane & 15)];
     }
-
     float4 stage[kVec];
     auto issue = [&](int64_t t) {
-        // rows t*16 .. t*16+15 are contiguous: 16*288 floats = 1152 float4
         const int64_t base = t * kTile * kRow;
-        const int64_t lim = M * kRow;
 #pragma unroll
         for (int k = 0; k < kVec; ++k) {
             const int64_t e = base + (int64_t)(k * 64 + lane) * 4;
-            const int64_t ec = e < lim ? e : lim - 4;          // clamp (ragged last tile), no branch
+            const int64_t ec = e < lim ? e : lim - 4;
             stage[k] = *reinterpret_cast<const float4 *>(x + ec);
         }
     };
-    if (tile < ntiles) issue(tile);
-    __syncthreads();   // weights in LDS
-
-    for (; tile < ntiles; tile += stride) {
-        // staged tile -> LDS (padded rows)
+    auto store = [&](int64_t t) {   // o_lds -> y rows of tile t (coalesced 16-byte stores)
+        const int64_t obase = t * kTile * kRow;
 #pragma unroll
         for (int k = 0; k < kVec; ++k) {
-            const int e = (k * 64 + lane) * 4;                 // element within the tile
-            const int r = e / kRow, c = e - r * kRow;          // kRow % 4 == 0: one row per float4
+            const int e = (k * 64 + lane) * 4;
+            const int r = e / kRow, c = e - r * kRow;
+            const float *sp = os + r * kStride + c;
+            if (obase + e < lim) *reinterpret_cast<float4 *>(y + obase + e) = make_float4(sp[0], sp[1], sp[2], sp[3]);
+        }
+    };
+    if (tile < ntiles) issue(tile);
+
+    int64_t pending = -1;   // tile whose outputs sit in o_lds
+    for (; tile < ntiles; tile += stride) {
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int e = (k * 64 + lane) * 4;
+            const int r = e / kRow, c = e - r * kRow;
             float *d = as + r * kStride + c;
             d[0] = stage[k].x; d[1] = stage[k].y; d[2] = stage[k].z; d[3] = stage[k].w;
         }
-        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes done
+        if (pending >= 0) store(pending);     // older than the loads below
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): LDS writes landed, o_lds reads done
         __builtin_amdgcn_wave_barrier();
         const int64_t next = tile + stride;
-        if (next < ntiles) issue(next);       // in flight during the MFMAs
+        if (next < ntiles) issue(next);
 
         f32x4 acc[kCells][2];
 #pragma unroll
         for (int q = 0; q < kCells; ++q) acc[q][0] = acc[q][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        const int ar = lane & 15;          // A row (sample within the tile)
-        const int ak = lane >> 4;          // A/B k within the 4-wide step
+        const int ar = lane & 15;
+        const int ak = lane >> 4;
         const float *arow = as + ar * kStride;
 #pragma unroll
-        for (int q = 0; q < kCells; ++q) {
+        for (int p = 0; p < kCells; ++p) {
 #pragma unroll
-            for (int p = 0; p < kCells; ++p) {
-                const int tap = tap_of(p, q);
-                if (tap < 0) continue;
-                const float *wt0 = w_lds + ((tap * 2 + 0) * kC) * 16 + ak * 16 + (lane & 15);
-                const float *wt1 = w_lds + ((tap * 2 + 1) * kC) * 16 + ak * 16 + (lane & 15);
+            for (int s = 0; s < kC / 4; ++s) {
+                const float a = arow[(4 * s + ak) * kCells + p];
 #pragma unroll
-                for (int s = 0; s < kC / 4; ++s) {
-                    const float a = arow[(4 * s + ak) * kCells + p];
-                    acc[q][0] = mfma(a, wt0[s * 64], acc[q][0]);
-                    acc[q][1] = mfma(a, wt1[s * 64], acc[q][1]);
+                for (int q = 0; q < kCells; ++q) {
+                    const int tap = tap_of(p, q);
+                    if (tap < 0) continue;
+                    acc[q][0] = mfma(a, wreg[tap][0][s], acc[q][0]);
+                    acc[q][1] = mfma(a, wreg[tap][1][s], acc[q][1]);
                 }
             }
         }
-
-        // epilogue: accumulators -> LDS tile [row][co*9 + q] -> coalesced stores
-        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int q = 0; q < kCells; ++q)
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = (lane >> 4) * 4 + r;       // C/D: row = (lane>>4)*4 + reg
-                    const int co = ct * 16 + (lane & 15);      //      col = lane & 15
-                    as[row * kStride + co * kCells + q] = acc[q][ct][r] + bias_v[ct];
+                    const int row = (lane >> 4) * 4 + r;
+                    const int co = ct * 16 + (lane & 15);
+                    os[row * kStride + co * kCells + q] = acc[q][ct][r] + bias_v[ct];
                 }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-        const int64_t obase = tile * kTile * kRow;
-        const int64_t lim = M * kRow;
-#pragma unroll
-        for (int k = 0; k < kVec; ++k) {
-            const int e = (k * 64 + lane) * 4;
-            const int r = e / kRow, c = e - r * kRow;
-            const float *sp = as + r * kStride + c;
-            if (obase + e < lim) *reinterpret_cast<float4 *>(y + obase + e) = make_float4(sp[0], sp[1], sp[2], sp[3]);
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
+        pending = tile;
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // this wave's o_lds writes and a_lds reads done
         __builtin_amdgcn_wave_barrier();
     }
+    if (pending >= 0) store(pending);
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -301,7 +313,7 @@ __global__ void conv3x3_pack_kernel(const float *__restrict__ w, int flip, float
     wpk[i] = v;
 }
 
-// One 4-wave workgroup per CU (LDS: 111 KB forward, 148 KB weight gradient);
+// One 4-wave workgroup per CU (LDS: 145 KB forward, 148 KB weight gradient);
 // the waves walk row tiles grid-stride so the next tile's loads overlap MFMAs.
 constexpr int kGrid = 256;
 
@@ -339,7 +351,7 @@ int hrl_conv3x3_forward(const float *x, int64_t M, int64_t C_in, int64_t C_out, 
                        wpk);
     int rc = status();
     if (rc) return rc;
-    hipLaunchKernelGGL(conv3x3_kernel, dim3(grid_for(M)), dim3(kThreads), 0, s, x, M, wpk, bias, y);
+    hipLaunchKernelGGL(conv3x3_reg_kernel, dim3(grid_for(M)), dim3(kThreads), 0, s, x, M, wpk, bias, y);
     return status();
 }
 
