@@ -64,13 +64,22 @@ SIGNATURES = {
                                          ctypes.c_void_p]),
     'hrl_colsum_workspace_bytes': (ctypes.c_int64, [_i64, _i64]),
     'hrl_colsum': (ctypes.c_int, [_f32p, _i64, _i64, _f32p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_bn_finalize_stats': (ctypes.c_int, [ctypes.c_void_p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p,
+                                             ctypes.c_double, ctypes.c_double, _f32p, _f32p, _f32p, _f32p,
+                                             ctypes.c_void_p]),
+    'hrl_bn_apply': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _f32p, _f32p, ctypes.c_int, _f32p, ctypes.c_void_p]),
+    'hrl_conv3x3_stats_blocks': (ctypes.c_int64, [_i64]),
+    'hrl_conv3x3_forward_ex': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_int, _f32p,
+                                              ctypes.c_void_p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_conv3x3_wgrad_ex': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _i64, _f32p, ctypes.c_void_p, _i64,
+                                            ctypes.c_void_p]),
     'hrl_lstm_gates_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p,
                                               ctypes.c_void_p]),
     'hrl_lstm_gates_backward': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p,
                                                ctypes.c_void_p]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib = None
 

@@ -460,6 +460,29 @@ int hrl_bn_forward_train(const float *x, int64_t N, int64_t C, int64_t HW, const
     return launch_status();
 }
 
+int hrl_bn_finalize_stats(const double *part, int64_t nparts, int64_t C, int64_t count, const float *weight,
+                          const float *bias, float *running_mean, float *running_var, double momentum, double eps,
+                          float *save_mean, float *save_invstd, float *alpha, float *beta, void *stream) {
+    if (!part || !save_mean || !save_invstd || !alpha || !beta || nparts < 1 || C < 1 || count < 1)
+        return HRL_EINVAL;
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)C), dim3(kThreads), 0, static_cast<hipStream_t>(stream), 0,
+                       part, (int)nparts, (int)C, (double)count, weight, bias, running_mean, running_var,
+                       (float)momentum, eps, save_mean, save_invstd, alpha, beta, (float *)nullptr, (float *)nullptr);
+    return launch_status();
+}
+
+int hrl_bn_apply(const float *x, int64_t N, int64_t C, int64_t HW, const float *alpha, const float *beta, int relu,
+                 float *y, void *stream) {
+    if (!x || !y || !alpha || !beta) return HRL_EINVAL;
+    const bool vec = (C * HW) % 4 == 0 && aligned16(x) && aligned16(y);
+    Geo g;
+    if (!make_geo(N, C, HW, vec ? 4 : 1, g)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (vec) relu ? launch_apply<4, true>(g, s, x, alpha, beta, y) : launch_apply<4, false>(g, s, x, alpha, beta, y);
+    else relu ? launch_apply<1, true>(g, s, x, alpha, beta, y) : launch_apply<1, false>(g, s, x, alpha, beta, y);
+    return launch_status();
+}
+
 int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW, const float *weight,
                     const float *bias, const float *save_mean, const float *save_invstd, int relu, float *dx,
                     float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream) {

@@ -10,18 +10,20 @@
 //
 // with v_mfma_f32_16x16x4_f32 (exact fp32 products, k-ordered accumulation).
 //
-// conv3x3_reg_kernel (forward; also the input gradient, run on dY with the
-// kernel flipped and transposed — a 'same' conv's adjoint):
+// conv3x3_kernel<PRO, STATS> (forward; also the input gradient, run on dY
+// with the kernel flipped and transposed — a 'same' conv's adjoint):
 //   * a workgroup = 4 waves; each wave owns a 16-row tile of the (N, C*9)
 //     NCHW rows per iteration and walks row tiles grid-stride;
-//   * the packed weights [tap][co-tile][ci][16] live in VGPRs (144 per lane);
+//   * the packed weights [tap][co-tile][ci][16] (36 KB) sit in LDS;
 //   * each wave's A tile is 16 rows x 288 floats in LDS with a row stride of
 //     290 (== 2 mod 32), conflict-free for the A fragment reads;
 //   * the next row tile's global loads are issued before the MFMA loop and
 //     land in registers while the MFMAs run;
 //   * 9 output cells x 2 column tiles = 18 accumulators; the epilogue stages
 //     the 16x288 output tile through LDS and leaves with coalesced 16-byte
-//     stores, issued one iteration later (see the kernel).
+//     stores;
+//   * optional fusions with the BatchNorm+ReLU around it (PRO / STATS below)
+//     so a conv -> BN -> ReLU chain writes each activation once.
 //   Measured (tools/conv_bench.py, M = 131072): 125-138 us per launch, the
 //   784 MFMAs per tile at ~1.7 GHz, the clock the chip holds under this
 //   MFMA+LDS load on random data (MI355X_MICROARCH.md, DVFS give-back).
@@ -64,39 +66,44 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 
 // ------------------------------------------------------------------ forward / input gradient
 // x: (M, 288) rows; wpk: packed [tap][ct][ci][16] = W'[tap][ci][ct*16+j]; y: (M, 288)
-// Forward / input gradient, the production kernel.
-//  * each wave keeps ALL packed weight fragments in VGPRs (144 floats per lane:
-//    9 taps x 2 column tiles x 8 k-steps); the MFMA loop reads only the A
-//    fragment from LDS, one ds_read per up to 18 MFMAs;
+// Forward / input gradient.
+//  * the packed weights [tap][co-tile][ci][16] (36 KB) are staged in LDS once
+//    per workgroup; the B fragment of lane l (k = l>>4, j = l&15) is a
+//    bank-conflict-free ds_read_b32;
 //  * p-major MFMA order: one A fragment feeds every output cell q it reaches
 //    (up to 18 independent accumulators), hiding the 40-cycle dependent-MFMA
-//    latency; each accumulator still sums in (p, s) order;
-//  * software-pipelined epilogue: tile i's outputs go to a second LDS buffer
-//    and are stored to HBM during iteration i+1, BEFORE tile i+2's loads are
-//    issued.  Loads and stores share one in-order vmcnt counter, so storing at
-//    the end of an iteration made the next iteration's wait for its staged
-//    loads also drain every store (an HBM write latency per tile).
-__global__ __launch_bounds__(kThreads) void conv3x3_reg_kernel(const float *__restrict__ x, int64_t M,
-                                                               const float *__restrict__ wpk,
-                                                               const float *__restrict__ bias,
-                                                               float *__restrict__ y) {
-    __shared__ float a_lds[kWaves][kTile * kStride];       // 4 x 18.1 KB: staged inputs
-    __shared__ float o_lds[kWaves][kTile * kStride];       // 4 x 18.1 KB: outputs awaiting their store
+//    latency; each accumulator sums in (p, s) order;
+//  PRO:   the input is the previous block's raw conv output and the kernel
+//         applies that block's BatchNorm+ReLU, relu(x*alpha[c] + beta[c]),
+//         while staging it (the activation is never written to HBM);
+//  STATS: the epilogue accumulates per-channel sum / sum of squares of the
+//         output (fp64) and writes one partial per workgroup,
+//         stats[block][c][2], the layout bn_finalize_kernel folds.
+template <bool PRO, bool STATS>
+__global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restrict__ x, int64_t M,
+                                                           const float *__restrict__ wpk,
+                                                           const float *__restrict__ bias,
+                                                           const float *__restrict__ in_alpha,
+                                                           const float *__restrict__ in_beta,
+                                                           float *__restrict__ y, double *__restrict__ stats) {
+    __shared__ float w_lds[kTaps * 2 * kC * 16];           // 36 KB
+    __shared__ float a_lds[kWaves][kTile * kStride];       // 4 x 18.1 KB
+    __shared__ float ab_lds[2 * kC];                       // PRO: alpha | beta
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    float wreg[kTaps][2][kC / 4];
-#pragma unroll
-    for (int t = 0; t < kTaps; ++t)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-            for (int s = 0; s < kC / 4; ++s) wreg[t][ct][s] = wpk[((t * 2 + ct) * kC + 4 * s) * 16 + lane];
+    for (int i = threadIdx.x; i < kTaps * 2 * kC * 16; i += kThreads) w_lds[i] = wpk[i];
+    if constexpr (PRO) {
+        if (threadIdx.x < kC) {
+            ab_lds[threadIdx.x] = in_alpha[threadIdx.x];
+            ab_lds[kC + threadIdx.x] = in_beta[threadIdx.x];
+        }
+    }
+    double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};   // STATS: this lane's two output channels
 
     const int64_t ntiles = (M + kTile - 1) / kTile;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
     float *as = a_lds[wave];
-    float *os = o_lds[wave];
     const int64_t lim = M * kRow;
     float bias_v[2] = {0.f, 0.f};
     if (bias) {
@@ -105,47 +112,48 @@ __global__ __launch_bounds__(kThreads) void conv3x3_reg_kernel(const float *__re
     }
     float4 stage[kVec];
     auto issue = [&](int64_t t) {
+        // rows t*16 .. t*16+15 are contiguous: 16*288 floats = 1152 float4
         const int64_t base = t * kTile * kRow;
 #pragma unroll
         for (int k = 0; k < kVec; ++k) {
             const int64_t e = base + (int64_t)(k * 64 + lane) * 4;
-            const int64_t ec = e < lim ? e : lim - 4;
+            const int64_t ec = e < lim ? e : lim - 4;          // clamp (ragged last tile), no branch
             stage[k] = *reinterpret_cast<const float4 *>(x + ec);
         }
     };
-    auto store = [&](int64_t t) {   // o_lds -> y rows of tile t (coalesced 16-byte stores)
-        const int64_t obase = t * kTile * kRow;
-#pragma unroll
-        for (int k = 0; k < kVec; ++k) {
-            const int e = (k * 64 + lane) * 4;
-            const int r = e / kRow, c = e - r * kRow;
-            const float *sp = os + r * kStride + c;
-            if (obase + e < lim) *reinterpret_cast<float4 *>(y + obase + e) = make_float4(sp[0], sp[1], sp[2], sp[3]);
-        }
-    };
     if (tile < ntiles) issue(tile);
+    __syncthreads();   // weights (and alpha/beta) in LDS
 
-    int64_t pending = -1;   // tile whose outputs sit in o_lds
     for (; tile < ntiles; tile += stride) {
+        // staged tile -> LDS (padded rows), through the previous block's BN+ReLU with PRO
 #pragma unroll
         for (int k = 0; k < kVec; ++k) {
-            const int e = (k * 64 + lane) * 4;
-            const int r = e / kRow, c = e - r * kRow;
+            const int e = (k * 64 + lane) * 4;                 // element within the tile
+            const int r = e / kRow, c = e - r * kRow;          // kRow % 4 == 0: one row per float4
             float *d = as + r * kStride + c;
-            d[0] = stage[k].x; d[1] = stage[k].y; d[2] = stage[k].z; d[3] = stage[k].w;
+            float v[4] = {stage[k].x, stage[k].y, stage[k].z, stage[k].w};
+            if constexpr (PRO) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int ch = (c + j) / kCells;
+                    const float t = v[j] * ab_lds[ch] + ab_lds[kC + ch];   // bn_apply_kernel's float ops
+                    v[j] = t < 0.f ? 0.f : t;
+                }
+            }
+            d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
         }
-        if (pending >= 0) store(pending);     // older than the loads below
-        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): LDS writes landed, o_lds reads done
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes done
         __builtin_amdgcn_wave_barrier();
         const int64_t next = tile + stride;
-        if (next < ntiles) issue(next);
+        if (next < ntiles) issue(next);       // in flight during the MFMAs
 
         f32x4 acc[kCells][2];
 #pragma unroll
         for (int q = 0; q < kCells; ++q) acc[q][0] = acc[q][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        const int ar = lane & 15;
-        const int ak = lane >> 4;
+        const int ar = lane & 15;          // A row (sample within the tile)
+        const int ak = lane >> 4;          // A/B k within the 4-wide step
         const float *arow = as + ar * kStride;
+        const float *wl = w_lds + ak * 16 + (lane & 15);
 #pragma unroll
         for (int p = 0; p < kCells; ++p) {
 #pragma unroll
@@ -155,32 +163,72 @@ __global__ __launch_bounds__(kThreads) void conv3x3_reg_kernel(const float *__re
                 for (int q = 0; q < kCells; ++q) {
                     const int tap = tap_of(p, q);
                     if (tap < 0) continue;
-                    acc[q][0] = mfma(a, wreg[tap][0][s], acc[q][0]);
-                    acc[q][1] = mfma(a, wreg[tap][1][s], acc[q][1]);
+                    acc[q][0] = mfma(a, wl[((tap * 2 + 0) * kC) * 16 + s * 64], acc[q][0]);
+                    acc[q][1] = mfma(a, wl[((tap * 2 + 1) * kC) * 16 + s * 64], acc[q][1]);
                 }
             }
         }
+
+        // epilogue: accumulators -> LDS tile [row][co*9 + q] -> coalesced stores
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int q = 0; q < kCells; ++q)
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = (lane >> 4) * 4 + r;
-                    const int co = ct * 16 + (lane & 15);
-                    os[row * kStride + co * kCells + q] = acc[q][ct][r] + bias_v[ct];
+                    const int row = (lane >> 4) * 4 + r;       // C/D: row = (lane>>4)*4 + reg
+                    const int co = ct * 16 + (lane & 15);      //      col = lane & 15
+                    const float v = acc[q][ct][r] + bias_v[ct];
+                    as[row * kStride + co * kCells + q] = v;
+                    if constexpr (STATS) {
+                        if (tile * kTile + row < M) {
+                            s1[ct] += (double)v;
+                            s2[ct] += (double)v * (double)v;
+                        }
+                    }
                 }
-        pending = tile;
-        __builtin_amdgcn_s_waitcnt(0xc07f);   // this wave's o_lds writes and a_lds reads done
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int64_t obase = tile * kTile * kRow;
+#pragma unroll
+        for (int k = 0; k < kVec; ++k) {
+            const int e = (k * 64 + lane) * 4;
+            const int r = e / kRow, c = e - r * kRow;
+            const float *sp = as + r * kStride + c;
+            if (obase + e < lim) *reinterpret_cast<float4 *>(y + obase + e) = make_float4(sp[0], sp[1], sp[2], sp[3]);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
     }
-    if (pending >= 0) store(pending);
+    if constexpr (STATS) {
+        // fold the lanes sharing a channel (4 row groups) and the 4 waves in a fixed order
+        __syncthreads();
+        double *red = reinterpret_cast<double *>(&a_lds[0][0]);   // [wave][group][32][2]
+        const int grp = lane >> 4;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+            const int co = ct * 16 + (lane & 15);
+            red[((wave * 4 + grp) * kC + co) * 2 + 0] = s1[ct];
+            red[((wave * 4 + grp) * kC + co) * 2 + 1] = s2[ct];
+        }
+        __syncthreads();
+        if (threadIdx.x < 2 * kC) {
+            const int co = threadIdx.x >> 1, k = threadIdx.x & 1;
+            double t = 0.0;
+            for (int i = 0; i < kWaves * 4; ++i) t += red[(i * kC + co) * 2 + k];
+            stats[((int64_t)blockIdx.x * kC + co) * 2 + k] = t;
+        }
+    }
 }
 
 // ------------------------------------------------------------------ weight gradient
 // dW[tap][ci][co] = sum_rows sum_{(p,q): tap(p,q) = tap} x[row, ci, p] * dy[row, co, q]
 // MFMA C tile = 16 ci x 16 co; A[i = ci][k = row], B[k = row][j = co]
+template <bool PRO>
 __global__ __launch_bounds__(kThreads) void conv3x3_wgrad_kernel(const float *__restrict__ x,
+                                                                 const float *__restrict__ in_alpha,
+                                                                 const float *__restrict__ in_beta,
                                                                  const float *__restrict__ dy, int64_t M,
                                                                  float *__restrict__ partial) {
     // one LDS array: per-wave x and dy tiles during the loop, the 4 wave partials after it
@@ -190,6 +238,14 @@ __global__ __launch_bounds__(kThreads) void conv3x3_wgrad_kernel(const float *__
     const int wave = threadIdx.x >> 6;
     float *xs = lds + wave * kTile * kStride;
     float *gs = lds + (kWaves + wave) * kTile * kStride;
+    __shared__ float ab_lds[2 * kC];   // PRO: x is a raw conv output, staged as relu(x*alpha + beta)
+    if constexpr (PRO) {
+        if (threadIdx.x < kC) {
+            ab_lds[threadIdx.x] = in_alpha[threadIdx.x];
+            ab_lds[kC + threadIdx.x] = in_beta[threadIdx.x];
+        }
+        __syncthreads();
+    }
     const int64_t ntiles = (M + kTile - 1) / kTile;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
 
@@ -219,7 +275,16 @@ __global__ __launch_bounds__(kThreads) void conv3x3_wgrad_kernel(const float *__
             const int e = (k * 64 + lane) * 4;
             const int r = e / kRow, c = e - r * kRow;
             float *d = xs + r * kStride + c;
-            d[0] = sx[k].x; d[1] = sx[k].y; d[2] = sx[k].z; d[3] = sx[k].w;
+            float v[4] = {sx[k].x, sx[k].y, sx[k].z, sx[k].w};
+            if constexpr (PRO) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int ch = (c + j) / kCells;
+                    const float t = v[j] * ab_lds[ch] + ab_lds[kC + ch];
+                    v[j] = t < 0.f ? 0.f : t;
+                }
+            }
+            d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
             float *h = gs + r * kStride + c;
             h[0] = sg[k].x; h[1] = sg[k].y; h[2] = sg[k].z; h[3] = sg[k].w;
         }
@@ -313,7 +378,7 @@ __global__ void conv3x3_pack_kernel(const float *__restrict__ w, int flip, float
     wpk[i] = v;
 }
 
-// One 4-wave workgroup per CU (LDS: 145 KB forward, 148 KB weight gradient);
+// One 4-wave workgroup per CU (LDS: 109 KB forward, 145 KB weight gradient);
 // the waves walk row tiles grid-stride so the next tile's loads overlap MFMAs.
 constexpr int kGrid = 256;
 
@@ -339,35 +404,70 @@ int64_t hrl_conv3x3_workspace_bytes(int64_t M) {
     return (int64_t)grid_for(M) * kTaps * kC * kC * 4 + (int64_t)kTaps * 2 * kC * 16 * 4 * 2;
 }
 
-int hrl_conv3x3_forward(const float *x, int64_t M, int64_t C_in, int64_t C_out, const float *weight,
-                        const float *bias, int flip, float *y, void *workspace, int64_t workspace_bytes,
-                        void *stream) {
-    if (C_in != kC || C_out != kC || M < 1 || !x || !weight || !y || !workspace) return HRL_EINVAL;
+int64_t hrl_conv3x3_stats_blocks(int64_t M) { return M < 1 ? -1 : grid_for(M); }
+
+int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, const float *in_beta,
+                           const float *weight, const float *bias, int flip, float *y, double *stats,
+                           void *workspace, int64_t workspace_bytes, void *stream) {
+    if (M < 1 || !x || !weight || !y || !workspace) return HRL_EINVAL;
     if (!aligned16(x) || !aligned16(y) || workspace_bytes < hrl_conv3x3_workspace_bytes(M)) return HRL_EINVAL;
-    if (flip && bias) return HRL_EINVAL;
+    if ((in_alpha == nullptr) != (in_beta == nullptr)) return HRL_EINVAL;
+    if (flip && (bias || in_alpha || stats)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     float *wpk = static_cast<float *>(workspace);
     hipLaunchKernelGGL(conv3x3_pack_kernel, dim3((kTaps * 2 * kC * 16 + 255) / 256), dim3(256), 0, s, weight, flip,
                        wpk);
     int rc = status();
     if (rc) return rc;
-    hipLaunchKernelGGL(conv3x3_reg_kernel, dim3(grid_for(M)), dim3(kThreads), 0, s, x, M, wpk, bias, y);
+    const dim3 grid(grid_for(M)), block(kThreads);
+    if (in_alpha && stats)
+        hipLaunchKernelGGL((conv3x3_kernel<true, true>), grid, block, 0, s, x, M, wpk, bias, in_alpha, in_beta,
+                           y, stats);
+    else if (in_alpha)
+        hipLaunchKernelGGL((conv3x3_kernel<true, false>), grid, block, 0, s, x, M, wpk, bias, in_alpha, in_beta,
+                           y, stats);
+    else if (stats)
+        hipLaunchKernelGGL((conv3x3_kernel<false, true>), grid, block, 0, s, x, M, wpk, bias, in_alpha, in_beta,
+                           y, stats);
+    else
+        hipLaunchKernelGGL((conv3x3_kernel<false, false>), grid, block, 0, s, x, M, wpk, bias, in_alpha,
+                           in_beta, y, stats);
     return status();
 }
 
-int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, int64_t C_out, float *dweight,
-                      void *workspace, int64_t workspace_bytes, void *stream) {
-    if (C_in != kC || C_out != kC || M < 1 || !x || !dy || !dweight || !workspace) return HRL_EINVAL;
+int hrl_conv3x3_forward(const float *x, int64_t M, int64_t C_in, int64_t C_out, const float *weight,
+                        const float *bias, int flip, float *y, void *workspace, int64_t workspace_bytes,
+                        void *stream) {
+    if (C_in != kC || C_out != kC) return HRL_EINVAL;
+    return hrl_conv3x3_forward_ex(x, M, nullptr, nullptr, weight, bias, flip, y, nullptr, workspace,
+                                  workspace_bytes, stream);
+}
+
+int hrl_conv3x3_wgrad_ex(const float *x, const float *in_alpha, const float *in_beta, const float *dy, int64_t M,
+                         float *dweight, void *workspace, int64_t workspace_bytes, void *stream) {
+    if (M < 1 || !x || !dy || !dweight || !workspace) return HRL_EINVAL;
+    if ((in_alpha == nullptr) != (in_beta == nullptr)) return HRL_EINVAL;
     if (!aligned16(x) || !aligned16(dy) || workspace_bytes < hrl_conv3x3_workspace_bytes(M)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int grid = grid_for(M);
     float *partial = static_cast<float *>(workspace) + kTaps * 2 * kC * 16 * 2;
-    hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(grid), dim3(kThreads), 0, s, x, dy, M, partial);
+    if (in_alpha)
+        hipLaunchKernelGGL((conv3x3_wgrad_kernel<true>), dim3(grid), dim3(kThreads), 0, s, x, in_alpha, in_beta, dy,
+                           M, partial);
+    else
+        hipLaunchKernelGGL((conv3x3_wgrad_kernel<false>), dim3(grid), dim3(kThreads), 0, s, x, in_alpha, in_beta,
+                           dy, M, partial);
     int rc = status();
     if (rc) return rc;
     hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, partial, grid,
                        dweight);
     return status();
+}
+
+int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, int64_t C_out, float *dweight,
+                      void *workspace, int64_t workspace_bytes, void *stream) {
+    if (C_in != kC || C_out != kC) return HRL_EINVAL;
+    return hrl_conv3x3_wgrad_ex(x, nullptr, nullptr, dy, M, dweight, workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

@@ -416,11 +416,134 @@ class _MultiBoardConv(nn.Module):
         return tuple(outs)
 
 
+class _BoardChain(torch.autograd.Function):
+    """A chain of [3x3 conv 32->32 (no bias) -> BatchNorm (training) -> ReLU] blocks on 3x3 boards.
+
+    The TicTacToe body (tictactoe.py:57-65).  Fused around the MFMA conv
+    (csrc/hrl_conv.hip, conv3x3_kernel<PRO, STATS>): each conv's epilogue
+    emits the BatchNorm statistics of its output, and the next conv (and, in
+    backward, the weight-gradient kernel) applies the BatchNorm+ReLU to its
+    input while staging it.  Only the raw conv outputs y_i and the chain's
+    final activation are written to HBM; the BatchNorm backward is the plain
+    HIP one (hrl_bn_backward, ReLU mask recomputed from y_i).
+    """
+
+    @staticmethod
+    def forward(ctx, h0, meta, *params):
+        lib = _native.load()
+        h0 = h0.contiguous()
+        M = h0.shape[0]
+        dev = h0.device
+        stream = _native.stream_of(dev)
+        P = _native.ptr
+        ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        nblk = lib.hrl_conv3x3_stats_blocks(M)
+        stats = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
+        x, a_prev, b_prev = h0, None, None
+        saved = [h0]
+        for i, (rm, rv, momentum, eps) in enumerate(meta):
+            w, gamma, beta = params[3 * i:3 * i + 3]
+            y = torch.empty_like(h0)
+            _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(a_prev), P(b_prev), P(w), None, 0, P(y), P(stats),
+                                                     P(ws), ws_bytes, stream), 'hrl_conv3x3_forward_ex')
+            coef = torch.empty(4, 32, dtype=torch.float32, device=dev)   # mean, invstd, alpha, beta
+            _native.check(lib.hrl_bn_finalize_stats(P(stats), nblk, 32, M * 9, P(gamma), P(beta), P(rm), P(rv),
+                                                    float(momentum), float(eps), P(coef[0]), P(coef[1]),
+                                                    P(coef[2]), P(coef[3]), stream), 'hrl_bn_finalize_stats')
+            saved += [y, coef]
+            x, a_prev, b_prev = y, coef[2], coef[3]
+        out = torch.empty_like(h0)
+        _native.check(lib.hrl_bn_apply(P(x), M, 32, 9, P(a_prev), P(b_prev), 1, P(out), stream), 'hrl_bn_apply')
+        ctx.save_for_backward(*saved, *params)
+        ctx.n = len(meta)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _native.load()
+        n = ctx.n
+        t = ctx.saved_tensors
+        h0 = t[0]
+        ys = [t[1 + 2 * i] for i in range(n)]
+        coefs = [t[2 + 2 * i] for i in range(n)]
+        params = t[1 + 2 * n:]
+        M = h0.shape[0]
+        dev = h0.device
+        stream = _native.stream_of(dev)
+        P = _native.ptr
+        ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        bn_ws_bytes = lib.hrl_bn_workspace_bytes(M, 32, 9)
+        bn_ws = torch.empty(bn_ws_bytes, dtype=torch.uint8, device=dev)
+        g = g.contiguous()
+        grads = [None] * (3 * n)
+        for i in reversed(range(n)):
+            w, gamma, beta = params[3 * i:3 * i + 3]
+            dy = torch.empty_like(h0)
+            dgam = torch.empty(32, dtype=torch.float32, device=dev)
+            dbet = torch.empty(32, dtype=torch.float32, device=dev)
+            _native.check(lib.hrl_bn_backward(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(coefs[i][0]),
+                                              P(coefs[i][1]), 1, P(dy), P(dgam), P(dbet), P(bn_ws), bn_ws_bytes,
+                                              stream), 'hrl_bn_backward')
+            x = h0 if i == 0 else ys[i - 1]
+            a = None if i == 0 else coefs[i - 1][2]
+            b = None if i == 0 else coefs[i - 1][3]
+            dw = torch.empty_like(w)
+            _native.check(lib.hrl_conv3x3_wgrad_ex(P(x), P(a), P(b), P(dy), M, P(dw), P(ws), ws_bytes, stream),
+                          'hrl_conv3x3_wgrad_ex')
+            grads[3 * i:3 * i + 3] = [dw, dgam, dbet]
+            if i > 0 or ctx.needs_input_grad[0]:
+                g = torch.empty_like(h0)
+                _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g), None, P(ws),
+                                                         ws_bytes, stream), 'hrl_conv3x3_forward_ex(flip)')
+            else:
+                g = None
+        return (g, None, *grads)
+
+
+class _ConvBNChain(nn.Module):
+    """[BoardConv2d -> BatchNorm2d(fused_relu)] x n as one _BoardChain (set up by fuse_bn_relu).
+
+    The layers are referenced, not registered (parameters and state_dict
+    unchanged).  Anything but a training-mode 32-channel 3x3-board batch on the
+    GPU runs the layers one by one.
+    """
+
+    def __init__(self, convs, bns):
+        super().__init__()
+        object.__setattr__(self, 'convs', list(convs))
+        object.__setattr__(self, 'bns', list(bns))
+
+    @staticmethod
+    def layers_ok(convs, bns):
+        return all(type(c) is BoardConv2d and c.bias is None and tuple(c.weight.shape) == (32, 32, 3, 3)
+                   and _board_conv_ok(c) for c in convs) and \
+            all(isinstance(b, BatchNorm2d) and b.affine and b.track_running_stats and b.momentum is not None
+                and b.num_features == 32 for b in bns)
+
+    def forward(self, x):
+        convs, bns = self.convs, self.bns
+        fused = (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and tuple(x.shape[1:]) == (32, 3, 3)
+                 and x.shape[0] > 0 and all(b.training and b.fused_relu for b in bns)
+                 and torch.is_grad_enabled())
+        if not fused:
+            for c, b in zip(convs, bns):
+                x = b(c(x))
+            return x
+        meta, params = [], []
+        for c, b in zip(convs, bns):
+            b.num_batches_tracked.add_(1)
+            meta.append((b.running_mean, b.running_var, b.momentum, b.eps))
+            params += [c.weight, b.weight, b.bias]
+        return _BoardChain.apply(x, meta, *params)
+
+
 class _LeafTracer(torch.fx.Tracer):
     """Trace the env net, keeping the HIP-backed modules as opaque calls."""
 
     def is_leaf_module(self, m, qualname):
-        return isinstance(m, (BatchNorm2d, BoardConv2d, Linear, _MultiBoardConv)) or \
+        return isinstance(m, (BatchNorm2d, BoardConv2d, Linear, _MultiBoardConv, _ConvBNChain)) or \
             super().is_leaf_module(m, qualname)
 
 
@@ -461,6 +584,8 @@ def fuse_bn_relu(model, example=None):
     for bn_node, relu_node in pairs:
         relu_node.replace_all_uses_with(bn_node)
         gm.graph.erase_node(relu_node)
+    bns = [gm.get_submodule(n.target) for n, _ in pairs]
+    chains = _fuse_chains(gm, set(n for n, _ in pairs))
     merged = 0
     for node in list(gm.graph.nodes):
         sibs = [u for u in node.users if u.op == 'call_module' and type(gm.get_submodule(u.target)) is BoardConv2d
@@ -483,7 +608,6 @@ def fuse_bn_relu(model, example=None):
         return 0
     gm.graph.lint()
     gm.recompile()
-    bns = [gm.get_submodule(n.target) for n, _ in pairs]
     if example is not None:
         was = model.training
         model.eval()
@@ -493,8 +617,9 @@ def fuse_bn_relu(model, example=None):
                 bn.fused_relu = True
             new = gm(example, None)
         model.train(was)
-        same = set(ref) == set(new) and all(
-            torch.allclose(ref[k], new[k], rtol=1e-5, atol=1e-6) for k in ref if ref[k] is not None)
+        same = _same_outputs(ref, new)
+        if same and chains and example.is_cuda:
+            same = _same_training_outputs(model, gm, bns, example)
         if not same:
             for bn in bns:
                 bn.fused_relu = False
@@ -502,7 +627,90 @@ def fuse_bn_relu(model, example=None):
     for bn in bns:
         bn.fused_relu = True
     model.forward = gm.forward
-    return len(pairs) + merged
+    return len(pairs) + merged + chains
+
+
+def _same_outputs(ref, new, rtol=1e-5, atol=1e-6):
+    return set(ref) == set(new) and all(
+        torch.allclose(ref[k], new[k], rtol=rtol, atol=atol) for k in ref if ref[k] is not None)
+
+
+def _same_training_outputs(model, gm, bns, example):
+    """Training-mode check of the fused chains (batch statistics): original vs rewritten
+    forward on the example, BatchNorm buffers restored afterwards."""
+    buffers = [(b.running_mean.clone(), b.running_var.clone(), b.num_batches_tracked.clone()) for b in bns]
+
+    def restore():
+        for b, (m, v, n) in zip(bns, buffers):
+            b.running_mean.copy_(m)
+            b.running_var.copy_(v)
+            b.num_batches_tracked.copy_(n)
+    was = model.training
+    model.train()
+    try:
+        for bn in bns:
+            bn.fused_relu = False
+        ref = model(example, None)
+        restore()
+        for bn in bns:
+            bn.fused_relu = True
+        new = gm(example, None)
+        restore()
+    finally:
+        model.train(was)
+    ref = {k: v.detach() for k, v in ref.items() if v is not None}
+    new = {k: v.detach() for k, v in new.items() if v is not None}
+    return _same_outputs(ref, new, rtol=1e-4, atol=1e-5)
+
+
+def _fuse_chains(gm, fused_bn_nodes):
+    """Replace maximal [BoardConv2d -> BatchNorm2d(+ReLU)] chains with one _ConvBNChain call.
+
+    A link continues while the conv's only user is the BN and the BN's only
+    user is the next conv; the last BN's output may have any users.  Returns
+    the number of chains."""
+    def conv_bn(node):
+        if node.op != 'call_module' or type(gm.get_submodule(node.target)) is not BoardConv2d or node.kwargs:
+            return None
+        users = list(node.users)
+        if len(users) != 1 or users[0] not in fused_bn_nodes or users[0].args != (node,):
+            return None
+        return users[0]
+
+    chains, seen = [], set()
+    for node in list(gm.graph.nodes):
+        if node in seen:
+            continue
+        bn = conv_bn(node)
+        if bn is None:
+            continue
+        links = [(node, bn)]
+        while True:
+            users = list(links[-1][1].users)
+            if len(users) != 1:
+                break
+            nxt = conv_bn(users[0])
+            if nxt is None:
+                break
+            links.append((users[0], nxt))
+        convs = [gm.get_submodule(c.target) for c, _ in links]
+        bns = [gm.get_submodule(b.target) for _, b in links]
+        if not _ConvBNChain.layers_ok(convs, bns):
+            continue
+        for c, b in links:
+            seen.update((c, b))
+        chains.append((links, convs, bns))
+    for k, (links, convs, bns) in enumerate(chains):
+        name = '_hrl_chain%d' % k
+        gm.add_submodule(name, _ConvBNChain(convs, bns))
+        first, last = links[0][0], links[-1][1]
+        with gm.graph.inserting_before(first):
+            call = gm.graph.call_module(name, first.args)
+        last.replace_all_uses_with(call)
+        for c, b in reversed(links):
+            gm.graph.erase_node(b)
+            gm.graph.erase_node(c)
+    return len(chains)
 
 
 def unfuse(model):

@@ -52,6 +52,17 @@ int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64
                     int relu, float *dx, float *dweight, float *dbias,
                     void *workspace, int64_t workspace_bytes, void *stream);
 
+/* The forward in pieces, for producers that compute the statistics themselves
+ * (hrl_conv3x3_forward_ex with stats): fold per-block partials part[nparts][C][2]
+ * = (sum x, sum x^2) over `count` = N*HW values into save_mean / save_invstd,
+ * the running statistics and the apply coefficients alpha = invstd*weight,
+ * beta = bias - mean*alpha; and apply y = x*alpha + beta [relu]. */
+int hrl_bn_finalize_stats(const double *part, int64_t nparts, int64_t C, int64_t count, const float *weight,
+                          const float *bias, float *running_mean, float *running_var, double momentum, double eps,
+                          float *save_mean, float *save_invstd, float *alpha, float *beta, void *stream);
+int hrl_bn_apply(const float *x, int64_t N, int64_t C, int64_t HW, const float *alpha, const float *beta, int relu,
+                 float *y, void *stream);
+
 /*
  * Tiny-board convolution as one dense matrix (handyrl_amd/nn.py BoardConv2d):
  * W_board[(ci*H*W + p), (co*H*W + q)] = W[co, ci, dy, dx] where input cell p
@@ -88,6 +99,23 @@ int hrl_conv3x3_forward(const float *x, int64_t M, int64_t C_in, int64_t C_out, 
                         void *stream);
 int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, int64_t C_out, float *dweight,
                       void *workspace, int64_t workspace_bytes, void *stream);
+
+/*
+ * The same kernels fused with the BatchNorm+ReLU around a conv -> BN -> ReLU
+ * chain (conv3x3_kernel<PRO, STATS>, csrc/hrl_conv.hip):
+ *   in_alpha / in_beta (32 floats, both or neither): x is the previous
+ *     block's raw conv output; the kernel reads relu(x*in_alpha[c] + in_beta[c]);
+ *   stats (forward only, may be NULL): per-workgroup fp64 partials
+ *     (sum y, sum y^2) per output channel, stats[hrl_conv3x3_stats_blocks(M)][32][2],
+ *     ready for hrl_bn_finalize_stats.
+ * hrl_conv3x3_forward / hrl_conv3x3_wgrad are these with everything NULL.
+ */
+int64_t hrl_conv3x3_stats_blocks(int64_t M);
+int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, const float *in_beta,
+                           const float *weight, const float *bias, int flip, float *y, double *stats,
+                           void *workspace, int64_t workspace_bytes, void *stream);
+int hrl_conv3x3_wgrad_ex(const float *x, const float *in_alpha, const float *in_beta, const float *dy, int64_t M,
+                         float *dweight, void *workspace, int64_t workspace_bytes, void *stream);
 
 /*
  * Fused ConvLSTM cell gates (GeisterNet DRC, handyrl/envs/geister.py:48-63;

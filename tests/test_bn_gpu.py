@@ -186,7 +186,7 @@ def test_fx_fusion_in_learner(cuda):
     keys = list(net.state_dict())
     step = LearnerStep(net, default_args(9, 64), cuda)
     step.step(tictactoe_batch(64, 9, cuda, seed=0))
-    assert step.fused_pairs == 4   # three BN->ReLU folds + the two head convs merged
+    assert step.fused_pairs == 5   # three BN->ReLU folds + the two head convs merged + one conv-BN chain
     assert all(m.fused_relu for m in net.modules() if isinstance(m, BatchNorm2d))
     assert list(net.state_dict()) == keys
 
@@ -225,3 +225,46 @@ def test_colsum_matches_fp64(cuda, M, N):
     ref = x.double().sum(0)
     assert torch.allclose(got.double(), ref, rtol=1e-6, atol=1e-4)
     assert torch.equal(_colsum(x), got)      # deterministic
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N', [37, 4096])
+def test_conv_bn_chain_matches_layer_by_layer(cuda, N):
+    """_BoardChain (stats in the conv epilogue, BN+ReLU in the next conv's / wgrad's prologue)
+    vs the same layers run one by one (HIP conv, HIP BN): output, every parameter gradient,
+    the input gradient and the running statistics.  N = 37 leaves a ragged last tile."""
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.nn import accelerate, _ConvBNChain
+    torch.manual_seed(0)
+    net = accelerate(SimpleConv2dModel()).to(cuda)
+    convs = [blk.conv for blk in net.blocks]
+    bns = [blk.bn for blk in net.blocks]
+    for b in bns:
+        b.fused_relu = True
+        b.weight.data.uniform_(0.5, 1.5)
+        b.bias.data.uniform_(-0.2, 0.2)
+    chain = _ConvBNChain(convs, bns)
+    x = torch.randn(N, 32, 3, 3, device=cuda)
+    g = torch.randn(N, 32, 3, 3, device=cuda)
+    params = [p for c, b in zip(convs, bns) for p in (c.weight, b.weight, b.bias)]
+    results = []
+    for fused in (False, True):
+        for b in bns:
+            b.reset_running_stats()
+        xi = x.clone().requires_grad_()
+        if fused:
+            y = chain(xi)
+        else:
+            y = xi
+            for c, b in zip(convs, bns):
+                y = b(c(y))
+        grads = torch.autograd.grad(y, [xi] + params, g)
+        stats = [t.clone() for b in bns for t in (b.running_mean, b.running_var, b.num_batches_tracked)]
+        results.append((y.detach(), grads, stats))
+    (y0, g0, s0), (y1, g1, s1) = results
+    torch.testing.assert_close(y1, y0, rtol=1e-5, atol=1e-5)
+    for a, b in zip(g1, g0):
+        err = float((a - b).norm() / b.norm().clamp(min=1e-12))
+        assert err < 1e-5, err
+    for a, b in zip(s1, s0):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
