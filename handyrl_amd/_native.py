@@ -70,7 +70,12 @@ SIGNATURES = {
     'hrl_bn_apply': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _f32p, _f32p, ctypes.c_int, _f32p, ctypes.c_void_p]),
     'hrl_conv3x3_stats_blocks': (ctypes.c_int64, [_i64]),
     'hrl_conv3x3_forward_ex': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_int, _f32p,
-                                              ctypes.c_void_p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
+                                              ctypes.c_int, _f32p, _f32p, _f32p, _f32p, ctypes.c_void_p,
+                                              ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_bn_finalize_backward': (ctypes.c_int, [ctypes.c_void_p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p,
+                                                _f32p, _f32p, ctypes.c_void_p]),
+    'hrl_bn_backward_apply': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p,
+                                             ctypes.c_int, _f32p, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_conv3x3_wgrad_ex': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _i64, _f32p, ctypes.c_void_p, _i64,
                                             ctypes.c_void_p]),
     'hrl_lstm_gates_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p,
@@ -79,7 +84,7 @@ SIGNATURES = {
                                                ctypes.c_void_p]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lib = None
 

@@ -483,6 +483,35 @@ int hrl_bn_apply(const float *x, int64_t N, int64_t C, int64_t HW, const float *
     return launch_status();
 }
 
+int hrl_bn_finalize_backward(const double *part, int64_t nparts, int64_t C, int64_t count, const float *weight,
+                             const float *save_invstd, float *dweight, float *dbias, float *kcoef, float *gmean,
+                             void *stream) {
+    if (!part || !save_invstd || !kcoef || !gmean || nparts < 1 || C < 1 || count < 1) return HRL_EINVAL;
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)C), dim3(kThreads), 0, static_cast<hipStream_t>(stream), 1,
+                       part, (int)nparts, (int)C, (double)count, weight, (const float *)nullptr, (float *)nullptr,
+                       (float *)nullptr, 0.f, 0.0, (float *)nullptr, const_cast<float *>(save_invstd), kcoef, gmean,
+                       dweight, dbias);
+    return launch_status();
+}
+
+int hrl_bn_backward_apply(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW, const float *weight,
+                          const float *bias, const float *save_mean, const float *save_invstd, int relu,
+                          const float *kcoef, const float *gmean, float *dx, void *stream) {
+    if (!x || !dy || !dx || !save_mean || !save_invstd || !kcoef || !gmean || dx == dy) return HRL_EINVAL;
+    const bool vec = (C * HW) % 4 == 0 && aligned16(x) && aligned16(dy) && aligned16(dx);
+    Geo g;
+    if (!make_geo(N, C, HW, vec ? 4 : 1, g)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (vec) {
+        if (relu) launch_bwd_apply<4, true>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx);
+        else launch_bwd_apply<4, false>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx);
+    } else {
+        if (relu) launch_bwd_apply<1, true>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx);
+        else launch_bwd_apply<1, false>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx);
+    }
+    return launch_status();
+}
+
 int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW, const float *weight,
                     const float *bias, const float *save_mean, const float *save_invstd, int relu, float *dx,
                     float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream) {

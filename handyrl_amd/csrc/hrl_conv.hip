@@ -75,30 +75,58 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 //    latency; each accumulator sums in (p, s) order;
 //  PRO:   the input is the previous block's raw conv output and the kernel
 //         applies that block's BatchNorm+ReLU, relu(x*alpha[c] + beta[c]),
-//         while staging it (the activation is never written to HBM);
-//  STATS: the epilogue accumulates per-channel sum / sum of squares of the
-//         output (fp64) and writes one partial per workgroup,
-//         stats[block][c][2], the layout bn_finalize_kernel folds.
-template <bool PRO, bool STATS>
+//         to each A fragment as it is read (a lane's channels are fixed, so
+//         alpha/beta are 16 registers); the activation never reaches HBM;
+//  EPI (what the epilogue does besides storing y):
+//   1 STATS: per output channel sum and sum of squares of y, fp32 per tile
+//            (36 values per lane) folded into fp64;
+//   2 BNRED: y is the gradient w.r.t. relu(ref*alpha + beta) of the block
+//            before (input gradient of a chain); sums g = [ref*alpha+beta > 0] y
+//            and g*(ref - mean) per channel -- bn_bwd_reduce_kernel's sums,
+//            without re-reading y;
+//   3 MASK:  y *= [ref > 0] before the store (the backward of a ReLU on the
+//            chain's input, threshold_backward);
+//   partials go to part[block][c][2] (fp64), the layout bn_finalize_kernel folds.
+//   ref tiles (EPI 2, 3) are loaded with the next input tile and transposed
+//   to the accumulator layout through the tile's LDS buffer.
+template <bool PRO, int EPI>
 __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restrict__ x, int64_t M,
                                                            const float *__restrict__ wpk,
                                                            const float *__restrict__ bias,
                                                            const float *__restrict__ in_alpha,
                                                            const float *__restrict__ in_beta,
-                                                           float *__restrict__ y, double *__restrict__ stats) {
+                                                           const float *__restrict__ ref,
+                                                           const float *__restrict__ ep_mean,
+                                                           const float *__restrict__ ep_alpha,
+                                                           const float *__restrict__ ep_beta,
+                                                           float *__restrict__ y, double *__restrict__ part) {
+    constexpr bool kRef = EPI == 2 || EPI == 3;
+    constexpr bool kSums = EPI == 1 || EPI == 2;
     __shared__ float w_lds[kTaps * 2 * kC * 16];           // 36 KB
     __shared__ float a_lds[kWaves][kTile * kStride];       // 4 x 18.1 KB
-    __shared__ float ab_lds[2 * kC];                       // PRO: alpha | beta
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < kTaps * 2 * kC * 16; i += kThreads) w_lds[i] = wpk[i];
+    // PRO: a lane's A fragments are input channels 4s + (lane>>4), s = 0..7
+    float pa[PRO ? kC / 4 : 1], pb[PRO ? kC / 4 : 1];
     if constexpr (PRO) {
-        if (threadIdx.x < kC) {
-            ab_lds[threadIdx.x] = in_alpha[threadIdx.x];
-            ab_lds[kC + threadIdx.x] = in_beta[threadIdx.x];
+#pragma unroll
+        for (int s = 0; s < kC / 4; ++s) {
+            pa[s] = in_alpha[4 * s + (lane >> 4)];
+            pb[s] = in_beta[4 * s + (lane >> 4)];
         }
     }
-    double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};   // STATS: this lane's two output channels
+    // epilogue: a lane's outputs are channels (lane & 15) and 16 + (lane & 15)
+    float em[2] = {0.f, 0.f}, ea[2] = {1.f, 1.f}, eb[2] = {0.f, 0.f};
+    if constexpr (EPI == 2) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+            em[ct] = ep_mean[ct * 16 + (lane & 15)];
+            ea[ct] = ep_alpha[ct * 16 + (lane & 15)];
+            eb[ct] = ep_beta[ct * 16 + (lane & 15)];
+        }
+    }
+    double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};   // EPI 1, 2: this lane's two channels
 
     const int64_t ntiles = (M + kTile - 1) / kTile;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
@@ -111,41 +139,36 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
         bias_v[1] = bias[16 + (lane & 15)];
     }
     float4 stage[kVec];
-    auto issue = [&](int64_t t) {
+    float4 rstage[kRef ? kVec : 1];
+    auto load_tile = [&](const float *src, int64_t t, float4 *dst) {
         // rows t*16 .. t*16+15 are contiguous: 16*288 floats = 1152 float4
         const int64_t base = t * kTile * kRow;
 #pragma unroll
         for (int k = 0; k < kVec; ++k) {
             const int64_t e = base + (int64_t)(k * 64 + lane) * 4;
             const int64_t ec = e < lim ? e : lim - 4;          // clamp (ragged last tile), no branch
-            stage[k] = *reinterpret_cast<const float4 *>(x + ec);
+            dst[k] = *reinterpret_cast<const float4 *>(src + ec);
         }
     };
-    if (tile < ntiles) issue(tile);
-    __syncthreads();   // weights (and alpha/beta) in LDS
-
-    for (; tile < ntiles; tile += stride) {
-        // staged tile -> LDS (padded rows), through the previous block's BN+ReLU with PRO
+    auto to_lds = [&](const float4 *src) {
 #pragma unroll
         for (int k = 0; k < kVec; ++k) {
             const int e = (k * 64 + lane) * 4;                 // element within the tile
             const int r = e / kRow, c = e - r * kRow;          // kRow % 4 == 0: one row per float4
             float *d = as + r * kStride + c;
-            float v[4] = {stage[k].x, stage[k].y, stage[k].z, stage[k].w};
-            if constexpr (PRO) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int ch = (c + j) / kCells;
-                    const float t = v[j] * ab_lds[ch] + ab_lds[kC + ch];   // bn_apply_kernel's float ops
-                    v[j] = t < 0.f ? 0.f : t;
-                }
-            }
-            d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+            d[0] = src[k].x; d[1] = src[k].y; d[2] = src[k].z; d[3] = src[k].w;
         }
+    };
+    if (tile < ntiles) load_tile(x, tile, stage);
+    __syncthreads();   // weights in LDS
+
+    for (; tile < ntiles; tile += stride) {
+        to_lds(stage);                        // staged tile -> LDS (padded rows)
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes done
         __builtin_amdgcn_wave_barrier();
+        if constexpr (kRef) load_tile(ref, tile, rstage);   // this tile's reference, for the epilogue
         const int64_t next = tile + stride;
-        if (next < ntiles) issue(next);       // in flight during the MFMAs
+        if (next < ntiles) load_tile(x, next, stage);        // in flight during the MFMAs
 
         f32x4 acc[kCells][2];
 #pragma unroll
@@ -158,7 +181,11 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
         for (int p = 0; p < kCells; ++p) {
 #pragma unroll
             for (int s = 0; s < kC / 4; ++s) {
-                const float a = arow[(4 * s + ak) * kCells + p];
+                float a = arow[(4 * s + ak) * kCells + p];
+                if constexpr (PRO) {   // input channel 4s+ak: the previous block's BN+ReLU (bn_apply_kernel's ops)
+                    const float t = a * pa[s] + pb[s];
+                    a = t < 0.f ? 0.f : t;
+                }
 #pragma unroll
                 for (int q = 0; q < kCells; ++q) {
                     const int tap = tap_of(p, q);
@@ -169,8 +196,45 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
             }
         }
 
-        // epilogue: accumulators -> LDS tile [row][co*9 + q] -> coalesced stores
+        const int64_t valid = M - tile * kTile;          // rows of this tile inside the batch
         __builtin_amdgcn_wave_barrier();
+        if constexpr (kRef) {
+            // reference tile -> LDS, read back in the accumulator layout
+            to_lds(rstage);
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            float t1[2] = {0.f, 0.f}, t2[2] = {0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < kCells; ++q)
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = (lane >> 4) * 4 + r;
+                        const int co = ct * 16 + (lane & 15);
+                        const float rv = as[row * kStride + co * kCells + q];
+                        if constexpr (EPI == 3) {
+                            if (!(rv > 0.f)) acc[q][ct][r] = 0.f;
+                        } else {
+                            // bn_bwd_reduce_kernel's mask and sums (float products, fp32 per tile here)
+                            const float gm = (rv * ea[ct] + eb[ct] > 0.f && row < valid) ? acc[q][ct][r] : 0.f;
+                            t1[ct] += gm;
+                            t2[ct] += gm * (rv - em[ct]);
+                        }
+                    }
+            if constexpr (EPI == 2) {
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    s1[ct] += (double)t1[ct];
+                    s2[ct] += (double)t2[ct];
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+        }
+
+        // accumulators -> LDS tile [row][co*9 + q] -> coalesced stores
+        float t1[2] = {0.f, 0.f}, t2[2] = {0.f, 0.f};   // EPI 1: this tile's fp32 partials
 #pragma unroll
         for (int q = 0; q < kCells; ++q)
 #pragma unroll
@@ -181,13 +245,19 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
                     const int co = ct * 16 + (lane & 15);      //      col = lane & 15
                     const float v = acc[q][ct][r] + bias_v[ct];
                     as[row * kStride + co * kCells + q] = v;
-                    if constexpr (STATS) {
-                        if (tile * kTile + row < M) {
-                            s1[ct] += (double)v;
-                            s2[ct] += (double)v * (double)v;
-                        }
+                    if constexpr (EPI == 1) {
+                        const float u = row < valid ? v : 0.f;
+                        t1[ct] += u;
+                        t2[ct] += u * u;
                     }
                 }
+        if constexpr (EPI == 1) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                s1[ct] += (double)t1[ct];
+                s2[ct] += (double)t2[ct];
+            }
+        }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
         const int64_t obase = tile * kTile * kRow;
@@ -201,7 +271,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
     }
-    if constexpr (STATS) {
+    if constexpr (kSums) {
         // fold the lanes sharing a channel (4 row groups) and the 4 waves in a fixed order
         __syncthreads();
         double *red = reinterpret_cast<double *>(&a_lds[0][0]);   // [wave][group][32][2]
@@ -217,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
             const int co = threadIdx.x >> 1, k = threadIdx.x & 1;
             double t = 0.0;
             for (int i = 0; i < kWaves * 4; ++i) t += red[(i * kC + co) * 2 + k];
-            stats[((int64_t)blockIdx.x * kC + co) * 2 + k] = t;
+            part[((int64_t)blockIdx.x * kC + co) * 2 + k] = t;
         }
     }
 }
@@ -238,13 +308,14 @@ __global__ __launch_bounds__(kThreads) void conv3x3_wgrad_kernel(const float *__
     const int wave = threadIdx.x >> 6;
     float *xs = lds + wave * kTile * kStride;
     float *gs = lds + (kWaves + wave) * kTile * kStride;
-    __shared__ float ab_lds[2 * kC];   // PRO: x is a raw conv output, staged as relu(x*alpha + beta)
+    // PRO: x is a raw conv output read as relu(x*alpha + beta); a lane's A
+    // fragments are channels (lane & 15) and 16 + (lane & 15)
+    float pa0 = 1.f, pb0 = 0.f, pa1 = 1.f, pb1 = 0.f;
     if constexpr (PRO) {
-        if (threadIdx.x < kC) {
-            ab_lds[threadIdx.x] = in_alpha[threadIdx.x];
-            ab_lds[kC + threadIdx.x] = in_beta[threadIdx.x];
-        }
-        __syncthreads();
+        pa0 = in_alpha[lane & 15];
+        pb0 = in_beta[lane & 15];
+        pa1 = in_alpha[16 + (lane & 15)];
+        pb1 = in_beta[16 + (lane & 15)];
     }
     const int64_t ntiles = (M + kTile - 1) / kTile;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
@@ -275,16 +346,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_wgrad_kernel(const float *__
             const int e = (k * 64 + lane) * 4;
             const int r = e / kRow, c = e - r * kRow;
             float *d = xs + r * kStride + c;
-            float v[4] = {sx[k].x, sx[k].y, sx[k].z, sx[k].w};
-            if constexpr (PRO) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int ch = (c + j) / kCells;
-                    const float t = v[j] * ab_lds[ch] + ab_lds[kC + ch];
-                    v[j] = t < 0.f ? 0.f : t;
-                }
-            }
-            d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+            d[0] = sx[k].x; d[1] = sx[k].y; d[2] = sx[k].z; d[3] = sx[k].w;
             float *h = gs + r * kStride + c;
             h[0] = sg[k].x; h[1] = sg[k].y; h[2] = sg[k].z; h[3] = sg[k].w;
         }
@@ -301,8 +363,13 @@ __global__ __launch_bounds__(kThreads) void conv3x3_wgrad_kernel(const float *__
 #pragma unroll
                 for (int s = 0; s < kTile / 4; ++s) {
                     const int row = 4 * s + kk;
-                    const float a0 = xs[row * kStride + (0 * 16 + i16) * kCells + p];
-                    const float a1 = xs[row * kStride + (1 * 16 + i16) * kCells + p];
+                    float a0 = xs[row * kStride + (0 * 16 + i16) * kCells + p];
+                    float a1 = xs[row * kStride + (1 * 16 + i16) * kCells + p];
+                    if constexpr (PRO) {
+                        const float t0 = a0 * pa0 + pb0, t1 = a1 * pa1 + pb1;
+                        a0 = t0 < 0.f ? 0.f : t0;
+                        a1 = t1 < 0.f ? 0.f : t1;
+                    }
                     const float b0 = gs[row * kStride + (0 * 16 + i16) * kCells + q];
                     const float b1 = gs[row * kStride + (1 * 16 + i16) * kCells + q];
                     acc[tap][0][0] = mfma(a0, b0, acc[tap][0][0]);
@@ -407,12 +474,17 @@ int64_t hrl_conv3x3_workspace_bytes(int64_t M) {
 int64_t hrl_conv3x3_stats_blocks(int64_t M) { return M < 1 ? -1 : grid_for(M); }
 
 int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, const float *in_beta,
-                           const float *weight, const float *bias, int flip, float *y, double *stats,
-                           void *workspace, int64_t workspace_bytes, void *stream) {
+                           const float *weight, const float *bias, int flip, float *y, int epilogue,
+                           const float *ref, const float *ep_mean, const float *ep_alpha, const float *ep_beta,
+                           double *part, void *workspace, int64_t workspace_bytes, void *stream) {
     if (M < 1 || !x || !weight || !y || !workspace) return HRL_EINVAL;
     if (!aligned16(x) || !aligned16(y) || workspace_bytes < hrl_conv3x3_workspace_bytes(M)) return HRL_EINVAL;
     if ((in_alpha == nullptr) != (in_beta == nullptr)) return HRL_EINVAL;
-    if (flip && (bias || in_alpha || stats)) return HRL_EINVAL;
+    if (epilogue < 0 || epilogue > 3) return HRL_EINVAL;
+    if ((epilogue == 1 || epilogue == 2) && !part) return HRL_EINVAL;
+    if ((epilogue == 2 || epilogue == 3) && (!ref || !aligned16(ref))) return HRL_EINVAL;
+    if (epilogue == 2 && (!ep_mean || !ep_alpha || !ep_beta)) return HRL_EINVAL;
+    if (epilogue >= 2 && bias) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     float *wpk = static_cast<float *>(workspace);
     hipLaunchKernelGGL(conv3x3_pack_kernel, dim3((kTaps * 2 * kC * 16 + 255) / 256), dim3(256), 0, s, weight, flip,
@@ -420,18 +492,17 @@ int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, con
     int rc = status();
     if (rc) return rc;
     const dim3 grid(grid_for(M)), block(kThreads);
-    if (in_alpha && stats)
-        hipLaunchKernelGGL((conv3x3_kernel<true, true>), grid, block, 0, s, x, M, wpk, bias, in_alpha, in_beta,
-                           y, stats);
-    else if (in_alpha)
-        hipLaunchKernelGGL((conv3x3_kernel<true, false>), grid, block, 0, s, x, M, wpk, bias, in_alpha, in_beta,
-                           y, stats);
-    else if (stats)
-        hipLaunchKernelGGL((conv3x3_kernel<false, true>), grid, block, 0, s, x, M, wpk, bias, in_alpha, in_beta,
-                           y, stats);
-    else
-        hipLaunchKernelGGL((conv3x3_kernel<false, false>), grid, block, 0, s, x, M, wpk, bias, in_alpha,
-                           in_beta, y, stats);
+#define HRL_CONV_LAUNCH(PRO, EPI)                                                                            \
+    hipLaunchKernelGGL((conv3x3_kernel<PRO, EPI>), grid, block, 0, s, x, M, wpk, bias, in_alpha, in_beta, ref, \
+                       ep_mean, ep_alpha, ep_beta, y, part)
+    const bool pro = in_alpha != nullptr;
+    switch (epilogue) {
+    case 0: if (pro) HRL_CONV_LAUNCH(true, 0); else HRL_CONV_LAUNCH(false, 0); break;
+    case 1: if (pro) HRL_CONV_LAUNCH(true, 1); else HRL_CONV_LAUNCH(false, 1); break;
+    case 2: if (pro) HRL_CONV_LAUNCH(true, 2); else HRL_CONV_LAUNCH(false, 2); break;
+    default: if (pro) HRL_CONV_LAUNCH(true, 3); else HRL_CONV_LAUNCH(false, 3); break;
+    }
+#undef HRL_CONV_LAUNCH
     return status();
 }
 
@@ -439,8 +510,8 @@ int hrl_conv3x3_forward(const float *x, int64_t M, int64_t C_in, int64_t C_out, 
                         const float *bias, int flip, float *y, void *workspace, int64_t workspace_bytes,
                         void *stream) {
     if (C_in != kC || C_out != kC) return HRL_EINVAL;
-    return hrl_conv3x3_forward_ex(x, M, nullptr, nullptr, weight, bias, flip, y, nullptr, workspace,
-                                  workspace_bytes, stream);
+    return hrl_conv3x3_forward_ex(x, M, nullptr, nullptr, weight, bias, flip, y, 0, nullptr, nullptr, nullptr,
+                                  nullptr, nullptr, workspace, workspace_bytes, stream);
 }
 
 int hrl_conv3x3_wgrad_ex(const float *x, const float *in_alpha, const float *in_beta, const float *dy, int64_t M,

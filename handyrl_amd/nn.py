@@ -417,19 +417,23 @@ class _MultiBoardConv(nn.Module):
 
 
 class _BoardChain(torch.autograd.Function):
-    """A chain of [3x3 conv 32->32 (no bias) -> BatchNorm (training) -> ReLU] blocks on 3x3 boards.
+    """[relu ->] [3x3 conv 32->32 (no bias) -> BatchNorm (training) -> ReLU] x n on 3x3 boards.
 
-    The TicTacToe body (tictactoe.py:57-65).  Fused around the MFMA conv
-    (csrc/hrl_conv.hip, conv3x3_kernel<PRO, STATS>): each conv's epilogue
-    emits the BatchNorm statistics of its output, and the next conv (and, in
-    backward, the weight-gradient kernel) applies the BatchNorm+ReLU to its
-    input while staging it.  Only the raw conv outputs y_i and the chain's
-    final activation are written to HBM; the BatchNorm backward is the plain
-    HIP one (hrl_bn_backward, ReLU mask recomputed from y_i).
+    The TicTacToe body (tictactoe.py:57-65; ``relu_in``: the stem's ReLU in
+    front of it, tictactoe.py:62).  Fused around the MFMA conv
+    (csrc/hrl_conv.hip, conv3x3_kernel<PRO, EPI>):
+      forward   conv_i's epilogue emits the BatchNorm statistics of its output
+                y_i; conv_{i+1} (and in backward the weight-gradient kernel)
+                applies BN_i + ReLU to y_i as it reads it;
+      backward  the input-gradient launch of conv_{i+1} also produces BN_i's
+                backward sums from y_i in its epilogue, so only BN_{n-1}
+                needs the separate reduce pass; with ``relu_in`` the first
+                input-gradient launch applies the stem ReLU's mask.
+    Only the raw conv outputs y_i and the chain's output reach HBM.
     """
 
     @staticmethod
-    def forward(ctx, h0, meta, *params):
+    def forward(ctx, h0, meta, relu_in, *params):
         lib = _native.load()
         h0 = h0.contiguous()
         M = h0.shape[0]
@@ -439,24 +443,30 @@ class _BoardChain(torch.autograd.Function):
         ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         nblk = lib.hrl_conv3x3_stats_blocks(M)
-        stats = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
-        x, a_prev, b_prev = h0, None, None
+        part = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
+        unit = torch.stack([torch.ones(32, device=dev), torch.zeros(32, device=dev)]) if relu_in else None
+        x = h0
+        a_prev, b_prev = (unit[0], unit[1]) if relu_in else (None, None)
         saved = [h0]
         for i, (rm, rv, momentum, eps) in enumerate(meta):
             w, gamma, beta = params[3 * i:3 * i + 3]
             y = torch.empty_like(h0)
-            _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(a_prev), P(b_prev), P(w), None, 0, P(y), P(stats),
-                                                     P(ws), ws_bytes, stream), 'hrl_conv3x3_forward_ex')
+            _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(a_prev), P(b_prev), P(w), None, 0, P(y), 1, None, None,
+                                                     None, None, P(part), P(ws), ws_bytes, stream),
+                          'hrl_conv3x3_forward_ex')
             coef = torch.empty(4, 32, dtype=torch.float32, device=dev)   # mean, invstd, alpha, beta
-            _native.check(lib.hrl_bn_finalize_stats(P(stats), nblk, 32, M * 9, P(gamma), P(beta), P(rm), P(rv),
+            _native.check(lib.hrl_bn_finalize_stats(P(part), nblk, 32, M * 9, P(gamma), P(beta), P(rm), P(rv),
                                                     float(momentum), float(eps), P(coef[0]), P(coef[1]),
                                                     P(coef[2]), P(coef[3]), stream), 'hrl_bn_finalize_stats')
             saved += [y, coef]
             x, a_prev, b_prev = y, coef[2], coef[3]
         out = torch.empty_like(h0)
         _native.check(lib.hrl_bn_apply(P(x), M, 32, 9, P(a_prev), P(b_prev), 1, P(out), stream), 'hrl_bn_apply')
+        if relu_in:
+            saved.append(unit)
         ctx.save_for_backward(*saved, *params)
         ctx.n = len(meta)
+        ctx.relu_in = relu_in
         return out
 
     @staticmethod
@@ -467,7 +477,12 @@ class _BoardChain(torch.autograd.Function):
         h0 = t[0]
         ys = [t[1 + 2 * i] for i in range(n)]
         coefs = [t[2 + 2 * i] for i in range(n)]
-        params = t[1 + 2 * n:]
+        k = 1 + 2 * n
+        unit = None
+        if ctx.relu_in:
+            unit = t[k]
+            k += 1
+        params = t[k:]
         M = h0.shape[0]
         dev = h0.device
         stream = _native.stream_of(dev)
@@ -476,44 +491,68 @@ class _BoardChain(torch.autograd.Function):
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         bn_ws_bytes = lib.hrl_bn_workspace_bytes(M, 32, 9)
         bn_ws = torch.empty(bn_ws_bytes, dtype=torch.uint8, device=dev)
+        nblk = lib.hrl_conv3x3_stats_blocks(M)
+        part = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
         g = g.contiguous()
         grads = [None] * (3 * n)
+        have_sums = False   # part holds BN_i's backward sums from the previous input-gradient launch
         for i in reversed(range(n)):
             w, gamma, beta = params[3 * i:3 * i + 3]
+            mean, invstd = coefs[i][0], coefs[i][1]
             dy = torch.empty_like(h0)
             dgam = torch.empty(32, dtype=torch.float32, device=dev)
             dbet = torch.empty(32, dtype=torch.float32, device=dev)
-            _native.check(lib.hrl_bn_backward(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(coefs[i][0]),
-                                              P(coefs[i][1]), 1, P(dy), P(dgam), P(dbet), P(bn_ws), bn_ws_bytes,
-                                              stream), 'hrl_bn_backward')
-            x = h0 if i == 0 else ys[i - 1]
-            a = None if i == 0 else coefs[i - 1][2]
-            b = None if i == 0 else coefs[i - 1][3]
+            if have_sums:
+                kg = torch.empty(2, 32, dtype=torch.float32, device=dev)
+                _native.check(lib.hrl_bn_finalize_backward(P(part), nblk, 32, M * 9, P(gamma), P(invstd), P(dgam),
+                                                           P(dbet), P(kg[0]), P(kg[1]), stream),
+                              'hrl_bn_finalize_backward')
+                _native.check(lib.hrl_bn_backward_apply(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(mean),
+                                                        P(invstd), 1, P(kg[0]), P(kg[1]), P(dy), stream),
+                              'hrl_bn_backward_apply')
+            else:
+                _native.check(lib.hrl_bn_backward(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(mean), P(invstd),
+                                                  1, P(dy), P(dgam), P(dbet), P(bn_ws), bn_ws_bytes, stream),
+                              'hrl_bn_backward')
+            if i == 0:
+                x, a, b = h0, (unit[0] if unit is not None else None), (unit[1] if unit is not None else None)
+            else:
+                x, a, b = ys[i - 1], coefs[i - 1][2], coefs[i - 1][3]
             dw = torch.empty_like(w)
             _native.check(lib.hrl_conv3x3_wgrad_ex(P(x), P(a), P(b), P(dy), M, P(dw), P(ws), ws_bytes, stream),
                           'hrl_conv3x3_wgrad_ex')
             grads[3 * i:3 * i + 3] = [dw, dgam, dbet]
-            if i > 0 or ctx.needs_input_grad[0]:
+            if i > 0:   # dL/dh_i, and BN_{i-1}'s backward sums in the same launch
                 g = torch.empty_like(h0)
-                _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g), None, P(ws),
-                                                         ws_bytes, stream), 'hrl_conv3x3_forward_ex(flip)')
+                _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g), 2, P(ys[i - 1]),
+                                                         P(coefs[i - 1][0]), P(coefs[i - 1][2]),
+                                                         P(coefs[i - 1][3]), P(part), P(ws), ws_bytes, stream),
+                              'hrl_conv3x3_forward_ex(flip, bn sums)')
+                have_sums = True
+            elif ctx.needs_input_grad[0]:
+                g = torch.empty_like(h0)
+                _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g),
+                                                         3 if ctx.relu_in else 0, P(h0) if ctx.relu_in else None,
+                                                         None, None, None, None, P(ws), ws_bytes, stream),
+                              'hrl_conv3x3_forward_ex(flip)')
             else:
                 g = None
-        return (g, None, *grads)
+        return (g, None, None, *grads)
 
 
 class _ConvBNChain(nn.Module):
-    """[BoardConv2d -> BatchNorm2d(fused_relu)] x n as one _BoardChain (set up by fuse_bn_relu).
+    """[relu ->] [BoardConv2d -> BatchNorm2d(fused_relu)] x n as one _BoardChain (set up by fuse_bn_relu).
 
     The layers are referenced, not registered (parameters and state_dict
     unchanged).  Anything but a training-mode 32-channel 3x3-board batch on the
     GPU runs the layers one by one.
     """
 
-    def __init__(self, convs, bns):
+    def __init__(self, convs, bns, relu_in=False):
         super().__init__()
         object.__setattr__(self, 'convs', list(convs))
         object.__setattr__(self, 'bns', list(bns))
+        self.relu_in = relu_in
 
     @staticmethod
     def layers_ok(convs, bns):
@@ -528,6 +567,8 @@ class _ConvBNChain(nn.Module):
                  and x.shape[0] > 0 and all(b.training and b.fused_relu for b in bns)
                  and torch.is_grad_enabled())
         if not fused:
+            if self.relu_in:
+                x = torch.relu(x)
             for c, b in zip(convs, bns):
                 x = b(c(x))
             return x
@@ -536,7 +577,7 @@ class _ConvBNChain(nn.Module):
             b.num_batches_tracked.add_(1)
             meta.append((b.running_mean, b.running_var, b.momentum, b.eps))
             params += [c.weight, b.weight, b.bias]
-        return _BoardChain.apply(x, meta, *params)
+        return _BoardChain.apply(x, meta, self.relu_in, *params)
 
 
 class _LeafTracer(torch.fx.Tracer):
@@ -702,14 +743,19 @@ def _fuse_chains(gm, fused_bn_nodes):
         chains.append((links, convs, bns))
     for k, (links, convs, bns) in enumerate(chains):
         name = '_hrl_chain%d' % k
-        gm.add_submodule(name, _ConvBNChain(convs, bns))
         first, last = links[0][0], links[-1][1]
+        src = first.args[0]
+        relu_in = (isinstance(src, torch.fx.Node) and _is_relu(gm, src) and len(src.users) == 1
+                   and src.op != 'call_module')
+        gm.add_submodule(name, _ConvBNChain(convs, bns, relu_in=relu_in))
         with gm.graph.inserting_before(first):
-            call = gm.graph.call_module(name, first.args)
+            call = gm.graph.call_module(name, (src.args[0],) if relu_in else first.args)
         last.replace_all_uses_with(call)
         for c, b in reversed(links):
             gm.graph.erase_node(b)
             gm.graph.erase_node(c)
+        if relu_in:
+            gm.graph.erase_node(src)
     return len(chains)
 
 

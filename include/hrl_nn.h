@@ -62,6 +62,16 @@ int hrl_bn_finalize_stats(const double *part, int64_t nparts, int64_t C, int64_t
                           float *save_mean, float *save_invstd, float *alpha, float *beta, void *stream);
 int hrl_bn_apply(const float *x, int64_t N, int64_t C, int64_t HW, const float *alpha, const float *beta, int relu,
                  float *y, void *stream);
+/* The backward in pieces: fold (sum g, sum g*(x-mean)) partials into dweight,
+ * dbias and the apply coefficients kcoef, gmean (C floats each); then
+ * dx = ((g - gmean) - (x - mean)*kcoef) * invstd * weight, g masked by the
+ * recomputed ReLU when relu != 0 (hrl_bn_backward = reduce + these two). */
+int hrl_bn_finalize_backward(const double *part, int64_t nparts, int64_t C, int64_t count, const float *weight,
+                             const float *save_invstd, float *dweight, float *dbias, float *kcoef, float *gmean,
+                             void *stream);
+int hrl_bn_backward_apply(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW, const float *weight,
+                          const float *bias, const float *save_mean, const float *save_invstd, int relu,
+                          const float *kcoef, const float *gmean, float *dx, void *stream);
 
 /*
  * Tiny-board convolution as one dense matrix (handyrl_amd/nn.py BoardConv2d):
@@ -102,18 +112,24 @@ int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, 
 
 /*
  * The same kernels fused with the BatchNorm+ReLU around a conv -> BN -> ReLU
- * chain (conv3x3_kernel<PRO, STATS>, csrc/hrl_conv.hip):
+ * chain (conv3x3_kernel<PRO, EPI>, csrc/hrl_conv.hip):
  *   in_alpha / in_beta (32 floats, both or neither): x is the previous
  *     block's raw conv output; the kernel reads relu(x*in_alpha[c] + in_beta[c]);
- *   stats (forward only, may be NULL): per-workgroup fp64 partials
- *     (sum y, sum y^2) per output channel, stats[hrl_conv3x3_stats_blocks(M)][32][2],
- *     ready for hrl_bn_finalize_stats.
- * hrl_conv3x3_forward / hrl_conv3x3_wgrad are these with everything NULL.
+ *   epilogue 0: none;
+ *            1: forward statistics, part = per-workgroup fp64 (sum y, sum y^2)
+ *               per output channel -> hrl_bn_finalize_stats;
+ *            2: (input gradient of a chain) y is dL/d relu(ref*ep_alpha + ep_beta);
+ *               part = (sum g, sum g*(ref - ep_mean)) with g = y masked where
+ *               ref*ep_alpha + ep_beta <= 0 -> hrl_bn_finalize_backward;
+ *            3: y *= [ref > 0] (backward of a ReLU on the chain input).
+ *   part: hrl_conv3x3_stats_blocks(M) x 32 x 2 doubles; ref: (M, 288) like y.
+ * hrl_conv3x3_forward / hrl_conv3x3_wgrad are these with nothing fused.
  */
 int64_t hrl_conv3x3_stats_blocks(int64_t M);
 int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, const float *in_beta,
-                           const float *weight, const float *bias, int flip, float *y, double *stats,
-                           void *workspace, int64_t workspace_bytes, void *stream);
+                           const float *weight, const float *bias, int flip, float *y, int epilogue,
+                           const float *ref, const float *ep_mean, const float *ep_alpha, const float *ep_beta,
+                           double *part, void *workspace, int64_t workspace_bytes, void *stream);
 int hrl_conv3x3_wgrad_ex(const float *x, const float *in_alpha, const float *in_beta, const float *dy, int64_t M,
                          float *dweight, void *workspace, int64_t workspace_bytes, void *stream);
 

@@ -229,8 +229,10 @@ def test_colsum_matches_fp64(cuda, M, N):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('N', [37, 4096])
-def test_conv_bn_chain_matches_layer_by_layer(cuda, N):
-    """_BoardChain (stats in the conv epilogue, BN+ReLU in the next conv's / wgrad's prologue)
+@pytest.mark.parametrize('relu_in', [False, True])
+def test_conv_bn_chain_matches_layer_by_layer(cuda, N, relu_in):
+    """_BoardChain (BN stats in the conv epilogue, BN+ReLU in the next conv's / wgrad's
+    prologue, BN-backward sums in the input-gradient epilogue, optional ReLU on the input)
     vs the same layers run one by one (HIP conv, HIP BN): output, every parameter gradient,
     the input gradient and the running statistics.  N = 37 leaves a ragged last tile."""
     from handyrl_amd.envs.tictactoe import SimpleConv2dModel
@@ -243,7 +245,7 @@ def test_conv_bn_chain_matches_layer_by_layer(cuda, N):
         b.fused_relu = True
         b.weight.data.uniform_(0.5, 1.5)
         b.bias.data.uniform_(-0.2, 0.2)
-    chain = _ConvBNChain(convs, bns)
+    chain = _ConvBNChain(convs, bns, relu_in=relu_in)
     x = torch.randn(N, 32, 3, 3, device=cuda)
     g = torch.randn(N, 32, 3, 3, device=cuda)
     params = [p for c, b in zip(convs, bns) for p in (c.weight, b.weight, b.bias)]
@@ -255,7 +257,7 @@ def test_conv_bn_chain_matches_layer_by_layer(cuda, N):
         if fused:
             y = chain(xi)
         else:
-            y = xi
+            y = torch.relu(xi) if relu_in else xi
             for c, b in zip(convs, bns):
                 y = b(c(y))
         grads = torch.autograd.grad(y, [xi] + params, g)
