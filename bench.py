@@ -159,7 +159,7 @@ def pmc_traffic(B, T):
     return None
 
 
-def cpu_baseline(B=1024, T=32, steps=3):
+def cpu_baseline(B=2048, T=32, steps=6):
     """The CPU learner oracle on this host, 1 thread (train.py as shipped: model.py:8)."""
     from oracle.learner import CpuLearner
     threads = torch.get_num_threads()

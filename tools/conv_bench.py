@@ -52,12 +52,38 @@ def main():
     def wgrad():
         _native.check(lib.hrl_conv3x3_wgrad(P(x), P(dy), M, 32, 32, P(dw), P(ws), ws_bytes, stream), 'wgrad')
 
+    # fused variants (conv -> BN -> ReLU chains, nn._BoardChain)
+    nblk = lib.hrl_conv3x3_stats_blocks(M)
+    part = torch.empty(nblk * 64, dtype=torch.float64, device=dev)
+    al = torch.rand(32, device=dev) + 0.5
+    be = torch.randn(32, device=dev) * 0.1
+    mu = torch.randn(32, device=dev) * 0.1
+    ref = torch.randn(M, 288, device=dev, generator=g)
+
+    def fwd_pro_stats():
+        _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(al), P(be), P(w), None, 0, P(y), 1, None, None, None,
+                                                 None, P(part), P(ws), ws_bytes, stream), 'fwd_pro_stats')
+
+    def dgrad_bnred():
+        _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(y), 2, P(ref), P(mu), P(al),
+                                                 P(be), P(part), P(ws), ws_bytes, stream), 'dgrad_bnred')
+
+    def dgrad_mask():
+        _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(y), 3, P(ref), None, None,
+                                                 None, None, P(ws), ws_bytes, stream), 'dgrad_mask')
+
+    def wgrad_pro():
+        _native.check(lib.hrl_conv3x3_wgrad_ex(P(x), P(al), P(be), P(dy), M, P(dw), P(ws), ws_bytes, stream),
+                      'wgrad_pro')
+
     # correctness spot check against torch (fp32)
     fwd()
     ref = torch.nn.functional.conv2d(x.view(M, 32, 3, 3), w, b, padding=1).view(M, 288)
     err = float((y - ref).abs().max())
     res = {'M': M, 'fwd_max_abs_err': err}
-    for name, fn in (('fwd', fwd), ('dgrad', dgrad), ('wgrad', wgrad)):
+    for name, fn in (('fwd', fwd), ('dgrad', dgrad), ('wgrad', wgrad), ('fwd_pro_stats', fwd_pro_stats),
+                     ('dgrad_bnred', dgrad_bnred), ('dgrad_mask', dgrad_mask), ('wgrad_pro', wgrad_pro),
+                     ('fwd_again', fwd)):
         for _ in range(3):
             fn()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
