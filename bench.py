@@ -209,8 +209,9 @@ def secondary_t9(device, steps=10, warmup=3, B=4096, T=9):
 def secondary_rollout(device, E=16384, reps=5):
     """Device self-play throughput: E concurrent TicTacToe games, one batched forward per ply."""
     from handyrl_amd.rollout import TicTacToeBatch, DeviceGenerator, DeviceReplay
+    from handyrl_amd.nn import accelerate
     torch.manual_seed(0)
-    net = SimpleConv2dModel().to(device)
+    net = accelerate(SimpleConv2dModel().to(device))
     gen = DeviceGenerator(TicTacToeBatch(E, device), net)
     rep = DeviceReplay(4 * E, 9, (3, 3, 3), 9, 2, device)
     g = torch.Generator(device=device).manual_seed(0)

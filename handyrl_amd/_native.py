@@ -67,6 +67,8 @@ SIGNATURES = {
     'hrl_bn_finalize_stats': (ctypes.c_int, [ctypes.c_void_p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p,
                                              ctypes.c_double, ctypes.c_double, _f32p, _f32p, _f32p, _f32p,
                                              ctypes.c_void_p]),
+    'hrl_bn_forward_eval': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_double,
+                                           ctypes.c_int, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_bn_apply': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _f32p, _f32p, ctypes.c_int, _f32p, ctypes.c_void_p]),
     'hrl_conv3x3_stats_blocks': (ctypes.c_int64, [_i64]),
     'hrl_conv3x3_forward_ex': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_int, _f32p,
@@ -84,7 +86,7 @@ SIGNATURES = {
                                                ctypes.c_void_p]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lib = None
 

@@ -215,6 +215,18 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
     }
 }
 
+// ---- eval-mode coefficients from the running statistics ----
+__global__ void bn_eval_coef_kernel(int C, const float *__restrict__ weight, const float *__restrict__ bias,
+                                    const float *__restrict__ running_mean, const float *__restrict__ running_var,
+                                    double eps, float *__restrict__ alpha, float *__restrict__ beta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float invstd = (float)(1.0 / sqrt((double)running_var[c] + eps));
+    const float a = invstd * (weight ? weight[c] : 1.0f);
+    alpha[c] = a;
+    beta[c] = (bias ? bias[c] : 0.0f) - running_mean[c] * a;
+}
+
 // ---- forward apply: y = x*alpha[c] + beta[c] ----
 // relu(v) as torch.relu: negatives to 0, NaN stays NaN
 __device__ __forceinline__ float relu(float v) { return v < 0.f ? 0.f : v; }
@@ -481,6 +493,19 @@ int hrl_bn_apply(const float *x, int64_t N, int64_t C, int64_t HW, const float *
     if (vec) relu ? launch_apply<4, true>(g, s, x, alpha, beta, y) : launch_apply<4, false>(g, s, x, alpha, beta, y);
     else relu ? launch_apply<1, true>(g, s, x, alpha, beta, y) : launch_apply<1, false>(g, s, x, alpha, beta, y);
     return launch_status();
+}
+
+int hrl_bn_forward_eval(const float *x, int64_t N, int64_t C, int64_t HW, const float *weight, const float *bias,
+                        const float *running_mean, const float *running_var, double eps, int relu, float *y,
+                        float *coef, void *stream) {
+    if (!x || !y || !running_mean || !running_var || !coef) return HRL_EINVAL;
+    if (N == 0) return HRL_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, (int)C, weight, bias,
+                       running_mean, running_var, eps, coef, coef + C);
+    const int rc = launch_status();
+    if (rc) return rc;
+    return hrl_bn_apply(x, N, C, HW, coef, coef + C, relu, y, stream);
 }
 
 int hrl_bn_finalize_backward(const double *part, int64_t nparts, int64_t C, int64_t count, const float *weight,

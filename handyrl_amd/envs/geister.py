@@ -182,6 +182,7 @@ class GeisterBatch:
     A = 214
     P = 2
     MAX_PLIES = 202
+    ALTERNATING = True   # the mover is ply % 2 in every live game (colours alternate, geister.py:389)
     OBS_SHAPE = {'board': (BOARD_PLANES, *BOARD), 'scalar': (SCALARS,)}
     MOVES = 144
     # initial squares of the 8 pieces of each colour (geister.py:179-182); 'B2' = x 1, y 1

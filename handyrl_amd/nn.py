@@ -89,6 +89,22 @@ def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps, 
     return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu)
 
 
+def batch_norm_eval(x, weight, bias, running_mean, running_var, eps, relu=False):
+    """Inference BatchNorm [+ ReLU] from the running statistics (hrl_bn_forward_eval); not differentiable."""
+    if torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)):
+        y = torch.nn.functional.batch_norm(x, running_mean, running_var, weight, bias, False, 0.0, eps)
+        return torch.relu(y) if relu else y
+    x = x.contiguous()
+    N, C = x.shape[0], x.shape[1]
+    y = torch.empty_like(x)
+    coef = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+    _native.check(_native.load().hrl_bn_forward_eval(
+        _native.ptr(x), N, C, x[0, 0].numel(), _native.ptr(weight), _native.ptr(bias), _native.ptr(running_mean),
+        _native.ptr(running_var), float(eps), int(relu), _native.ptr(y), _native.ptr(coef),
+        _native.stream_of(x.device)), 'hrl_bn_forward_eval')
+    return y
+
+
 BOARD_MAX_CELLS = 16
 ROWS_MIN_CHUNKED = 4096
 
@@ -327,8 +343,12 @@ class BatchNorm2d(nn.BatchNorm2d):
 
     def forward(self, x):
         row = x.shape[1] * x.shape[2] * x.shape[3] if x.dim() == 4 else 0
-        use_hip = (self.training and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
-                   and x.shape[0] > 0 and (row <= _MAX_ROW_SCALAR or (row % 4 == 0 and row <= _MAX_ROW)))
+        shape_ok = (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+                    and x.shape[0] > 0 and (row <= _MAX_ROW_SCALAR or (row % 4 == 0 and row <= _MAX_ROW)))
+        if shape_ok and not self.training and self.track_running_stats and self.running_mean is not None:
+            return batch_norm_eval(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps,
+                                   self.fused_relu)
+        use_hip = shape_ok and self.training
         if not use_hip:
             y = super().forward(x)
             return torch.relu(y) if self.fused_relu else y

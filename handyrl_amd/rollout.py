@@ -39,6 +39,7 @@ class TicTacToeBatch:
     A = 9
     P = 2
     MAX_PLIES = 9
+    ALTERNATING = True   # the mover is ply % 2 in every live game
     OBS_SHAPE = (3, 3, 3)
     LINES = ((0, 1, 2), (3, 4, 5), (6, 7, 8), (0, 3, 6), (1, 4, 7), (2, 5, 8), (0, 4, 8), (2, 4, 6))
 
@@ -142,7 +143,14 @@ class DeviceGenerator:
             active = ~env.terminal()
             player = env.turn()
             o = env.observation(player)
-            h_in = None if hidden is None else map_r(hidden, lambda h: h[rows, player])
+            # envs whose mover is ply % P in every live game (TicTacToe, Geister): the mover's state is a view
+            mover = t % P if getattr(env, 'ALTERNATING', False) else None
+            if hidden is None:
+                h_in = None
+            elif mover is not None:
+                h_in = map_r(hidden, lambda h: h[:, mover])
+            else:
+                h_in = map_r(hidden, lambda h: h[rows, player])
             out = self.net(o, h_in)
             m = torch.where(env.legal(), 0.0, 1e32)                        # generation.py:50-51
             p = out['policy'] - m
@@ -160,8 +168,11 @@ class DeviceGenerator:
                 reward[:, t] = torch.where(act, env.reward(), reward[:, t])
             if hidden is not None:
                 def advance(h, nh):
-                    cur = h[rows, player]
-                    h[rows, player] = torch.where(active.view(-1, *([1] * (nh.dim() - 1))), nh, cur)
+                    m = active.view(-1, *([1] * (nh.dim() - 1)))
+                    if mover is not None:
+                        h[:, mover].copy_(torch.where(m, nh, h[:, mover]))
+                    else:
+                        h[rows, player] = torch.where(m, nh, h[rows, player])
                 bimap_r(hidden, out['hidden'], advance)
             env.step(a, active)
         self.net.train(was_training)

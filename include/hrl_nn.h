@@ -62,6 +62,13 @@ int hrl_bn_finalize_stats(const double *part, int64_t nparts, int64_t C, int64_t
                           float *save_mean, float *save_invstd, float *alpha, float *beta, void *stream);
 int hrl_bn_apply(const float *x, int64_t N, int64_t C, int64_t HW, const float *alpha, const float *beta, int relu,
                  float *y, void *stream);
+/* Eval-mode forward (inference, e.g. self-play): y = x*alpha + beta [relu] with
+ * alpha = weight / sqrt(running_var + eps), beta = bias - running_mean*alpha
+ * (the vendor inference BatchNorm takes ~0.5 ms on (2048, 32, 6, 6)).
+ * coef: 2*C floats of scratch (alpha | beta). */
+int hrl_bn_forward_eval(const float *x, int64_t N, int64_t C, int64_t HW, const float *weight, const float *bias,
+                        const float *running_mean, const float *running_var, double eps, int relu, float *y,
+                        float *coef, void *stream);
 /* The backward in pieces: fold (sum g, sum g*(x-mean)) partials into dweight,
  * dbias and the apply coefficients kcoef, gmean (C floats each); then
  * dx = ((g - gmean) - (x - mean)*kcoef) * invstd * weight, g masked by the

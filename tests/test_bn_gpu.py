@@ -270,3 +270,27 @@ def test_conv_bn_chain_matches_layer_by_layer(cuda, N, relu_in):
         assert err < 1e-5, err
     for a, b in zip(s1, s0):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(2048, 32, 6, 6), (37, 8, 6, 6), (5, 1, 6, 6), (64, 32, 3, 3)])
+@pytest.mark.parametrize('relu', [False, True])
+def test_bn_eval_matches_torch(cuda, shape, relu):
+    """Inference BatchNorm (hrl_bn_forward_eval: x*alpha + beta from the running statistics)
+    vs torch's eval batch_norm; tolerance 2e-6 relative (alpha/beta rounding)."""
+    from handyrl_amd.nn import BatchNorm2d
+    torch.manual_seed(shape[0])
+    C = shape[1]
+    bn = BatchNorm2d(C).to(cuda).eval()
+    bn.fused_relu = relu
+    bn.running_mean.uniform_(-1, 1)
+    bn.running_var.uniform_(0.5, 2)
+    bn.weight.data.uniform_(0.5, 1.5)
+    bn.bias.data.uniform_(-0.5, 0.5)
+    x = torch.randn(*shape, device=cuda) * 3
+    with torch.no_grad():
+        y = bn(x)
+        ref = torch.nn.functional.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
+        if relu:
+            ref = torch.relu(ref)
+    torch.testing.assert_close(y, ref, rtol=2e-6, atol=2e-6)
