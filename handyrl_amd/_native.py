@@ -80,13 +80,21 @@ SIGNATURES = {
                                              ctypes.c_int, _f32p, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_conv3x3_wgrad_ex': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _i64, _f32p, ctypes.c_void_p, _i64,
                                             ctypes.c_void_p]),
+    'hrl_hidden_gather': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_void_p]),
+    'hrl_hidden_gather_backward': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, ctypes.c_int, ctypes.c_void_p,
+                                                  ctypes.c_int, _f32p, ctypes.c_void_p]),
+    'hrl_hidden_update': (ctypes.c_int, [_f32p, ctypes.c_void_p, _i64, _f32p, _i64, _i64, ctypes.c_int,
+                                         ctypes.c_void_p, _f32p, ctypes.c_void_p]),
+    'hrl_hidden_update_backward': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, ctypes.c_int, ctypes.c_void_p,
+                                                  _f32p, ctypes.c_void_p, ctypes.c_void_p]),
     'hrl_lstm_gates_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p,
                                               ctypes.c_void_p]),
     'hrl_lstm_gates_backward': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p,
                                                ctypes.c_void_p]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lib = None
 
@@ -121,6 +129,16 @@ def check(code, what):
 def ptr(t):
     """Device pointer of a tensor (None -> NULL)."""
     return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def ptr_array(tensors):
+    """A C array of device pointers (None -> NULL) for the multi-tensor entry points."""
+    arr = (ctypes.c_void_p * len(tensors))(*[None if t is None else t.data_ptr() for t in tensors])
+    return arr
+
+
+def i64_array(values):
+    return (ctypes.c_int64 * len(values))(*values)
 
 
 def stream_of(device):

@@ -118,13 +118,26 @@ class GradAllReduce:
             self._launch_ready()
         return hook
 
+    enabled = True
+
     def _launch_ready(self):
+        if not self.enabled:
+            return
         # launch strictly in bucket order so every rank issues the same sequence
         while self._next < len(self.buckets) and self._pending[self._next] == 0:
             lo, hi = self.buckets[self._next]
             self._works[self._next] = dist.all_reduce(self.fg.flat[lo:hi], op=dist.ReduceOp.SUM,
                                                       group=self.group, async_op=True)
             self._next += 1
+
+    def set_live(self, live):
+        """Only params with live[i] fire their accumulate hook (the others get no gradient, as under the
+        reference's autograd); a bucket is complete when its live params are."""
+        self.bucket_size = [0] * len(self.buckets)
+        for j, b in self.param_bucket.items():
+            if live[j]:
+                self.bucket_size[b] += 1
+        self._pending = list(self.bucket_size)
 
     def finish(self):
         """Launch any bucket whose params got no gradient, then wait for all of them."""

@@ -98,9 +98,19 @@ class DRC(nn.Module):
         ws = [blk.conv.weight for blk in self.blocks]
         bias = [blk.conv.bias for blk in self.blocks]
         pad = self.blocks[0].conv.padding
-        w_x = torch.cat([w[:, :cin] for w in ws])
-        b_x = None if bias[0] is None else torch.cat(bias)
-        zx = F.conv2d(x, w_x, b_x, padding=pad).chunk(len(self.blocks), dim=-3)
+        n = len(self.blocks)
+
+        def x_half(layers):
+            w_x = torch.cat([ws[i][:, :cin] for i in layers])
+            b_x = None if bias[0] is None else torch.cat([bias[i] for i in layers])
+            return F.conv2d(x, w_x, b_x, padding=pad).chunk(len(layers), dim=-3)
+        if torch.is_grad_enabled() and n > 1:
+            # Only the last layer reaches the output (every cell reads x and its own state), so the
+            # others must stay outside its autograd graph: their weights then get no gradient at
+            # all, as with the reference's cells, and the optimizer leaves them alone.
+            zx = x_half(range(n - 1)) + x_half([n - 1])
+        else:
+            zx = x_half(range(n))
         w_h = [w[:, cin:].contiguous() for w in ws]
         for _ in range(num_repeats):
             for i in range(len(self.blocks)):

@@ -324,6 +324,65 @@ def lstm_gates(zx, zh, c):
     return _LSTMGates.apply(zx, zh, c)
 
 
+class _HiddenGather(torch.autograd.Function):
+    """Per-step recurrent input from the flat state (csrc/hrl_hidden.hip, train.py:157-164).
+
+    H: leaf-major flat state, leaf l (B, P, *shapes[l]).  Returns the leaves
+    sum_p H_l * m (sum=True, (B, *shape)) or H_l * m reshaped to (B*P, *shape).
+    """
+
+    @staticmethod
+    def forward(ctx, H, m, summed, shapes, B, P):
+        F = [int(torch.Size(sh).numel()) for sh in shapes]
+        rows = B if summed else B * P
+        # one allocation per leaf: the net's convolutions see ordinary, allocator-aligned tensors
+        outs = [torch.empty(rows, *sh, dtype=H.dtype, device=H.device) for sh in shapes]
+        _native.check(_native.load().hrl_hidden_gather(
+            _native.ptr(H), _native.ptr(m), B, P, len(F), _native.i64_array(F), int(summed), _native.ptr_array(outs),
+            _native.stream_of(H.device)), 'hrl_hidden_gather')
+        ctx.save_for_backward(m)
+        ctx.meta = (summed, F, B, P, H.numel())
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        (m,) = ctx.saved_tensors
+        summed, F, B, P, n = ctx.meta
+        g = [None if x is None else x.contiguous() for x in grads]
+        dH = torch.empty(n, dtype=m.dtype, device=m.device)
+        _native.check(_native.load().hrl_hidden_gather_backward(
+            _native.ptr_array(g), _native.ptr(m), B, P, len(F), _native.i64_array(F), int(summed), _native.ptr(dH),
+            _native.stream_of(m.device)), 'hrl_hidden_gather_backward')
+        return dH, None, None, None, None, None
+
+
+class _HiddenUpdate(torch.autograd.Function):
+    """New flat state H * (1 - m) + nh * m (csrc/hrl_hidden.hip, train.py:167-174); nh leaves (B*Pn, *shape)."""
+
+    @staticmethod
+    def forward(ctx, H, m, B, P, Pn, F, *nh):
+        nh = [x.contiguous() for x in nh]
+        out = torch.empty_like(H)
+        _native.check(_native.load().hrl_hidden_update(
+            _native.ptr(H), _native.ptr_array(nh), Pn, _native.ptr(m), B, P, len(F), _native.i64_array(F),
+            _native.ptr(out), _native.stream_of(H.device)), 'hrl_hidden_update')
+        ctx.save_for_backward(m)
+        ctx.meta = (B, P, Pn, F, [x.shape for x in nh])
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (m,) = ctx.saved_tensors
+        B, P, Pn, F, nh_shapes = ctx.meta
+        dout = dout.contiguous()
+        dH = torch.empty_like(dout)
+        dnh = [torch.empty(sh, dtype=dout.dtype, device=dout.device) for sh in nh_shapes]
+        _native.check(_native.load().hrl_hidden_update_backward(
+            _native.ptr(dout), _native.ptr(m), B, P, Pn, len(F), _native.i64_array(F), _native.ptr(dH),
+            _native.ptr_array(dnh), _native.stream_of(dout.device)), 'hrl_hidden_update_backward')
+        return (dH, None, None, None, None, None, *dnh)
+
+
 def _board_conv_ok(m):
     k = m.kernel_size
     return (m.stride == (1, 1) and m.dilation == (1, 1) and m.groups == 1 and m.padding_mode == 'zeros'

@@ -48,6 +48,8 @@ def forward_prediction(model, hidden, batch, args):
     if hidden is None:
         obs = map_r(observations, lambda o: o.reshape(-1, *o.shape[3:]))
         outputs = model(obs, None)
+    elif _flat_hidden_ok(hidden, tmask):
+        outputs = _unroll_flat_hidden(model, hidden, batch, args)
     else:
         per_t = {}
         tbt_single = args['turn_based_training'] and not args['observation']
@@ -81,6 +83,70 @@ def forward_prediction(model, hidden, batch, args):
         else:
             result[k] = o.mul(batch['observation_mask'])
     return result
+
+
+def _leaves(x):
+    if isinstance(x, (list, tuple)):
+        return [l for v in x for l in _leaves(v)]
+    if isinstance(x, dict):
+        return [l for v in x.values() for l in _leaves(v)]
+    return [x]
+
+
+def _rebuild(template, it):
+    if isinstance(template, (list, tuple)):
+        return type(template)(_rebuild(v, it) for v in template)
+    if isinstance(template, dict):
+        return type(template)((k, _rebuild(v, it)) for k, v in template.items())
+    return next(it)
+
+
+FLAT_HIDDEN = False  # recurrent state through csrc/hrl_hidden.hip (one flat buffer); off: it defeats
+                     # autograd's pruning of state that never reaches an output
+
+
+def _flat_hidden_ok(hidden, tmask):
+    if not FLAT_HIDDEN:
+        return False
+    leaves = _leaves(hidden)
+    if not (0 < len(leaves) <= 16) or not all(isinstance(h, torch.Tensor) for h in leaves):
+        return False
+    B, P = leaves[0].shape[:2]
+    return (tmask.is_cuda and all(h.is_cuda and h.dtype == torch.float32 and h.dim() >= 2
+                                  and tuple(h.shape[:2]) == (B, P) for h in leaves)
+            and tmask.shape[0] == B and tmask.shape[2] == P)
+
+
+def _unroll_flat_hidden(model, hidden, batch, args):
+    """The recurrent branch on the GPU: the state of every hidden tensor in one flat buffer,
+    masked/summed and mixed by one HIP launch each per step (nn._HiddenGather / _HiddenUpdate).
+    Same arithmetic as the torch formulation below (train.py:155-174)."""
+    from .nn import _HiddenGather, _HiddenUpdate
+    observations = batch['observation']
+    tmask = batch['turn_mask']
+    B, T, P = tmask.shape[:3]
+    leaves = _leaves(hidden)
+    shapes = [tuple(h.shape[2:]) for h in leaves]
+    F = [int(torch.Size(sh).numel()) for sh in shapes]
+    H = torch.cat([h.reshape(-1) for h in leaves])
+    masks = batch['observation_mask'].reshape(B, T, P).transpose(0, 1).contiguous()   # (T, B, P)
+    summed = args['turn_based_training'] and not args['observation']
+    per_t = {}
+    for t in range(T):
+        obs = map_r(observations, lambda o: o[:, t].reshape(-1, *o.shape[3:]))
+        m = masks[t]
+        h_in = _rebuild(hidden, iter(_HiddenGather.apply(H, m, summed, shapes, B, P)))
+        out_t = model(obs, h_in)
+        next_hidden = None
+        for k, o in out_t.items():
+            if k == 'hidden':
+                next_hidden = o
+            else:
+                per_t.setdefault(k, []).append(o)
+        nh = _leaves(next_hidden)
+        Pn = nh[0].shape[0] // B
+        H = _HiddenUpdate.apply(H, m, B, P, Pn, F, *nh)
+    return {k: torch.stack(o, dim=1) for k, o in per_t.items() if o[0] is not None}
 
 
 def compose_losses(outputs, log_selected_policies, total_advantages, targets, batch, args):

@@ -29,7 +29,7 @@ import torch.nn as nn
 from . import distributed as hdist
 from .nn import accelerate, fuse_bn_relu
 from .train import forward_prediction, loss_terms
-from .util import bimap_r
+from .util import map_r, bimap_r
 
 DEFAULT_LR = 3e-8  # train.py:318
 
@@ -57,11 +57,12 @@ class LearnerStep:
         # one fused multi-tensor Adam kernel on the GPU (train.py:322: Adam, weight_decay 1e-5)
         fused = device.type == 'cuda'
         if self.graph:
-            self.optimizer = torch.optim.Adam(self.params, lr=torch.tensor(lr, device=device),
-                                              weight_decay=1e-5, capturable=True, fused=True)
+            self._opt_kwargs = dict(lr=torch.tensor(lr, device=device), weight_decay=1e-5, capturable=True,
+                                    fused=True)
         else:
-            self.optimizer = torch.optim.Adam(self.params, lr=lr, weight_decay=1e-5, fused=fused,
-                                              foreach=None if fused else True)
+            self._opt_kwargs = dict(lr=lr, weight_decay=1e-5, fused=fused, foreach=None if fused else True)
+        self.optimizer = torch.optim.Adam(self.params, **self._opt_kwargs)
+        self.live = None        # params that receive a gradient (set on the first batch)
         self._graph = None
         self._static = None
         self._static_out = None
@@ -76,7 +77,44 @@ class LearnerStep:
                 group['lr'] = lr
 
     # -- one update ----------------------------------------------------------
+    def _probe_live(self, batch, hidden):
+        """Which parameters receive a gradient at all (reference semantics: torch.optim.Adam skips a
+        parameter whose .grad stays None -- no update, no weight decay; e.g. GeisterNet's first two DRC
+        blocks never reach an output, geister.py:91-94).  One forward/backward on a 2-trajectory slice
+        of the first batch with every .grad set to None; BatchNorm buffers are restored afterwards."""
+        def head(x):
+            return x[:2] if isinstance(x, torch.Tensor) and x.dim() > 0 else x
+        small = map_r(batch, head)
+        small_hidden = None if hidden is None else map_r(hidden, head)
+        buffers = [b.detach().clone() for b in self.net.buffers()]
+        views = [p.grad for p in self.params]
+        for p in self.params:
+            p.grad = None
+        if self.reducer is not None:
+            self.reducer.enabled = False
+        try:
+            outputs = forward_prediction(self.net, small_hidden, small, self.args)
+            losses, _ = self.loss_fn(outputs, small, self.args)
+            losses['total'].backward()
+            live = [p.grad is not None for p in self.params]
+        finally:
+            for p, v in zip(self.params, views):
+                p.grad = v
+            for b, saved in zip(self.net.buffers(), buffers):
+                b.copy_(saved)
+            if self.reducer is not None:
+                self.reducer.enabled = True
+        self.live = live
+        if not all(live):
+            kw = dict(self._opt_kwargs)
+            kw['lr'] = self.optimizer.param_groups[0]['lr']   # keep a set_lr() made before the first step
+            self.optimizer = torch.optim.Adam([p for p, l in zip(self.params, live) if l], **kw)
+            if self.reducer is not None:
+                self.reducer.set_live(live)
+
     def _body(self, batch, hidden):
+        if self.live is None:
+            self._probe_live(batch, hidden)
         if self._fuse_pending:
             self._fuse_pending = False
             obs = batch['observation']
@@ -126,13 +164,28 @@ class LearnerStep:
             raise RuntimeError('HIP-graph capture of the multi-GPU step is not supported; use graph=False')
         self._static = batch
         self._static_hidden = hidden  # recurrent nets: the window's initial state (zeros, train.py:375)
-        # warm up on a side stream (allocator pools, MIOpen kernel selection, lazy state)
+        # Warm up on a side stream (allocator pools, MIOpen kernel selection, lazy optimizer state),
+        # then put the training state back so the first replay is the first update: parameters and
+        # buffers restored in place, Adam's moments and step counts zeroed in place (the graph keeps
+        # pointing at the same tensors).
+        params = list(self.net.parameters())
+        saved_p = [p.detach().clone() for p in params]
+        saved_b = [b.detach().clone() for b in self.net.buffers()]
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             for _ in range(3):
                 self._body(batch, hidden)
         torch.cuda.current_stream(self.device).wait_stream(side)
+        with torch.no_grad():
+            for p, v in zip(params, saved_p):
+                p.copy_(v)
+            for b, v in zip(self.net.buffers(), saved_b):
+                b.copy_(v)
+            for state in self.optimizer.state.values():
+                for v in state.values():
+                    if isinstance(v, torch.Tensor):
+                        v.zero_()
         self._graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._graph):
             self._static_out = self._body(batch, hidden)

@@ -156,6 +156,26 @@ int hrl_lstm_gates_backward(const float *gates, const float *c, const float *c_o
                             const float *dc_out, int64_t N, int64_t H, int64_t HW, float *dz, float *dc,
                             void *stream);
 
+/*
+ * Recurrent state plumbing of forward_prediction (handyrl/train.py:155-174),
+ * one launch for all state tensors (csrc/hrl_hidden.hip).  The state is one
+ * leaf-major buffer: leaf l is (B, P, F[l]) floats, leaves back to back.
+ * mask: (B, P) observation mask of the step.
+ *   gather:  out[l] = sum_p H_l[:, p] * mask[:, p]  -> (B, F[l])      (sum != 0)
+ *                     H_l * mask                     -> (B, P, F[l])   (sum == 0)
+ *   update:  out_l = H_l * (1 - mask) + nh[l] * mask, nh[l]: (B, Pn, F[l]), Pn = 1 or P
+ * and their adjoints (a NULL dout[l] in the gather backward is a zero gradient).
+ * At most 16 leaves.
+ */
+int hrl_hidden_gather(const float *H, const float *mask, int64_t B, int64_t P, int nleaves, const int64_t *F,
+                      int sum, float *const *out, void *stream);
+int hrl_hidden_gather_backward(const float *const *dout, const float *mask, int64_t B, int64_t P, int nleaves,
+                               const int64_t *F, int sum, float *dH, void *stream);
+int hrl_hidden_update(const float *H, const float *const *nh, int64_t Pn, const float *mask, int64_t B, int64_t P,
+                      int nleaves, const int64_t *F, float *out, void *stream);
+int hrl_hidden_update_backward(const float *dout, const float *mask, int64_t B, int64_t P, int64_t Pn, int nleaves,
+                               const int64_t *F, float *dH, float *const *dnh, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -197,3 +197,41 @@ def test_drc_hip_path_matches_reference_cells(golden, cuda):
     # fp32 reassociation (x/h halves summed in the gate kernel, HIP BN): norm-relative 1e-4
     errs = {n: float((res[1][1][n] - gp).norm() / gp.norm().clamp(min=1e-12)) for n, gp in res[0][1].items()}
     assert max(errs.values()) < 1e-4, sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('graph', [False, True])
+def test_gpu_recurrent_learner_matches_cpu_oracle(cuda, graph):
+    """Three recurrent learner steps (LearnerStep on the GPU, HIP graph or eager) vs the oracle's
+    CPU learner (train.py:375-385) from the same seeded GeisterNet on the same batch: per-step
+    losses and grad norms, and every parameter afterwards.  GeisterNet's first two DRC blocks never
+    reach an output (geister.py:91-94): their .grad stays None under the reference's autograd, so
+    Adam leaves them untouched -- they must be bit-identical to their initial values."""
+    from handyrl_amd.synthetic import geister_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    B, T = 8, 8
+    args = default_args(T, B)
+    batch = geister_batch(B, T, cuda, seed=3)
+    cpu_batch = {k: ({kk: vv.cpu() for kk, vv in v.items()} if isinstance(v, dict) else v.cpu())
+                 for k, v in batch.items()}
+    ref = seeded_net()
+    init = {n: p.detach().clone() for n, p in ref.named_parameters()}
+    oracle = ol.CpuLearner(ref, args)
+    net = seeded_net()
+    step = LearnerStep(net, args, cuda, graph=graph)
+
+    def zeros(device):
+        return tuple([h.to(device) for h in hs] for hs in net.init_hidden([B, 2]))
+    for i in range(3):
+        r = oracle.step(cpu_batch, zeros('cpu'))
+        out = step.step(batch, zeros(cuda))
+        assert abs(float(out['total']) - r['total']) <= 1e-4 * max(1.0, abs(r['total'])), (i, float(out['total']), r)
+        assert abs(float(out['grad_norm']) - r['grad_norm']) <= 1e-3 * max(1e-3, r['grad_norm']), i
+    dead = [n for (n, _), live in zip(step.net.named_parameters(), step.live) if not live]
+    assert sorted(dead) == sorted('body.blocks.%d.conv.%s' % (i, k) for i in (0, 1) for k in ('weight', 'bias'))
+    got = dict(step.net.named_parameters())
+    for n, p in ref.named_parameters():
+        if n in dead:
+            assert torch.equal(got[n].detach().cpu(), init[n]), n
+        else:
+            torch.testing.assert_close(got[n].detach().cpu(), p.detach(), rtol=1e-4, atol=2e-6, msg=n)

@@ -79,8 +79,8 @@ def test_graph_step_equals_eager(cuda):
     graph = LearnerStep(g_net, args, cuda, graph=True)
     for _ in range(5):
         e_out = eager.step(batch)
-    graph.step(batch)          # capture: 3 warm-up updates + 1 replay
-    g_out = graph.step(batch)  # 5th update
+    for _ in range(5):         # the capture's warm-up updates are rolled back: 5 replays = 5 updates
+        g_out = graph.step(batch)
     torch.cuda.synchronize()
     for k in ('p', 'v', 'ent', 'total'):
         _close(g_out[k].item(), e_out[k].item(), rtol=1e-5, what=k)

@@ -54,12 +54,18 @@ def main():
     ap.add_argument('--graph', type=int, nargs='+', default=[0, 1])
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--flat', type=int, nargs='+', default=[1], help='train.FLAT_HIDDEN values to compare')
     opts = ap.parse_args()
     device = torch.device('cuda', 0)
-    for T in opts.T:
-        for B in opts.B:
-            for g in opts.graph:
-                print(json.dumps(run(B, T, g, opts.steps, opts.warmup, device)), flush=True)
+    import handyrl_amd.train as train_mod
+    for flat in opts.flat:
+        train_mod.FLAT_HIDDEN = bool(flat)
+        for T in opts.T:
+            for B in opts.B:
+                for g in opts.graph:
+                    r = run(B, T, g, opts.steps, opts.warmup, device)
+                    r['flat_hidden'] = flat
+                    print(json.dumps(r), flush=True)
 
 
 if __name__ == '__main__':
