@@ -80,21 +80,21 @@ SIGNATURES = {
                                              ctypes.c_int, _f32p, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_conv3x3_wgrad_ex': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _i64, _f32p, ctypes.c_void_p, _i64,
                                             ctypes.c_void_p]),
-    'hrl_hidden_gather': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
-                                         ctypes.c_void_p, ctypes.c_void_p]),
+    'hrl_hidden_gather': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     'hrl_hidden_gather_backward': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, ctypes.c_int, ctypes.c_void_p,
-                                                  ctypes.c_int, _f32p, ctypes.c_void_p]),
-    'hrl_hidden_update': (ctypes.c_int, [_f32p, ctypes.c_void_p, _i64, _f32p, _i64, _i64, ctypes.c_int,
-                                         ctypes.c_void_p, _f32p, ctypes.c_void_p]),
-    'hrl_hidden_update_backward': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, ctypes.c_int, ctypes.c_void_p,
-                                                  _f32p, ctypes.c_void_p, ctypes.c_void_p]),
+                                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    'hrl_hidden_update': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, _i64, _f32p, _i64, _i64, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    'hrl_hidden_update_backward': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, _i64, ctypes.c_int,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     'hrl_lstm_gates_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p,
                                               ctypes.c_void_p]),
     'hrl_lstm_gates_backward': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p,
                                                ctypes.c_void_p]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lib = None
 

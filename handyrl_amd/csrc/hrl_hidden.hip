@@ -9,10 +9,11 @@
 //   h'    = h * (1 - m) + nh * m               (nh broadcast over players if it has one)
 //
 // GeisterNet carries 6 state tensors, so in torch that is ~36 elementwise
-// launches forward and more backward per step.  Here the state of all
-// tensors lives in ONE leaf-major buffer (leaf l: (B, P, F_l) contiguous at
-// offset off_l) and each operation and its adjoint is one launch over all
-// leaves.  Arithmetic is torch's: (1 - m) first, products, then the sum
+// launches forward and more backward per step.  Here each operation and its
+// adjoint is ONE launch over all state tensors (a table of per-tensor
+// pointers).  The tensors stay separate: a state tensor whose gradient is
+// None (it never reaches an output) is simply left out of the backward
+// launch, preserving autograd's pruning.  Arithmetic is torch's: (1 - m) first, products, then the sum
 // (p ascending; P = 2 in every turn-based env, where it matches torch.sum).
 // Elementwise, HBM-bound.
 
@@ -27,16 +28,16 @@ namespace {
 constexpr int kMaxLeaves = 16;
 constexpr int kThreads = 256;
 
-// Leaf table.  Launch geometry: blockIdx.z = leaf, blockIdx.y strides over the
-// row index (b, or (b, p)), threads run along the leaf's contiguous features in
-// float4 (all F % 4 == 0, the usual board-state case) or floats -- no integer
-// division anywhere.
+// Per-leaf table.  Launch geometry: blockIdx.z = leaf, blockIdx.y strides over
+// rows (b), threads run along the leaf's contiguous features in float4 (every
+// F % 4 == 0 and 16-byte aligned pointers) or floats -- no integer division.
 struct Leaves {
     int n;
-    int F[kMaxLeaves];          // floats per (b, p) of each leaf
-    int64_t off[kMaxLeaves];    // offset of leaf l in the leaf-major (B, P, F_l) state buffer
-    const float *src[kMaxLeaves];
-    float *dst[kMaxLeaves];
+    int F[kMaxLeaves];
+    const float *a[kMaxLeaves];   // gather: H; gather bwd: g; update: H; update bwd: dout
+    const float *b[kMaxLeaves];   // update: nh
+    float *c[kMaxLeaves];         // gather: out; gather bwd: dH; update: out; update bwd: dH
+    float *d[kMaxLeaves];         // update bwd: dnh
 };
 
 template <int VW>
@@ -44,14 +45,12 @@ struct V;
 template <>
 struct V<4> {
     using T = float4;
-    static __device__ __forceinline__ T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
     static __device__ __forceinline__ T mul(T a, float s) { return make_float4(a.x * s, a.y * s, a.z * s, a.w * s); }
     static __device__ __forceinline__ T add(T a, T b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 };
 template <>
 struct V<1> {
     using T = float;
-    static __device__ __forceinline__ T zero() { return 0.f; }
     static __device__ __forceinline__ T mul(T a, float s) { return a * s; }
     static __device__ __forceinline__ T add(T a, T b) { return a + b; }
 };
@@ -62,16 +61,15 @@ struct V<1> {
     const int v = blockIdx.x * kThreads + threadIdx.x;                                    \
     if (v >= nv) return;
 
-// gather, summed over players: out_l[b, v] = sum_p H_l[b, p, v] * m[b, p]
+// gather, summed over players: out[b, v] = sum_p H[b, p, v] * m[b, p]
 template <int VW>
-__global__ __launch_bounds__(kThreads) void hidden_gather_sum_kernel(const float *__restrict__ H,
-                                                                     const float *__restrict__ m, int B, int P,
+__global__ __launch_bounds__(kThreads) void hidden_gather_sum_kernel(const float *__restrict__ m, int B, int P,
                                                                      Leaves L) {
     using W = V<VW>;
     using T = typename W::T;
     HRL_LEAF_LOOP
-    const T *h = reinterpret_cast<const T *>(H + L.off[l]);
-    T *out = reinterpret_cast<T *>(L.dst[l]);
+    const T *h = reinterpret_cast<const T *>(L.a[l]);
+    T *out = reinterpret_cast<T *>(L.c[l]);
     for (int b = blockIdx.y; b < B; b += gridDim.y) {
         T acc = W::mul(h[(int64_t)(b * P) * nv + v], m[b * P]);
         for (int p = 1; p < P; ++p) acc = W::add(acc, W::mul(h[(int64_t)(b * P + p) * nv + v], m[b * P + p]));
@@ -79,48 +77,44 @@ __global__ __launch_bounds__(kThreads) void hidden_gather_sum_kernel(const float
     }
 }
 
-// gather, one row per player: out_l[bp, v] = H_l[bp, v] * m[bp]
+// gather, one row per player: out[bp, v] = H[bp, v] * m[bp]
 template <int VW>
-__global__ __launch_bounds__(kThreads) void hidden_gather_keep_kernel(const float *__restrict__ H,
-                                                                      const float *__restrict__ m, int BP, Leaves L) {
+__global__ __launch_bounds__(kThreads) void hidden_gather_keep_kernel(const float *__restrict__ m, int BP, Leaves L) {
     using W = V<VW>;
     using T = typename W::T;
     HRL_LEAF_LOOP
-    const T *h = reinterpret_cast<const T *>(H + L.off[l]);
-    T *out = reinterpret_cast<T *>(L.dst[l]);
+    const T *h = reinterpret_cast<const T *>(L.a[l]);
+    T *out = reinterpret_cast<T *>(L.c[l]);
     for (int r = blockIdx.y; r < BP; r += gridDim.y) out[(int64_t)r * nv + v] = W::mul(h[(int64_t)r * nv + v], m[r]);
 }
 
-// adjoint of the gather: dH_l[b, p, v] = g_l[b or bp, v] * m[b, p]; a NULL g_l is a zero gradient
+// adjoint of the gather: dH[b, p, v] = g[b or bp, v] * m[b, p]
 template <int VW>
 __global__ __launch_bounds__(kThreads) void hidden_gather_bwd_kernel(const float *__restrict__ m, int B, int P,
-                                                                     int summed, Leaves L, float *__restrict__ dH) {
+                                                                     int summed, Leaves L) {
     using W = V<VW>;
     using T = typename W::T;
     HRL_LEAF_LOOP
-    const T *g = reinterpret_cast<const T *>(L.src[l]);
-    T *d = reinterpret_cast<T *>(dH + L.off[l]);
+    const T *g = reinterpret_cast<const T *>(L.a[l]);
+    T *d = reinterpret_cast<T *>(L.c[l]);
     for (int b = blockIdx.y; b < B; b += gridDim.y) {
         for (int p = 0; p < P; ++p) {
             const int bp = b * P + p;
-            T val = W::zero();
-            if (g) val = W::mul(g[(int64_t)(summed ? b : bp) * nv + v], m[bp]);
-            d[(int64_t)bp * nv + v] = val;
+            d[(int64_t)bp * nv + v] = W::mul(g[(int64_t)(summed ? b : bp) * nv + v], m[bp]);
         }
     }
 }
 
-// update: out_l[b, p, v] = H_l[b, p, v] * (1 - m[b, p]) + nh_l[b, p or 0, v] * m[b, p]
+// update: out[b, p, v] = H[b, p, v] * (1 - m[b, p]) + nh[b, p or 0, v] * m[b, p]
 template <int VW>
-__global__ __launch_bounds__(kThreads) void hidden_update_kernel(const float *__restrict__ H,
-                                                                 const float *__restrict__ m, int B, int P, int Pn,
-                                                                 Leaves L, float *__restrict__ out) {
+__global__ __launch_bounds__(kThreads) void hidden_update_kernel(const float *__restrict__ m, int B, int P, int Pn,
+                                                                 Leaves L) {
     using W = V<VW>;
     using T = typename W::T;
     HRL_LEAF_LOOP
-    const T *h = reinterpret_cast<const T *>(H + L.off[l]);
-    const T *nh = reinterpret_cast<const T *>(L.src[l]);
-    T *o = reinterpret_cast<T *>(out + L.off[l]);
+    const T *h = reinterpret_cast<const T *>(L.a[l]);
+    const T *nh = reinterpret_cast<const T *>(L.b[l]);
+    T *o = reinterpret_cast<T *>(L.c[l]);
     for (int b = blockIdx.y; b < B; b += gridDim.y) {
         for (int p = 0; p < P; ++p) {
             const int bp = b * P + p;
@@ -133,15 +127,14 @@ __global__ __launch_bounds__(kThreads) void hidden_update_kernel(const float *__
 
 // adjoint of the update: dH = dout * (1 - m); dnh = sum_p dout * m (Pn = 1) or dout * m
 template <int VW>
-__global__ __launch_bounds__(kThreads) void hidden_update_bwd_kernel(const float *__restrict__ dout,
-                                                                     const float *__restrict__ m, int B, int P,
-                                                                     int Pn, Leaves L, float *__restrict__ dH) {
+__global__ __launch_bounds__(kThreads) void hidden_update_bwd_kernel(const float *__restrict__ m, int B, int P, int Pn,
+                                                                     Leaves L) {
     using W = V<VW>;
     using T = typename W::T;
     HRL_LEAF_LOOP
-    const T *g = reinterpret_cast<const T *>(dout + L.off[l]);
-    T *d = reinterpret_cast<T *>(dH + L.off[l]);
-    T *dn = reinterpret_cast<T *>(L.dst[l]);
+    const T *g = reinterpret_cast<const T *>(L.a[l]);
+    T *d = reinterpret_cast<T *>(L.c[l]);
+    T *dn = reinterpret_cast<T *>(L.d[l]);
     for (int b = blockIdx.y; b < B; b += gridDim.y) {
         if (Pn == 1) {
             T acc = W::mul(g[(int64_t)(b * P) * nv + v], m[b * P]);
@@ -164,23 +157,22 @@ int status() {
 
 bool aligned16(const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// leaf table; vw = 4 when every leaf allows float4 access
-bool build(int n, const int64_t *F, int64_t B, int64_t P, const float *const *src, float *const *dst,
-           const float *a, const float *b, Leaves &L, int &vw, int &fmax) {
-    if (n < 1 || n > kMaxLeaves || B < 0 || P < 1 || B * P > (int64_t)1 << 30) return false;
+// fill the table from up to four pointer arrays (NULL arrays are skipped); false on a bad argument
+bool build(int n, const int64_t *F, int64_t B, int64_t P, const float *const *a, const float *const *b,
+           float *const *c, float *const *d, Leaves &L, int &vw, int &fmax) {
+    if (n < 1 || n > kMaxLeaves || B < 0 || P < 1 || B * P > ((int64_t)1 << 30) || !F || !a || !c) return false;
     L.n = n;
-    vw = aligned16(a) && aligned16(b) ? 4 : 1;
+    vw = 4;
     fmax = 0;
-    int64_t off = 0;
     for (int l = 0; l < n; ++l) {
-        if (F[l] < 1 || F[l] > (1 << 30)) return false;
+        if (F[l] < 1 || F[l] > (1 << 28) || !a[l] || !c[l] || (b && !b[l]) || (d && !d[l])) return false;
         L.F[l] = (int)F[l];
-        L.off[l] = off;
-        L.src[l] = src ? src[l] : nullptr;
-        L.dst[l] = dst ? dst[l] : nullptr;
-        if (F[l] % 4 || (off * 4) % 16 || !aligned16(L.src[l]) || !aligned16(L.dst[l])) vw = 1;
+        L.a[l] = a[l];
+        L.b[l] = b ? b[l] : nullptr;
+        L.c[l] = c[l];
+        L.d[l] = d ? d[l] : nullptr;
+        if (F[l] % 4 || !aligned16(L.a[l]) || !aligned16(L.b[l]) || !aligned16(L.c[l]) || !aligned16(L.d[l])) vw = 1;
         if (F[l] > fmax) fmax = (int)F[l];
-        off += B * P * F[l];
     }
     return true;
 }
@@ -196,70 +188,62 @@ dim3 grid_of(int fmax, int vw, int64_t rows, int n) {
 
 extern "C" {
 
-int hrl_hidden_gather(const float *H, const float *mask, int64_t B, int64_t P, int nleaves, const int64_t *F,
+int hrl_hidden_gather(const float *const *H, const float *mask, int64_t B, int64_t P, int nleaves, const int64_t *F,
                       int sum, float *const *out, void *stream) {
-    if (!H || !mask || !F || !out) return HRL_EINVAL;
     Leaves L;
     int vw, fmax;
-    if (!build(nleaves, F, B, P, nullptr, out, H, nullptr, L, vw, fmax)) return HRL_EINVAL;
-    for (int l = 0; l < nleaves; ++l)
-        if (!out[l]) return HRL_EINVAL;
+    if (!mask || !build(nleaves, F, B, P, H, nullptr, out, nullptr, L, vw, fmax)) return HRL_EINVAL;
     if (B == 0) return HRL_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 grid = grid_of(fmax, vw, sum ? B : B * P, nleaves);
     if (sum) {
-        if (vw == 4) hipLaunchKernelGGL(hidden_gather_sum_kernel<4>, grid, dim3(kThreads), 0, s, H, mask, (int)B, (int)P, L);
-        else hipLaunchKernelGGL(hidden_gather_sum_kernel<1>, grid, dim3(kThreads), 0, s, H, mask, (int)B, (int)P, L);
+        if (vw == 4) hipLaunchKernelGGL(hidden_gather_sum_kernel<4>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, L);
+        else hipLaunchKernelGGL(hidden_gather_sum_kernel<1>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, L);
     } else {
-        if (vw == 4) hipLaunchKernelGGL(hidden_gather_keep_kernel<4>, grid, dim3(kThreads), 0, s, H, mask, (int)(B * P), L);
-        else hipLaunchKernelGGL(hidden_gather_keep_kernel<1>, grid, dim3(kThreads), 0, s, H, mask, (int)(B * P), L);
+        if (vw == 4) hipLaunchKernelGGL(hidden_gather_keep_kernel<4>, grid, dim3(kThreads), 0, s, mask, (int)(B * P), L);
+        else hipLaunchKernelGGL(hidden_gather_keep_kernel<1>, grid, dim3(kThreads), 0, s, mask, (int)(B * P), L);
     }
     return status();
 }
 
 int hrl_hidden_gather_backward(const float *const *dout, const float *mask, int64_t B, int64_t P, int nleaves,
-                               const int64_t *F, int sum, float *dH, void *stream) {
-    if (!dout || !mask || !F || !dH) return HRL_EINVAL;
+                               const int64_t *F, int sum, float *const *dH, void *stream) {
     Leaves L;
     int vw, fmax;
-    if (!build(nleaves, F, B, P, dout, nullptr, dH, nullptr, L, vw, fmax)) return HRL_EINVAL;
+    if (!mask || !build(nleaves, F, B, P, dout, nullptr, dH, nullptr, L, vw, fmax)) return HRL_EINVAL;
     if (B == 0) return HRL_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 grid = grid_of(fmax, vw, B, nleaves);
-    if (vw == 4) hipLaunchKernelGGL(hidden_gather_bwd_kernel<4>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, sum, L, dH);
-    else hipLaunchKernelGGL(hidden_gather_bwd_kernel<1>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, sum, L, dH);
+    if (vw == 4) hipLaunchKernelGGL(hidden_gather_bwd_kernel<4>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, sum, L);
+    else hipLaunchKernelGGL(hidden_gather_bwd_kernel<1>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, sum, L);
     return status();
 }
 
-int hrl_hidden_update(const float *H, const float *const *nh, int64_t Pn, const float *mask, int64_t B, int64_t P,
-                      int nleaves, const int64_t *F, float *out, void *stream) {
-    if (!H || !nh || !mask || !F || !out || (Pn != 1 && Pn != P)) return HRL_EINVAL;
+int hrl_hidden_update(const float *const *H, const float *const *nh, int64_t Pn, const float *mask, int64_t B,
+                      int64_t P, int nleaves, const int64_t *F, float *const *out, void *stream) {
     Leaves L;
     int vw, fmax;
-    if (!build(nleaves, F, B, P, nh, nullptr, H, out, L, vw, fmax)) return HRL_EINVAL;
-    for (int l = 0; l < nleaves; ++l)
-        if (!nh[l]) return HRL_EINVAL;
+    if (!mask || !nh || (Pn != 1 && Pn != P)) return HRL_EINVAL;
+    if (!build(nleaves, F, B, P, H, nh, out, nullptr, L, vw, fmax)) return HRL_EINVAL;
     if (B == 0) return HRL_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 grid = grid_of(fmax, vw, B, nleaves);
-    if (vw == 4) hipLaunchKernelGGL(hidden_update_kernel<4>, grid, dim3(kThreads), 0, s, H, mask, (int)B, (int)P, (int)Pn, L, out);
-    else hipLaunchKernelGGL(hidden_update_kernel<1>, grid, dim3(kThreads), 0, s, H, mask, (int)B, (int)P, (int)Pn, L, out);
+    if (vw == 4) hipLaunchKernelGGL(hidden_update_kernel<4>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, (int)Pn, L);
+    else hipLaunchKernelGGL(hidden_update_kernel<1>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, (int)Pn, L);
     return status();
 }
 
-int hrl_hidden_update_backward(const float *dout, const float *mask, int64_t B, int64_t P, int64_t Pn, int nleaves,
-                               const int64_t *F, float *dH, float *const *dnh, void *stream) {
-    if (!dout || !mask || !F || !dH || !dnh || (Pn != 1 && Pn != P)) return HRL_EINVAL;
+int hrl_hidden_update_backward(const float *const *dout, const float *mask, int64_t B, int64_t P, int64_t Pn,
+                               int nleaves, const int64_t *F, float *const *dH, float *const *dnh, void *stream) {
     Leaves L;
     int vw, fmax;
-    if (!build(nleaves, F, B, P, nullptr, dnh, dout, dH, L, vw, fmax)) return HRL_EINVAL;
-    for (int l = 0; l < nleaves; ++l)
-        if (!dnh[l]) return HRL_EINVAL;
+    if (!mask || !dnh || (Pn != 1 && Pn != P)) return HRL_EINVAL;
+    if (!build(nleaves, F, B, P, dout, nullptr, dH, dnh, L, vw, fmax)) return HRL_EINVAL;
     if (B == 0) return HRL_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 grid = grid_of(fmax, vw, B, nleaves);
-    if (vw == 4) hipLaunchKernelGGL(hidden_update_bwd_kernel<4>, grid, dim3(kThreads), 0, s, dout, mask, (int)B, (int)P, (int)Pn, L, dH);
-    else hipLaunchKernelGGL(hidden_update_bwd_kernel<1>, grid, dim3(kThreads), 0, s, dout, mask, (int)B, (int)P, (int)Pn, L, dH);
+    if (vw == 4) hipLaunchKernelGGL(hidden_update_bwd_kernel<4>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, (int)Pn, L);
+    else hipLaunchKernelGGL(hidden_update_bwd_kernel<1>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, (int)Pn, L);
     return status();
 }
 

@@ -280,6 +280,7 @@ class _LSTMGates(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, zx, zh, c):
+        ctx.set_materialize_grads(False)   # a cell whose outputs reach no loss stays out of backward
         N, G, Hh, Ww = zh.shape
         H, HW = G // 4, Hh * Ww
         zh = zh.contiguous()
@@ -300,6 +301,8 @@ class _LSTMGates(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh, dc_out):
+        if dh is None and dc_out is None:
+            return None, None, None
         gates, c, c_out = ctx.saved_tensors
         N, G, Hh, Ww = gates.shape
         dz = torch.empty_like(gates)
@@ -324,63 +327,88 @@ def lstm_gates(zx, zh, c):
     return _LSTMGates.apply(zx, zh, c)
 
 
-class _HiddenGather(torch.autograd.Function):
-    """Per-step recurrent input from the flat state (csrc/hrl_hidden.hip, train.py:157-164).
+def _live(xs):
+    return [k for k, x in enumerate(xs) if x is not None]
 
-    H: leaf-major flat state, leaf l (B, P, *shapes[l]).  Returns the leaves
-    sum_p H_l * m (sum=True, (B, *shape)) or H_l * m reshaped to (B*P, *shape).
+
+class _HiddenGather(torch.autograd.Function):
+    """Per-step recurrent input (csrc/hrl_hidden.hip, train.py:157-164), one launch for every state tensor.
+
+    apply(m, summed, B, P, *H): H[l] is (B, P, *shape_l); returns sum_p H[l] * m (summed, (B, *shape_l))
+    or H[l] * m as (B*P, *shape_l).  Tensors whose output gradient is None get None back.
     """
 
     @staticmethod
-    def forward(ctx, H, m, summed, shapes, B, P):
-        F = [int(torch.Size(sh).numel()) for sh in shapes]
+    def forward(ctx, m, summed, B, P, *H):
+        ctx.set_materialize_grads(False)   # a state tensor without a gradient stays None (pruned)
+        H = [h.contiguous() for h in H]
         rows = B if summed else B * P
-        # one allocation per leaf: the net's convolutions see ordinary, allocator-aligned tensors
-        outs = [torch.empty(rows, *sh, dtype=H.dtype, device=H.device) for sh in shapes]
+        outs = [torch.empty(rows, *h.shape[2:], dtype=h.dtype, device=h.device) for h in H]
+        F = [h[0, 0].numel() for h in H]
         _native.check(_native.load().hrl_hidden_gather(
-            _native.ptr(H), _native.ptr(m), B, P, len(F), _native.i64_array(F), int(summed), _native.ptr_array(outs),
-            _native.stream_of(H.device)), 'hrl_hidden_gather')
+            _native.ptr_array(H), _native.ptr(m), B, P, len(H), _native.i64_array(F), int(summed),
+            _native.ptr_array(outs), _native.stream_of(m.device)), 'hrl_hidden_gather')
         ctx.save_for_backward(m)
-        ctx.meta = (summed, F, B, P, H.numel())
+        ctx.meta = (summed, B, P, [tuple(h.shape) for h in H])
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *grads):
         (m,) = ctx.saved_tensors
-        summed, F, B, P, n = ctx.meta
-        g = [None if x is None else x.contiguous() for x in grads]
-        dH = torch.empty(n, dtype=m.dtype, device=m.device)
-        _native.check(_native.load().hrl_hidden_gather_backward(
-            _native.ptr_array(g), _native.ptr(m), B, P, len(F), _native.i64_array(F), int(summed), _native.ptr(dH),
-            _native.stream_of(m.device)), 'hrl_hidden_gather_backward')
-        return dH, None, None, None, None, None
+        summed, B, P, shapes = ctx.meta
+        live = _live(grads)
+        dH = [None] * len(grads)
+        if live:
+            g = [grads[k].contiguous() for k in live]
+            d = [torch.empty(shapes[k], dtype=m.dtype, device=m.device) for k in live]
+            F = [int(torch.Size(shapes[k][2:]).numel()) for k in live]
+            _native.check(_native.load().hrl_hidden_gather_backward(
+                _native.ptr_array(g), _native.ptr(m), B, P, len(live), _native.i64_array(F), int(summed),
+                _native.ptr_array(d), _native.stream_of(m.device)), 'hrl_hidden_gather_backward')
+            for k, t in zip(live, d):
+                dH[k] = t
+        return (None, None, None, None, *dH)
 
 
 class _HiddenUpdate(torch.autograd.Function):
-    """New flat state H * (1 - m) + nh * m (csrc/hrl_hidden.hip, train.py:167-174); nh leaves (B*Pn, *shape)."""
+    """New state H[l] * (1 - m) + nh[l] * m (csrc/hrl_hidden.hip, train.py:167-174), one launch for all.
+
+    apply(m, B, P, Pn, n, *H, *nh): H[l] (B, P, *shape_l), nh[l] (B*Pn, *shape_l).  Tensors whose
+    output gradient is None get None back (their producers are pruned, as with the torch ops).
+    """
 
     @staticmethod
-    def forward(ctx, H, m, B, P, Pn, F, *nh):
-        nh = [x.contiguous() for x in nh]
-        out = torch.empty_like(H)
+    def forward(ctx, m, B, P, Pn, n, *tensors):
+        ctx.set_materialize_grads(False)   # a state tensor without a gradient stays None (pruned)
+        H = [h.contiguous() for h in tensors[:n]]
+        nh = [x.contiguous() for x in tensors[n:]]
+        outs = [torch.empty_like(h) for h in H]
+        F = [h[0, 0].numel() for h in H]
         _native.check(_native.load().hrl_hidden_update(
-            _native.ptr(H), _native.ptr_array(nh), Pn, _native.ptr(m), B, P, len(F), _native.i64_array(F),
-            _native.ptr(out), _native.stream_of(H.device)), 'hrl_hidden_update')
+            _native.ptr_array(H), _native.ptr_array(nh), Pn, _native.ptr(m), B, P, n, _native.i64_array(F),
+            _native.ptr_array(outs), _native.stream_of(m.device)), 'hrl_hidden_update')
         ctx.save_for_backward(m)
-        ctx.meta = (B, P, Pn, F, [x.shape for x in nh])
-        return out
+        ctx.meta = (B, P, Pn, n, [tuple(h.shape) for h in H], [tuple(x.shape) for x in nh])
+        return tuple(outs)
 
     @staticmethod
-    def backward(ctx, dout):
+    def backward(ctx, *douts):
         (m,) = ctx.saved_tensors
-        B, P, Pn, F, nh_shapes = ctx.meta
-        dout = dout.contiguous()
-        dH = torch.empty_like(dout)
-        dnh = [torch.empty(sh, dtype=dout.dtype, device=dout.device) for sh in nh_shapes]
-        _native.check(_native.load().hrl_hidden_update_backward(
-            _native.ptr(dout), _native.ptr(m), B, P, Pn, len(F), _native.i64_array(F), _native.ptr(dH),
-            _native.ptr_array(dnh), _native.stream_of(dout.device)), 'hrl_hidden_update_backward')
-        return (dH, None, None, None, None, None, *dnh)
+        B, P, Pn, n, h_shapes, nh_shapes = ctx.meta
+        live = _live(douts)
+        dH, dnh = [None] * n, [None] * n
+        if live:
+            g = [douts[k].contiguous() for k in live]
+            a = [torch.empty(h_shapes[k], dtype=m.dtype, device=m.device) for k in live]
+            b = [torch.empty(nh_shapes[k], dtype=m.dtype, device=m.device) for k in live]
+            F = [int(torch.Size(h_shapes[k][2:]).numel()) for k in live]
+            _native.check(_native.load().hrl_hidden_update_backward(
+                _native.ptr_array(g), _native.ptr(m), B, P, Pn, len(live), _native.i64_array(F),
+                _native.ptr_array(a), _native.ptr_array(b), _native.stream_of(m.device)),
+                'hrl_hidden_update_backward')
+            for k, x, y in zip(live, a, b):
+                dH[k], dnh[k] = x, y
+        return (None, None, None, None, None, *dH, *dnh)
 
 
 def _board_conv_ok(m):

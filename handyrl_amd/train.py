@@ -101,8 +101,7 @@ def _rebuild(template, it):
     return next(it)
 
 
-FLAT_HIDDEN = False  # recurrent state through csrc/hrl_hidden.hip (one flat buffer); off: it defeats
-                     # autograd's pruning of state that never reaches an output
+FLAT_HIDDEN = True   # recurrent state plumbing through csrc/hrl_hidden.hip on the GPU (False: torch ops)
 
 
 def _flat_hidden_ok(hidden, tmask):
@@ -118,24 +117,23 @@ def _flat_hidden_ok(hidden, tmask):
 
 
 def _unroll_flat_hidden(model, hidden, batch, args):
-    """The recurrent branch on the GPU: the state of every hidden tensor in one flat buffer,
-    masked/summed and mixed by one HIP launch each per step (nn._HiddenGather / _HiddenUpdate).
-    Same arithmetic as the torch formulation below (train.py:155-174)."""
+    """The recurrent branch on the GPU: the masking/summing and the mixing of every hidden tensor
+    run as one HIP launch each per step (nn._HiddenGather / _HiddenUpdate), with the arithmetic of
+    the torch formulation below (train.py:155-174).  The tensors stay separate autograd values, so
+    state that never reaches an output is pruned exactly as with the torch ops."""
     from .nn import _HiddenGather, _HiddenUpdate
     observations = batch['observation']
     tmask = batch['turn_mask']
     B, T, P = tmask.shape[:3]
     leaves = _leaves(hidden)
-    shapes = [tuple(h.shape[2:]) for h in leaves]
-    F = [int(torch.Size(sh).numel()) for sh in shapes]
-    H = torch.cat([h.reshape(-1) for h in leaves])
+    n = len(leaves)
     masks = batch['observation_mask'].reshape(B, T, P).transpose(0, 1).contiguous()   # (T, B, P)
     summed = args['turn_based_training'] and not args['observation']
     per_t = {}
     for t in range(T):
         obs = map_r(observations, lambda o: o[:, t].reshape(-1, *o.shape[3:]))
         m = masks[t]
-        h_in = _rebuild(hidden, iter(_HiddenGather.apply(H, m, summed, shapes, B, P)))
+        h_in = _rebuild(hidden, iter(_HiddenGather.apply(m, summed, B, P, *leaves)))
         out_t = model(obs, h_in)
         next_hidden = None
         for k, o in out_t.items():
@@ -145,7 +143,7 @@ def _unroll_flat_hidden(model, hidden, batch, args):
                 per_t.setdefault(k, []).append(o)
         nh = _leaves(next_hidden)
         Pn = nh[0].shape[0] // B
-        H = _HiddenUpdate.apply(H, m, B, P, Pn, F, *nh)
+        leaves = list(_HiddenUpdate.apply(m, B, P, Pn, n, *leaves, *nh))
     return {k: torch.stack(o, dim=1) for k, o in per_t.items() if o[0] is not None}
 
 

@@ -158,23 +158,23 @@ int hrl_lstm_gates_backward(const float *gates, const float *c, const float *c_o
 
 /*
  * Recurrent state plumbing of forward_prediction (handyrl/train.py:155-174),
- * one launch for all state tensors (csrc/hrl_hidden.hip).  The state is one
- * leaf-major buffer: leaf l is (B, P, F[l]) floats, leaves back to back.
+ * one launch for all state tensors (csrc/hrl_hidden.hip).  Each state tensor
+ * l is (B, P, F[l]) floats (arrays of per-tensor device pointers; at most 16).
  * mask: (B, P) observation mask of the step.
- *   gather:  out[l] = sum_p H_l[:, p] * mask[:, p]  -> (B, F[l])      (sum != 0)
- *                     H_l * mask                     -> (B, P, F[l])   (sum == 0)
- *   update:  out_l = H_l * (1 - mask) + nh[l] * mask, nh[l]: (B, Pn, F[l]), Pn = 1 or P
- * and their adjoints (a NULL dout[l] in the gather backward is a zero gradient).
- * At most 16 leaves.
+ *   gather:  out[l] = sum_p H[l][:, p] * mask[:, p]  -> (B, F[l])      (sum != 0)
+ *                     H[l] * mask                     -> (B, P, F[l])   (sum == 0)
+ *   update:  out[l] = H[l] * (1 - mask) + nh[l] * mask, nh[l]: (B, Pn, F[l]), Pn = 1 or P
+ * and their adjoints.  A tensor whose gradient is None is left out of the
+ * backward call, so autograd's pruning is kept.
  */
-int hrl_hidden_gather(const float *H, const float *mask, int64_t B, int64_t P, int nleaves, const int64_t *F,
+int hrl_hidden_gather(const float *const *H, const float *mask, int64_t B, int64_t P, int nleaves, const int64_t *F,
                       int sum, float *const *out, void *stream);
 int hrl_hidden_gather_backward(const float *const *dout, const float *mask, int64_t B, int64_t P, int nleaves,
-                               const int64_t *F, int sum, float *dH, void *stream);
-int hrl_hidden_update(const float *H, const float *const *nh, int64_t Pn, const float *mask, int64_t B, int64_t P,
-                      int nleaves, const int64_t *F, float *out, void *stream);
-int hrl_hidden_update_backward(const float *dout, const float *mask, int64_t B, int64_t P, int64_t Pn, int nleaves,
-                               const int64_t *F, float *dH, float *const *dnh, void *stream);
+                               const int64_t *F, int sum, float *const *dH, void *stream);
+int hrl_hidden_update(const float *const *H, const float *const *nh, int64_t Pn, const float *mask, int64_t B,
+                      int64_t P, int nleaves, const int64_t *F, float *const *out, void *stream);
+int hrl_hidden_update_backward(const float *const *dout, const float *mask, int64_t B, int64_t P, int64_t Pn,
+                               int nleaves, const int64_t *F, float *const *dH, float *const *dnh, void *stream);
 
 #ifdef __cplusplus
 }
