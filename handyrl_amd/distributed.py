@@ -120,6 +120,16 @@ class GradAllReduce:
 
     enabled = True
 
+    def mark_ready(self, params):
+        """Params whose gradient was written outside autograd (nn.DeferredGrads.flush): count them
+        as accumulated, as their post-accumulate hook would."""
+        index = {id(p): i for i, p in enumerate(self.fg.params)}
+        for p in params:
+            i = index.get(id(p))
+            if i is not None:
+                self._pending[self.param_bucket[i]] -= 1
+        self._launch_ready()
+
     def _launch_ready(self):
         if not self.enabled:
             return

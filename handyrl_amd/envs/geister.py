@@ -93,14 +93,19 @@ class DRC(nn.Module):
         kernel adds the two (nn.lstm_gates).  A third fewer cell FLOPs, no
         concatenation, one gate launch per cell and direction.
         """
-        from ..nn import lstm_gates
+        from .. import nn as hnn
+        from ..nn import lstm_gates, conv2d
         cin = x.shape[-3]
         ws = [blk.conv.weight for blk in self.blocks]
         bias = [blk.conv.bias for blk in self.blocks]
         pad = self.blocks[0].conv.padding
         n = len(self.blocks)
+        c_all = ws[0].shape[1]
+        deferred = hnn._DEFER is not None   # LearnerStep batches the weight gradients over the unroll
 
         def x_half(layers):
+            if len(layers) == 1 and deferred:   # the weight's input-channel slice, gradient deferred
+                return (conv2d(x, ws[layers[0]], bias[layers[0]], pad, in_slice=(0, cin)),)
             w_x = torch.cat([ws[i][:, :cin] for i in layers])
             b_x = None if bias[0] is None else torch.cat([bias[i] for i in layers])
             return F.conv2d(x, w_x, b_x, padding=pad).chunk(len(layers), dim=-3)
@@ -108,13 +113,16 @@ class DRC(nn.Module):
             # Only the last layer reaches the output (every cell reads x and its own state), so the
             # others must stay outside its autograd graph: their weights then get no gradient at
             # all, as with the reference's cells, and the optimizer leaves them alone.
-            zx = x_half(range(n - 1)) + x_half([n - 1])
+            zx = x_half(list(range(n - 1))) + x_half([n - 1])
         else:
-            zx = x_half(range(n))
-        w_h = [w[:, cin:].contiguous() for w in ws]
+            zx = x_half(list(range(n)))
+        w_h = None if deferred else [w[:, cin:].contiguous() for w in ws]
         for _ in range(num_repeats):
             for i in range(len(self.blocks)):
-                zh = F.conv2d(hs[i], w_h[i], None, padding=pad)
+                if deferred:
+                    zh = conv2d(hs[i], ws[i], None, pad, in_slice=(cin, c_all))
+                else:
+                    zh = F.conv2d(hs[i], w_h[i], None, padding=pad)
                 hs[i], cs[i] = lstm_gates(zx[i], zh, cs[i])
         return hs[-1], (hs, cs)
 

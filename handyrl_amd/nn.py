@@ -30,6 +30,7 @@ import operator
 import torch
 import torch.fx
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import _native
 
@@ -37,6 +38,123 @@ __all__ = ['BatchNorm2d', 'BoardConv2d', 'Linear', 'accelerate', 'batch_norm_tra
 
 _MAX_ROW = 3072        # float4 path (row width a multiple of 4)
 _MAX_ROW_SCALAR = 1024  # scalar path
+
+
+class DeferredGrads:
+    """Weight gradients of a recurrent unroll, batched over time.
+
+    A recurrent learner step runs the net T times (train.py:155-174), so every
+    weight is used T (or, inside GeisterNet's DRC, 3T) times and autograd
+    computes one weight-gradient convolution per use and adds them up.  Inside
+    ``with deferred_weight_grads() as d:`` the HIP layers return no weight
+    gradient; they record (input, output gradient) instead, and ``d.flush()``
+    -- after backward -- computes each weight's gradient with ONE batched call
+    over all recorded uses and adds it into ``.grad``.  Same sum, different
+    fp32 association.  Only LearnerStep enables it (it calls flush).
+    """
+
+    def __init__(self):
+        self.conv = {}     # (param, bias param, in slice, padding) -> [(x, dy)]
+        self.affine = {}   # (weight, bias) -> [(dweight, dbias)]
+
+    def add_conv(self, key, x, dy):
+        self.conv.setdefault(key, []).append((x, dy))
+
+    def add_affine(self, key, dw, db):
+        self.affine.setdefault(key, []).append((dw, db))
+
+    @torch.no_grad()
+    def flush(self):
+        """Accumulate the deferred gradients into .grad; returns the parameters that got one."""
+        touched = []
+        for (w, b, sl, pad), rec in self.conv.items():
+            X = torch.cat([r[0] for r in rec]) if len(rec) > 1 else rec[0][0]
+            DY = torch.cat([r[1] for r in rec]) if len(rec) > 1 else rec[0][1]
+            wv = w if sl is None else w[:, sl[0]:sl[1]]
+            _, dw, db = torch.ops.aten.convolution_backward(
+                DY, X, wv, [wv.shape[0]] if b is not None else None, [1, 1], list(pad), [1, 1], False, [0, 0], 1,
+                [False, True, b is not None])
+            _add_grad(w, dw, sl)
+            touched.append(w)
+            if b is not None:
+                _add_grad(b, db, None)
+                touched.append(b)
+        for (w, b), rec in self.affine.items():
+            if w is not None:
+                _add_grad(w, torch.stack([r[0] for r in rec]).sum(0), None)
+                touched.append(w)
+            if b is not None:
+                _add_grad(b, torch.stack([r[1] for r in rec]).sum(0), None)
+                touched.append(b)
+        self.conv.clear()
+        self.affine.clear()
+        return touched
+
+
+def _add_grad(p, g, sl):
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    if sl is None:
+        p.grad.add_(g)
+    else:
+        p.grad[:, sl[0]:sl[1]].add_(g)
+
+
+_DEFER = None
+
+
+class deferred_weight_grads:
+    """Context manager: defer the HIP layers' weight gradients into a DeferredGrads (see there)."""
+
+    def __enter__(self):
+        global _DEFER
+        self.prev = _DEFER
+        _DEFER = DeferredGrads()
+        return _DEFER
+
+    def __exit__(self, *exc):
+        global _DEFER
+        _DEFER = self.prev
+        return False
+
+
+class _DeferredConv(torch.autograd.Function):
+    """conv2d (stride 1, 'same') whose weight/bias gradient is deferred to DeferredGrads.flush().
+
+    ``sl`` selects input channels [sl[0], sl[1]) of the weight (a ConvLSTM cell's h or x half)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, sl, pad, rec):
+        ctx.set_materialize_grads(False)
+        wv = w if sl is None else w[:, sl[0]:sl[1]]
+        y = F.conv2d(x, wv, b, padding=pad)
+        ctx.save_for_backward(x, w)
+        ctx.meta = (sl, pad, rec, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if dy is None:
+            return None, None, None, None, None, None
+        x, w = ctx.saved_tensors
+        sl, pad, rec, b = ctx.meta
+        dy = dy.contiguous()
+        wv = w if sl is None else w[:, sl[0]:sl[1]]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(dy, x, wv, None, [1, 1], list(pad), [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        rec.add_conv((w, b, sl, tuple(pad)), x, dy)
+        return dx, None, None, None, None, None
+
+
+def conv2d(x, w, b=None, padding=(0, 0), in_slice=None):
+    """F.conv2d (stride 1) of the env nets; inside deferred_weight_grads() the weight gradient is
+    batched over the unroll (DeferredGrads)."""
+    if _DEFER is not None and torch.is_grad_enabled() and w.requires_grad:
+        return _DeferredConv.apply(x, w, b, in_slice, tuple(padding), _DEFER)
+    wv = w if in_slice is None else w[:, in_slice[0]:in_slice[1]]
+    return F.conv2d(x, wv, b, padding=padding)
 
 
 class _BatchNormTrain(torch.autograd.Function):
@@ -62,6 +180,7 @@ class _BatchNormTrain(torch.autograd.Function):
         ctx.save_for_backward(x, weight, bias, mean, invstd)
         ctx.has_bias = bias is not None
         ctx.relu = bool(relu)
+        ctx.defer = _DEFER if (weight is not None and weight.requires_grad) else None
         return y
 
     @staticmethod
@@ -81,6 +200,9 @@ class _BatchNormTrain(torch.autograd.Function):
             _native.ptr(invstd), int(ctx.relu), _native.ptr(dx), _native.ptr(dw), _native.ptr(db),
             _native.ptr(ws), ws_bytes, _native.stream_of(x.device))
         _native.check(code, 'hrl_bn_backward')
+        if ctx.defer is not None and (dw is not None or db is not None):
+            ctx.defer.add_affine((weight, bias if ctx.has_bias else None), dw, db)
+            return dx, None, None, None, None, None, None, None
         return dx, dw, db, None, None, None, None, None
 
 
@@ -172,6 +294,9 @@ class BoardConv2d(nn.Conv2d):
     def forward(self, x):
         if not (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
                 and x.shape[2] * x.shape[3] <= BOARD_MAX_CELLS):
+            if _DEFER is not None and x.is_cuda and self.padding_mode == 'zeros' and self.stride == (1, 1) \
+                    and self.dilation == (1, 1) and self.groups == 1 and isinstance(self.padding, tuple):
+                return conv2d(x, self.weight, self.bias, self.padding)
             return super().forward(x)
         N, Cin, H, W = x.shape
         if (H, W) == (3, 3) and self.kernel_size == (3, 3) and Cin == 32 and self.out_channels == 32 and N > 0:

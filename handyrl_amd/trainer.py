@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from . import distributed as hdist
-from .nn import accelerate, fuse_bn_relu
+from .nn import accelerate, fuse_bn_relu, deferred_weight_grads
 from .train import forward_prediction, loss_terms
 from .util import map_r, bimap_r
 
@@ -63,6 +63,7 @@ class LearnerStep:
             self._opt_kwargs = dict(lr=lr, weight_decay=1e-5, fused=fused, foreach=None if fused else True)
         self.optimizer = torch.optim.Adam(self.params, **self._opt_kwargs)
         self.live = None        # params that receive a gradient (set on the first batch)
+        self.defer = hip_layers and device.type == 'cuda'   # batched weight gradients for recurrent steps
         self._graph = None
         self._static = None
         self._static_out = None
@@ -121,9 +122,19 @@ class LearnerStep:
             if hidden is None and isinstance(obs, torch.Tensor):
                 self.fused_pairs = fuse_bn_relu(self.net, obs[:2].reshape(-1, *obs.shape[3:]))
         self.grads.zero()
-        outputs = forward_prediction(self.net, hidden, batch, self.args)
-        losses, dcnt = self.loss_fn(outputs, batch, self.args)
-        losses['total'].backward()
+        if hidden is not None and self.defer:
+            # recurrent unroll: every weight is used T times; batch its weight gradients (nn.DeferredGrads)
+            with deferred_weight_grads() as deferred:
+                outputs = forward_prediction(self.net, hidden, batch, self.args)
+                losses, dcnt = self.loss_fn(outputs, batch, self.args)
+                losses['total'].backward()
+            touched = deferred.flush()
+            if self.reducer is not None:
+                self.reducer.mark_ready(touched)
+        else:
+            outputs = forward_prediction(self.net, hidden, batch, self.args)
+            losses, dcnt = self.loss_fn(outputs, batch, self.args)
+            losses['total'].backward()
         if self.reducer is not None:
             self.reducer.finish()
         gnorm = self.grads.clip_(4.0)
