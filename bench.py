@@ -297,7 +297,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--batch', type=int, default=4096, help='trajectories per GPU (B)')
     ap.add_argument('--seq', type=int, default=32, help='forward_steps (T)')
-    ap.add_argument('--graph', type=int, default=1, help='capture the 1-GPU step in a HIP graph')
+    ap.add_argument('--graph', type=int, default=1, help='capture the step in HIP graphs (N>1: backward and update graphs around the all-reduce)')
     ap.add_argument('--cpu-baseline', type=int, default=1)
     ap.add_argument('--scan-iters', type=int, default=200)
     ap.add_argument('--secondary', type=int, default=1, help='also time the B=4096 T=9 config (N=1)')
@@ -317,7 +317,7 @@ def main():
     net = SimpleConv2dModel().to(device)
     net.train()
     batch = tictactoe_batch(B, T, device, seed=1000 + rank)  # each rank its own shard
-    use_graph = bool(opts.graph) and world == 1
+    use_graph = bool(opts.graph)
     learner = LearnerStep(net, args, device, graph=use_graph, world_size=world)
 
     for _ in range(opts.warmup):

@@ -9,8 +9,11 @@
 // (train.py:248-253 issue 2-4 separate compute_target calls).
 //
 // Work decomposition (one wave64 per workgroup):
-//   * a wave owns G = 64 / C consecutive trajectories; lane = g*C + c owns one
-//     value column (trajectory g, column c) and walks it backwards in time;
+//   * a wave owns G <= 64 / C consecutive trajectories; lane = g*C + c owns one
+//     value column (trajectory g, column c) and walks it backwards in time.
+//     G = 64 / C at large B; at small B fewer, so the launch still has ~1024
+//     waves: a wave's latency is its serial chain plus its share of the
+//     load/transpose instructions, which shrinks with G;
 //   * time is processed in chunks of up to TCHUNK steps.  Each chunk of every
 //     input is loaded with coalesced 16-byte loads (the wave's trajectories are
 //     contiguous in the (B,T,C) layout), ALL inputs' loads are issued before
@@ -27,6 +30,8 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "../../include/hrl_targets.h"
 
@@ -124,6 +129,7 @@ struct Staged {
             if (nv == 0) return;
 #pragma unroll
             for (int k = 0; k < kMaxVec; ++k) {
+                if (k * kWave >= nv) break;   // wave-uniform: small tiles issue fewer rounds
                 // clamp instead of branching so every load issues back to back
                 const int vi = min(k * kWave + lane, nv - 1);
                 int go; int slot;
@@ -134,6 +140,7 @@ struct Staged {
         } else {
 #pragma unroll
             for (int k = 0; k < kMaxScalar; ++k) {
+                if (k * kWave >= c.n) break;
                 const int e = min(k * kWave + lane, c.n - 1);
                 int go; int slot;
                 c.locate(e, go, slot);
@@ -149,6 +156,7 @@ struct Staged {
             const int nv = c.n >> 2;
 #pragma unroll
             for (int k = 0; k < kMaxVec; ++k) {
+                if (k * kWave >= nv) break;
                 const int e = (k * kWave + lane) * 4;
                 if (e < 4 * nv) {
                     const int g = fdiv(e, c.invL);
@@ -167,6 +175,7 @@ struct Staged {
         } else {
 #pragma unroll
             for (int k = 0; k < kMaxScalar; ++k) {
+                if (k * kWave >= c.n) break;
                 const int e = k * kWave + lane;
                 if (e < c.n) {
                     int go; int slot;
@@ -218,6 +227,7 @@ struct Args {
     float *targets, *advantages;
     int64_t B;
     int T, C, retT, rhoC, rhoDiv;
+    int G;      // trajectories per wave (<= 64 / C; fewer when B is small, to spread waves)
     Coef k;
 };
 
@@ -273,7 +283,7 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
     extern __shared__ float lds[];
     const int lane = threadIdx.x;
     const int C = a.C;
-    const int G = kWave / C;
+    const int G = a.G;
     const int J = G * C;                      // value columns per wave
     const int T = a.T;
     const int tmax = T < kTChunk ? T : kTChunk;
@@ -306,11 +316,34 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
 
     Carry s{0.f, 0.f, 0.f, 0.f, 0.f};
     const int nchunks = (T + kTChunk - 1) / kTChunk;
-    for (int ch = nchunks - 1; ch >= 0; --ch) {
+
+    // One time step: the reference recurrences on the carry, outputs into the LDS tiles.
+    auto one_step = [&](int tt, int t0, float v, float r, float rho, float cc, float ret_t) {
+        const bool last = (t0 + tt == T - 1);
+        const int iv = vbase + tt * C;
+        float adv, adv_unused;
+        Carry nx = s;
+        if constexpr (TGT != kNone && TGT != ADV) {
+            const float tgt = step<TGT>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv_unused);
+            step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
+            t_tgt[iv] = tgt;
+        } else {
+            const float tgt = step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
+            if constexpr (TGT != kNone) t_tgt[iv] = tgt;
+        }
+        t_adv[iv] = adv;
+        nx.v_next = v;
+        s = nx;
+    };
+
+    // Software pipeline over chunks (walking time backwards): chunk ch's inputs
+    // arrive in registers one iteration ahead, so the global-load latency of
+    // chunk ch-1 overlaps chunk ch's LDS transpose and recurrence.
+    Chunk cv, cr, cret, crho, ccs;
+    Staged<VEC> sv, sr, sret, srho, scs;
+    auto setup_and_load = [&](int ch) {
         const int t0 = ch * kTChunk;
         const int tc = min(kTChunk, T - t0);
-
-        Chunk cv, cr, cret, crho, ccs;
         cv.setup(a.values, b0, T, C, t0, tc, ntraj, Lpv);
         if constexpr (REW) cr.setup(a.rewards, b0, T, C, t0, tc, ntraj, Lpv);
         if constexpr (kRet) cret.setup(a.returns, b0, T, C, t0, tc, ntraj, Lpv);
@@ -318,58 +351,68 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
             crho.setup(a.rhos, b0, T, a.rhoC, t0, tc, ntraj, Lpr);
             ccs.setup(a.cs, b0, T, a.rhoC, t0, tc, ntraj, Lpr);
         }
-
-        // issue every input's loads before the first LDS write
-        Staged<VEC> sv, sr, sret, srho, scs;
+        // every input's loads are issued before the first is consumed
         sv.load(cv);
         if constexpr (REW) sr.load(cr);
         if constexpr (kRet) sret.load(cret);
         if constexpr (kRho) { srho.load(crho); scs.load(ccs); }
+    };
+    setup_and_load(nchunks - 1);
+    // Consume the bootstrap load here (in straight-line code the wait covers only that
+    // load); afterwards `boot` is a plain register, so the waitcnt pass does not put a
+    // full vmcnt(0) -- draining the prefetched chunk -- in front of the recurrence.
+    asm volatile("" : "+v"(boot));
+
+    auto process = [&](int ch, auto prefetch) {
+        const int t0 = ch * kTChunk;
+        const int tc = min(kTChunk, T - t0);
+
         sv.to_lds(cv, t_v);
         if constexpr (REW) sr.to_lds(cr, t_r);
         if constexpr (kRet) sret.to_lds(cret, t_ret);
         if constexpr (kRho) { srho.to_lds(crho, t_rho); scs.to_lds(ccs, t_cs); }
+        const Chunk out = cv;          // this chunk's output geometry
+        // the next chunk's loads stay in flight through this chunk (unconditional in this
+        // instantiation, so no register phi forces an early wait on them)
+        if constexpr (decltype(prefetch)::value) setup_and_load(ch - 1);
         __syncthreads();
 
         if (active) {
-            for (int tt = tc - 1; tt >= 0; --tt) {
-                const bool last = (t0 + tt == T - 1);
-                const int iv = vbase + tt * C;
-                const int ir = rbase + tt * a.rhoC;
-                const float v = t_v[iv];
-                const float r = REW ? t_r[iv] : 0.f;
-                const float rho = kRho ? t_rho[ir] : 0.f;
-                const float cc = kRho ? t_cs[ir] : 0.f;
-                const float ret_t = kRet ? t_ret[iv] : boot;
-
-                float adv, adv_unused;
-                Carry nx = s;
-                if constexpr (TGT != kNone && TGT != ADV) {
-                    const float tgt = step<TGT>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv_unused);
-                    step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
-                    t_tgt[iv] = tgt;
-                } else {
-                    const float tgt = step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
-                    if constexpr (TGT != kNone) t_tgt[iv] = tgt;
+            // every LDS read is issued ahead of the dependent chain (tc is wave-uniform, so the
+            // guards of a partial chunk are scalar branches)
+            float xv[kTChunk], xr[kTChunk], xrho[kTChunk], xc[kTChunk], xret[kTChunk];
+#pragma unroll
+            for (int tt = 0; tt < kTChunk; ++tt) {
+                if (tt < tc) {
+                    const int iv = vbase + tt * C;
+                    const int ir = rbase + tt * a.rhoC;
+                    xv[tt] = t_v[iv];
+                    xr[tt] = REW ? t_r[iv] : 0.f;
+                    xrho[tt] = kRho ? t_rho[ir] : 0.f;
+                    xc[tt] = kRho ? t_cs[ir] : 0.f;
+                    xret[tt] = kRet ? t_ret[iv] : boot;
                 }
-                t_adv[iv] = adv;
-                nx.v_next = v;
-                s = nx;
+            }
+#pragma unroll
+            for (int tt = kTChunk - 1; tt >= 0; --tt) {
+                if (tt < tc) one_step(tt, t0, xv[tt], xr[tt], xrho[tt], xc[tt], xret[tt]);
             }
         }
         __syncthreads();
 
         const int64_t off = b0 * (int64_t)T * C + (int64_t)t0 * C;
-        if constexpr (TGT != kNone) store_chunk<VEC>(cv, t_tgt, a.targets + off);
-        store_chunk<VEC>(cv, t_adv, a.advantages + off);
-    }
+        if constexpr (TGT != kNone) store_chunk<VEC>(out, t_tgt, a.targets + off);
+        store_chunk<VEC>(out, t_adv, a.advantages + off);
+    };
+    for (int ch = nchunks - 1; ch > 0; --ch) process(ch, std::true_type{});
+    process(0, std::false_type{});
 }
 
 template <int TGT, int ADV, bool REW, bool RETT, bool VEC>
 int launch_one(const Args &a, hipStream_t stream) {
     constexpr bool kRho = (TGT == HRL_ALG_VTRACE) || (ADV == HRL_ALG_VTRACE);
     constexpr bool kRet = RETT && (ADV == HRL_ALG_MC);
-    const int G = kWave / a.C;
+    const int G = a.G;
     const int tmax = a.T < kTChunk ? a.T : kTChunk;
     const int vtiles = 1 + (REW ? 1 : 0) + (kRet ? 1 : 0) + (TGT != kNone ? 1 : 0) + 1;
     const size_t vt = (size_t)G * padded_row(tmax * a.C, a.C);
@@ -454,6 +497,16 @@ int prepare(int target_alg, int adv_alg, const float *values, const float *retur
     a.k.l = (float)lmb;
     a.k.g = (float)gamma;
     a.k.gl = (float)(gamma * lmb);
+    // Waves per launch: a wave's trajectories are walked by one serial chain, so at small B
+    // spread them over at least ~1024 waves (one per SIMD) instead of filling every lane.
+    {
+        // G stays a multiple of 4 (or 64 / C itself), so every wave's first trajectory starts
+        // 16-byte aligned whenever the tensors are (the float4 path's precondition).
+        const int gmax = kWave / a.C;
+        int g = gmax < 4 ? gmax : 4;
+        while (g * 2 <= gmax && B / (g * 2) >= 1024) g *= 2;
+        a.G = g;
+    }
     const int tgt = (targets == nullptr || target_alg == HRL_ALG_MC) ? kNone : target_alg;
     return dispatch(tgt, adv_alg, a, static_cast<hipStream_t>(stream));
 }

@@ -161,6 +161,17 @@ class GradAllReduce:
         self._works = [None] * len(self.buckets)
         self._next = 0
 
+    def reset(self):
+        """Forget partially counted buckets (after a capture, whose hooks counted but launched nothing)."""
+        self._pending = list(self.bucket_size)
+        self._works = [None] * len(self.buckets)
+        self._next = 0
+
+    def all_reduce_flat(self):
+        """SUM all-reduce of the whole flat buffer as one message, ordered on the current stream
+        (the graph-captured step: between the backward graph and the clip/Adam graph)."""
+        dist.all_reduce(self.fg.flat, op=dist.ReduceOp.SUM, group=self.group)
+
     def remove(self):
         for h in self._hooks:
             h.remove()

@@ -65,6 +65,7 @@ class LearnerStep:
         self.live = None        # params that receive a gradient (set on the first batch)
         self.defer = hip_layers and device.type == 'cuda'   # batched weight gradients for recurrent steps
         self._graph = None
+        self._graph_update = None
         self._static = None
         self._static_out = None
         self.stats = None
@@ -113,7 +114,8 @@ class LearnerStep:
             if self.reducer is not None:
                 self.reducer.set_live(live)
 
-    def _body(self, batch, hidden):
+    def _grads(self, batch, hidden):
+        """zero -> forward_prediction -> losses -> backward; returns (losses, dcnt)."""
         if self.live is None:
             self._probe_live(batch, hidden)
         if self._fuse_pending:
@@ -135,14 +137,22 @@ class LearnerStep:
             outputs = forward_prediction(self.net, hidden, batch, self.args)
             losses, dcnt = self.loss_fn(outputs, batch, self.args)
             losses['total'].backward()
-        if self.reducer is not None:
-            self.reducer.finish()
+        return losses, dcnt
+
+    def _update(self, losses, dcnt):
+        """clip_grad_norm_(4.0) on the (all-reduced) gradients, then Adam (train.py:384-385)."""
         gnorm = self.grads.clip_(4.0)
         self.optimizer.step()
         out = {k: v.detach() for k, v in losses.items()}
         out['dcnt'] = dcnt
         out['grad_norm'] = gnorm
         return out
+
+    def _body(self, batch, hidden):
+        losses, dcnt = self._grads(batch, hidden)
+        if self.reducer is not None:
+            self.reducer.finish()
+        return self._update(losses, dcnt)
 
     def _accumulate(self, out):
         vec = torch.stack([out[k].reshape(()) for k in sorted(out)])
@@ -164,6 +174,11 @@ class LearnerStep:
                 if hidden is not None and hidden is not self._static_hidden:
                     bimap_r(self._static_hidden, hidden, lambda dst, src: dst.copy_(src, non_blocking=True))
             self._graph.replay()
+            if self._graph_update is not None:
+                # data parallel: the gradient exchange runs between the two graphs (eager RCCL
+                # all-reduce of the flat buffer, one message), then clip + Adam replay
+                self.reducer.all_reduce_flat()
+                self._graph_update.replay()
             out = self._static_out
         else:
             out = self._body(batch, hidden)
@@ -171,14 +186,18 @@ class LearnerStep:
         return out
 
     def _capture(self, batch, hidden):
-        if self.reducer is not None:
-            raise RuntimeError('HIP-graph capture of the multi-GPU step is not supported; use graph=False')
+        """Capture the step in HIP graphs.
+
+        One GPU: the whole step is one graph.  Data parallel: two graphs -- (zero, forward, loss,
+        backward) and (clip, Adam) -- with the SUM all-reduce of the flat gradient buffer issued
+        eagerly between their replays, so no collective is captured.
+        """
         self._static = batch
         self._static_hidden = hidden  # recurrent nets: the window's initial state (zeros, train.py:375)
         # Warm up on a side stream (allocator pools, MIOpen kernel selection, lazy optimizer state),
         # then put the training state back so the first replay is the first update: parameters and
         # buffers restored in place, Adam's moments and step counts zeroed in place (the graph keeps
-        # pointing at the same tensors).
+        # pointing at the same tensors).  Every rank runs the same warm-up (its collectives included).
         params = list(self.net.parameters())
         saved_p = [p.detach().clone() for p in params]
         saved_b = [b.detach().clone() for b in self.net.buffers()]
@@ -197,9 +216,24 @@ class LearnerStep:
                 for v in state.values():
                     if isinstance(v, torch.Tensor):
                         v.zero_()
-        self._graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._graph):
-            self._static_out = self._body(batch, hidden)
+        if self.reducer is None:
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._static_out = self._body(batch, hidden)
+            return
+        torch.cuda.synchronize(self.device)
+        self.reducer.enabled = False     # no collective inside a capture
+        try:
+            grads_graph, update_graph = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            # thread-local capture: the process group's watchdog thread may query its events meanwhile
+            with torch.cuda.graph(grads_graph, capture_error_mode='thread_local'):
+                losses, dcnt = self._grads(batch, hidden)
+            with torch.cuda.graph(update_graph, capture_error_mode='thread_local'):
+                self._static_out = self._update(losses, dcnt)
+        finally:
+            self.reducer.enabled = True
+            self.reducer.reset()
+        self._graph, self._graph_update = grads_graph, update_graph
 
     def load_batch(self, batch):
         """Copy a new batch into the captured graph's static input tensors."""

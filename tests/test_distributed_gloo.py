@@ -123,7 +123,7 @@ def test_bucket_layout_covers_flat_buffer():
     assert fg.flat.numel() == sum(p.numel() for p in net.parameters())
 
 
-def _gpu_rank_main(rank, world, port, out_path, steps):
+def _gpu_rank_main(rank, world, port, out_path, steps, graph=False):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK='0')
     from handyrl_amd.trainer import LearnerStep
@@ -138,7 +138,7 @@ def _gpu_rank_main(rank, world, port, out_path, steps):
     shard = {k: v[rank * B // world:(rank + 1) * B // world].contiguous() for k, v in batch.items()}
     torch.manual_seed(0)
     net = SmallNet()
-    step = LearnerStep(net, args, dev, world_size=world, bucket_bytes=1024)
+    step = LearnerStep(net, args, dev, world_size=world, bucket_bytes=1024, graph=graph)
     for _ in range(steps):
         step.step(shard)
     sums, _ = step.pop_stats()
@@ -152,12 +152,15 @@ def _gpu_rank_main(rank, world, port, out_path, steps):
 
 
 @pytest.mark.gpu
-def test_two_rank_gpu_step_matches_full_batch(cuda):
+@pytest.mark.parametrize('graph', [False, True])
+def test_two_rank_gpu_step_matches_full_batch(cuda, graph):
+    """Eager (hook-launched buckets) and graph-captured (backward graph, flat all-reduce, update graph)
+    data-parallel steps both reproduce the full-batch single-process update."""
     from handyrl_amd.trainer import LearnerStep
-    steps = 2
+    steps = 3
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, 'r0.pt')
-        mp.spawn(_gpu_rank_main, args=(2, _free_port(), out, steps), nprocs=2, join=True)
+        mp.spawn(_gpu_rank_main, args=(2, _free_port(), out, steps, graph), nprocs=2, join=True)
         res = torch.load(out, weights_only=True)
     batch, args = make_batch_and_args(B=64, T=9)
     batch = {k: v.to(cuda) for k, v in batch.items()}

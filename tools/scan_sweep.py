@@ -11,3 +11,17 @@ for T in (32, 9):
         r = time_scan(dev, B, T, 50 if cold else 200, cold=cold)
         print('T=%3d B=%8d %-4s %9.2f us  %8.1f GB/s  %5.1f%%' % (T, B, 'cold' if cold else 'hot', r['us_per_launch'],
               r['GBps'], 100 * r['GBps'] / HBM_PEAK_GBS), flush=True)
+
+# launch floor: the same graph timing around a 1-element torch kernel
+x = torch.zeros(1, device=dev)
+g = torch.cuda.CUDAGraph()
+x.add_(1)
+torch.cuda.synchronize()
+with torch.cuda.graph(g):
+    for _ in range(200):
+        x.add_(1)
+g.replay()
+torch.cuda.synchronize()
+s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+s.record(); g.replay(); e.record(); e.synchronize()
+print('graph launch floor (1-element add): %.2f us' % (s.elapsed_time(e) * 1e3 / 200), flush=True)
