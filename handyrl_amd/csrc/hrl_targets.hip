@@ -515,7 +515,7 @@ int prepare(int target_alg, int adv_alg, const float *values, const float *retur
 
 extern "C" {
 
-int hrl_abi_version(void) { return 8; }
+int hrl_abi_version(void) { return 9; }
 
 const char *hrl_strerror(int code) {
     if (code == HRL_OK) return "success";

@@ -1,0 +1,514 @@
+// hrl_torus.hip — 3x3 convolution on a torus board with fp32 MFMA (gfx950).
+//
+// GeeseNet (handyrl/envs/kaggle/hungry_geese.py:23-57, config C4) is 13
+// TorusConv2d layers on the 7x11 Hungry Geese board: the reference wraps the
+// board with two torch.cat copies and runs a 'valid' 3x3 conv
+// (hungry_geese.py:30-35).  Here the wrap is addressing:
+//
+//   y[n, co, q] = b[co] + sum_{ci, tap} W[co, ci, tap] * x[n, ci, nbr(q, tap)]
+//   nbr(q, tap) = ((r + ky - 1) mod H) * W + (c + kx - 1) mod W,  q = r*W + c, tap = ky*3 + kx
+//
+// torus_conv_kernel<KS, VEC, STATS> (forward; also the input gradient, run on
+// dy with the weights transposed and the taps mirrored -- on a torus the
+// adjoint of the conv is again a conv):
+//   * one wave computes one sample at a time as the GEMM
+//       Y^T (cells x 32) = Im2col^T (cells x 9*Cin) . W^T (9*Cin x 32)
+//     with v_mfma_f32_16x16x4_f32 (exact fp32 products): 5 cell tiles x 2
+//     channel tiles = 10 accumulators, 9 * KS k-steps of 4 input channels;
+//   * the sample (Cin x HW floats) is staged in LDS as [ci][cell] rows of
+//     stride 81; the A fragment of lane l is the gather
+//     tile[ci][nbr(cell, tap)] with the 45 neighbour offsets of the lane's
+//     cells precomputed in registers;
+//   * the packed weights [tap][k-step][co-tile][64] sit in LDS once per
+//     workgroup (B fragments are consecutive, conflict-free ds_read_b32);
+//   * the next sample's global loads are in flight during the MFMAs; the
+//     output goes through the (dead) input tile to coalesced stores;
+//   * STATS: the epilogue also sums y and y^2 per output channel (fp32 per
+//     sample, fp64 across samples, fixed-order folds) for the BatchNorm
+//     that follows every GeeseNet conv -> hrl_bn_finalize_stats.
+// torus_wgrad_kernel<KS>: dW[co, ci, tap] = sum_{n, q} dy[n, co, q] x[n, ci, nbr(q, tap)]
+//   and db[co] = sum dy, per wave as C (co x ci) += dY (co x cells) . X_tap (cells x ci)
+//   over 20 k-steps of 4 cells per sample (36 accumulators: 9 taps x 2 x 2
+//   tiles); the neighbour of the k-step's cell comes from an LDS table.
+//   Waves fold through LDS and workgroups through a fixed-order reduce
+//   (deterministic).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hrl_nn.h"
+#include "../../include/hrl_targets.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCo = 32;                  // output channels (2 MFMA column tiles)
+constexpr int kMT = 5;                   // 16-cell tiles: boards of at most 80 cells
+constexpr int kMaxCells = kMT * 16;
+constexpr int kS = 81;                   // LDS row stride: odd, 16 consecutive rows -> 16 banks
+constexpr int kTaps = 9;
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kTile = kCo * kS;          // floats of one wave's sample tile (>= KS*4 rows)
+constexpr int kKCells = kMaxCells / 4;   // wgrad k-steps per sample (20)
+
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int torus_nbr(int q, int H, int W, int tap) {
+    const int r = q / W, c = q - r * W;
+    int rr = r + tap / 3 - 1, cc = c + tap % 3 - 1;
+    rr = rr < 0 ? rr + H : (rr >= H ? rr - H : rr);
+    cc = cc < 0 ? cc + W : (cc >= W ? cc - W : cc);
+    return rr * W + cc;
+}
+
+// floor(e / d) for 0 <= e < 2^20 given inv = 1/d (exact: see hrl_targets.hip fdiv)
+__device__ __forceinline__ int fdiv(int e, float inv) { return (int)(((float)e + 0.5f) * inv); }
+
+// ------------------------------------------------------------------ sample staging
+// One sample's n_elem = C*HW floats: global (contiguous) -> registers -> LDS [c][cell] rows.
+template <bool VEC, int NLD>
+struct Stage {
+    float4 v[VEC ? NLD : 1];
+    float s[VEC ? 1 : NLD];
+
+    __device__ __forceinline__ void load(const float *src, int n_elem, int lane) {
+        if constexpr (VEC) {
+            const int nv = n_elem >> 2;
+#pragma unroll
+            for (int k = 0; k < NLD; ++k) {
+                const int i = min(k * 64 + lane, nv - 1);   // clamp: loads issue back to back
+                v[k] = reinterpret_cast<const float4 *>(src)[i];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NLD; ++k) s[k] = src[min(k * 64 + lane, n_elem - 1)];
+        }
+    }
+    __device__ __forceinline__ void to_lds(float *tile, int n_elem, int HW, float inv_hw, int lane) const {
+        if constexpr (VEC) {
+            const int nv = n_elem >> 2;
+#pragma unroll
+            for (int k = 0; k < NLD; ++k) {
+                const int i = k * 64 + lane;
+                if (i < nv) {
+                    const float x4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int e = 4 * i + j;
+                        const int c = fdiv(e, inv_hw);
+                        tile[c * kS + (e - c * HW)] = x4[j];
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NLD; ++k) {
+                const int e = k * 64 + lane;
+                if (e < n_elem) {
+                    const int c = fdiv(e, inv_hw);
+                    tile[c * kS + (e - c * HW)] = s[k];
+                }
+            }
+        }
+    }
+};
+
+// LDS tile [c][cell] -> one sample's output (n_elem = channels*HW floats, contiguous)
+__device__ __forceinline__ void store_sample(const float *tile, float *dst, int n_elem, bool vec, int HW,
+                                             float inv_hw, int lane) {
+    if (vec) {
+        const int nv = n_elem >> 2;
+        for (int i = lane; i < nv; i += 64) {
+            float x4[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int e = 4 * i + j;
+                const int c = fdiv(e, inv_hw);
+                x4[j] = tile[c * kS + (e - c * HW)];
+            }
+            reinterpret_cast<float4 *>(dst)[i] = make_float4(x4[0], x4[1], x4[2], x4[3]);
+        }
+    } else {
+        for (int e = lane; e < n_elem; e += 64) {
+            const int c = fdiv(e, inv_hw);
+            dst[e] = tile[c * kS + (e - c * HW)];
+        }
+    }
+}
+
+__device__ __forceinline__ void lds_fence() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS operations done
+    __builtin_amdgcn_wave_barrier();
+}
+
+// ------------------------------------------------------------------ forward / input gradient
+// x: (N, Cin, HW); wpk: [tap][KS][2][64]; y: (N, out_c, HW), out_c <= 32 (the first out_c channels of
+// the 32 computed); part: [grid][32][2] (STATS)
+template <int KS, bool VEC, bool STATS>
+__global__ __launch_bounds__(kThreads) void torus_conv_kernel(const float *__restrict__ x, int64_t N, int Cin,
+                                                              int H, int W, const float *__restrict__ wpk,
+                                                              const float *__restrict__ bias, int out_c,
+                                                              bool vec_out, float *__restrict__ y,
+                                                              double *__restrict__ part) {
+    constexpr int kNW = kTaps * KS * 2 * 64;
+    constexpr int kNLd = VEC ? (KS * 4 * kMaxCells / 4 + 63) / 64 : (KS * 4 * kMaxCells + 63) / 64;
+    __shared__ float w_lds[kNW];
+    __shared__ float tiles[kWaves * kTile];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int HW = H * W;
+    const float inv_hw = 1.0f / (float)HW;
+    const int in_elem = Cin * HW;
+    float *tile = tiles + wave * kTile;
+
+    for (int i = threadIdx.x; i < kNW; i += kThreads) w_lds[i] = wpk[i];
+    // channel rows Cin .. 4*KS-1 stay zero (their packed weights are zero too; no NaN * 0)
+    for (int i = lane; i < kTile; i += 64) tile[i] = 0.f;
+
+    // the lane's A-fragment cells: q = mt*16 + (lane & 15); cells past the board read cell q - HW
+    int nbr[kMT][kTaps];
+#pragma unroll
+    for (int mt = 0; mt < kMT; ++mt) {
+        int q = mt * 16 + (lane & 15);
+        while (q >= HW) q -= HW;
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) nbr[mt][t] = torus_nbr(q, H, W, t) + (lane >> 4) * kS;
+    }
+    float bias_v[2] = {0.f, 0.f};
+    if (bias) {
+        bias_v[0] = bias[lane & 15];
+        bias_v[1] = bias[16 + (lane & 15)];
+    }
+    double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
+
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    int64_t n = (int64_t)blockIdx.x * kWaves + wave;
+    Stage<VEC, kNLd> st;
+    if (n < N) st.load(x + n * in_elem, in_elem, lane);
+    __syncthreads();   // weights in LDS, tiles zeroed
+
+    for (; n < N; n += stride) {
+        st.to_lds(tile, in_elem, HW, inv_hw, lane);
+        lds_fence();
+        const int64_t next = n + stride;
+        if (next < N) st.load(x + next * in_elem, in_elem, lane);   // in flight during the MFMAs
+
+        f32x4 acc[kMT][2];
+#pragma unroll
+        for (int mt = 0; mt < kMT; ++mt) acc[mt][0] = acc[mt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        const float *wl = w_lds + lane;
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const float b0 = wl[((t * KS + s) * 2 + 0) * 64];
+                const float b1 = wl[((t * KS + s) * 2 + 1) * 64];
+#pragma unroll
+                for (int mt = 0; mt < kMT; ++mt) {
+                    const float a = tile[nbr[mt][t] + s * 4 * kS];
+                    acc[mt][0] = mfma(a, b0, acc[mt][0]);
+                    acc[mt][1] = mfma(a, b1, acc[mt][1]);
+                }
+            }
+        }
+        lds_fence();   // every lane's A reads done before the tile is overwritten
+
+        // accumulators (cell = mt*16 + (lane>>4)*4 + r, co = ct*16 + (lane&15)) -> tile [co][cell]
+        float t1[2] = {0.f, 0.f}, t2[2] = {0.f, 0.f};
+#pragma unroll
+        for (int mt = 0; mt < kMT; ++mt)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int cell = mt * 16 + (lane >> 4) * 4 + r;
+                    const int co = ct * 16 + (lane & 15);
+                    if (cell < HW) {
+                        const float v = acc[mt][ct][r] + bias_v[ct];
+                        tile[co * kS + cell] = v;
+                        if constexpr (STATS) {
+                            t1[ct] += v;
+                            t2[ct] += v * v;
+                        }
+                    }
+                }
+        if constexpr (STATS) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                s1[ct] += (double)t1[ct];
+                s2[ct] += (double)t2[ct];
+            }
+        }
+        lds_fence();
+        store_sample(tile, y + n * (out_c * HW), out_c * HW, vec_out, HW, inv_hw, lane);
+        lds_fence();
+        // padding rows must read as zero again for the next sample (the output tile used them)
+        for (int i = in_elem / HW * kS + lane; i < KS * 4 * kS; i += 64) tile[i] = 0.f;
+    }
+    if constexpr (STATS) {
+        // fold the 4 lanes sharing a channel and the 4 waves in a fixed order
+        __syncthreads();
+        double *red = reinterpret_cast<double *>(tiles);   // [wave][group][32][2]
+        const int grp = lane >> 4;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+            const int co = ct * 16 + (lane & 15);
+            red[((wave * 4 + grp) * kCo + co) * 2 + 0] = s1[ct];
+            red[((wave * 4 + grp) * kCo + co) * 2 + 1] = s2[ct];
+        }
+        __syncthreads();
+        if (threadIdx.x < 2 * kCo) {
+            const int co = threadIdx.x >> 1, k = threadIdx.x & 1;
+            double t = 0.0;
+            for (int i = 0; i < kWaves * 4; ++i) t += red[(i * kCo + co) * 2 + k];
+            part[((int64_t)blockIdx.x * kCo + co) * 2 + k] = t;
+        }
+    }
+}
+
+// W (32, Cin, 3, 3) -> packed [tap][KS][ct][64]: lane l of k-step s holds W^T[ci = 4s + (l>>4)][co = 16ct + (l&15)].
+// flip = 1 (KS = 8): the input gradient's weights, W'[co' = ci][ci' = co][tap] = W[co][ci][8 - tap],
+// output channels ci >= Cin zero.
+__global__ void torus_pack_kernel(const float *__restrict__ w, int Cin, int KS, int flip, float *__restrict__ wpk) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kTaps * KS * 2 * 64) return;
+    const int l = i & 63, ct = (i >> 6) & 1, s = (i >> 7) % KS, tap = i / (128 * KS);
+    const int oc = ct * 16 + (l & 15);   // output channel of this conv
+    const int ic = s * 4 + (l >> 4);     // input channel of this conv
+    float v = 0.f;
+    if (!flip) {
+        if (ic < Cin) v = w[(oc * Cin + ic) * kTaps + tap];
+    } else {
+        if (oc < Cin) v = w[(ic * Cin + oc) * kTaps + (kTaps - 1 - tap)];
+    }
+    wpk[i] = v;
+}
+
+// ------------------------------------------------------------------ weight gradient
+// partial[block]: [tap][ci 32][co 32] then db [32]
+template <int KS, bool VEC>
+__global__ __launch_bounds__(kThreads) void torus_wgrad_kernel(const float *__restrict__ x,
+                                                               const float *__restrict__ dy, int64_t N, int Cin,
+                                                               int H, int W, float *__restrict__ partial) {
+    constexpr int kNLdX = VEC ? (KS * 4 * kMaxCells / 4 + 63) / 64 : (KS * 4 * kMaxCells + 63) / 64;
+    constexpr int kNLdG = (kCo * kMaxCells / 4 + 63) / 64;   // dy samples: 32*HW floats
+    constexpr int kJT = (KS * 4 + 15) / 16;                   // ci tiles
+    constexpr int kPart = kTaps * kCo * kCo + kCo;
+    __shared__ float lds[2 * kWaves * kTile];                 // per wave: x tile, dy tile
+    __shared__ int nbr_tab[kMaxCells * kTaps];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int HW = H * W;
+    const float inv_hw = 1.0f / (float)HW;
+    const int in_elem = Cin * HW, g_elem = kCo * HW;
+    float *xs = lds + wave * kTile;
+    float *gs = lds + (kWaves + wave) * kTile;
+    for (int i = threadIdx.x; i < kMaxCells * kTaps; i += kThreads) {
+        const int q = i / kTaps, t = i - q * kTaps;
+        nbr_tab[i] = q < HW ? torus_nbr(q, H, W, t) : 0;   // cells past the board: dy is zero there
+    }
+    for (int i = lane; i < kTile; i += 64) { xs[i] = 0.f; gs[i] = 0.f; }
+    __syncthreads();
+
+    f32x4 acc[kTaps][2][kJT];
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int jt = 0; jt < kJT; ++jt) acc[t][it][jt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float bsum[2] = {0.f, 0.f};
+
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    int64_t n = (int64_t)blockIdx.x * kWaves + wave;
+    Stage<VEC, kNLdX> sx;
+    Stage<VEC, VEC ? kNLdG : (kCo * kMaxCells + 63) / 64> sg;
+    if (n < N) {
+        sx.load(x + n * in_elem, in_elem, lane);
+        sg.load(dy + n * g_elem, g_elem, lane);
+    }
+    const int i16 = lane & 15, kk = lane >> 4;
+    for (; n < N; n += stride) {
+        sx.to_lds(xs, in_elem, HW, inv_hw, lane);
+        sg.to_lds(gs, g_elem, HW, inv_hw, lane);
+        lds_fence();
+        const int64_t next = n + stride;
+        if (next < N) {
+            sx.load(x + next * in_elem, in_elem, lane);
+            sg.load(dy + next * g_elem, g_elem, lane);
+        }
+#pragma unroll 2
+        for (int ks = 0; ks < kKCells; ++ks) {
+            const int cell = ks * 4 + kk;
+            const float a0 = gs[i16 * kS + cell];
+            const float a1 = gs[(16 + i16) * kS + cell];
+            bsum[0] += a0;
+            bsum[1] += a1;
+            const int *nb = nbr_tab + cell * kTaps;
+#pragma unroll
+            for (int t = 0; t < kTaps; ++t) {
+                const int p = nb[t];
+#pragma unroll
+                for (int jt = 0; jt < kJT; ++jt) {
+                    const float b = xs[(jt * 16 + i16) * kS + p];
+                    acc[t][0][jt] = mfma(a0, b, acc[t][0][jt]);
+                    acc[t][1][jt] = mfma(a1, b, acc[t][1][jt]);
+                }
+            }
+        }
+        lds_fence();
+    }
+    // fold the 4 waves in a fixed order ((w0 + w1) + w2) + w3 through the (now free) tile LDS;
+    // one partial per workgroup
+    float *red = lds;
+    float *bred = lds + kPart;   // [wave][k group][32]
+    static_assert(2 * kWaves * kTile >= kPart + kWaves * 4 * kCo, "fold buffer");
+    __syncthreads();
+#pragma unroll 1
+    for (int w = 0; w < kWaves; ++w) {
+        if (wave == w) {
+#pragma unroll
+            for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+                for (int it = 0; it < 2; ++it)
+#pragma unroll
+                    for (int jt = 0; jt < kJT; ++jt)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            // C[i = co][j = ci]: row = (lane>>4)*4 + r, col = lane & 15
+                            const int co = it * 16 + (lane >> 4) * 4 + r;
+                            const int ci = jt * 16 + (lane & 15);
+                            float *d = red + (t * kCo + ci) * kCo + co;
+                            *d = w == 0 ? acc[t][it][jt][r] : *d + acc[t][it][jt][r];
+                        }
+#pragma unroll
+            for (int it = 0; it < 2; ++it) bred[(wave * 4 + kk) * kCo + it * 16 + i16] = bsum[it];
+        }
+        __syncthreads();
+    }
+    float *out = partial + (int64_t)blockIdx.x * kPart;
+    for (int i = threadIdx.x; i < kTaps * kCo * kCo; i += kThreads) out[i] = red[i];
+    if (threadIdx.x < kCo) {
+        float b = 0.f;
+        for (int i = 0; i < kWaves * 4; ++i) b += bred[i * kCo + threadIdx.x];
+        out[kTaps * kCo * kCo + threadIdx.x] = b;
+    }
+}
+
+// fold per-workgroup partials (fixed order, fp64) into dW (32, Cin, 3, 3) and db (32)
+__global__ __launch_bounds__(256) void torus_wgrad_reduce_kernel(const float *__restrict__ partial, int nparts,
+                                                                 int Cin, float *__restrict__ dw,
+                                                                 float *__restrict__ db) {
+    constexpr int kPart = kTaps * kCo * kCo + kCo;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // partial index
+    if (i >= kPart) return;
+    double s = 0.0;
+    for (int w = 0; w < nparts; ++w) s += (double)partial[(int64_t)w * kPart + i];
+    if (i < kTaps * kCo * kCo) {
+        const int co = i % kCo, ci = (i / kCo) % kCo, tap = i / (kCo * kCo);
+        if (ci < Cin) dw[(co * Cin + ci) * kTaps + tap] = (float)s;
+    } else if (db) {
+        db[i - kTaps * kCo * kCo] = (float)s;
+    }
+}
+
+constexpr int kGridConv = 512;    // 2 workgroups per CU (78 KB LDS each)
+constexpr int kGridWgrad = 256;   // 1 workgroup per CU (83 KB of tiles + the neighbour table)
+
+int status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
+}
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int grid_for(int64_t N, int cap) {
+    const int64_t blocks = (N + kWaves - 1) / kWaves;
+    return (int)(blocks < cap ? blocks : cap);
+}
+
+bool shape_ok(int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W) {
+    return N >= 1 && Cout == kCo && (Cin == 17 || Cin == 32) && H >= 1 && W >= 1 && H * W <= kMaxCells &&
+           N * Cin * H * W < ((int64_t)1 << 40);
+}
+
+constexpr int64_t kPackFloats = kTaps * 8 * 2 * 64;
+constexpr int64_t kPartFloats = kTaps * kCo * kCo + kCo;
+
+}  // namespace
+
+extern "C" {
+
+int64_t hrl_torus_workspace_bytes(int64_t N) {
+    if (N < 1) return -1;
+    return (kPackFloats + (int64_t)grid_for(N, kGridWgrad) * kPartFloats) * 4;
+}
+
+int64_t hrl_torus_stats_blocks(int64_t N) { return N < 1 ? -1 : grid_for(N, kGridConv); }
+
+int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
+                           const float *weight, const float *bias, int flip, float *y, double *part, void *workspace,
+                           int64_t workspace_bytes, void *stream) {
+    if (!shape_ok(N, Cin, Cout, H, W) || !x || !weight || !y || !workspace) return HRL_EINVAL;
+    if (flip && bias) return HRL_EINVAL;
+    if (workspace_bytes < hrl_torus_workspace_bytes(N)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // the conv this launch computes: forward Cin -> 32; flip: 32 -> Cin (the forward's adjoint)
+    const int in_c = flip ? (int)kCo : (int)Cin;
+    const int out_c = flip ? (int)Cin : (int)kCo;
+    const int KS = in_c == 17 ? 5 : 8;
+    float *wpk = static_cast<float *>(workspace);
+    hipLaunchKernelGGL(torus_pack_kernel, dim3((kTaps * KS * 128 + 255) / 256), dim3(256), 0, s, weight, (int)Cin, KS,
+                       flip, wpk);
+    int rc = status();
+    if (rc) return rc;
+    const int HW = (int)(H * W);
+    const bool vec = (in_c * HW) % 4 == 0 && aligned16(x);
+    const bool vec_out = (out_c * HW) % 4 == 0 && aligned16(y);
+    const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
+#define HRL_TORUS_LAUNCH(KS_, VEC_, ST_)                                                                           \
+    hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_>), grid, block, 0, s, x, N, in_c, (int)H, (int)W, wpk,    \
+                       bias, out_c, vec_out, y, part)
+    const bool st = part != nullptr;
+    if (KS == 8) {
+        if (vec) { if (st) HRL_TORUS_LAUNCH(8, true, true); else HRL_TORUS_LAUNCH(8, true, false); }
+        else { if (st) HRL_TORUS_LAUNCH(8, false, true); else HRL_TORUS_LAUNCH(8, false, false); }
+    } else {
+        if (st) HRL_TORUS_LAUNCH(5, false, true); else HRL_TORUS_LAUNCH(5, false, false);
+    }
+#undef HRL_TORUS_LAUNCH
+    return status();
+}
+
+int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
+                         float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream) {
+    if (!shape_ok(N, Cin, Cout, H, W) || !x || !dy || !dweight || !workspace) return HRL_EINVAL;
+    if (workspace_bytes < hrl_torus_workspace_bytes(N)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int HW = (int)(H * W);
+    const bool vec = (Cin * HW) % 4 == 0 && (kCo * HW) % 4 == 0 && aligned16(x) && aligned16(dy);
+    const int grid = grid_for(N, kGridWgrad);
+    float *partial = static_cast<float *>(workspace) + kPackFloats;
+    if (Cin == kCo) {
+        if (vec)
+            hipLaunchKernelGGL((torus_wgrad_kernel<8, true>), dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)Cin,
+                               (int)H, (int)W, partial);
+        else
+            hipLaunchKernelGGL((torus_wgrad_kernel<8, false>), dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)Cin,
+                               (int)H, (int)W, partial);
+    } else {
+        hipLaunchKernelGGL((torus_wgrad_kernel<5, false>), dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)Cin,
+                           (int)H, (int)W, partial);
+    }
+    int rc = status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(torus_wgrad_reduce_kernel, dim3((int)((kPartFloats + 255) / 256)), dim3(256), 0, s, partial,
+                       grid, (int)Cin, dweight, dbias);
+    return status();
+}
+
+}  // extern "C"

@@ -1,0 +1,96 @@
+"""Hungry Geese network: the feed-forward torus-conv model of config C4.
+
+Architecture and state_dict keys follow GeeseNet in
+handyrl/envs/kaggle/hungry_geese.py (:23-57), with the modules constructed in
+the same order (so ``torch.manual_seed(s); GeeseNet()`` draws the same
+initial weights as the reference module would):
+
+* TorusConv2d (:23-35): 3x3 convolution on the 7x11 torus -- the board wraps
+  in both directions -- followed by BatchNorm2d when ``bn``; the reference
+  builds the wrap with two concatenations and a 'valid' conv;
+* stem 17 -> 32, then 12 residual blocks h = relu(h + bn(conv(h))) (:48-51);
+* heads (:52-55): h_head = sum over cells of h * x[:, :1] (the goose-head
+  plane), h_avg = mean over cells; policy Linear(32, 4), value
+  tanh(Linear(64, 1)), both bias-free.  116,928 parameters.
+
+The rules live in kaggle_environments, which is not installed here, so this
+module has no batched rules; ``Environment`` gates on the import exactly as
+the reference module does (hungry_geese.py:18).  The learner trains GeeseNet
+on make_batch-layout batches (solo training, turn_based_training=False:
+P = Pp = 1, train.py:57-58), see synthetic.geese_batch.
+
+On the GPU the torus convolutions run as csrc/hrl_torus.hip (wrap-around
+addressing in the kernel, no padded copy) once ``nn.accelerate`` has swapped
+``TorusConv2d`` for its HIP form.
+"""
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+BOARD = (7, 11)
+PLANES = 17
+ACTIONS = 4
+
+
+class TorusConv2d(nn.Module):
+    """kxk convolution with wrap-around (torus) padding, then optional BatchNorm2d."""
+
+    def __init__(self, input_dim, output_dim, kernel_size, bn):
+        super().__init__()
+        self.edge_size = (kernel_size[0] // 2, kernel_size[1] // 2)
+        self.conv = nn.Conv2d(input_dim, output_dim, kernel_size=kernel_size)
+        self.bn = nn.BatchNorm2d(output_dim) if bn else None
+
+    def wrap(self, x):
+        eh, ew = self.edge_size
+        h = torch.cat([x[:, :, :, -ew:], x, x[:, :, :, :ew]], dim=3)
+        return torch.cat([h[:, :, -eh:], h, h[:, :, :eh]], dim=2)
+
+    use_hip = False   # set by nn.accelerate: the conv runs as csrc/hrl_torus.hip (no wrapped copy)
+
+    def forward(self, x):
+        if self.use_hip:
+            from ..nn import torus_conv2d, torus_supported
+            if not torus_supported(x, self.conv.weight):
+                raise RuntimeError('TorusConv2d: shape %s x %s is outside the HIP torus conv'
+                                   % (tuple(x.shape), tuple(self.conv.weight.shape)))
+            h = torus_conv2d(x, self.conv.weight, self.conv.bias)
+        else:
+            h = self.conv(self.wrap(x))
+        return self.bn(h) if self.bn is not None else h
+
+
+class GeeseNet(nn.Module):
+    def __init__(self, layers=12, filters=32):
+        super().__init__()
+        self.conv0 = TorusConv2d(PLANES, filters, (3, 3), True)
+        self.blocks = nn.ModuleList([TorusConv2d(filters, filters, (3, 3), True) for _ in range(layers)])
+        self.head_p = nn.Linear(filters, ACTIONS, bias=False)
+        self.head_v = nn.Linear(filters * 2, 1, bias=False)
+
+    def forward(self, x, _=None):
+        h = F.relu(self.conv0(x))
+        for block in self.blocks:
+            h = F.relu(h + block(h))
+        n, c = h.size(0), h.size(1)
+        h_head = (h * x[:, :1]).view(n, c, -1).sum(-1)
+        h_avg = h.view(n, c, -1).mean(-1)
+        p = self.head_p(h_head)
+        v = torch.tanh(self.head_v(torch.cat([h_head, h_avg], 1)))
+        return {'policy': p, 'value': v}
+
+
+class Environment:
+    """The reference's rules wrap kaggle_environments (hungry_geese.py:18, :60-230): gated on that import."""
+
+    def __init__(self, args=None):
+        try:
+            import kaggle_environments  # noqa: F401
+        except ImportError as e:
+            raise ImportError('Hungry Geese rules need kaggle_environments, which is not installed; '
+                              'GeeseNet trains on make_batch-layout batches without it') from e
+        raise NotImplementedError('Hungry Geese rules: use handyrl.envs.kaggle.hungry_geese (reference plugin)')
+
+    def net(self):
+        return GeeseNet

@@ -356,6 +356,62 @@ class _Conv3x3(torch.autograd.Function):
         return dx, dw, db
 
 
+def torus_supported(x, weight):
+    """Shapes csrc/hrl_torus.hip covers: 3x3, 17 or 32 -> 32 channels, boards of at most 80 cells."""
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[0] > 0
+            and weight.shape[0] == 32 and weight.shape[1] in (17, 32) and tuple(weight.shape[2:]) == (3, 3)
+            and x.shape[1] == weight.shape[1] and x.shape[2] * x.shape[3] <= 80)
+
+
+class _TorusConv(torch.autograd.Function):
+    """3x3 conv on a torus board (GeeseNet TorusConv2d): csrc/hrl_torus.hip, fp32 MFMA, wrap as addressing."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        x = x.contiguous()
+        N, Cin, H, W = x.shape
+        lib = _native.load()
+        ws_bytes = lib.hrl_torus_workspace_bytes(N)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+        y = torch.empty(N, 32, H, W, device=x.device, dtype=x.dtype)
+        w = weight.contiguous()
+        _native.check(lib.hrl_torus_conv_forward(_native.ptr(x), N, Cin, 32, H, W, _native.ptr(w),
+                                                 _native.ptr(bias), 0, _native.ptr(y), None, _native.ptr(ws),
+                                                 ws_bytes, _native.stream_of(x.device)), 'hrl_torus_conv_forward')
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        N, Cin, H, W = x.shape
+        lib = _native.load()
+        ws_bytes = lib.hrl_torus_workspace_bytes(N)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+        stream = _native.stream_of(x.device)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _native.check(lib.hrl_torus_conv_forward(_native.ptr(dy), N, Cin, 32, H, W, _native.ptr(w), None, 1,
+                                                     _native.ptr(dx), None, _native.ptr(ws), ws_bytes, stream),
+                          'hrl_torus_conv_forward(flip)')
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dw = torch.empty_like(w)
+            db = torch.empty(32, device=x.device, dtype=x.dtype) if ctx.has_bias else None
+            _native.check(lib.hrl_torus_conv_wgrad(_native.ptr(x), _native.ptr(dy), N, Cin, 32, H, W,
+                                                   _native.ptr(dw), _native.ptr(db), _native.ptr(ws), ws_bytes,
+                                                   stream), 'hrl_torus_conv_wgrad')
+            if not ctx.needs_input_grad[1]:
+                dw = None
+        return dx, dw, db
+
+
+def torus_conv2d(x, weight, bias=None):
+    return _TorusConv.apply(x, weight, bias)
+
+
 class _BoardWeight(torch.autograd.Function):
     """W -> W_board (csrc/hrl_board.hip); backward folds dW_board onto W (deterministic)."""
 

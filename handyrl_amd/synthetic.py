@@ -19,7 +19,7 @@ follows make_batch: masks 0, action_mask 1e32, progress 1, value = outcome.
 import torch
 
 
-def tictactoe_batch(B, T, device, seed=0, obs_shape=(3, 3, 3), A=9, P=2, min_len=5):
+def tictactoe_batch(B, T, device, seed=0, obs_shape=(3, 3, 3), A=9, P=2, min_len=5, illegal_p=0.3):
     g = torch.Generator(device=device).manual_seed(seed)
     dev = device
 
@@ -35,7 +35,7 @@ def tictactoe_batch(B, T, device, seed=0, obs_shape=(3, 3, 3), A=9, P=2, min_len
     onehot = torch.nn.functional.one_hot(turn, P).float() * valid.unsqueeze(-1)   # (B,T,P)
     tmask = onehot.unsqueeze(-1)                                  # (B,T,P,1)
 
-    illegal = (rand(B, T, 1, A) < 0.3)
+    illegal = (rand(B, T, 1, A) < illegal_p)
     illegal[..., 0] = False
     amask = illegal.float() * 1e32
     amask = torch.where(valid.view(B, T, 1, 1) > 0, amask, torch.full_like(amask, 1e32))
@@ -47,8 +47,11 @@ def tictactoe_batch(B, T, device, seed=0, obs_shape=(3, 3, 3), A=9, P=2, min_len
     action = score.argmax(-1, keepdim=True)                       # (B,T,1,1) int64
     action = action * valid.view(B, T, 1, 1).long()
 
-    o0 = torch.randint(-1, 2, (B, 1, 1, 1), device=dev, generator=g).float()
-    outcome = torch.cat([o0, -o0], dim=2)                         # (B,1,2,1) zero-sum
+    if P == 2:
+        o0 = torch.randint(-1, 2, (B, 1, 1, 1), device=dev, generator=g).float()
+        outcome = torch.cat([o0, -o0], dim=2)                     # (B,1,2,1) zero-sum
+    else:   # rank outcomes of a 4-player game, one per trained player
+        outcome = (torch.randint(0, 4, (B, 1, P, 1), device=dev, generator=g).float() * 2 - 3) / 3
     values = torch.tanh(torch.randn(B, T, P, 1, device=dev, generator=g)) * tmask
     values = values + outcome * (1 - valid.view(B, T, 1, 1))      # padded with the outcome
 
@@ -82,6 +85,30 @@ def geister_batch(B, T, device, seed=0, P=2, min_len=5):
     scalar = (torch.rand(B, T, 1, 18, device=device, generator=g) < 0.5).float() * valid
     batch['observation'] = {'board': batch['observation'], 'scalar': scalar.contiguous()}
     return batch
+
+
+def geese_batch(B, T, device, seed=0, min_len=5):
+    """C4 Hungry Geese batch, solo training (turn_based_training=False: make_batch keeps one random
+    player per window, train.py:57-58, so P = Pp = 1): observation (B,T,1,17,7,11), A = 4, every
+    action legal (hungry_geese.py:187-189), rank outcomes in {-1, -1/3, 1/3, 1}."""
+    batch = tictactoe_batch(B, T, device, seed=seed, obs_shape=(17, 7, 11), A=4, P=1, min_len=min_len,
+                            illegal_p=0.0)
+    # sparse planes like the real observation (hungry_geese.py:211-230: heads, tails, bodies,
+    # previous heads, food): plane 0 is the trained goose's head, one cell
+    g = torch.Generator(device=device).manual_seed(seed + 1)
+    valid = batch['episode_mask'].view(B, T, 1, 1, 1, 1)
+    obs = (torch.rand(B, T, 1, 17, 7, 11, device=device, generator=g) < 0.06).float()
+    head = torch.randint(0, 77, (B, T, 1), device=device, generator=g)
+    obs[:, :, :, 0] = torch.nn.functional.one_hot(head, 77).float().view(B, T, 1, 7, 11)
+    batch['observation'] = (obs * valid).contiguous()
+    return batch
+
+
+def geese_args(T, batch_size=None):
+    """Learner arguments of config C4: solo (non-turn-based) training, UPGO policy target."""
+    args = default_args(T, batch_size)
+    args['turn_based_training'] = False
+    return args
 
 
 def default_args(T, batch_size=None):

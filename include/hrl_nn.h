@@ -176,6 +176,28 @@ int hrl_hidden_update(const float *const *H, const float *const *nh, int64_t Pn,
 int hrl_hidden_update_backward(const float *const *dout, const float *mask, int64_t B, int64_t P, int64_t Pn,
                                int nleaves, const int64_t *F, float *const *dH, float *const *dnh, void *stream);
 
+/*
+ * 3x3 convolution on a torus board, 17 or 32 -> 32 channels, H*W <= 80
+ * (GeeseNet's TorusConv2d, handyrl/envs/kaggle/hungry_geese.py:23-35: the
+ * reference's wrap-around concatenation + 'valid' conv, with the wrap as
+ * addressing) with fp32 MFMA (csrc/hrl_torus.hip).  x: (N, Cin, H, W),
+ * y: (N, 32, H, W), weight (32, Cin, 3, 3), bias (32) or NULL.
+ * flip = 0: y = conv(x, W) + bias.  flip = 1 (no bias): y = conv^T(x, W), the input
+ * gradient of the forward: x is then (N, 32, H, W) and y (N, Cin, H, W).  part != NULL: also the per-workgroup
+ * fp64 (sum y, sum y^2) per channel, hrl_torus_stats_blocks(N) x 32 x 2
+ * doubles -> hrl_bn_finalize_stats (GeeseNet's BatchNorm after every conv).
+ * hrl_torus_conv_wgrad: dweight (32, Cin, 3, 3) and dbias (32, may be NULL)
+ * for input x and output gradient dy; deterministic.
+ * workspace: hrl_torus_workspace_bytes(N) bytes.
+ */
+int64_t hrl_torus_workspace_bytes(int64_t N);
+int64_t hrl_torus_stats_blocks(int64_t N);
+int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
+                           const float *weight, const float *bias, int flip, float *y, double *part, void *workspace,
+                           int64_t workspace_bytes, void *stream);
+int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
+                         float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,141 @@
+"""GeeseNet (config C4, handyrl/envs/kaggle/hungry_geese.py:23-57) and its HIP torus convolution.
+
+Parity status: the reference module imports kaggle_environments at its top
+(hungry_geese.py:18), which is not installed here, so the reference GeeseNet
+cannot run in this container.  The restatement is pinned to the reference
+SOURCE (module order, state_dict keys, the 116,928 parameters counted in
+SURVEY.md §8e); its torch-CPU forward is the oracle for the HIP path, and the
+learner step is checked against the CPU oracle learner (oracle/learner.py,
+itself pinned to reference goldens).  Reference-output parity for GeeseNet is
+unpinned.
+"""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from handyrl_amd.envs.hungry_geese import GeeseNet, TorusConv2d
+from oracle import learner as ol
+
+
+def test_geesenet_matches_reference_structure():
+    net = GeeseNet()
+    assert sum(p.numel() for p in net.parameters()) == 116928
+    keys = list(net.state_dict().keys())
+    assert keys[:7] == ['conv0.conv.weight', 'conv0.conv.bias', 'conv0.bn.weight', 'conv0.bn.bias',
+                        'conv0.bn.running_mean', 'conv0.bn.running_var', 'conv0.bn.num_batches_tracked']
+    assert 'blocks.11.bn.running_var' in keys and keys[-2:] == ['head_p.weight', 'head_v.weight']
+
+
+def test_torus_wrap_is_circular_padding():
+    torch.manual_seed(0)
+    tc = TorusConv2d(5, 32, (3, 3), False)
+    x = torch.randn(3, 5, 7, 11)
+    ref = F.conv2d(F.pad(x, (1, 1, 1, 1), mode='circular'), tc.conv.weight, tc.conv.bias)
+    assert torch.equal(tc(x), ref)
+
+
+def _torus_ref(x, w, b):
+    return F.conv2d(F.pad(x, (1, 1, 1, 1), mode='circular'), w, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('cin,N,H,W', [(32, 37, 7, 11), (17, 21, 7, 11), (32, 5, 4, 5), (32, 9, 8, 10),
+                                       (17, 3, 3, 3), (32, 2000, 7, 11)])
+def test_torus_conv_matches_torch(cuda, cin, N, H, W):
+    """Forward, input gradient, weight and bias gradients of csrc/hrl_torus.hip vs torch-CPU fp32
+    (circular padding + conv2d) on ragged sample counts and several board shapes."""
+    from handyrl_amd.nn import torus_conv2d
+    g = torch.Generator().manual_seed(cin * 1000 + N)
+    x = torch.randn(N, cin, H, W, generator=g)
+    w = torch.randn(32, cin, 3, 3, generator=g) * 0.1
+    b = torch.randn(32, generator=g)
+    dy = torch.randn(N, 32, H, W, generator=g)
+    xc, wc, bc = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yc = _torus_ref(xc, wc, bc)
+    yc.backward(dy)
+    xg, wg, bg = (t.to(cuda).requires_grad_(True) for t in (x, w, b))
+    yg = torus_conv2d(xg, wg, bg)
+    yg.backward(dy.to(cuda))
+    torch.testing.assert_close(yg.detach().cpu(), yc.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(xg.grad.cpu(), xc.grad, rtol=1e-5, atol=1e-5)
+    # weight / bias gradients sum N*H*W unit-scale products: fp32 summation error grows like sqrt(terms)
+    tol = 2e-5 * (N * H * W) ** 0.5
+    torch.testing.assert_close(wg.grad.cpu(), wc.grad, rtol=1e-5, atol=tol)
+    torch.testing.assert_close(bg.grad.cpu(), bc.grad, rtol=1e-5, atol=tol)
+
+
+@pytest.mark.gpu
+def test_torus_conv_deterministic(cuda):
+    from handyrl_amd.nn import torus_conv2d
+    g = torch.Generator(device=cuda).manual_seed(1)
+    x = torch.randn(3000, 32, 7, 11, device=cuda, generator=g).requires_grad_(True)
+    w = (torch.randn(32, 32, 3, 3, device=cuda, generator=g) * 0.1).requires_grad_(True)
+    dy = torch.randn(3000, 32, 7, 11, device=cuda, generator=g)
+    outs = []
+    for _ in range(2):
+        x.grad = w.grad = None
+        y = torus_conv2d(x, w, None)
+        y.backward(dy)
+        outs.append((y.detach().clone(), x.grad.clone(), w.grad.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_geesenet_hip_forward_matches_cpu(cuda):
+    """Accelerated GeeseNet (HIP torus convs + HIP BatchNorm) vs the torch-CPU module, train mode
+    (batch statistics) and eval mode (running statistics)."""
+    from handyrl_amd.nn import accelerate
+    from handyrl_amd.synthetic import geese_batch
+    torch.manual_seed(0)
+    ref = GeeseNet()
+    net = GeeseNet()
+    net.load_state_dict(ref.state_dict())
+    net = accelerate(net.to(cuda))
+    assert all(m.use_hip for m in net.modules() if isinstance(m, TorusConv2d))
+    obs = geese_batch(6, 9, torch.device('cpu'), seed=2)['observation'].view(-1, 17, 7, 11)
+    for train in (True, False):
+        ref.train(train)
+        net.train(train)
+        with torch.no_grad():
+            r = ref(obs)
+            o = net(obs.to(cuda))
+        for k in ('policy', 'value'):
+            torch.testing.assert_close(o[k].cpu(), r[k], rtol=1e-4, atol=1e-5, msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('graph', [False, True])
+def test_geese_learner_matches_cpu_oracle(cuda, graph):
+    """Three learner steps on the C4 layout (solo training, P = Pp = 1, A = 4): LearnerStep with
+    the HIP torus convs vs the CPU oracle learner from the same seeded GeeseNet and batch.
+
+    The conv biases sit in front of a training-mode BatchNorm, so their exact gradient is zero and
+    both learners see rounding noise there; Adam turns noise into +-lr steps, so those 13 biases are
+    compared at the scale of the step size only."""
+    from handyrl_amd.synthetic import geese_batch, geese_args
+    from handyrl_amd.trainer import LearnerStep
+    B, T = 16, 8
+    args = geese_args(T, B)
+    batch = geese_batch(B, T, cuda, seed=3)
+    cpu_batch = {k: v.cpu() for k, v in batch.items()}
+    torch.manual_seed(0)
+    ref = GeeseNet()
+    net = GeeseNet()
+    net.load_state_dict(ref.state_dict())
+    oracle = ol.CpuLearner(ref, args)
+    step = LearnerStep(net, args, cuda, graph=graph)
+    lr = 3e-8 * B * T
+    for i in range(3):
+        r = oracle.step(cpu_batch)
+        out = step.step(batch)
+        for k in ('p', 'v', 'ent', 'total'):
+            assert abs(float(out[k]) - r[k]) <= 1e-4 * max(1.0, abs(r[k])), (i, k, float(out[k]), r[k])
+        assert abs(float(out['grad_norm']) - r['grad_norm']) <= 1e-3 * max(1e-3, r['grad_norm']), i
+    got = dict(step.net.named_parameters())
+    for n, p in ref.named_parameters():
+        if n.endswith('conv.bias'):
+            assert (got[n].detach().cpu() - p.detach()).abs().max() <= 6 * lr + 1e-7, n
+        else:
+            torch.testing.assert_close(got[n].detach().cpu(), p.detach(), rtol=1e-4, atol=2e-6, msg=n)
