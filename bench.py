@@ -259,6 +259,51 @@ def secondary_geister_learner(device, B=256, T=16, steps=10, warmup=3):
                                     'B=64 T=16, 1 thread, 929 env-steps/s (build container)'}
 
 
+def secondary_geese_learner(device, B=2048, T=64, steps=3, warmup=1):
+    """BASELINE.json configs[3]: Hungry Geese GeeseNet learner, B=2048 T=64, solo training (P = Pp = 1),
+    UPGO policy / VTRACE value targets; 13 torus 3x3 convs (csrc/hrl_torus.hip) over B*T boards."""
+    from handyrl_amd.envs.hungry_geese import GeeseNet
+    from handyrl_amd.synthetic import geese_batch, geese_args
+    from oracle.learner import CpuLearner
+    args = geese_args(T, B)
+    torch.manual_seed(0)
+    net = GeeseNet().to(device)
+    batch = geese_batch(B, T, device, seed=5)
+    learner = LearnerStep(net, args, device, graph=True)
+    for _ in range(max(warmup, 1)):
+        learner.step(batch)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        learner.step(batch)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    value = B * T * steps / dt
+    del learner, batch, net
+    torch.cuda.empty_cache()
+    # the CPU oracle learner on the same layout, 1 thread, bounded sample (B=16)
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        torch.manual_seed(0)
+        cb, cpu_batch = 16, geese_batch(16, T, torch.device('cpu'), seed=5)
+        cpu = CpuLearner(GeeseNet(), geese_args(T, cb))
+        cpu.step(cpu_batch)
+        c0 = time.perf_counter()
+        cpu.step(cpu_batch)
+        cpu_rate = cb * T / (time.perf_counter() - c0)
+    finally:
+        torch.set_num_threads(threads)
+    flops = 2.0 * B * T * 77 * 32 * 9 * (32 * 12 * 3 + 17 * 2)   # fwd + dgrad + wgrad (no stem dgrad)
+    return {'config': 'Hungry Geese GeeseNet learner B=%d T=%d (BASELINE.json configs[3]; solo training, '
+                      'UPGO/VTRACE)' % (B, T),
+            'value': round(value, 1), 'unit': 'env-steps/s', 'ms_per_step': round(dt / steps * 1e3, 3),
+            'conv_tflops_per_step': round(flops / 1e12, 3),
+            'cpu_oracle': {'value': round(cpu_rate, 1), 'unit': 'env-steps/s', 'cores': 1, 'kind': 'port',
+                           'sample': 'oracle.learner.CpuLearner, GeeseNet, B=16 T=64, 1 step after 1 warm-up'},
+            'vs_cpu_oracle': round(value / cpu_rate, 1)}
+
+
 def secondary_geister_rollout(device, E=2048, reps=2):
     """BASELINE.json configs[2]: Geister device self-play, E concurrent games, recurrent GeisterNet inference."""
     from handyrl_amd.envs.geister import GeisterNet, GeisterBatch
@@ -369,6 +414,7 @@ def main():
         ro = secondary_rollout(device) if (opts.secondary and world == 1) else None
         gro = secondary_geister_rollout(device) if (opts.secondary and world == 1) else None
         gle = secondary_geister_learner(device) if (opts.secondary and world == 1) else None
+        gee = secondary_geese_learner(device) if (opts.secondary and world == 1) else None
         line = {
             'metric': 'learner env-steps/sec at B=4096 T=32 (TicTacToe net, UPGO/VTRACE)',
             'value': round(value, 1),
@@ -402,6 +448,8 @@ def main():
             line['geister_rollout'] = gro
         if gle is not None:
             line['geister_learner'] = gle
+        if gee is not None:
+            line['geese_learner'] = gee
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -267,18 +267,58 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float *__restr
     }
 }
 
+// ---- residual apply: y = relu(res + (x*alpha[c] + beta[c])) (GeeseNet block, hungry_geese.py:50-51) ----
+template <int VW>
+__global__ __launch_bounds__(kThreads) void bn_res_apply_kernel(const float *__restrict__ x,
+                                                                const float *__restrict__ res, Geo g,
+                                                                const float *__restrict__ alpha,
+                                                                const float *__restrict__ beta,
+                                                                float *__restrict__ y) {
+    Lane ln;
+    ln.init(g);
+    float al[kMaxSlots][VW], be[kMaxSlots][VW];
+#pragma unroll
+    for (int k = 0; k < kMaxSlots; ++k)
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+            const int ch = ln.col[k] >= 0 ? (ln.col[k] * VW + j) / g.HW : 0;
+            al[k][j] = alpha[ch];
+            be[k][j] = beta[ch];
+        }
+    const int64_t r0 = (int64_t)blockIdx.x * g.rows_per_block;
+    const int64_t r1 = min(g.N, r0 + g.rows_per_block);
+    const int step = (g.ncol <= kThreads) ? g.rp : 1;
+    for (int64_t r = r0 + ln.ro; r < r1; r += step) {
+#pragma unroll
+        for (int k = 0; k < kMaxSlots; ++k) {
+            if (ln.col[k] >= 0) {
+                const int64_t off = r * g.S + ln.col[k] * VW;
+                float v[VW], rv[VW];
+                load_vec<VW>(x + off, v);
+                load_vec<VW>(res + off, rv);
+#pragma unroll
+                for (int j = 0; j < VW; ++j) v[j] = relu(rv[j] + (v[j] * al[k][j] + be[k][j]));
+                store_vec<VW>(y + off, v);
+            }
+        }
+    }
+}
+
 // ---- backward reduce: per-block sum(dy) and sum(dy*(x-mean)) per channel ----
 // With RELU the forward output was relu(x*alpha + beta): the incoming gradient
 // is masked where that pre-activation is <= 0 (threshold_backward), recomputed
 // here from x with the forward's own per-channel alpha/beta.
-template <int VW, bool RELU>
+// MASK = 2: the gradient is masked where an external tensor `mo` (the forward's output after a
+// ReLU, e.g. relu(h + bn(x)) of a residual block) is <= 0.
+template <int VW, bool RELU, int MASK>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const float *__restrict__ x,
                                                                  const float *__restrict__ dy, Geo g,
                                                                  const float *__restrict__ mean,
                                                                  const float *__restrict__ invstd,
                                                                  const float *__restrict__ weight,
                                                                  const float *__restrict__ bias,
-                                                                 double *__restrict__ part) {
+                                                                 double *__restrict__ part,
+                                                                 const float *__restrict__ mo) {
     extern __shared__ double sh[];
     Lane ln;
     ln.init(g);
@@ -303,13 +343,17 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const float *__
         for (int k = 0; k < kMaxSlots; ++k) {
             if (ln.col[k] >= 0) {
                 const int64_t off = r * g.S + ln.col[k] * VW;
-                float xv[VW], gv[VW];
+                float xv[VW], gv[VW], mv[VW];
                 load_vec<VW>(x + off, xv);
                 load_vec<VW>(dy + off, gv);
+                if constexpr (MASK == 2) load_vec<VW>(mo + off, mv);
 #pragma unroll
                 for (int j = 0; j < VW; ++j) {
                     if constexpr (RELU) {
                         if (!(xv[j] * al[k][j] + be[k][j] > 0.f)) gv[j] = 0.f;
+                    }
+                    if constexpr (MASK == 2) {
+                        if (!(mv[j] > 0.f)) gv[j] = 0.f;
                     }
                     a[k][j] += (double)gv[j];
                     b[k][j] += (double)gv[j] * (double)(xv[j] - mu[k][j]);
@@ -321,7 +365,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const float *__
 }
 
 // ---- backward apply: dx = ((dy - mean(dy)) - (x-mean)*k) * invstd * w ----
-template <int VW, bool RELU>
+template <int VW, bool RELU, int MASK>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float *__restrict__ x,
                                                                 const float *__restrict__ dy, Geo g,
                                                                 const float *__restrict__ mean,
@@ -330,7 +374,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float *__r
                                                                 const float *__restrict__ kcoef,
                                                                 const float *__restrict__ gmean,
                                                                 const float *__restrict__ bias,
-                                                                float *__restrict__ dx) {
+                                                                float *__restrict__ dx,
+                                                                const float *__restrict__ mo) {
     Lane ln;
     ln.init(g);
     float mu[kMaxSlots][VW], kk[kMaxSlots][VW], gm[kMaxSlots][VW], is[kMaxSlots][VW], ww[kMaxSlots][VW];
@@ -356,13 +401,17 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float *__r
         for (int k = 0; k < kMaxSlots; ++k) {
             if (ln.col[k] >= 0) {
                 const int64_t off = r * g.S + ln.col[k] * VW;
-                float xv[VW], gv[VW];
+                float xv[VW], gv[VW], mv[VW];
                 load_vec<VW>(x + off, xv);
                 load_vec<VW>(dy + off, gv);
+                if constexpr (MASK == 2) load_vec<VW>(mo + off, mv);
 #pragma unroll
                 for (int j = 0; j < VW; ++j) {
                     if constexpr (RELU) {
                         if (!(xv[j] * al[k][j] + be[k][j] > 0.f)) gv[j] = 0.f;
+                    }
+                    if constexpr (MASK == 2) {
+                        if (!(mv[j] > 0.f)) gv[j] = 0.f;
                     }
                     const float t = (xv[j] - mu[k][j]) * kk[k][j];
                     xv[j] = (((gv[j] - gm[k][j]) - t) * is[k][j]) * ww[k][j];
@@ -421,16 +470,16 @@ void launch_apply(const Geo &g, hipStream_t s, const float *x, const float *ca, 
 template <int VW, bool RELU>
 void launch_bwd(const Geo &g, hipStream_t s, size_t lds, const float *x, const float *dy, const float *mean,
                 const float *invstd, const float *weight, const float *bias, double *part) {
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<VW, RELU>), dim3(g.nblocks), dim3(kThreads), lds, s, x, dy, g, mean,
-                       invstd, weight, bias, part);
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<VW, RELU, 0>), dim3(g.nblocks), dim3(kThreads), lds, s, x, dy, g, mean,
+                       invstd, weight, bias, part, (const float *)nullptr);
 }
 
 template <int VW, bool RELU>
 void launch_bwd_apply(const Geo &g, hipStream_t s, const float *x, const float *dy, const float *mean,
                       const float *invstd, const float *weight, const float *kcoef, const float *gmean,
                       const float *bias, float *dx) {
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<VW, RELU>), dim3(g.nblocks), dim3(kThreads), 0, s, x, dy, g, mean, invstd,
-                       weight, kcoef, gmean, bias, dx);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<VW, RELU, 0>), dim3(g.nblocks), dim3(kThreads), 0, s, x, dy, g, mean,
+                       invstd, weight, kcoef, gmean, bias, dx, (const float *)nullptr);
 }
 
 }  // namespace
@@ -565,6 +614,52 @@ int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64
                   : launch_bwd_apply<4, false>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx);
     else relu ? launch_bwd_apply<1, true>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx)
               : launch_bwd_apply<1, false>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx);
+    return launch_status();
+}
+
+int hrl_bn_apply_residual(const float *x, const float *res, int64_t N, int64_t C, int64_t HW, const float *alpha,
+                          const float *beta, float *y, void *stream) {
+    if (!res) return hrl_bn_apply(x, N, C, HW, alpha, beta, 1, y, stream);
+    if (!x || !y || !alpha || !beta) return HRL_EINVAL;
+    const bool vec = (C * HW) % 4 == 0 && aligned16(x) && aligned16(res) && aligned16(y);
+    Geo g;
+    if (!make_geo(N, C, HW, vec ? 4 : 1, g)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (vec) hipLaunchKernelGGL(bn_res_apply_kernel<4>, dim3(g.nblocks), dim3(kThreads), 0, s, x, res, g, alpha, beta, y);
+    else hipLaunchKernelGGL(bn_res_apply_kernel<1>, dim3(g.nblocks), dim3(kThreads), 0, s, x, res, g, alpha, beta, y);
+    return launch_status();
+}
+
+int hrl_bn_backward_masked(const float *x, const float *dy, const float *out, int64_t N, int64_t C, int64_t HW,
+                           const float *weight, const float *save_mean, const float *save_invstd, float *dx,
+                           float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream) {
+    if (!x || !dy || !out || !dx || !save_mean || !save_invstd || !workspace || dx == dy) return HRL_EINVAL;
+    const bool vec = (C * HW) % 4 == 0 && aligned16(x) && aligned16(dy) && aligned16(dx) && aligned16(out);
+    Geo g;
+    if (!make_geo(N, C, HW, vec ? 4 : 1, g)) return HRL_EINVAL;
+    if (workspace_bytes < ws_bytes(g)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    double *part = static_cast<double *>(workspace);
+    float *kcoef = reinterpret_cast<float *>(part + (int64_t)g.nblocks * g.C * 2);
+    float *gmean = kcoef + g.C;
+    const size_t lds = sizeof(double) * 2 * g.S;
+    const dim3 grid(g.nblocks), block(kThreads);
+    const float *nul = nullptr;
+    if (vec) hipLaunchKernelGGL((bn_bwd_reduce_kernel<4, false, 2>), grid, block, lds, s, x, dy, g, save_mean,
+                                save_invstd, weight, nul, part, out);
+    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, false, 2>), grid, block, lds, s, x, dy, g, save_mean,
+                            save_invstd, weight, nul, part, out);
+    int rc = launch_status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(g.C), dim3(kThreads), 0, s, 1, part, g.nblocks, g.C,
+                       (double)N * (double)HW, weight, (const float *)nullptr, (float *)nullptr, (float *)nullptr,
+                       0.0f, 0.0, (float *)nullptr, const_cast<float *>(save_invstd), kcoef, gmean, dweight, dbias);
+    rc = launch_status();
+    if (rc) return rc;
+    if (vec) hipLaunchKernelGGL((bn_bwd_apply_kernel<4, false, 2>), grid, block, 0, s, x, dy, g, save_mean, save_invstd,
+                                weight, kcoef, gmean, nul, dx, out);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<1, false, 2>), grid, block, 0, s, x, dy, g, save_mean, save_invstd,
+                            weight, kcoef, gmean, nul, dx, out);
     return launch_status();
 }
 

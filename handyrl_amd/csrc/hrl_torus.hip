@@ -117,9 +117,10 @@ struct Stage {
     }
 };
 
-// LDS tile [c][cell] -> one sample's output (n_elem = channels*HW floats, contiguous)
+// LDS tile [c][cell] -> one sample's output (n_elem = channels*HW floats, contiguous);
+// with `add`: out = tile + add * [mask > 0] elementwise (add, mask shaped like the output)
 __device__ __forceinline__ void store_sample(const float *tile, float *dst, int n_elem, bool vec, int HW,
-                                             float inv_hw, int lane) {
+                                             float inv_hw, int lane, const float *add, const float *mask) {
     if (vec) {
         const int nv = n_elem >> 2;
         for (int i = lane; i < nv; i += 64) {
@@ -130,12 +131,22 @@ __device__ __forceinline__ void store_sample(const float *tile, float *dst, int 
                 const int c = fdiv(e, inv_hw);
                 x4[j] = tile[c * kS + (e - c * HW)];
             }
+            if (add) {
+                const float4 a = reinterpret_cast<const float4 *>(add)[i];
+                const float4 m = reinterpret_cast<const float4 *>(mask)[i];
+                x4[0] += m.x > 0.f ? a.x : 0.f;
+                x4[1] += m.y > 0.f ? a.y : 0.f;
+                x4[2] += m.z > 0.f ? a.z : 0.f;
+                x4[3] += m.w > 0.f ? a.w : 0.f;
+            }
             reinterpret_cast<float4 *>(dst)[i] = make_float4(x4[0], x4[1], x4[2], x4[3]);
         }
     } else {
         for (int e = lane; e < n_elem; e += 64) {
             const int c = fdiv(e, inv_hw);
-            dst[e] = tile[c * kS + (e - c * HW)];
+            float v = tile[c * kS + (e - c * HW)];
+            if (add) v += mask[e] > 0.f ? add[e] : 0.f;
+            dst[e] = v;
         }
     }
 }
@@ -149,11 +160,13 @@ __device__ __forceinline__ void lds_fence() {
 // x: (N, Cin, HW); wpk: [tap][KS][2][64]; y: (N, out_c, HW), out_c <= 32 (the first out_c channels of
 // the 32 computed); part: [grid][32][2] (STATS)
 template <int KS, bool VEC, bool STATS>
-__global__ __launch_bounds__(kThreads) void torus_conv_kernel(const float *__restrict__ x, int64_t N, int Cin,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void torus_conv_kernel(const float *__restrict__ x, int64_t N, int Cin,
                                                               int H, int W, const float *__restrict__ wpk,
                                                               const float *__restrict__ bias, int out_c,
                                                               bool vec_out, float *__restrict__ y,
-                                                              double *__restrict__ part) {
+                                                              double *__restrict__ part,
+                                                              const float *__restrict__ add,
+                                                              const float *__restrict__ add_mask) {
     constexpr int kNW = kTaps * KS * 2 * 64;
     constexpr int kNLd = VEC ? (KS * 4 * kMaxCells / 4 + 63) / 64 : (KS * 4 * kMaxCells + 63) / 64;
     __shared__ float w_lds[kNW];
@@ -169,14 +182,22 @@ __global__ __launch_bounds__(kThreads) void torus_conv_kernel(const float *__res
     // channel rows Cin .. 4*KS-1 stay zero (their packed weights are zero too; no NaN * 0)
     for (int i = lane; i < kTile; i += 64) tile[i] = 0.f;
 
-    // the lane's A-fragment cells: q = mt*16 + (lane & 15); cells past the board read cell q - HW
-    int nbr[kMT][kTaps];
+    // the lane's A-fragment cells: q = mt*16 + (lane & 15); cells past the board read cell q - HW.
+    // nbr(q, tap) = row part (ky) + column part (kx): 30 registers instead of 45.
+    int nrow[kMT][3], ncol[kMT][3];
 #pragma unroll
     for (int mt = 0; mt < kMT; ++mt) {
         int q = mt * 16 + (lane & 15);
         while (q >= HW) q -= HW;
+        const int r = q / W, c = q - r * W;
 #pragma unroll
-        for (int t = 0; t < kTaps; ++t) nbr[mt][t] = torus_nbr(q, H, W, t) + (lane >> 4) * kS;
+        for (int d = 0; d < 3; ++d) {
+            int rr = r + d - 1, cc = c + d - 1;
+            rr = rr < 0 ? rr + H : (rr >= H ? rr - H : rr);
+            cc = cc < 0 ? cc + W : (cc >= W ? cc - W : cc);
+            nrow[mt][d] = rr * W + (lane >> 4) * kS;
+            ncol[mt][d] = cc;
+        }
     }
     float bias_v[2] = {0.f, 0.f};
     if (bias) {
@@ -209,7 +230,7 @@ __global__ __launch_bounds__(kThreads) void torus_conv_kernel(const float *__res
                 const float b1 = wl[((t * KS + s) * 2 + 1) * 64];
 #pragma unroll
                 for (int mt = 0; mt < kMT; ++mt) {
-                    const float a = tile[nbr[mt][t] + s * 4 * kS];
+                    const float a = tile[nrow[mt][t / 3] + ncol[mt][t % 3] + s * 4 * kS];
                     acc[mt][0] = mfma(a, b0, acc[mt][0]);
                     acc[mt][1] = mfma(a, b1, acc[mt][1]);
                 }
@@ -244,7 +265,9 @@ __global__ __launch_bounds__(kThreads) void torus_conv_kernel(const float *__res
             }
         }
         lds_fence();
-        store_sample(tile, y + n * (out_c * HW), out_c * HW, vec_out, HW, inv_hw, lane);
+        const int64_t ob = n * (out_c * HW);
+        store_sample(tile, y + ob, out_c * HW, vec_out, HW, inv_hw, lane, add ? add + ob : nullptr,
+                     add ? add_mask + ob : nullptr);
         lds_fence();
         // padding rows must read as zero again for the next sample (the output tile used them)
         for (int i = in_elem / HW * kS + lane; i < KS * 4 * kS; i += 64) tile[i] = 0.f;
@@ -451,10 +474,12 @@ int64_t hrl_torus_workspace_bytes(int64_t N) {
 int64_t hrl_torus_stats_blocks(int64_t N) { return N < 1 ? -1 : grid_for(N, kGridConv); }
 
 int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
-                           const float *weight, const float *bias, int flip, float *y, double *part, void *workspace,
-                           int64_t workspace_bytes, void *stream) {
+                           const float *weight, const float *bias, int flip, float *y, double *part,
+                           const float *add, const float *add_mask, void *workspace, int64_t workspace_bytes,
+                           void *stream) {
     if (!shape_ok(N, Cin, Cout, H, W) || !x || !weight || !y || !workspace) return HRL_EINVAL;
     if (flip && bias) return HRL_EINVAL;
+    if ((add == nullptr) != (add_mask == nullptr)) return HRL_EINVAL;
     if (workspace_bytes < hrl_torus_workspace_bytes(N)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     // the conv this launch computes: forward Cin -> 32; flip: 32 -> Cin (the forward's adjoint)
@@ -468,11 +493,11 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
     if (rc) return rc;
     const int HW = (int)(H * W);
     const bool vec = (in_c * HW) % 4 == 0 && aligned16(x);
-    const bool vec_out = (out_c * HW) % 4 == 0 && aligned16(y);
+    const bool vec_out = (out_c * HW) % 4 == 0 && aligned16(y) && (!add || (aligned16(add) && aligned16(add_mask)));
     const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
 #define HRL_TORUS_LAUNCH(KS_, VEC_, ST_)                                                                           \
     hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_>), grid, block, 0, s, x, N, in_c, (int)H, (int)W, wpk,    \
-                       bias, out_c, vec_out, y, part)
+                       bias, out_c, vec_out, y, part, add, add_mask)
     const bool st = part != nullptr;
     if (KS == 8) {
         if (vec) { if (st) HRL_TORUS_LAUNCH(8, true, true); else HRL_TORUS_LAUNCH(8, true, false); }

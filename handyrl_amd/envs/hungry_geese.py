@@ -70,9 +70,16 @@ class GeeseNet(nn.Module):
         self.head_v = nn.Linear(filters * 2, 1, bias=False)
 
     def forward(self, x, _=None):
-        h = F.relu(self.conv0(x))
-        for block in self.blocks:
-            h = F.relu(h + block(h))
+        if self.training and self.conv0.use_hip and self.conv0.bn is not None:
+            # accelerated training step: each unit is one fused HIP Function (nn.torus_block)
+            from ..nn import torus_block
+            h = torus_block(x, self.conv0, residual=False)
+            for block in self.blocks:
+                h = torus_block(h, block, residual=True)
+        else:
+            h = F.relu(self.conv0(x))
+            for block in self.blocks:
+                h = F.relu(h + block(h))
         n, c = h.size(0), h.size(1)
         h_head = (h * x[:, :1]).view(n, c, -1).sum(-1)
         h_avg = h.view(n, c, -1).mean(-1)

@@ -376,8 +376,9 @@ class _TorusConv(torch.autograd.Function):
         y = torch.empty(N, 32, H, W, device=x.device, dtype=x.dtype)
         w = weight.contiguous()
         _native.check(lib.hrl_torus_conv_forward(_native.ptr(x), N, Cin, 32, H, W, _native.ptr(w),
-                                                 _native.ptr(bias), 0, _native.ptr(y), None, _native.ptr(ws),
-                                                 ws_bytes, _native.stream_of(x.device)), 'hrl_torus_conv_forward')
+                                                 _native.ptr(bias), 0, _native.ptr(y), None, None, None,
+                                                 _native.ptr(ws), ws_bytes, _native.stream_of(x.device)),
+                      'hrl_torus_conv_forward')
         ctx.save_for_backward(x, w)
         ctx.has_bias = bias is not None
         return y
@@ -395,7 +396,8 @@ class _TorusConv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             _native.check(lib.hrl_torus_conv_forward(_native.ptr(dy), N, Cin, 32, H, W, _native.ptr(w), None, 1,
-                                                     _native.ptr(dx), None, _native.ptr(ws), ws_bytes, stream),
+                                                     _native.ptr(dx), None, None, None, _native.ptr(ws), ws_bytes,
+                                                     stream),
                           'hrl_torus_conv_forward(flip)')
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             dw = torch.empty_like(w)
@@ -410,6 +412,97 @@ class _TorusConv(torch.autograd.Function):
 
 def torus_conv2d(x, weight, bias=None):
     return _TorusConv.apply(x, weight, bias)
+
+
+class _TorusBNBlock(torch.autograd.Function):
+    """One GeeseNet unit in training mode, out = relu([h +] bn(conv_torus(h))) (hungry_geese.py:48-51):
+
+    forward : torus conv with the BatchNorm statistics in its epilogue -> finalize (running stats)
+              -> one residual apply pass;
+    backward: masked BatchNorm backward (gradient * [out > 0]) -> weight gradient -> input gradient
+              whose store also adds the residual branch's masked gradient.
+    h and out are the only activations besides the conv output y that reach HBM.
+    """
+
+    @staticmethod
+    def forward(ctx, h, weight, bias, gamma, beta, running_mean, running_var, momentum, eps, residual):
+        h = h.contiguous()
+        N, Cin, H, W = h.shape
+        HW = H * W
+        dev = h.device
+        lib = _native.load()
+        stream = _native.stream_of(dev)
+        ws_bytes = lib.hrl_torus_workspace_bytes(N)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        nparts = lib.hrl_torus_stats_blocks(N)
+        part = torch.empty(nparts * 64, dtype=torch.float64, device=dev)
+        y = torch.empty(N, 32, H, W, device=dev, dtype=h.dtype)
+        w = weight.contiguous()
+        _native.check(lib.hrl_torus_conv_forward(_native.ptr(h), N, Cin, 32, H, W, _native.ptr(w), _native.ptr(bias),
+                                                 0, _native.ptr(y), _native.ptr(part), None, None, _native.ptr(ws),
+                                                 ws_bytes, stream), 'hrl_torus_conv_forward(stats)')
+        coef = torch.empty(4, 32, device=dev, dtype=h.dtype)   # save_mean, save_invstd, alpha, beta
+        _native.check(lib.hrl_bn_finalize_stats(_native.ptr(part), nparts, 32, N * HW, _native.ptr(gamma),
+                                                _native.ptr(beta), _native.ptr(running_mean),
+                                                _native.ptr(running_var), momentum, eps, _native.ptr(coef[0]),
+                                                _native.ptr(coef[1]), _native.ptr(coef[2]), _native.ptr(coef[3]),
+                                                stream), 'hrl_bn_finalize_stats')
+        out = torch.empty_like(y)
+        _native.check(lib.hrl_bn_apply_residual(_native.ptr(y), _native.ptr(h) if residual else None, N, 32, HW,
+                                                _native.ptr(coef[2]), _native.ptr(coef[3]), _native.ptr(out), stream),
+                      'hrl_bn_apply_residual')
+        ctx.save_for_backward(h, w, gamma, y, out, coef)
+        ctx.residual = residual
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w, gamma, y, out, coef = ctx.saved_tensors
+        g = g.contiguous()
+        N, Cin, H, W = h.shape
+        HW = H * W
+        dev = h.device
+        lib = _native.load()
+        stream = _native.stream_of(dev)
+        bn_ws_bytes = lib.hrl_bn_workspace_bytes(N, 32, HW)
+        ws_bytes = max(lib.hrl_torus_workspace_bytes(N), bn_ws_bytes)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        dy = torch.empty_like(y)
+        dgamma = torch.empty(32, device=dev, dtype=y.dtype)
+        dbeta = torch.empty(32, device=dev, dtype=y.dtype)
+        _native.check(lib.hrl_bn_backward_masked(_native.ptr(y), _native.ptr(g), _native.ptr(out), N, 32, HW,
+                                                 _native.ptr(gamma), _native.ptr(coef[0]), _native.ptr(coef[1]),
+                                                 _native.ptr(dy), _native.ptr(dgamma), _native.ptr(dbeta),
+                                                 _native.ptr(ws), bn_ws_bytes, stream), 'hrl_bn_backward_masked')
+        dw = torch.empty_like(w)
+        db = torch.empty(32, device=dev, dtype=y.dtype) if ctx.has_bias else None
+        _native.check(lib.hrl_torus_conv_wgrad(_native.ptr(h), _native.ptr(dy), N, Cin, 32, H, W, _native.ptr(dw),
+                                               _native.ptr(db), _native.ptr(ws), ws_bytes, stream),
+                      'hrl_torus_conv_wgrad')
+        dh = None
+        if ctx.needs_input_grad[0]:
+            dh = torch.empty_like(h)
+            add = g if ctx.residual else None
+            _native.check(lib.hrl_torus_conv_forward(_native.ptr(dy), N, Cin, 32, H, W, _native.ptr(w), None, 1,
+                                                     _native.ptr(dh), None, _native.ptr(add),
+                                                     _native.ptr(out) if ctx.residual else None, _native.ptr(ws),
+                                                     ws_bytes, stream), 'hrl_torus_conv_forward(flip, residual)')
+        return dh, dw, db, dgamma, dbeta, None, None, None, None, None
+
+
+def torus_block(h, unit, residual):
+    """relu([h +] unit(h)) for a training-mode TorusConv2d ``unit`` (conv + BatchNorm2d) as one fused
+    HIP Function; the BatchNorm module's batch counter and running statistics advance as in its forward."""
+    bn = unit.bn
+    momentum = 0.0 if bn.momentum is None else bn.momentum
+    if bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+        if bn.momentum is None:
+            momentum = 1.0 / float(bn.num_batches_tracked.item())
+    return _TorusBNBlock.apply(h, unit.conv.weight, unit.conv.bias, bn.weight, bn.bias,
+                               bn.running_mean if bn.track_running_stats else None,
+                               bn.running_var if bn.track_running_stats else None, momentum, bn.eps, residual)
 
 
 class _BoardWeight(torch.autograd.Function):

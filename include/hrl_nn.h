@@ -80,6 +80,17 @@ int hrl_bn_backward_apply(const float *x, const float *dy, int64_t N, int64_t C,
                           const float *bias, const float *save_mean, const float *save_invstd, int relu,
                           const float *kcoef, const float *gmean, float *dx, void *stream);
 
+/* Residual blocks (GeeseNet, hungry_geese.py:50-51: h' = relu(h + bn(conv(h)))):
+ * hrl_bn_apply_residual: y = relu(res + x*alpha + beta) (res NULL: relu(x*alpha + beta));
+ * hrl_bn_backward_masked: the BatchNorm backward of such a block, the incoming gradient dy
+ * (w.r.t. y) masked where out (= y) <= 0, i.e. dx = BNbwd(dy * [out > 0]); dweight/dbias may be NULL.
+ * workspace: hrl_bn_workspace_bytes(N, C, HW). */
+int hrl_bn_apply_residual(const float *x, const float *res, int64_t N, int64_t C, int64_t HW, const float *alpha,
+                          const float *beta, float *y, void *stream);
+int hrl_bn_backward_masked(const float *x, const float *dy, const float *out, int64_t N, int64_t C, int64_t HW,
+                           const float *weight, const float *save_mean, const float *save_invstd, float *dx,
+                           float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream);
+
 /*
  * Tiny-board convolution as one dense matrix (handyrl_amd/nn.py BoardConv2d):
  * W_board[(ci*H*W + p), (co*H*W + q)] = W[co, ci, dy, dx] where input cell p
@@ -186,6 +197,9 @@ int hrl_hidden_update_backward(const float *const *dout, const float *mask, int6
  * gradient of the forward: x is then (N, 32, H, W) and y (N, Cin, H, W).  part != NULL: also the per-workgroup
  * fp64 (sum y, sum y^2) per channel, hrl_torus_stats_blocks(N) x 32 x 2
  * doubles -> hrl_bn_finalize_stats (GeeseNet's BatchNorm after every conv).
+ * add != NULL (flip = 1, the input gradient of a residual block): y += add * [add_mask > 0]
+ * elementwise in the store (the residual branch's gradient, masked by the block's ReLU);
+ * add and add_mask are shaped like y.
  * hrl_torus_conv_wgrad: dweight (32, Cin, 3, 3) and dbias (32, may be NULL)
  * for input x and output gradient dy; deterministic.
  * workspace: hrl_torus_workspace_bytes(N) bytes.
@@ -193,8 +207,9 @@ int hrl_hidden_update_backward(const float *const *dout, const float *mask, int6
 int64_t hrl_torus_workspace_bytes(int64_t N);
 int64_t hrl_torus_stats_blocks(int64_t N);
 int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
-                           const float *weight, const float *bias, int flip, float *y, double *part, void *workspace,
-                           int64_t workspace_bytes, void *stream);
+                           const float *weight, const float *bias, int flip, float *y, double *part,
+                           const float *add, const float *add_mask, void *workspace, int64_t workspace_bytes,
+                           void *stream);
 int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
                          float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream);
 

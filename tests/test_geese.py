@@ -139,3 +139,36 @@ def test_geese_learner_matches_cpu_oracle(cuda, graph):
             assert (got[n].detach().cpu() - p.detach()).abs().max() <= 6 * lr + 1e-7, n
         else:
             torch.testing.assert_close(got[n].detach().cpu(), p.detach(), rtol=1e-4, atol=2e-6, msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('residual,cin,N', [(True, 32, 41), (False, 17, 23), (True, 32, 1500)])
+def test_fused_torus_block_matches_torch(cuda, residual, cin, N):
+    """nn.torus_block (conv with BN statistics in its epilogue, residual apply, masked BN backward,
+    residual gradient added in the input-gradient store) vs the reference formulation on the CPU,
+    relu([h +] bn(conv_torus(h))): output, every gradient and the BatchNorm running statistics."""
+    from handyrl_amd.nn import torus_block
+    torch.manual_seed(cin + N)
+    ref = TorusConv2d(cin, 32, (3, 3), True)
+    with torch.no_grad():
+        ref.bn.weight.uniform_(0.5, 1.5)
+        ref.bn.bias.uniform_(-0.2, 0.2)
+    unit = TorusConv2d(cin, 32, (3, 3), True)
+    unit.load_state_dict(ref.state_dict())
+    unit = unit.to(cuda)
+    unit.use_hip = True
+    h = torch.randn(N, cin, 7, 11)
+    g = torch.randn(N, 32, 7, 11)
+    hc = h.clone().requires_grad_(True)
+    oc = F.relu(hc + ref(hc)) if residual else F.relu(ref(hc))
+    oc.backward(g)
+    hg = h.to(cuda).requires_grad_(True)
+    og = torus_block(hg, unit, residual)
+    og.backward(g.to(cuda))
+    torch.testing.assert_close(og.detach().cpu(), oc.detach(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(hg.grad.cpu(), hc.grad, rtol=1e-4, atol=1e-4)
+    tol = 2e-5 * (N * 77) ** 0.5
+    for (n, p), q in zip(ref.named_parameters(), unit.parameters()):
+        torch.testing.assert_close(q.grad.cpu(), p.grad, rtol=1e-4, atol=tol, msg=n)
+    for n in ('running_mean', 'running_var', 'num_batches_tracked'):
+        torch.testing.assert_close(getattr(unit.bn, n).cpu(), getattr(ref.bn, n), rtol=1e-5, atol=1e-6, msg=n)
