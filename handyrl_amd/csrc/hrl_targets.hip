@@ -51,11 +51,13 @@ struct Coef {
     float gl;  // (float)(gamma * lmb)
 };
 
-// torch.max(a, b) on two tensors propagates NaN (losses.py:36).
+// torch.max(a, b) on two tensors propagates NaN (losses.py:36).  Written as selects
+// (v_cndmask), not early returns: the branches the early-return form compiled to
+// (two exec-mask regions per time step) sat on the scan's serial chain.
 __device__ __forceinline__ float max_nan(float x, float y) {
-    if (x != x) return x;
-    if (y != y) return y;
-    return x > y ? x : y;
+    float m = x > y ? x : y;
+    m = (y != y) ? y : m;
+    return (x != x) ? x : m;
 }
 
 // floor(e / d) for 0 <= e < 2^20 and d >= 1, given inv = 1.0f / d: the exact
@@ -317,21 +319,20 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
     Carry s{0.f, 0.f, 0.f, 0.f, 0.f};
     const int nchunks = (T + kTChunk - 1) / kTChunk;
 
-    // One time step: the reference recurrences on the carry, outputs into the LDS tiles.
-    auto one_step = [&](int tt, int t0, float v, float r, float rho, float cc, float ret_t) {
+    // One time step: the reference recurrences on the carry; results stay in registers (no LDS
+    // traffic on the serial chain, so no lgkmcnt waits between steps).
+    auto one_step = [&](int tt, int t0, float v, float r, float rho, float cc, float ret_t, float &tgt_out,
+                        float &adv_out) {
         const bool last = (t0 + tt == T - 1);
-        const int iv = vbase + tt * C;
         float adv, adv_unused;
         Carry nx = s;
         if constexpr (TGT != kNone && TGT != ADV) {
-            const float tgt = step<TGT>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv_unused);
+            tgt_out = step<TGT>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv_unused);
             step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
-            t_tgt[iv] = tgt;
         } else {
-            const float tgt = step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
-            if constexpr (TGT != kNone) t_tgt[iv] = tgt;
+            tgt_out = step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
         }
-        t_adv[iv] = adv;
+        adv_out = adv;
         nx.v_next = v;
         s = nx;
     };
@@ -393,9 +394,18 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
                     xret[tt] = kRet ? t_ret[iv] : boot;
                 }
             }
+            float ot[kTChunk], oa[kTChunk];
 #pragma unroll
             for (int tt = kTChunk - 1; tt >= 0; --tt) {
-                if (tt < tc) one_step(tt, t0, xv[tt], xr[tt], xrho[tt], xc[tt], xret[tt]);
+                if (tt < tc) one_step(tt, t0, xv[tt], xr[tt], xrho[tt], xc[tt], xret[tt], ot[tt], oa[tt]);
+            }
+#pragma unroll
+            for (int tt = 0; tt < kTChunk; ++tt) {
+                if (tt < tc) {
+                    const int iv = vbase + tt * C;
+                    if constexpr (TGT != kNone) t_tgt[iv] = ot[tt];
+                    t_adv[iv] = oa[tt];
+                }
             }
         }
         __syncthreads();
