@@ -1,0 +1,402 @@
+// hrl_heads.hip — the TicTacToe net's two output heads as one fused pass (gfx950).
+//
+// SimpleConv2dModel (handyrl/envs/tictactoe.py:35-49, 59-60) ends with two
+// Heads on the body output h (N, 32, 3, 3):
+//   conv1x1 32 -> Cm (+bias) -> LeakyReLU(0.1) -> flatten -> Linear(9*Cm -> out, no bias)
+// with (Cm, out) = (2, 9) for the policy and (1, 1) for the value (the model
+// applies tanh).  As library GEMMs this is ~10 launches forward and backward
+// on skinny shapes ([N,288]x[288,27], [N,18]x[18,9], ...) that hipBLASLt runs
+// at a fraction of HBM bandwidth, plus the board-weight expansions and the
+// activation kernels.  Here:
+//
+// heads_fwd_kernel: one wave owns 64 rows (samples) at a time; h streams in
+//   slices of 4 channels (36 floats per row) with coalesced float4 loads into
+//   an LDS tile [row][36] (stride 37: one row per lane, conflict-free), the
+//   next slice in flight while this one is consumed; each lane accumulates
+//   its row's 27 conv outputs in registers (bias first, channels in order),
+//   applies the LeakyReLU and the two fc heads.  Writes the activations a
+//   (N x 18 policy, N x 9 value: the backward's only saved state) and the
+//   outputs (N x 9, N x 1).  151 MB read at N = 131072 (HBM-bound).
+// heads_bwd_kernel: per row, dz = (dp . Wp | dv . Wv) * leaky'(a); the input
+//   gradient dh[c, q] = sum_m W1[m, c] dz[m, q] leaves through the same LDS
+//   tile with coalesced stores while h streams in again for the conv weight
+//   gradient; the conv weight/bias gradients accumulate per lane in
+//   registers, are folded across the wave with a fixed butterfly, and per
+//   wave into partials; fc_grad_kernel forms the fc weight gradients
+//   dp^T a_p and dv^T a_v (one thread per weight, rows in a fixed order) into
+//   the same partial rows; heads_reduce_kernel folds every column with a
+//   fixed-shape tree (deterministic).  151 MB read + 151 MB written.
+// Numerics: fp32 throughout (-ffp-contract=off); sums in a fixed order; the
+// LeakyReLU and its gradient follow torch (x > 0 ? x : x * 0.1f).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hrl_nn.h"
+#include "../../include/hrl_targets.h"
+
+namespace {
+
+constexpr int kC = 32;                 // body channels
+constexpr int kHW = 9;                 // 3x3 board
+constexpr int kRow = kC * kHW;         // 288 floats per sample
+constexpr int kMP = 2, kMV = 1;        // conv channels of the policy / value head
+constexpr int kM = kMP + kMV;          // 3
+constexpr int kZ = kM * kHW;           // 27 activations per sample
+constexpr int kZP = kMP * kHW;         // 18 (policy fc inputs)
+constexpr int kOP = 9;                 // policy outputs
+constexpr int kSC = 4;                 // channels per slice
+constexpr int kNS = kC / kSC;          // 8 slices
+constexpr int kSF = kSC * kHW;         // 36 floats per row slice
+constexpr int kSV = kSF / 4;           // 9 float4 per row slice
+constexpr int kTS = kSF + 1;           // LDS row stride (odd)
+constexpr float kSlope = 0.1f;
+
+// parameter-gradient partial layout (per workgroup): dW1 [3][32] | db1 [3] | dWp [9][18] | dWv [9]
+constexpr int kGW1 = 0;
+constexpr int kGB1 = kGW1 + kM * kC;
+constexpr int kGWP = kGB1 + kM;
+constexpr int kGWV = kGWP + kOP * kZP;
+constexpr int kGN = kGWV + kHW;        // 270
+
+struct Weights {
+    const float *w1p, *w1v, *b1p, *b1v, *wp, *wv;
+};
+
+__device__ __forceinline__ void lds_fence() {
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ float w1_at(const Weights &w, int m, int c) {
+    return m < kMP ? w.w1p[m * kC + c] : w.w1v[(m - kMP) * kC + c];
+}
+
+// the 64 rows [base, base+nrows) x slice s (channels 4s..4s+3): 576 float4, 9 per lane
+__device__ __forceinline__ void load_slice(const float *__restrict__ h, int64_t base, int nrows, int s, int lane,
+                                           float4 (&st)[kSV]) {
+#pragma unroll
+    for (int k = 0; k < kSV; ++k) {
+        const int i = k * 64 + lane;
+        const int r = i / kSV, c4 = i - r * kSV;
+        const int rr = r < nrows ? r : nrows - 1;
+        st[k] = *reinterpret_cast<const float4 *>(h + (base + rr) * kRow + s * kSF + c4 * 4);
+    }
+}
+
+__device__ __forceinline__ void slice_to_lds(const float4 (&st)[kSV], float *tile, int lane) {
+#pragma unroll
+    for (int k = 0; k < kSV; ++k) {
+        const int i = k * 64 + lane;
+        const int r = i / kSV, c4 = i - r * kSV;
+        float *d = tile + r * kTS + c4 * 4;
+        d[0] = st[k].x; d[1] = st[k].y; d[2] = st[k].z; d[3] = st[k].w;
+    }
+}
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(64) void heads_fwd_kernel(const float *__restrict__ h, int64_t N, Weights w,
+                                                       float *__restrict__ a_p, float *__restrict__ a_v,
+                                                       float *__restrict__ p_out, float *__restrict__ v_out) {
+    __shared__ float tile[64 * kTS];
+    __shared__ float sw1[kM * kC], sb1[kM], swp[kOP * kZP], swv[kHW];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < kM * kC; i += 64) sw1[i] = w1_at(w, i / kC, i % kC);
+    if (lane < kM) sb1[lane] = lane < kMP ? w.b1p[lane] : w.b1v[lane - kMP];
+    for (int i = lane; i < kOP * kZP; i += 64) swp[i] = w.wp[i];
+    if (lane < kHW) swv[lane] = w.wv[lane];
+    __syncthreads();
+
+    for (int64_t base = (int64_t)blockIdx.x * 64; base < N; base += (int64_t)gridDim.x * 64) {
+        const int nrows = (int)min<int64_t>(64, N - base);
+        float z[kZ];
+#pragma unroll
+        for (int m = 0; m < kM; ++m)
+#pragma unroll
+            for (int q = 0; q < kHW; ++q) z[m * kHW + q] = sb1[m];
+        float4 st[kSV];
+        load_slice(h, base, nrows, 0, lane, st);
+#pragma unroll 1
+        for (int s = 0; s < kNS; ++s) {
+            slice_to_lds(st, tile, lane);
+            lds_fence();
+            if (s + 1 < kNS) load_slice(h, base, nrows, s + 1, lane, st);   // in flight during the FMAs
+            float x[kSF];
+#pragma unroll
+            for (int j = 0; j < kSF; ++j) x[j] = tile[lane * kTS + j];
+#pragma unroll
+            for (int m = 0; m < kM; ++m)
+#pragma unroll
+                for (int cc = 0; cc < kSC; ++cc) {
+                    const float wv1 = sw1[m * kC + s * kSC + cc];
+#pragma unroll
+                    for (int q = 0; q < kHW; ++q) z[m * kHW + q] += wv1 * x[cc * kHW + q];
+                }
+            lds_fence();   // every lane's reads done before the next slice overwrites the tile
+        }
+        float a[kZ];
+#pragma unroll
+        for (int j = 0; j < kZ; ++j) a[j] = z[j] > 0.f ? z[j] : z[j] * kSlope;
+        if (lane < nrows) {
+            const int64_t n = base + lane;
+            float p[kOP];
+#pragma unroll
+            for (int k = 0; k < kOP; ++k) {
+                float t = 0.f;
+#pragma unroll
+                for (int j = 0; j < kZP; ++j) t += swp[k * kZP + j] * a[j];
+                p[k] = t;
+            }
+            float v = 0.f;
+#pragma unroll
+            for (int q = 0; q < kHW; ++q) v += swv[q] * a[kZP + q];
+#pragma unroll
+            for (int k = 0; k < kOP; ++k) p_out[n * kOP + k] = p[k];
+            v_out[n] = v;
+            if (a_p) {
+#pragma unroll
+                for (int j = 0; j < kZP; ++j) a_p[n * kZP + j] = a[j];
+#pragma unroll
+                for (int q = 0; q < kHW; ++q) a_v[n * kHW + q] = a[kZP + q];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ backward
+__device__ __forceinline__ float wave_sum(float v) {
+    // fixed butterfly over the 64 lanes: every lane ends with the same, order-fixed total
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__ h, int64_t N, Weights w,
+                                                       const float *__restrict__ a_p, const float *__restrict__ a_v,
+                                                       const float *__restrict__ dp, const float *__restrict__ dv,
+                                                       float *__restrict__ dh, float *__restrict__ part) {
+    __shared__ float tile[64 * kTS];
+    __shared__ float sw1[kM * kC], swp[kOP * kZP], swv[kHW];
+    __shared__ float gw1[kM * kC * 64];   // per-lane conv weight-gradient accumulators [m*32 + c][lane]
+    const int lane = threadIdx.x;
+    for (int i = lane; i < kM * kC; i += 64) sw1[i] = w1_at(w, i / kC, i % kC);
+    for (int i = lane; i < kOP * kZP; i += 64) swp[i] = w.wp[i];
+    if (lane < kHW) swv[lane] = w.wv[lane];
+    for (int i = lane; i < kM * kC * 64; i += 64) gw1[i] = 0.f;
+    __syncthreads();
+
+    float gb1[kM];
+#pragma unroll
+    for (int i = 0; i < kM; ++i) gb1[i] = 0.f;
+
+    for (int64_t base = (int64_t)blockIdx.x * 64; base < N; base += (int64_t)gridDim.x * 64) {
+        const int nrows = (int)min<int64_t>(64, N - base);
+        const bool valid = lane < nrows;
+        const int64_t n = base + (valid ? lane : 0);
+        float4 st[kSV];
+        load_slice(h, base, nrows, 0, lane, st);   // in flight while dz is formed
+        float a[kZ], g[kOP], gv;
+#pragma unroll
+        for (int j = 0; j < kZP; ++j) a[j] = a_p[n * kZP + j];
+#pragma unroll
+        for (int q = 0; q < kHW; ++q) a[kZP + q] = a_v[n * kHW + q];
+#pragma unroll
+        for (int k = 0; k < kOP; ++k) g[k] = valid ? dp[n * kOP + k] : 0.f;
+        gv = valid ? dv[n] : 0.f;
+        // the activation gradient (the fc weight gradients are dp^T a_p, dv^T a_v: host side)
+        float dz[kZ];
+#pragma unroll
+        for (int j = 0; j < kZP; ++j) {
+            float t = 0.f;
+#pragma unroll
+            for (int k = 0; k < kOP; ++k) t += g[k] * swp[k * kZP + j];
+            dz[j] = a[j] > 0.f ? t : t * kSlope;
+        }
+#pragma unroll
+        for (int q = 0; q < kHW; ++q) {
+            const float t = gv * swv[q];
+            dz[kZP + q] = a[kZP + q] > 0.f ? t : t * kSlope;
+        }
+#pragma unroll
+        for (int m = 0; m < kM; ++m) {
+            float t = 0.f;
+#pragma unroll
+            for (int q = 0; q < kHW; ++q) t += dz[m * kHW + q];
+            gb1[m] += t;
+        }
+#pragma unroll 1
+        for (int s = 0; s < kNS; ++s) {
+            slice_to_lds(st, tile, lane);
+            lds_fence();
+            if (s + 1 < kNS) load_slice(h, base, nrows, s + 1, lane, st);
+            float x[kSF];
+#pragma unroll
+            for (int j = 0; j < kSF; ++j) x[j] = tile[lane * kTS + j];
+            // conv weight gradient: dW1[m, c] += sum_q dz[m, q] * h[c, q]
+#pragma unroll
+            for (int m = 0; m < kM; ++m)
+#pragma unroll
+                for (int cc = 0; cc < kSC; ++cc) {
+                    float t = 0.f;
+#pragma unroll
+                    for (int q = 0; q < kHW; ++q) t += dz[m * kHW + q] * x[cc * kHW + q];
+                    gw1[(m * kC + s * kSC + cc) * 64 + lane] += t;   // this lane's own slot
+                }
+            // input gradient of this slice: dh[c, q] = sum_m W1[m, c] * dz[m, q] -> the lane's LDS row
+            lds_fence();
+#pragma unroll
+            for (int cc = 0; cc < kSC; ++cc)
+#pragma unroll
+                for (int q = 0; q < kHW; ++q) {
+                    float t = 0.f;
+#pragma unroll
+                    for (int m = 0; m < kM; ++m) t += sw1[m * kC + s * kSC + cc] * dz[m * kHW + q];
+                    tile[lane * kTS + cc * kHW + q] = t;
+                }
+            lds_fence();
+            // coalesced float4 stores of the 64 x 36 slice
+#pragma unroll
+            for (int k = 0; k < kSV; ++k) {
+                const int i = k * 64 + lane;
+                const int r = i / kSV, c4 = i - r * kSV;
+                if (r < nrows) {
+                    const float *sp = tile + r * kTS + c4 * 4;
+                    *reinterpret_cast<float4 *>(dh + (base + r) * kRow + s * kSF + c4 * 4) =
+                        make_float4(sp[0], sp[1], sp[2], sp[3]);
+                }
+            }
+            lds_fence();
+        }
+    }
+    // fold the lanes in a fixed order, one partial row per wave
+    float *out = part + (int64_t)blockIdx.x * kGN;
+    lds_fence();
+    for (int i = lane; i < kM * kC; i += 64) {
+        float t = 0.f;
+        for (int l = 0; l < 64; ++l) t += gw1[i * 64 + l];
+        out[kGW1 + i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < kM; ++i) {
+        const float t = wave_sum(gb1[i]);
+        if (lane == 0) out[kGB1 + i] = t;
+    }
+}
+
+// fc weight gradients: dWp[k][j] = sum_n dp[n,k] a_p[n,j], dWv[q] = sum_n dv[n] a_v[n,q]; workgroup b sums
+// its row range (rows in order) into partial row b, columns kGWP.. (one thread per weight)
+__global__ __launch_bounds__(256) void fc_grad_kernel(const float *__restrict__ a_p, const float *__restrict__ a_v,
+                                                      const float *__restrict__ dp, const float *__restrict__ dv,
+                                                      int64_t N, int64_t rows_per_block, float *__restrict__ part) {
+    const int t = threadIdx.x;
+    if (t >= kOP * kZP + kHW) return;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(N, r0 + rows_per_block);
+    const bool pol = t < kOP * kZP;
+    const int k = pol ? t / kZP : 0, j = pol ? t % kZP : t - kOP * kZP;
+    // rows in order into one accumulator; the loads of 8 rows are issued ahead of their FMAs
+    float acc = 0.f;
+    int64_t n = r0;
+    for (; n + 8 <= r1; n += 8) {
+        float x[8], y[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            x[u] = pol ? dp[(n + u) * kOP + k] : dv[n + u];
+            y[u] = pol ? a_p[(n + u) * kZP + j] : a_v[(n + u) * kHW + j];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += x[u] * y[u];
+    }
+    for (; n < r1; ++n) acc += pol ? dp[n * kOP + k] * a_p[n * kZP + j] : dv[n] * a_v[n * kHW + j];
+    part[(int64_t)blockIdx.x * kGN + kGWP + t] = acc;
+}
+
+// fixed-order fold of the per-workgroup partials: one workgroup per column, a strided fp64 sum per
+// thread, then a fixed-shape LDS tree (deterministic)
+__global__ __launch_bounds__(256) void heads_reduce_kernel(const float *__restrict__ part, int nparts,
+                                                           float *__restrict__ dw1p, float *__restrict__ dw1v,
+                                                           float *__restrict__ db1p, float *__restrict__ db1v,
+                                                           float *__restrict__ dwp, float *__restrict__ dwv) {
+    __shared__ double red[256];
+    const int i = blockIdx.x;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < nparts; b += 256) s += (double)part[(int64_t)b * kGN + i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    const float v = (float)red[0];
+    if (i < kGB1) {
+        const int m = i / kC, c = i % kC;
+        if (m < kMP) dw1p[m * kC + c] = v;
+        else dw1v[(m - kMP) * kC + c] = v;
+    } else if (i < kGWP) {
+        const int m = i - kGB1;
+        if (m < kMP) db1p[m] = v;
+        else db1v[m - kMP] = v;
+    } else if (i < kGWV) {
+        dwp[i - kGWP] = v;
+    } else {
+        dwv[i - kGWV] = v;
+    }
+}
+
+constexpr int kGrid = 1024;
+
+int status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
+}
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int grid_for(int64_t N) {
+    const int64_t blocks = (N + 63) / 64;
+    return (int)(blocks < kGrid ? blocks : kGrid);
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t hrl_heads_workspace_bytes(int64_t N) { return N < 1 ? -1 : (int64_t)grid_for(N) * kGN * 4; }
+
+int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *b1p, const float *w1v,
+                      const float *b1v, const float *wp, const float *wv, float *a_p, float *a_v, float *p_out,
+                      float *v_out, void *stream) {
+    if (N < 1 || !h || !w1p || !b1p || !w1v || !b1v || !wp || !wv || !p_out || !v_out) return HRL_EINVAL;
+    if ((a_p == nullptr) != (a_v == nullptr) || !aligned16(h)) return HRL_EINVAL;
+    const Weights w{w1p, w1v, b1p, b1v, wp, wv};
+    hipLaunchKernelGGL(heads_fwd_kernel, dim3(grid_for(N)), dim3(64), 0, static_cast<hipStream_t>(stream), h, N, w,
+                       a_p, a_v, p_out, v_out);
+    return status();
+}
+
+int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float *w1v, const float *wp,
+                       const float *wv, const float *a_p, const float *a_v, const float *dp, const float *dv,
+                       float *dh, float *dw1p, float *db1p, float *dw1v, float *db1v, float *dwp, float *dwv,
+                       void *workspace, int64_t workspace_bytes, void *stream) {
+    if (N < 1 || !h || !w1p || !w1v || !wp || !wv || !a_p || !a_v || !dp || !dv || !dh || !workspace)
+        return HRL_EINVAL;
+    if (!dw1p || !db1p || !dw1v || !db1v || !dwp || !dwv) return HRL_EINVAL;
+    if (!aligned16(h) || !aligned16(dh) || workspace_bytes < hrl_heads_workspace_bytes(N)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const Weights w{w1p, w1v, nullptr, nullptr, wp, wv};
+    const int grid = grid_for(N);
+    float *part = static_cast<float *>(workspace);
+    hipLaunchKernelGGL(heads_bwd_kernel, dim3(grid), dim3(64), 0, s, h, N, w, a_p, a_v, dp, dv, dh, part);
+    int rc = status();
+    if (rc) return rc;
+    const int64_t rows = (N + grid - 1) / grid;
+    hipLaunchKernelGGL(fc_grad_kernel, dim3(grid), dim3(256), 0, s, a_p, a_v, dp, dv, N, rows, part);
+    rc = status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(heads_reduce_kernel, dim3(kGN), dim3(256), 0, s, part, grid, dw1p, dw1v, db1p, db1v, dwp,
+                       dwv);
+    return status();
+}
+
+}  // extern "C"

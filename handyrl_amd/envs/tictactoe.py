@@ -34,6 +34,8 @@ class ConvUnit(nn.Module):
 class BoardHead(nn.Module):
     """1x1 conv -> LeakyReLU(0.1) -> flatten -> bias-free linear."""
 
+    LEAKY_SLOPE = 0.1   # nn.fuse_bn_relu fuses the policy/value pair into csrc/hrl_heads.hip
+
     def __init__(self, cin, hw, cmid, nout):
         super().__init__()
         self.flat = hw * cmid

@@ -505,6 +505,138 @@ def torus_block(h, unit, residual):
                                bn.running_var if bn.track_running_stats else None, momentum, bn.eps, residual)
 
 
+def _board_head_spec(m):
+    """(conv, fc) of a TicTacToe-style Head (tictactoe.py:35-49): 1x1 conv with bias and no BatchNorm ->
+    LeakyReLU(0.1) -> flatten -> bias-free Linear; None for anything else.  Matches the reference's Head
+    (``activation = nn.LeakyReLU(0.1)``) and envs.tictactoe.BoardHead (``LEAKY_SLOPE``)."""
+    unit, fc = getattr(m, 'conv', None), getattr(m, 'fc', None)
+    conv = getattr(unit, 'conv', None)
+    if not isinstance(fc, nn.Linear) or fc.bias is not None or not isinstance(conv, nn.Conv2d):
+        return None
+    if getattr(unit, 'bn', 0) is not None or conv.bias is None or conv.kernel_size != (1, 1) or \
+            conv.stride != (1, 1) or conv.groups != 1 or conv.padding_mode != 'zeros':
+        return None
+    act = getattr(m, 'activation', None)
+    slope = act.negative_slope if isinstance(act, nn.LeakyReLU) else getattr(m, 'LEAKY_SLOPE', None)
+    return (conv, fc) if slope == 0.1 else None
+
+
+def _head_pair(model):
+    """The (policy, value) heads csrc/hrl_heads.hip fuses: 32->2 conv + Linear(18, 9) and 32->1 conv +
+    Linear(9, 1) on a 3x3 board (SimpleConv2dModel, tictactoe.py:59-60), or None."""
+    pol = val = None
+    for m in model.modules():
+        spec = _board_head_spec(m)
+        if spec is None:
+            continue
+        conv, fc = spec
+        shape = (conv.in_channels, conv.out_channels, fc.in_features, fc.out_features)
+        if shape == (32, 2, 18, 9):
+            pol = m if pol is None else False
+        elif shape == (32, 1, 9, 1):
+            val = m if val is None else False
+    return (pol, val) if pol and val else None
+
+
+class _BoardHeadsFn(torch.autograd.Function):
+    """Both heads of SimpleConv2dModel as csrc/hrl_heads.hip (one streaming pass over h each way)."""
+
+    @staticmethod
+    def forward(ctx, h, w1p, b1p, w1v, b1v, wp, wv):
+        h = h.contiguous()
+        N = h.shape[0]
+        dev = h.device
+        lib = _native.load()
+        a_p = torch.empty(N, 18, device=dev, dtype=h.dtype)
+        a_v = torch.empty(N, 9, device=dev, dtype=h.dtype)
+        p = torch.empty(N, 9, device=dev, dtype=h.dtype)
+        v = torch.empty(N, 1, device=dev, dtype=h.dtype)
+        P = _native.ptr
+        w1p, w1v, wp, wv = w1p.contiguous(), w1v.contiguous(), wp.contiguous(), wv.contiguous()
+        _native.check(lib.hrl_heads_forward(P(h), N, P(w1p), P(b1p.contiguous()), P(w1v), P(b1v.contiguous()),
+                                            P(wp), P(wv), P(a_p), P(a_v), P(p), P(v), _native.stream_of(dev)),
+                      'hrl_heads_forward')
+        ctx.save_for_backward(h, w1p, w1v, wp, wv, a_p, a_v)
+        return p, v
+
+    @staticmethod
+    def backward(ctx, dp, dv):
+        h, w1p, w1v, wp, wv, a_p, a_v = ctx.saved_tensors
+        N = h.shape[0]
+        dev = h.device
+        lib = _native.load()
+        dp, dv = dp.contiguous(), dv.contiguous()
+        dh = torch.empty_like(h)
+        dw1p, dw1v = torch.empty_like(w1p), torch.empty_like(w1v)
+        db1p = torch.empty(2, device=dev, dtype=h.dtype)
+        db1v = torch.empty(1, device=dev, dtype=h.dtype)
+        ws_bytes = lib.hrl_heads_workspace_bytes(N)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        P = _native.ptr
+        dwp, dwv = torch.empty_like(wp), torch.empty_like(wv)
+        _native.check(lib.hrl_heads_backward(P(h), N, P(w1p), P(w1v), P(wp), P(wv), P(a_p), P(a_v), P(dp), P(dv),
+                                             P(dh), P(dw1p), P(db1p), P(dw1v), P(db1v), P(dwp), P(dwv), P(ws),
+                                             ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward')
+        return dh, dw1p, db1p, dw1v, db1v, dwp, dwv
+
+
+class _FusedHeads(nn.Module):
+    """The policy and value heads reading the same body output, as one _BoardHeadsFn (fuse_bn_relu's
+    rewrite).  The heads are referenced, not registered; other inputs run the heads one by one."""
+
+    def __init__(self, head_p, head_v):
+        super().__init__()
+        object.__setattr__(self, 'head_p', head_p)
+        object.__setattr__(self, 'head_v', head_v)
+
+    def forward(self, x):
+        if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and tuple(x.shape[1:]) == (32, 3, 3)
+                and x.shape[0] > 0):
+            return self.head_p(x), self.head_v(x)
+        (cp, fp), (cv, fv) = _board_head_spec(self.head_p), _board_head_spec(self.head_v)
+        params = (cp.weight, cp.bias, cv.weight, cv.bias, fp.weight, fv.weight)
+        if torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in params)):
+            return _BoardHeadsFn.apply(x, *params)
+        # inference (self-play, evaluation): outputs only, no saved activations
+        x = x.contiguous()
+        N = x.shape[0]
+        p = torch.empty(N, 9, device=x.device, dtype=x.dtype)
+        v = torch.empty(N, 1, device=x.device, dtype=x.dtype)
+        P = _native.ptr
+        _native.check(_native.load().hrl_heads_forward(P(x), N, P(cp.weight.contiguous()), P(cp.bias.contiguous()),
+                                                       P(cv.weight.contiguous()), P(cv.bias.contiguous()),
+                                                       P(fp.weight.contiguous()), P(fv.weight.contiguous()), None,
+                                                       None, P(p), P(v), _native.stream_of(x.device)),
+                      'hrl_heads_forward')
+        return p, v
+
+
+def _fuse_heads(gm, heads):
+    """Replace the two head calls on one activation with one _FusedHeads call; returns 0 or 1."""
+    head_p, head_v = heads
+    calls = {}
+    for node in gm.graph.nodes:
+        if node.op == 'call_module':
+            m = gm.get_submodule(node.target)
+            if m is head_p or m is head_v:
+                calls.setdefault('p' if m is head_p else 'v', []).append(node)
+    if len(calls.get('p', [])) != 1 or len(calls.get('v', [])) != 1:
+        return 0
+    np_, nv_ = calls['p'][0], calls['v'][0]
+    if np_.args != nv_.args or len(np_.args) != 1 or np_.kwargs or nv_.kwargs:
+        return 0
+    gm.add_submodule('_hrl_heads', _FusedHeads(head_p, head_v))
+    first = np_ if list(gm.graph.nodes).index(np_) < list(gm.graph.nodes).index(nv_) else nv_
+    with gm.graph.inserting_before(first):
+        call = gm.graph.call_module('_hrl_heads', np_.args)
+        outs = [gm.graph.call_function(operator.getitem, (call, i)) for i in range(2)]
+    np_.replace_all_uses_with(outs[0])
+    nv_.replace_all_uses_with(outs[1])
+    gm.graph.erase_node(np_)
+    gm.graph.erase_node(nv_)
+    return 1
+
+
 class _BoardWeight(torch.autograd.Function):
     """W -> W_board (csrc/hrl_board.hip); backward folds dW_board onto W (deterministic)."""
 
@@ -962,11 +1094,15 @@ class _ConvBNChain(nn.Module):
 
 
 class _LeafTracer(torch.fx.Tracer):
-    """Trace the env net, keeping the HIP-backed modules as opaque calls."""
+    """Trace the env net, keeping the HIP-backed modules (and ``leaves``) as opaque calls."""
+
+    def __init__(self, leaves=()):
+        super().__init__()
+        self.extra = set(id(m) for m in leaves)
 
     def is_leaf_module(self, m, qualname):
         return isinstance(m, (BatchNorm2d, BoardConv2d, Linear, _MultiBoardConv, _ConvBNChain)) or \
-            super().is_leaf_module(m, qualname)
+            id(m) in self.extra or super().is_leaf_module(m, qualname)
 
 
 def _is_relu(gm, node):
@@ -993,7 +1129,8 @@ def fuse_bn_relu(model, example=None):
     if hasattr(model, 'init_hidden') or 'forward' in model.__dict__:
         return 0
     try:
-        graph = _LeafTracer().trace(model)
+        heads = _head_pair(model)
+        graph = _LeafTracer(leaves=heads or ()).trace(model)
     except Exception:
         return 0
     gm = torch.fx.GraphModule(model, graph)
@@ -1026,7 +1163,8 @@ def fuse_bn_relu(model, example=None):
             gm.graph.erase_node(u)
             anchor = item
         merged += 1
-    if not pairs and not merged:
+    fused_heads = _fuse_heads(gm, heads) if heads else 0
+    if not pairs and not merged and not fused_heads:
         return 0
     gm.graph.lint()
     gm.recompile()
@@ -1039,7 +1177,7 @@ def fuse_bn_relu(model, example=None):
                 bn.fused_relu = True
             new = gm(example, None)
         model.train(was)
-        same = _same_outputs(ref, new)
+        same = _same_outputs(ref, new, rtol=1e-4, atol=1e-5)
         if same and chains and example.is_cuda:
             same = _same_training_outputs(model, gm, bns, example)
         if not same:
@@ -1049,7 +1187,7 @@ def fuse_bn_relu(model, example=None):
     for bn in bns:
         bn.fused_relu = True
     model.forward = gm.forward
-    return len(pairs) + merged + chains
+    return len(pairs) + merged + chains + fused_heads
 
 
 def _same_outputs(ref, new, rtol=1e-5, atol=1e-6):

@@ -213,6 +213,25 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
 int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
                          float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream);
 
+/*
+ * The TicTacToe net's two output heads fused (handyrl/envs/tictactoe.py:35-49, 59-60;
+ * csrc/hrl_heads.hip): on h (N, 32, 3, 3),
+ *   a_p = leaky_relu(conv1x1(h; w1p (2, 32), b1p (2)), 0.1)  (N, 18);  p = a_p @ wp^T, wp (9, 18)
+ *   a_v = leaky_relu(conv1x1(h; w1v (1, 32), b1v (1)), 0.1)  (N, 9);   v = a_v @ wv^T, wv (1, 9)
+ * hrl_heads_forward writes p (N, 9), v (N, 1) (the value before the model's tanh) and,
+ * when a_p / a_v are non-NULL, the activations the backward needs.
+ * hrl_heads_backward: from dp (N, 9), dv (N, 1): dh (N, 288) and every parameter gradient
+ * (deterministic).  workspace: hrl_heads_workspace_bytes(N) bytes.
+ */
+int64_t hrl_heads_workspace_bytes(int64_t N);
+int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *b1p, const float *w1v,
+                      const float *b1v, const float *wp, const float *wv, float *a_p, float *a_v, float *p_out,
+                      float *v_out, void *stream);
+int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float *w1v, const float *wp,
+                       const float *wv, const float *a_p, const float *a_v, const float *dp, const float *dv,
+                       float *dh, float *dw1p, float *db1p, float *dw1v, float *db1v, float *dwp, float *dwv,
+                       void *workspace, int64_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

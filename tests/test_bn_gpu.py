@@ -186,8 +186,9 @@ def test_fx_fusion_in_learner(cuda):
     keys = list(net.state_dict())
     step = LearnerStep(net, default_args(9, 64), cuda)
     step.step(tictactoe_batch(64, 9, cuda, seed=0))
-    assert step.fused_pairs == 5   # three BN->ReLU folds + the two head convs merged + one conv-BN chain
+    assert step.fused_pairs == 5   # three BN->ReLU folds + one conv-BN chain + the two heads as one kernel
     assert all(m.fused_relu for m in net.modules() if isinstance(m, BatchNorm2d))
+    assert hasattr(step.net, '_hrl_heads') if hasattr(step.net, 'graph') else True
     assert list(net.state_dict()) == keys
 
 
@@ -294,3 +295,36 @@ def test_bn_eval_matches_torch(cuda, shape, relu):
         if relu:
             ref = torch.relu(ref)
     torch.testing.assert_close(y, ref, rtol=2e-6, atol=2e-6)
+
+
+@pytest.mark.parametrize('N', [1, 63, 64, 65, 4099])
+def test_fused_heads_match_torch_cpu(cuda, N):
+    """csrc/hrl_heads.hip (both TicTacToe heads in one pass, tictactoe.py:35-49) vs the heads on the
+    CPU: policy/value outputs, the body-output gradient and every head parameter's gradient, on
+    ragged row counts; the inference path (no autograd) gives the same outputs."""
+    import copy
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.nn import _FusedHeads
+    torch.manual_seed(N)
+    net = SimpleConv2dModel()
+    ref_p, ref_v = net.head_p, net.head_v
+    gp, gv = copy.deepcopy(ref_p).to(cuda), copy.deepcopy(ref_v).to(cuda)
+    fused = _FusedHeads(gp, gv)
+    h = torch.randn(N, 32, 3, 3)
+    dp, dv = torch.randn(N, 9), torch.randn(N, 1)
+    hc = h.clone().requires_grad_(True)
+    (ref_p(hc) * dp).sum().backward()
+    (ref_v(hc) * dv).sum().backward()
+    hg = h.to(cuda).requires_grad_(True)
+    p, v = fused(hg)
+    torch.autograd.backward([p, v], [dp.to(cuda), dv.to(cuda)])
+    np.testing.assert_allclose(p.detach().cpu().numpy(), ref_p(h).detach().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(v.detach().cpu().numpy(), ref_v(h).detach().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(hg.grad.cpu().numpy(), hc.grad.numpy(), rtol=1e-5, atol=1e-5)
+    tol = 2e-5 * max(1.0, (N * 9) ** 0.5)
+    for (n, a), b in zip(list(ref_p.named_parameters()) + list(ref_v.named_parameters()),
+                         list(gp.parameters()) + list(gv.parameters())):
+        np.testing.assert_allclose(b.grad.cpu().numpy(), a.grad.numpy(), rtol=1e-4, atol=tol, err_msg=n)
+    with torch.no_grad():
+        p2, v2 = fused(h.to(cuda))
+    assert torch.equal(p2, p.detach()) and torch.equal(v2, v.detach())
