@@ -58,6 +58,7 @@ class FlatGrads:
         numel = sum(p.numel() for p in self.params)
         dev = self.params[0].device
         self.flat = torch.zeros(numel, dtype=torch.float32, device=dev)
+        self._total = None
         self.slices = []
         off = 0
         for p in self.params:
@@ -73,7 +74,17 @@ class FlatGrads:
         return torch.linalg.vector_norm(self.flat, 2)
 
     def clip_(self, max_norm):
-        """clip_grad_norm_(params, max_norm) on the flat buffer, without a host sync (train.py:384)."""
+        """clip_grad_norm_(params, max_norm) on the flat buffer, without a host sync (train.py:384);
+        on the GPU one csrc/hrl_optim.hip launch instead of six torch ops."""
+        if self.flat.is_cuda:
+            from . import _native
+            if self._total is None:
+                self._total = torch.empty((), dtype=torch.float32, device=self.flat.device)
+            _native.check(_native.load().hrl_clip_grad_norm(_native.ptr(self.flat), self.flat.numel(),
+                                                            float(max_norm), _native.ptr(self._total),
+                                                            _native.stream_of(self.flat.device)),
+                          'hrl_clip_grad_norm')
+            return self._total
         total = self.norm()
         coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
         self.flat.mul_(coef)

@@ -118,6 +118,47 @@ class deferred_weight_grads:
         return False
 
 
+_DIRECT = None
+
+
+class direct_grads:
+    """Context manager (LearnerStep, feed-forward steps): the HIP Functions write a parameter's
+    gradient straight into ``p.grad`` -- a view of the learner's flat gradient buffer, zeroed at the
+    start of the step -- instead of returning it to autograd, whose AccumulateGrad would launch one
+    add kernel per parameter.  Only the first gradient of a parameter in the step is written that
+    way; any further use of the same parameter returns its gradient as usual, so sums stay right."""
+
+    def __enter__(self):
+        global _DIRECT
+        self.prev = _DIRECT
+        _DIRECT = set()
+        return self
+
+    def __exit__(self, *exc):
+        global _DIRECT
+        _DIRECT = self.prev
+        return False
+
+
+def _grad_buffer(p):
+    """(buffer, direct) for p's gradient: p.grad itself when it may be written in place (see
+    direct_grads), else a fresh tensor to return to autograd."""
+    if p is None:
+        return None, False
+    g = p.grad
+    if (_DIRECT is not None and p.requires_grad and g is not None and id(p) not in _DIRECT
+            and g.is_contiguous() and g.dtype == p.dtype and g.shape == p.shape):
+        _DIRECT.add(id(p))
+        return g, True
+    return torch.empty_like(p), False
+
+
+def _ret(buf_direct):
+    """What backward returns for a gradient from _grad_buffer: None when it was written in place."""
+    buf, direct = buf_direct
+    return None if direct else buf
+
+
 class _DeferredConv(torch.autograd.Function):
     """conv2d (stride 1, 'same') whose weight/bias gradient is deferred to DeferredGrads.flush().
 
@@ -557,6 +598,7 @@ class _BoardHeadsFn(torch.autograd.Function):
                                             P(wp), P(wv), P(a_p), P(a_v), P(p), P(v), _native.stream_of(dev)),
                       'hrl_heads_forward')
         ctx.save_for_backward(h, w1p, w1v, wp, wv, a_p, a_v)
+        ctx.biases = (b1p, b1v)
         return p, v
 
     @staticmethod
@@ -567,17 +609,16 @@ class _BoardHeadsFn(torch.autograd.Function):
         lib = _native.load()
         dp, dv = dp.contiguous(), dv.contiguous()
         dh = torch.empty_like(h)
-        dw1p, dw1v = torch.empty_like(w1p), torch.empty_like(w1v)
-        db1p = torch.empty(2, device=dev, dtype=h.dtype)
-        db1v = torch.empty(1, device=dev, dtype=h.dtype)
+        b1p, b1v = ctx.biases
+        bufs = [_grad_buffer(t) for t in (w1p, b1p, w1v, b1v, wp, wv)]
         ws_bytes = lib.hrl_heads_workspace_bytes(N)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         P = _native.ptr
-        dwp, dwv = torch.empty_like(wp), torch.empty_like(wv)
+        dw1p, db1p, dw1v, db1v, dwp, dwv = (b[0] for b in bufs)
         _native.check(lib.hrl_heads_backward(P(h), N, P(w1p), P(w1v), P(wp), P(wv), P(a_p), P(a_v), P(dp), P(dv),
                                              P(dh), P(dw1p), P(db1p), P(dw1v), P(db1v), P(dwp), P(dwv), P(ws),
                                              ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward')
-        return dh, dw1p, db1p, dw1v, db1v, dwp, dwv
+        return (dh, *(_ret(b) for b in bufs))
 
 
 class _FusedHeads(nn.Module):
@@ -648,16 +689,17 @@ class _BoardWeight(torch.autograd.Function):
         _native.check(_native.load().hrl_board_weight(_native.ptr(w), Cout, Cin, kh, kw, H, W, _native.ptr(out),
                                                        _native.stream_of(w.device)), 'hrl_board_weight')
         ctx.geom = (Cout, Cin, kh, kw, H, W)
+        ctx.weight = weight
         return out
 
     @staticmethod
     def backward(ctx, grad):
         Cout, Cin, kh, kw, H, W = ctx.geom
         g = grad.contiguous()
-        out = torch.empty(Cout, Cin, kh, kw, dtype=g.dtype, device=g.device)
-        _native.check(_native.load().hrl_board_fold(_native.ptr(g), Cout, Cin, kh, kw, H, W, _native.ptr(out),
+        buf = _grad_buffer(ctx.weight)
+        _native.check(_native.load().hrl_board_fold(_native.ptr(g), Cout, Cin, kh, kw, H, W, _native.ptr(buf[0]),
                                                      _native.stream_of(g.device)), 'hrl_board_fold')
-        return out, None, None
+        return _ret(buf), None, None
 
 
 class _BoardBias(torch.autograd.Function):
@@ -669,16 +711,17 @@ class _BoardBias(torch.autograd.Function):
         _native.check(_native.load().hrl_board_bias(_native.ptr(bias.contiguous()), bias.shape[0], HW,
                                                      _native.ptr(out), _native.stream_of(bias.device)), 'hrl_board_bias')
         ctx.shape = (bias.shape[0], HW)
+        ctx.bias = bias
         return out
 
     @staticmethod
     def backward(ctx, grad):
         Cout, HW = ctx.shape
         g = grad.contiguous()
-        out = torch.empty(Cout, dtype=g.dtype, device=g.device)
-        _native.check(_native.load().hrl_board_bias_fold(_native.ptr(g), Cout, HW, _native.ptr(out),
+        buf = _grad_buffer(ctx.bias)
+        _native.check(_native.load().hrl_board_bias_fold(_native.ptr(g), Cout, HW, _native.ptr(buf[0]),
                                                           _native.stream_of(g.device)), 'hrl_board_bias_fold')
-        return out, None
+        return _ret(buf), None
 
 
 class _LSTMGates(torch.autograd.Function):
@@ -1013,8 +1056,8 @@ class _BoardChain(torch.autograd.Function):
             w, gamma, beta = params[3 * i:3 * i + 3]
             mean, invstd = coefs[i][0], coefs[i][1]
             dy = torch.empty_like(h0)
-            dgam = torch.empty(32, dtype=torch.float32, device=dev)
-            dbet = torch.empty(32, dtype=torch.float32, device=dev)
+            bw, bgam, bbet = _grad_buffer(w), _grad_buffer(gamma), _grad_buffer(beta)
+            dgam, dbet = bgam[0], bbet[0]
             if have_sums:
                 kg = torch.empty(2, 32, dtype=torch.float32, device=dev)
                 _native.check(lib.hrl_bn_finalize_backward(P(part), nblk, 32, M * 9, P(gamma), P(invstd), P(dgam),
@@ -1031,10 +1074,10 @@ class _BoardChain(torch.autograd.Function):
                 x, a, b = h0, (unit[0] if unit is not None else None), (unit[1] if unit is not None else None)
             else:
                 x, a, b = ys[i - 1], coefs[i - 1][2], coefs[i - 1][3]
-            dw = torch.empty_like(w)
+            dw = bw[0]
             _native.check(lib.hrl_conv3x3_wgrad_ex(P(x), P(a), P(b), P(dy), M, P(dw), P(ws), ws_bytes, stream),
                           'hrl_conv3x3_wgrad_ex')
-            grads[3 * i:3 * i + 3] = [dw, dgam, dbet]
+            grads[3 * i:3 * i + 3] = [_ret(bw), _ret(bgam), _ret(bbet)]
             if i > 0:   # dL/dh_i, and BN_{i-1}'s backward sums in the same launch
                 g = torch.empty_like(h0)
                 _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g), 2, P(ys[i - 1]),

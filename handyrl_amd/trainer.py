@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from . import distributed as hdist
-from .nn import accelerate, fuse_bn_relu, deferred_weight_grads
+from .nn import accelerate, fuse_bn_relu, deferred_weight_grads, direct_grads
 from .train import forward_prediction, loss_terms
 from .util import map_r, bimap_r
 
@@ -134,9 +134,12 @@ class LearnerStep:
             if self.reducer is not None:
                 self.reducer.mark_ready(touched)
         else:
-            outputs = forward_prediction(self.net, hidden, batch, self.args)
-            losses, dcnt = self.loss_fn(outputs, batch, self.args)
-            losses['total'].backward()
+            # the HIP Functions write single-use parameter gradients straight into the flat buffer
+            # (zeroed above) instead of autograd's per-parameter accumulate-adds (nn.direct_grads)
+            with direct_grads():
+                outputs = forward_prediction(self.net, hidden, batch, self.args)
+                losses, dcnt = self.loss_fn(outputs, batch, self.args)
+                losses['total'].backward()
         return losses, dcnt
 
     def _update(self, losses, dcnt):

@@ -232,6 +232,11 @@ int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float 
                        float *dh, float *dw1p, float *db1p, float *dw1v, float *db1v, float *dwp, float *dwv,
                        void *workspace, int64_t workspace_bytes, void *stream);
 
+/* clip_grad_norm_(params, max_norm) on the learner's flat gradient buffer (handyrl/train.py:384)
+ * in one launch: total = ||grads||_2 (fp64 fold) -> *total_norm; grads *= min(max_norm / (total + 1e-6), 1).
+ * grads 16-byte aligned, n floats (csrc/hrl_optim.hip). */
+int hrl_clip_grad_norm(float *grads, int64_t n, double max_norm, float *total_norm, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
