@@ -176,3 +176,56 @@ def test_two_rank_gpu_step_matches_full_batch(cuda, graph):
     assert torch.allclose(p0, ref, rtol=1e-5, atol=1e-6), (p0 - ref).abs().max()
     for k in ('p', 'v', 'ent', 'total', 'dcnt'):
         assert abs(res['sums'][k] - ref_sums[k]) <= 1e-4 * max(1.0, abs(ref_sums[k])), k
+
+
+def _rccl_rank_main(rank, world, port, out_path, steps):
+    """One rank over the real RCCL backend: LearnerStep with a reducer (world_size forced to 2 so the
+    data-parallel path is built) in HIP-graph mode -- backward graph, eager RCCL all-reduce, update graph --
+    on a one-rank communicator, where the SUM all-reduce is the identity."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK='0')
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.synthetic import tictactoe_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group('nccl', rank=rank, world_size=world, device_id=dev)
+    B, T = 64, 9
+    args = default_args(T, B)
+    batch = tictactoe_batch(B, T, dev, seed=4)
+    torch.manual_seed(0)
+    step = LearnerStep(SimpleConv2dModel(), args, dev, graph=True, world_size=2)
+    assert step.reducer is not None
+    for _ in range(steps):
+        step.step(batch)
+    sums, _ = step.pop_stats()
+    flat = torch.cat([p.detach().reshape(-1) for p in step.net.parameters()]).cpu()
+    torch.save({'params': flat, 'sums': sums, 'split': step._graph_update is not None}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_graph_step_matches_single_gpu_step(cuda):
+    """The graph-captured data-parallel step over RCCL (the bench's N > 1 path) on a one-rank
+    communicator equals the plain single-GPU graph step."""
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.synthetic import tictactoe_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    steps = 3
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, 'r0.pt')
+        mp.spawn(_rccl_rank_main, args=(1, _free_port(), out, steps), nprocs=1, join=True)
+        res = torch.load(out, weights_only=True)
+    assert res['split']
+    B, T = 64, 9
+    batch = tictactoe_batch(B, T, cuda, seed=4)
+    torch.manual_seed(0)
+    step = LearnerStep(SimpleConv2dModel(), default_args(T, B), cuda, graph=True)
+    for _ in range(steps):
+        step.step(batch)
+    ref_sums, _ = step.pop_stats()
+    ref = torch.cat([p.detach().reshape(-1) for p in step.net.parameters()]).cpu()
+    torch.testing.assert_close(res['params'], ref, rtol=1e-5, atol=1e-6)
+    for k in ('p', 'v', 'ent', 'total', 'dcnt'):
+        assert abs(res['sums'][k] - ref_sums[k]) <= 1e-4 * max(1.0, abs(ref_sums[k])), k
