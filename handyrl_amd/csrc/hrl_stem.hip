@@ -1,0 +1,294 @@
+// hrl_stem.hip — the 3x3-board stem convolution (Cin <= 3 -> 32 channels) with fp32 MFMA (gfx950).
+//
+// SimpleConv2dModel's first layer (handyrl/envs/tictactoe.py:57) is a 3x3
+// 'same' conv of the 3 observation planes into 32 channels, with bias, over
+// N = B*T samples.  On a 3x3 board the layer is the dense matrix
+//   Y[n, co*9 + q] = sum_k X_aug[n, k] * Wb[k, co*9 + q],
+//   X_aug = [x (Cin*9 values) | 1],  Wb[ci*9 + p, co*9 + q] = W[co, ci, tap(p, q)] (0 off the board),
+//   Wb[Cin*9, co*9 + q] = b[co]
+// (K = Cin*9 + 1 <= 28).  As a library GEMM it needed the ones column
+// concatenated onto x, the expanded weight built, and ran at ~2x its HBM
+// bound; the weight gradient was a chunked batched GEMM plus folds.  Here:
+//
+// stem_fwd_kernel: each wave keeps its B fragments of Wb (7 k-steps x 18
+//   column tiles = 126 floats per lane) in registers for the whole launch;
+//   per 16-sample tile it reads the A fragments straight from x (the ones
+//   column is synthesized), runs 126 v_mfma_f32_16x16x4_f32 and stores the
+//   16 x 288 output from the accumulators (64-byte row segments).  Bound:
+//   the 151 MB output write at N = 131072.
+// stem_wgrad_kernel: dWb = X_aug^T dY as MFMA tiles (features x columns,
+//   36 accumulators) over 4-sample k-steps, dy tiles staged through LDS with
+//   coalesced float4 loads; the 4 waves fold through LDS in a fixed order and
+//   the workgroup folds the (p, q) pairs of each tap, so a partial is dW
+//   (32, Cin, 3, 3) | db (32); stem_reduce_kernel sums the partials with a
+//   fixed-shape tree (fp64).  Deterministic.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hrl_nn.h"
+#include "../../include/hrl_targets.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCo = 32;
+constexpr int kCells = 9;
+constexpr int kCols = kCo * kCells;    // 288 outputs per sample
+constexpr int kNT = kCols / 16;        // 18 column tiles
+constexpr int kKMax = 28;              // Cin*9 + 1 <= 28 (Cin <= 3)
+constexpr int kKS = kKMax / 4;         // 7 k-steps
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kWbStride = kCols + 16;  // LDS row stride of Wb
+
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// tap index of input cell p feeding output cell q on the 3x3 board, or -1
+__device__ __forceinline__ int tap_of(int p, int q) {
+    const int dy = p / 3 - q / 3 + 1, dx = p % 3 - q % 3 + 1;
+    return (dy < 0 || dy > 2 || dx < 0 || dx > 2) ? -1 : dy * 3 + dx;
+}
+
+// Wb entry (k, col) for weights w (32, Cin, 3, 3) and bias b (may be NULL)
+__device__ __forceinline__ float wb_at(const float *w, const float *b, int Cin, int k, int col) {
+    const int co = col / kCells, q = col - co * kCells;
+    if (k < Cin * kCells) {
+        const int ci = k / kCells, p = k - ci * kCells;
+        const int t = tap_of(p, q);
+        return t < 0 ? 0.f : w[(co * Cin + ci) * 9 + t];
+    }
+    return (k == Cin * kCells && b) ? b[co] : 0.f;
+}
+
+// X_aug[n, k]: x value, the ones column (bias), or zero padding
+__device__ __forceinline__ float xa_at(const float *x, int64_t n, int64_t N, int Cin, bool bias, int k) {
+    if (n >= N) return 0.f;
+    if (k < Cin * kCells) return x[n * (Cin * kCells) + k];
+    return (k == Cin * kCells && bias) ? 1.f : 0.f;
+}
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(kThreads) void stem_fwd_kernel(const float *__restrict__ x, int64_t N, int Cin,
+                                                            const float *__restrict__ w, const float *__restrict__ b,
+                                                            float *__restrict__ y) {
+    __shared__ float wb[kKMax * kWbStride];
+    for (int i = threadIdx.x; i < kKMax * kCols; i += kThreads) {
+        const int k = i / kCols, col = i - k * kCols;
+        wb[k * kWbStride + col] = wb_at(w, b, Cin, k, col);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i16 = lane & 15, kk = lane >> 4;
+    // this lane's B fragments: Wb[ks*4 + kk][nt*16 + i16]
+    float bf[kKS][kNT];
+#pragma unroll
+    for (int ks = 0; ks < kKS; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt) bf[ks][nt] = wb[(ks * 4 + kk) * kWbStride + nt * 16 + i16];
+    const bool bias = b != nullptr;
+    const int64_t ntiles = (N + 15) / 16;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    int64_t t = (int64_t)blockIdx.x * kWaves + wave;
+    float af[kKS];
+    auto load_a = [&](int64_t tt) {
+#pragma unroll
+        for (int ks = 0; ks < kKS; ++ks) af[ks] = xa_at(x, tt * 16 + i16, N, Cin, bias, ks * 4 + kk);
+    };
+    if (t < ntiles) load_a(t);
+    for (; t < ntiles; t += stride) {
+        f32x4 acc[kNT];
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < kKS; ++ks)
+#pragma unroll
+            for (int nt = 0; nt < kNT; ++nt) acc[nt] = mfma(af[ks], bf[ks][nt], acc[nt]);
+        const int64_t next = t + stride;
+        if (next < ntiles) load_a(next);   // in flight during the stores
+        // C/D layout: row = kk*4 + r (sample in the tile), col = nt*16 + i16
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t n = t * 16 + kk * 4 + r;
+            if (n < N) {
+                float *yr = y + n * kCols + i16;
+#pragma unroll
+                for (int nt = 0; nt < kNT; ++nt) yr[nt * 16] = acc[nt][r];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ weight gradient
+constexpr int kDyStride = kCols + 4;   // LDS row stride of a staged dy tile (16 B aligned rows)
+constexpr int kNOut = kCo * 3 * 9 + kCo;   // folded outputs per partial (Cin <= 3): dW then db
+
+// Per 16-sample tile: dy rows staged in LDS with coalesced float4 loads (the next tile's in flight during
+// the MFMAs); dWb = X_aug^T dY accumulates in MFMA tiles (features x columns).  At the end the 4 waves
+// fold in a fixed order and the workgroup folds the (p, q) pairs of each tap: one partial of
+// 32*Cin*9 + 32 values per workgroup, [dW (co, ci, tap) | db (co)].
+__global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const float *__restrict__ x,
+                                                              const float *__restrict__ dy, int64_t N, int Cin,
+                                                              int bias, float *__restrict__ partial) {
+    __shared__ float lds[kWaves * 16 * kDyStride > 32 * kCols ? kWaves * 16 * kDyStride : 32 * kCols];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i16 = lane & 15, kk = lane >> 4;
+    float *tile = lds + wave * 16 * kDyStride;
+    f32x4 acc[2][kNT];
+#pragma unroll
+    for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt) acc[it][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int64_t ntiles = (N + 15) / 16;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    constexpr int kV = 16 * kCols / 4 / 64;   // 18 float4 per lane per tile
+    float4 st[kV];
+    float xa[4][2];   // the tile's A values (features i16 and 16 + i16 of sample ks*4 + kk)
+    auto load = [&](int64_t tt) {
+        const int64_t lim = N * kCols;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int64_t n = tt * 16 + ks * 4 + kk;
+            xa[ks][0] = xa_at(x, n, N, Cin, bias != 0, i16);
+            xa[ks][1] = xa_at(x, n, N, Cin, bias != 0, 16 + i16);
+        }
+#pragma unroll
+        for (int k = 0; k < kV; ++k) {
+            const int64_t e = tt * 16 * kCols + (int64_t)(k * 64 + lane) * 4;
+            st[k] = e < lim ? *reinterpret_cast<const float4 *>(dy + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    int64_t t = (int64_t)blockIdx.x * kWaves + wave;
+    if (t < ntiles) load(t);
+    for (; t < ntiles; t += stride) {
+#pragma unroll
+        for (int k = 0; k < kV; ++k) {
+            const int e = (k * 64 + lane) * 4;
+            const int r = e / kCols, c = e - r * kCols;
+            *reinterpret_cast<float4 *>(tile + r * kDyStride + c) = st[k];
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        float a[4][2];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) { a[ks][0] = xa[ks][0]; a[ks][1] = xa[ks][1]; }
+        if (t + stride < ntiles) load(t + stride);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {   // the MFMA k = sample t*16 + ks*4 + kk
+            const float a0 = a[ks][0], a1 = a[ks][1];
+            const float *br = tile + (ks * 4 + kk) * kDyStride + i16;
+#pragma unroll
+            for (int nt = 0; nt < kNT; ++nt) {
+                const float bv = br[nt * 16];
+                acc[0][nt] = mfma(a0, bv, acc[0][nt]);
+                acc[1][nt] = mfma(a1, bv, acc[1][nt]);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+    }
+    // fold the 4 waves in a fixed order ((w0 + w1) + w2) + w3 into red[k][col]
+    float *red = lds;
+    __syncthreads();
+#pragma unroll 1
+    for (int w = 0; w < kWaves; ++w) {
+        if (wave == w) {
+#pragma unroll
+            for (int it = 0; it < 2; ++it)
+#pragma unroll
+                for (int nt = 0; nt < kNT; ++nt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float *d = red + (it * 16 + kk * 4 + r) * kCols + nt * 16 + i16;
+                        *d = w == 0 ? acc[it][nt][r] : *d + acc[it][nt][r];
+                    }
+        }
+        __syncthreads();
+    }
+    // fold the cell pairs of each tap (q, then p, in order): dW[co][ci][tap], then db[co]
+    float *out = partial + (int64_t)blockIdx.x * kNOut;
+    const int nw = kCo * Cin * 9;
+    for (int o = threadIdx.x; o < nw + kCo; o += kThreads) {
+        float s = 0.f;
+        if (o < nw) {
+            const int co = o / (Cin * 9), ci = (o / 9) % Cin, tap = o % 9;
+            const int ky = tap / 3, kx = tap % 3;
+            for (int q = 0; q < kCells; ++q) {   // the input cell of output cell q under this tap
+                const int py = q / 3 + ky - 1, px = q % 3 + kx - 1;
+                if (py >= 0 && py < 3 && px >= 0 && px < 3)
+                    s += red[(ci * kCells + py * 3 + px) * kCols + co * kCells + q];
+            }
+        } else if (bias) {
+            const int co = o - nw;
+            for (int q = 0; q < kCells; ++q) s += red[(Cin * kCells) * kCols + co * kCells + q];
+        }
+        out[o] = s;
+    }
+}
+
+// fixed-order fold of the workgroup partials: one workgroup per output, strided fp64 sums, LDS tree
+__global__ __launch_bounds__(256) void stem_reduce_kernel(const float *__restrict__ partial, int nparts, int nw,
+                                                          float *__restrict__ dw, float *__restrict__ db) {
+    __shared__ double red[256];
+    const int o = blockIdx.x;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < nparts; b += 256) s += (double)partial[(int64_t)b * kNOut + o];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (o < nw) dw[o] = (float)red[0];
+        else if (db) db[o - nw] = (float)red[0];
+    }
+}
+
+constexpr int kGrid = 256;
+
+int status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
+}
+
+int grid_for(int64_t N, int cap) {
+    const int64_t blocks = ((N + 15) / 16 + kWaves - 1) / kWaves;
+    return (int)(blocks < cap ? blocks : cap);
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t hrl_stem_workspace_bytes(int64_t N) { return N < 1 ? -1 : (int64_t)grid_for(N, kGrid) * kNOut * 4; }
+
+int hrl_stem_forward(const float *x, int64_t N, int64_t Cin, const float *weight, const float *bias, float *y,
+                     void *stream) {
+    if (N < 1 || Cin < 1 || Cin > 3 || !x || !weight || !y) return HRL_EINVAL;
+    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid_for(N, 2 * kGrid)), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), x, N, (int)Cin, weight, bias, y);
+    return status();
+}
+
+int hrl_stem_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, float *dweight, float *dbias,
+                   void *workspace, int64_t workspace_bytes, void *stream) {
+    if (N < 1 || Cin < 1 || Cin > 3 || !x || !dy || !dweight || !workspace) return HRL_EINVAL;
+    if (workspace_bytes < hrl_stem_workspace_bytes(N)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int grid = grid_for(N, kGrid);
+    float *partial = static_cast<float *>(workspace);
+    hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)Cin, dbias ? 1 : 0,
+                       partial);
+    int rc = status();
+    if (rc) return rc;
+    const int nw = kCo * (int)Cin * 9;
+    hipLaunchKernelGGL(stem_reduce_kernel, dim3(nw + (dbias ? kCo : 0)), dim3(256), 0, s, partial, grid, nw, dweight,
+                       dbias);
+    return status();
+}
+
+}  // extern "C"

@@ -342,6 +342,9 @@ class BoardConv2d(nn.Conv2d):
         N, Cin, H, W = x.shape
         if (H, W) == (3, 3) and self.kernel_size == (3, 3) and Cin == 32 and self.out_channels == 32 and N > 0:
             return _Conv3x3.apply(x.contiguous(), self.weight, self.bias)   # block-sparse MFMA kernels
+        if ((H, W) == (3, 3) and self.kernel_size == (3, 3) and Cin <= 3 and self.out_channels == 32 and N > 0
+                and not x.requires_grad):
+            return _StemConv.apply(x.contiguous(), self.weight, self.bias)  # the observation stem
         w_board = _BoardWeight.apply(self.weight, H, W)              # (Cin*HW, Cout*HW)
         bias = _BoardBias.apply(self.bias, H * W) if self.bias is not None else None
         x2 = x.reshape(N, Cin * H * W)
@@ -676,6 +679,39 @@ def _fuse_heads(gm, heads):
     gm.graph.erase_node(np_)
     gm.graph.erase_node(nv_)
     return 1
+
+
+class _StemConv(torch.autograd.Function):
+    """3x3 conv of <= 3 observation planes into 32 channels on a 3x3 board (tictactoe.py:57):
+    csrc/hrl_stem.hip (fp32 MFMA on the dense board matrix, B fragments held in registers)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        N, Cin = x.shape[0], x.shape[1]
+        lib = _native.load()
+        y = torch.empty(N, 32, 3, 3, device=x.device, dtype=x.dtype)
+        w = weight.contiguous()
+        b = bias.contiguous() if bias is not None else None
+        _native.check(lib.hrl_stem_forward(_native.ptr(x), N, Cin, _native.ptr(w), _native.ptr(b), _native.ptr(y),
+                                           _native.stream_of(x.device)), 'hrl_stem_forward')
+        ctx.save_for_backward(x, w)
+        ctx.params = (weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        weight, bias = ctx.params
+        N, Cin = x.shape[0], x.shape[1]
+        lib = _native.load()
+        ws_bytes = lib.hrl_stem_workspace_bytes(N)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+        bw = _grad_buffer(weight)
+        bb = _grad_buffer(bias) if bias is not None else (None, False)
+        _native.check(lib.hrl_stem_wgrad(_native.ptr(x), _native.ptr(dy.contiguous()), N, Cin, _native.ptr(bw[0]),
+                                         _native.ptr(bb[0]), _native.ptr(ws), ws_bytes,
+                                         _native.stream_of(x.device)), 'hrl_stem_wgrad')
+        return None, _ret(bw), _ret(bb)
 
 
 class _BoardWeight(torch.autograd.Function):

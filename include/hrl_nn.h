@@ -232,6 +232,17 @@ int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float 
                        float *dh, float *dw1p, float *db1p, float *dw1v, float *db1v, float *dwp, float *dwv,
                        void *workspace, int64_t workspace_bytes, void *stream);
 
+/* The 3x3-board stem conv, Cin <= 3 -> 32 channels, with bias (TicTacToe, tictactoe.py:57), as fp32
+ * MFMA on the dense board matrix (csrc/hrl_stem.hip): x (N, Cin, 3, 3), y (N, 32, 3, 3),
+ * weight (32, Cin, 3, 3), bias (32) or NULL.  hrl_stem_wgrad: dweight and dbias (may be NULL),
+ * deterministic; workspace hrl_stem_workspace_bytes(N) bytes.  (No input gradient: the stem reads
+ * the observation.) */
+int64_t hrl_stem_workspace_bytes(int64_t N);
+int hrl_stem_forward(const float *x, int64_t N, int64_t Cin, const float *weight, const float *bias, float *y,
+                     void *stream);
+int hrl_stem_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, float *dweight, float *dbias,
+                   void *workspace, int64_t workspace_bytes, void *stream);
+
 /* clip_grad_norm_(params, max_norm) on the learner's flat gradient buffer (handyrl/train.py:384)
  * in one launch: total = ||grads||_2 (fp64 fold) -> *total_norm; grads *= min(max_norm / (total + 1e-6), 1).
  * grads 16-byte aligned, n floats (csrc/hrl_optim.hip). */

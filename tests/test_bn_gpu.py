@@ -328,3 +328,25 @@ def test_fused_heads_match_torch_cpu(cuda, N):
     with torch.no_grad():
         p2, v2 = fused(h.to(cuda))
     assert torch.equal(p2, p.detach()) and torch.equal(v2, v.detach())
+
+
+@pytest.mark.parametrize('N,cin,bias', [(1, 3, True), (17, 3, True), (4099, 3, True), (50, 2, False), (33, 1, True)])
+def test_stem_conv_matches_torch_cpu(cuda, N, cin, bias):
+    """csrc/hrl_stem.hip (the observation stem, tictactoe.py:57): forward and the weight / bias gradients
+    vs torch-CPU conv2d on ragged sample counts (the input is the observation: no input gradient)."""
+    from handyrl_amd.nn import BoardConv2d
+    torch.manual_seed(N + cin)
+    ref = nn.Conv2d(cin, 32, 3, padding=1, bias=bias)
+    hip = BoardConv2d(cin, 32, 3, padding=1, bias=bias).to(cuda)
+    hip.load_state_dict(ref.state_dict())
+    x = (torch.rand(N, cin, 3, 3) < 0.5).float()
+    dy = torch.randn(N, 32, 3, 3)
+    yr = ref(x)
+    yh = hip(x.to(cuda))
+    np.testing.assert_allclose(yh.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-5, atol=1e-5)
+    yr.backward(dy)
+    yh.backward(dy.to(cuda))
+    tol = 2e-5 * max(1.0, (N * 9) ** 0.5)
+    np.testing.assert_allclose(hip.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-5, atol=tol)
+    if bias:
+        np.testing.assert_allclose(hip.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-5, atol=tol)
