@@ -26,6 +26,10 @@
 //   dp^T a_p and dv^T a_v (one thread per weight, rows in a fixed order) into
 //   the same partial rows; heads_reduce_kernel folds every column with a
 //   fixed-shape tree (deterministic).  151 MB read + 151 MB written.
+// With the body's last BatchNorm fused in front (BnIn; nn._ChainHeadsFn) both
+// kernels read that BN's raw input y and apply relu(y*alpha + beta) per slice,
+// and the backward also emits the BN's backward sums, so the body's output
+// never reaches HBM and its last BN needs no separate reduce pass.
 // Numerics: fp32 throughout (-ffp-contract=off); sums in a fixed order; the
 // LeakyReLU and its gradient follow torch (x > 0 ? x : x * 0.1f).
 
@@ -63,6 +67,19 @@ struct Weights {
     const float *w1p, *w1v, *b1p, *b1v, *wp, *wv;
 };
 
+// Optional BatchNorm + ReLU in front of the heads (the body's last BN, fused_chain_heads): h = relu(y*alpha + beta)
+// computed as each slice is read; the backward also forms that BN's backward sums (sum g*m, sum g*m*(y - mean),
+// m = [y*alpha + beta > 0]) per channel, fp64 per workgroup -> part[block][32][2] (hrl_bn_finalize_backward).
+struct BnIn {
+    const float *alpha, *beta, *mean;
+    double *part;
+};
+
+__device__ __forceinline__ float bn_relu(float y, float a, float b) {
+    const float t = y * a + b;   // bn_apply_kernel's float operations
+    return t < 0.f ? 0.f : t;
+}
+
 __device__ __forceinline__ void lds_fence() {
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
@@ -95,12 +112,16 @@ __device__ __forceinline__ void slice_to_lds(const float4 (&st)[kSV], float *til
 }
 
 // ------------------------------------------------------------------ forward
-__global__ __launch_bounds__(64) void heads_fwd_kernel(const float *__restrict__ h, int64_t N, Weights w,
+__global__ __launch_bounds__(64) void heads_fwd_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
                                                        float *__restrict__ a_p, float *__restrict__ a_v,
                                                        float *__restrict__ p_out, float *__restrict__ v_out) {
     __shared__ float tile[64 * kTS];
-    __shared__ float sw1[kM * kC], sb1[kM], swp[kOP * kZP], swv[kHW];
+    __shared__ float sw1[kM * kC], sb1[kM], swp[kOP * kZP], swv[kHW], sal[kC], sbe[kC];
     const int lane = threadIdx.x;
+    if (bn.alpha && lane < kC) {
+        sal[lane] = bn.alpha[lane];
+        sbe[lane] = bn.beta[lane];
+    }
     for (int i = lane; i < kM * kC; i += 64) sw1[i] = w1_at(w, i / kC, i % kC);
     if (lane < kM) sb1[lane] = lane < kMP ? w.b1p[lane] : w.b1v[lane - kMP];
     for (int i = lane; i < kOP * kZP; i += 64) swp[i] = w.wp[i];
@@ -124,6 +145,10 @@ __global__ __launch_bounds__(64) void heads_fwd_kernel(const float *__restrict__
             float x[kSF];
 #pragma unroll
             for (int j = 0; j < kSF; ++j) x[j] = tile[lane * kTS + j];
+            if (bn.alpha) {
+#pragma unroll
+                for (int j = 0; j < kSF; ++j) x[j] = bn_relu(x[j], sal[s * kSC + j / kHW], sbe[s * kSC + j / kHW]);
+            }
 #pragma unroll
             for (int m = 0; m < kM; ++m)
 #pragma unroll
@@ -171,18 +196,26 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-__global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__ h, int64_t N, Weights w,
+__global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
                                                        const float *__restrict__ a_p, const float *__restrict__ a_v,
                                                        const float *__restrict__ dp, const float *__restrict__ dv,
                                                        float *__restrict__ dh, float *__restrict__ part) {
     __shared__ float tile[64 * kTS];
-    __shared__ float sw1[kM * kC], swp[kOP * kZP], swv[kHW];
+    __shared__ float sw1[kM * kC], swp[kOP * kZP], swv[kHW], sal[kC], sbe[kC], smu[kC];
     __shared__ float gw1[kM * kC * 64];   // per-lane conv weight-gradient accumulators [m*32 + c][lane]
+    __shared__ float gbn[kC * 2 * 64];    // per-lane BN backward sums [c][2][lane] (bn.part)
     const int lane = threadIdx.x;
     for (int i = lane; i < kM * kC; i += 64) sw1[i] = w1_at(w, i / kC, i % kC);
     for (int i = lane; i < kOP * kZP; i += 64) swp[i] = w.wp[i];
     if (lane < kHW) swv[lane] = w.wv[lane];
     for (int i = lane; i < kM * kC * 64; i += 64) gw1[i] = 0.f;
+    if (bn.alpha && lane < kC) {
+        sal[lane] = bn.alpha[lane];
+        sbe[lane] = bn.beta[lane];
+        smu[lane] = bn.part ? bn.mean[lane] : 0.f;
+    }
+    if (bn.part)
+        for (int i = lane; i < kC * 2 * 64; i += 64) gbn[i] = 0.f;
     __syncthreads();
 
     float gb1[kM];
@@ -229,9 +262,13 @@ __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__
             slice_to_lds(st, tile, lane);
             lds_fence();
             if (s + 1 < kNS) load_slice(h, base, nrows, s + 1, lane, st);
-            float x[kSF];
+            float x[kSF], yraw[kSF];
 #pragma unroll
-            for (int j = 0; j < kSF; ++j) x[j] = tile[lane * kTS + j];
+            for (int j = 0; j < kSF; ++j) x[j] = yraw[j] = tile[lane * kTS + j];
+            if (bn.alpha) {
+#pragma unroll
+                for (int j = 0; j < kSF; ++j) x[j] = bn_relu(x[j], sal[s * kSC + j / kHW], sbe[s * kSC + j / kHW]);
+            }
             // conv weight gradient: dW1[m, c] += sum_q dz[m, q] * h[c, q]
 #pragma unroll
             for (int m = 0; m < kM; ++m)
@@ -245,14 +282,27 @@ __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__
             // input gradient of this slice: dh[c, q] = sum_m W1[m, c] * dz[m, q] -> the lane's LDS row
             lds_fence();
 #pragma unroll
-            for (int cc = 0; cc < kSC; ++cc)
+            for (int cc = 0; cc < kSC; ++cc) {
+                const int c = s * kSC + cc;
+                float t1 = 0.f, t2 = 0.f;   // this row's BN backward sums of channel c
 #pragma unroll
                 for (int q = 0; q < kHW; ++q) {
                     float t = 0.f;
 #pragma unroll
-                    for (int m = 0; m < kM; ++m) t += sw1[m * kC + s * kSC + cc] * dz[m * kHW + q];
+                    for (int m = 0; m < kM; ++m) t += sw1[m * kC + c] * dz[m * kHW + q];
                     tile[lane * kTS + cc * kHW + q] = t;
+                    if (bn.part) {   // bn_bwd_reduce_kernel's mask and products
+                        const float y = yraw[cc * kHW + q];
+                        const float gm = (y * sal[c] + sbe[c] > 0.f) ? t : 0.f;
+                        t1 += gm;
+                        t2 += gm * (y - smu[c]);
+                    }
                 }
+                if (bn.part) {
+                    gbn[(c * 2 + 0) * 64 + lane] += t1;
+                    gbn[(c * 2 + 1) * 64 + lane] += t2;
+                }
+            }
             lds_fence();
             // coalesced float4 stores of the 64 x 36 slice
 #pragma unroll
@@ -280,6 +330,12 @@ __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__
     for (int i = 0; i < kM; ++i) {
         const float t = wave_sum(gb1[i]);
         if (lane == 0) out[kGB1 + i] = t;
+    }
+    if (bn.part) {   // lanes in order, fp64: part[block][c][2]
+        const int c = lane >> 1, k = lane & 1;
+        double t = 0.0;
+        for (int l = 0; l < 64; ++l) t += (double)gbn[(c * 2 + k) * 64 + l];
+        bn.part[((int64_t)blockIdx.x * kC + c) * 2 + k] = t;
     }
 }
 
@@ -364,30 +420,37 @@ extern "C" {
 
 int64_t hrl_heads_workspace_bytes(int64_t N) { return N < 1 ? -1 : (int64_t)grid_for(N) * kGN * 4; }
 
+int64_t hrl_heads_bn_parts(int64_t N) { return N < 1 ? -1 : grid_for(N); }
+
 int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *b1p, const float *w1v,
-                      const float *b1v, const float *wp, const float *wv, float *a_p, float *a_v, float *p_out,
-                      float *v_out, void *stream) {
+                      const float *b1v, const float *wp, const float *wv, const float *bn_alpha, const float *bn_beta,
+                      float *a_p, float *a_v, float *p_out, float *v_out, void *stream) {
     if (N < 1 || !h || !w1p || !b1p || !w1v || !b1v || !wp || !wv || !p_out || !v_out) return HRL_EINVAL;
-    if ((a_p == nullptr) != (a_v == nullptr) || !aligned16(h)) return HRL_EINVAL;
+    if ((a_p == nullptr) != (a_v == nullptr) || (bn_alpha == nullptr) != (bn_beta == nullptr) || !aligned16(h))
+        return HRL_EINVAL;
     const Weights w{w1p, w1v, b1p, b1v, wp, wv};
+    const BnIn bn{bn_alpha, bn_beta, nullptr, nullptr};
     hipLaunchKernelGGL(heads_fwd_kernel, dim3(grid_for(N)), dim3(64), 0, static_cast<hipStream_t>(stream), h, N, w,
-                       a_p, a_v, p_out, v_out);
+                       bn, a_p, a_v, p_out, v_out);
     return status();
 }
 
 int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float *w1v, const float *wp,
-                       const float *wv, const float *a_p, const float *a_v, const float *dp, const float *dv,
+                       const float *wv, const float *bn_alpha, const float *bn_beta, const float *bn_mean,
+                       double *bn_part, const float *a_p, const float *a_v, const float *dp, const float *dv,
                        float *dh, float *dw1p, float *db1p, float *dw1v, float *db1v, float *dwp, float *dwv,
                        void *workspace, int64_t workspace_bytes, void *stream) {
     if (N < 1 || !h || !w1p || !w1v || !wp || !wv || !a_p || !a_v || !dp || !dv || !dh || !workspace)
         return HRL_EINVAL;
     if (!dw1p || !db1p || !dw1v || !db1v || !dwp || !dwv) return HRL_EINVAL;
+    if ((bn_alpha == nullptr) != (bn_beta == nullptr) || (bn_part && (!bn_alpha || !bn_mean))) return HRL_EINVAL;
     if (!aligned16(h) || !aligned16(dh) || workspace_bytes < hrl_heads_workspace_bytes(N)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const Weights w{w1p, w1v, nullptr, nullptr, wp, wv};
+    const BnIn bn{bn_alpha, bn_beta, bn_mean, bn_part};
     const int grid = grid_for(N);
     float *part = static_cast<float *>(workspace);
-    hipLaunchKernelGGL(heads_bwd_kernel, dim3(grid), dim3(64), 0, s, h, N, w, a_p, a_v, dp, dv, dh, part);
+    hipLaunchKernelGGL(heads_bwd_kernel, dim3(grid), dim3(64), 0, s, h, N, w, bn, a_p, a_v, dp, dv, dh, part);
     int rc = status();
     if (rc) return rc;
     const int64_t rows = (N + grid - 1) / grid;

@@ -598,8 +598,8 @@ class _BoardHeadsFn(torch.autograd.Function):
         P = _native.ptr
         w1p, w1v, wp, wv = w1p.contiguous(), w1v.contiguous(), wp.contiguous(), wv.contiguous()
         _native.check(lib.hrl_heads_forward(P(h), N, P(w1p), P(b1p.contiguous()), P(w1v), P(b1v.contiguous()),
-                                            P(wp), P(wv), P(a_p), P(a_v), P(p), P(v), _native.stream_of(dev)),
-                      'hrl_heads_forward')
+                                            P(wp), P(wv), None, None, P(a_p), P(a_v), P(p), P(v),
+                                            _native.stream_of(dev)), 'hrl_heads_forward')
         ctx.save_for_backward(h, w1p, w1v, wp, wv, a_p, a_v)
         ctx.biases = (b1p, b1v)
         return p, v
@@ -618,9 +618,9 @@ class _BoardHeadsFn(torch.autograd.Function):
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         P = _native.ptr
         dw1p, db1p, dw1v, db1v, dwp, dwv = (b[0] for b in bufs)
-        _native.check(lib.hrl_heads_backward(P(h), N, P(w1p), P(w1v), P(wp), P(wv), P(a_p), P(a_v), P(dp), P(dv),
-                                             P(dh), P(dw1p), P(db1p), P(dw1v), P(db1v), P(dwp), P(dwv), P(ws),
-                                             ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward')
+        _native.check(lib.hrl_heads_backward(P(h), N, P(w1p), P(w1v), P(wp), P(wv), None, None, None, None, P(a_p),
+                                             P(a_v), P(dp), P(dv), P(dh), P(dw1p), P(db1p), P(dw1v), P(db1v), P(dwp),
+                                             P(dwv), P(ws), ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward')
         return (dh, *(_ret(b) for b in bufs))
 
 
@@ -650,7 +650,7 @@ class _FusedHeads(nn.Module):
         _native.check(_native.load().hrl_heads_forward(P(x), N, P(cp.weight.contiguous()), P(cp.bias.contiguous()),
                                                        P(cv.weight.contiguous()), P(cv.bias.contiguous()),
                                                        P(fp.weight.contiguous()), P(fv.weight.contiguous()), None,
-                                                       None, P(p), P(v), _native.stream_of(x.device)),
+                                                       None, None, None, P(p), P(v), _native.stream_of(x.device)),
                       'hrl_heads_forward')
         return p, v
 
@@ -1008,6 +1008,114 @@ class _MultiBoardConv(nn.Module):
         return tuple(outs)
 
 
+_UNIT = {}
+
+
+def _unit_coefs(dev):
+    """(alpha, beta) = (1, 0) per channel: the stem ReLU in front of a chain as an identity BN + ReLU (cached)."""
+    u = _UNIT.get(dev)
+    if u is None:
+        u = _UNIT[dev] = torch.stack([torch.ones(32, device=dev), torch.zeros(32, device=dev)])
+    return u
+
+
+def _chain_forward(h0, meta, relu_in, params, apply_out=True):
+    """Forward of a conv -> BN -> ReLU chain (see _BoardChain): returns (out | None, ys, coefs, unit)."""
+    lib = _native.load()
+    M = h0.shape[0]
+    dev = h0.device
+    stream = _native.stream_of(dev)
+    P = _native.ptr
+    ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    nblk = lib.hrl_conv3x3_stats_blocks(M)
+    part = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
+    unit = _unit_coefs(dev) if relu_in else None
+    x = h0
+    a_prev, b_prev = (unit[0], unit[1]) if relu_in else (None, None)
+    ys, coefs = [], []
+    for i, (rm, rv, momentum, eps) in enumerate(meta):
+        w, gamma, beta = params[3 * i:3 * i + 3]
+        y = torch.empty_like(h0)
+        _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(a_prev), P(b_prev), P(w), None, 0, P(y), 1, None, None,
+                                                 None, None, P(part), P(ws), ws_bytes, stream),
+                      'hrl_conv3x3_forward_ex')
+        coef = torch.empty(4, 32, dtype=torch.float32, device=dev)   # mean, invstd, alpha, beta
+        _native.check(lib.hrl_bn_finalize_stats(P(part), nblk, 32, M * 9, P(gamma), P(beta), P(rm), P(rv),
+                                                float(momentum), float(eps), P(coef[0]), P(coef[1]),
+                                                P(coef[2]), P(coef[3]), stream), 'hrl_bn_finalize_stats')
+        ys.append(y)
+        coefs.append(coef)
+        x, a_prev, b_prev = y, coef[2], coef[3]
+    out = None
+    if apply_out:
+        out = torch.empty_like(h0)
+        _native.check(lib.hrl_bn_apply(P(x), M, 32, 9, P(a_prev), P(b_prev), 1, P(out), stream), 'hrl_bn_apply')
+    return out, ys, coefs, unit
+
+
+def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, part_in=None, nblk_in=0):
+    """Backward of the chain from g = dL/d(chain output); with part_in the last BN's backward sums were already
+    formed by the consumer (fused heads).  Returns (dL/dh0 | None, parameter gradients)."""
+    lib = _native.load()
+    n = len(ys)
+    M = h0.shape[0]
+    dev = h0.device
+    stream = _native.stream_of(dev)
+    P = _native.ptr
+    ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    bn_ws_bytes = lib.hrl_bn_workspace_bytes(M, 32, 9)
+    bn_ws = torch.empty(bn_ws_bytes, dtype=torch.uint8, device=dev)
+    nblk = lib.hrl_conv3x3_stats_blocks(M)
+    part = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
+    g = g.contiguous()
+    grads = [None] * (3 * n)
+    sums, sums_n = (part_in, nblk_in) if part_in is not None else (None, 0)   # BN_i's backward sums, if formed
+    for i in reversed(range(n)):
+        w, gamma, beta = params[3 * i:3 * i + 3]
+        mean, invstd = coefs[i][0], coefs[i][1]
+        dy = torch.empty_like(h0)
+        bw, bgam, bbet = _grad_buffer(w), _grad_buffer(gamma), _grad_buffer(beta)
+        dgam, dbet = bgam[0], bbet[0]
+        if sums is not None:
+            kg = torch.empty(2, 32, dtype=torch.float32, device=dev)
+            _native.check(lib.hrl_bn_finalize_backward(P(sums), sums_n, 32, M * 9, P(gamma), P(invstd), P(dgam),
+                                                       P(dbet), P(kg[0]), P(kg[1]), stream),
+                          'hrl_bn_finalize_backward')
+            _native.check(lib.hrl_bn_backward_apply(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(mean),
+                                                    P(invstd), 1, P(kg[0]), P(kg[1]), P(dy), stream),
+                          'hrl_bn_backward_apply')
+        else:
+            _native.check(lib.hrl_bn_backward(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(mean), P(invstd),
+                                              1, P(dy), P(dgam), P(dbet), P(bn_ws), bn_ws_bytes, stream),
+                          'hrl_bn_backward')
+        if i == 0:
+            x, a, b = h0, (unit[0] if unit is not None else None), (unit[1] if unit is not None else None)
+        else:
+            x, a, b = ys[i - 1], coefs[i - 1][2], coefs[i - 1][3]
+        dw = bw[0]
+        _native.check(lib.hrl_conv3x3_wgrad_ex(P(x), P(a), P(b), P(dy), M, P(dw), P(ws), ws_bytes, stream),
+                      'hrl_conv3x3_wgrad_ex')
+        grads[3 * i:3 * i + 3] = [_ret(bw), _ret(bgam), _ret(bbet)]
+        if i > 0:   # dL/dh_i, and BN_{i-1}'s backward sums in the same launch
+            g = torch.empty_like(h0)
+            _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g), 2, P(ys[i - 1]),
+                                                     P(coefs[i - 1][0]), P(coefs[i - 1][2]),
+                                                     P(coefs[i - 1][3]), P(part), P(ws), ws_bytes, stream),
+                          'hrl_conv3x3_forward_ex(flip, bn sums)')
+            sums, sums_n = part, nblk
+        elif need_input_grad:
+            g = torch.empty_like(h0)
+            _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g),
+                                                     3 if relu_in else 0, P(h0) if relu_in else None,
+                                                     None, None, None, None, P(ws), ws_bytes, stream),
+                          'hrl_conv3x3_forward_ex(flip)')
+        else:
+            g = None
+    return g, grads
+
+
 class _BoardChain(torch.autograd.Function):
     """[relu ->] [3x3 conv 32->32 (no bias) -> BatchNorm (training) -> ReLU] x n on 3x3 boards.
 
@@ -1026,110 +1134,80 @@ class _BoardChain(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h0, meta, relu_in, *params):
-        lib = _native.load()
         h0 = h0.contiguous()
-        M = h0.shape[0]
-        dev = h0.device
-        stream = _native.stream_of(dev)
-        P = _native.ptr
-        ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        nblk = lib.hrl_conv3x3_stats_blocks(M)
-        part = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
-        unit = torch.stack([torch.ones(32, device=dev), torch.zeros(32, device=dev)]) if relu_in else None
-        x = h0
-        a_prev, b_prev = (unit[0], unit[1]) if relu_in else (None, None)
-        saved = [h0]
-        for i, (rm, rv, momentum, eps) in enumerate(meta):
-            w, gamma, beta = params[3 * i:3 * i + 3]
-            y = torch.empty_like(h0)
-            _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(a_prev), P(b_prev), P(w), None, 0, P(y), 1, None, None,
-                                                     None, None, P(part), P(ws), ws_bytes, stream),
-                          'hrl_conv3x3_forward_ex')
-            coef = torch.empty(4, 32, dtype=torch.float32, device=dev)   # mean, invstd, alpha, beta
-            _native.check(lib.hrl_bn_finalize_stats(P(part), nblk, 32, M * 9, P(gamma), P(beta), P(rm), P(rv),
-                                                    float(momentum), float(eps), P(coef[0]), P(coef[1]),
-                                                    P(coef[2]), P(coef[3]), stream), 'hrl_bn_finalize_stats')
-            saved += [y, coef]
-            x, a_prev, b_prev = y, coef[2], coef[3]
-        out = torch.empty_like(h0)
-        _native.check(lib.hrl_bn_apply(P(x), M, 32, 9, P(a_prev), P(b_prev), 1, P(out), stream), 'hrl_bn_apply')
-        if relu_in:
-            saved.append(unit)
-        ctx.save_for_backward(*saved, *params)
+        out, ys, coefs, unit = _chain_forward(h0, meta, relu_in, params)
+        ctx.save_for_backward(h0, *ys, *coefs, *params)
         ctx.n = len(meta)
         ctx.relu_in = relu_in
         return out
 
     @staticmethod
     def backward(ctx, g):
-        lib = _native.load()
         n = ctx.n
         t = ctx.saved_tensors
-        h0 = t[0]
-        ys = [t[1 + 2 * i] for i in range(n)]
-        coefs = [t[2 + 2 * i] for i in range(n)]
-        k = 1 + 2 * n
-        unit = None
-        if ctx.relu_in:
-            unit = t[k]
-            k += 1
-        params = t[k:]
-        M = h0.shape[0]
+        h0, ys, coefs, params = t[0], list(t[1:1 + n]), list(t[1 + n:1 + 2 * n]), t[1 + 2 * n:]
+        unit = _unit_coefs(h0.device) if ctx.relu_in else None
+        g_in, grads = _chain_backward(h0, ys, coefs, unit, params, ctx.relu_in, g, ctx.needs_input_grad[0])
+        return (g_in, None, None, *grads)
+
+
+class _ChainHeadsFn(torch.autograd.Function):
+    """The TicTacToe body chain and both heads as one Function: the chain's last BN + ReLU is applied by the
+    heads kernels as they read its raw input (csrc/hrl_heads.hip BnIn), so the body output never reaches HBM;
+    the heads backward also forms that BN's backward sums, so the chain backward needs no reduce pass."""
+
+    @staticmethod
+    def forward(ctx, h0, meta, relu_in, w1p, b1p, w1v, b1v, wp, wv, *params):
+        h0 = h0.contiguous()
+        _, ys, coefs, unit = _chain_forward(h0, meta, relu_in, params, apply_out=False)
+        y, coef = ys[-1], coefs[-1]
+        N = h0.shape[0]
         dev = h0.device
-        stream = _native.stream_of(dev)
+        lib = _native.load()
+        a_p = torch.empty(N, 18, device=dev, dtype=h0.dtype)
+        a_v = torch.empty(N, 9, device=dev, dtype=h0.dtype)
+        p = torch.empty(N, 9, device=dev, dtype=h0.dtype)
+        v = torch.empty(N, 1, device=dev, dtype=h0.dtype)
         P = _native.ptr
-        ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+        w1p, w1v, wp, wv = w1p.contiguous(), w1v.contiguous(), wp.contiguous(), wv.contiguous()
+        _native.check(lib.hrl_heads_forward(P(y), N, P(w1p), P(b1p.contiguous()), P(w1v), P(b1v.contiguous()),
+                                            P(wp), P(wv), P(coef[2]), P(coef[3]), P(a_p), P(a_v), P(p), P(v),
+                                            _native.stream_of(dev)), 'hrl_heads_forward(bn)')
+        ctx.save_for_backward(h0, *ys, *coefs, a_p, a_v, w1p, w1v, wp, wv, *params)
+        ctx.biases = (b1p, b1v)
+        ctx.n = len(meta)
+        ctx.relu_in = relu_in
+        return p, v
+
+    @staticmethod
+    def backward(ctx, dp, dv):
+        n = ctx.n
+        t = ctx.saved_tensors
+        h0, ys, coefs = t[0], list(t[1:1 + n]), list(t[1 + n:1 + 2 * n])
+        a_p, a_v, w1p, w1v, wp, wv = t[1 + 2 * n:7 + 2 * n]
+        params = t[7 + 2 * n:]
+        b1p, b1v = ctx.biases
+        N = h0.shape[0]
+        dev = h0.device
+        lib = _native.load()
+        P = _native.ptr
+        y, coef = ys[-1], coefs[-1]
+        dp, dv = dp.contiguous(), dv.contiguous()
+        dh = torch.empty_like(h0)
+        hbufs = [_grad_buffer(x) for x in (w1p, b1p, w1v, b1v, wp, wv)]
+        ws_bytes = lib.hrl_heads_workspace_bytes(N)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        bn_ws_bytes = lib.hrl_bn_workspace_bytes(M, 32, 9)
-        bn_ws = torch.empty(bn_ws_bytes, dtype=torch.uint8, device=dev)
-        nblk = lib.hrl_conv3x3_stats_blocks(M)
-        part = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
-        g = g.contiguous()
-        grads = [None] * (3 * n)
-        have_sums = False   # part holds BN_i's backward sums from the previous input-gradient launch
-        for i in reversed(range(n)):
-            w, gamma, beta = params[3 * i:3 * i + 3]
-            mean, invstd = coefs[i][0], coefs[i][1]
-            dy = torch.empty_like(h0)
-            bw, bgam, bbet = _grad_buffer(w), _grad_buffer(gamma), _grad_buffer(beta)
-            dgam, dbet = bgam[0], bbet[0]
-            if have_sums:
-                kg = torch.empty(2, 32, dtype=torch.float32, device=dev)
-                _native.check(lib.hrl_bn_finalize_backward(P(part), nblk, 32, M * 9, P(gamma), P(invstd), P(dgam),
-                                                           P(dbet), P(kg[0]), P(kg[1]), stream),
-                              'hrl_bn_finalize_backward')
-                _native.check(lib.hrl_bn_backward_apply(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(mean),
-                                                        P(invstd), 1, P(kg[0]), P(kg[1]), P(dy), stream),
-                              'hrl_bn_backward_apply')
-            else:
-                _native.check(lib.hrl_bn_backward(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(mean), P(invstd),
-                                                  1, P(dy), P(dgam), P(dbet), P(bn_ws), bn_ws_bytes, stream),
-                              'hrl_bn_backward')
-            if i == 0:
-                x, a, b = h0, (unit[0] if unit is not None else None), (unit[1] if unit is not None else None)
-            else:
-                x, a, b = ys[i - 1], coefs[i - 1][2], coefs[i - 1][3]
-            dw = bw[0]
-            _native.check(lib.hrl_conv3x3_wgrad_ex(P(x), P(a), P(b), P(dy), M, P(dw), P(ws), ws_bytes, stream),
-                          'hrl_conv3x3_wgrad_ex')
-            grads[3 * i:3 * i + 3] = [_ret(bw), _ret(bgam), _ret(bbet)]
-            if i > 0:   # dL/dh_i, and BN_{i-1}'s backward sums in the same launch
-                g = torch.empty_like(h0)
-                _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g), 2, P(ys[i - 1]),
-                                                         P(coefs[i - 1][0]), P(coefs[i - 1][2]),
-                                                         P(coefs[i - 1][3]), P(part), P(ws), ws_bytes, stream),
-                              'hrl_conv3x3_forward_ex(flip, bn sums)')
-                have_sums = True
-            elif ctx.needs_input_grad[0]:
-                g = torch.empty_like(h0)
-                _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g),
-                                                         3 if ctx.relu_in else 0, P(h0) if ctx.relu_in else None,
-                                                         None, None, None, None, P(ws), ws_bytes, stream),
-                              'hrl_conv3x3_forward_ex(flip)')
-            else:
-                g = None
-        return (g, None, None, *grads)
+        nparts = lib.hrl_heads_bn_parts(N)
+        bn_part = torch.empty(nparts * 64, dtype=torch.float64, device=dev)
+        dw1p, db1p, dw1v, db1v, dwp, dwv = (b[0] for b in hbufs)
+        _native.check(lib.hrl_heads_backward(P(y), N, P(w1p), P(w1v), P(wp), P(wv), P(coef[2]), P(coef[3]),
+                                             P(coef[0]), P(bn_part), P(a_p), P(a_v), P(dp), P(dv), P(dh), P(dw1p),
+                                             P(db1p), P(dw1v), P(db1v), P(dwp), P(dwv), P(ws), ws_bytes,
+                                             _native.stream_of(dev)), 'hrl_heads_backward(bn)')
+        unit = _unit_coefs(dev) if ctx.relu_in else None
+        g_in, grads = _chain_backward(h0, ys, coefs, unit, params, ctx.relu_in, dh, ctx.needs_input_grad[0],
+                                      part_in=bn_part, nblk_in=nparts)
+        return (g_in, None, None, *(_ret(b) for b in hbufs), *grads)
 
 
 class _ConvBNChain(nn.Module):
@@ -1155,21 +1233,65 @@ class _ConvBNChain(nn.Module):
 
     def forward(self, x):
         convs, bns = self.convs, self.bns
-        fused = (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and tuple(x.shape[1:]) == (32, 3, 3)
-                 and x.shape[0] > 0 and all(b.training and b.fused_relu for b in bns)
-                 and torch.is_grad_enabled())
-        if not fused:
+        if not self.fused_ok(x):
             if self.relu_in:
                 x = torch.relu(x)
             for c, b in zip(convs, bns):
                 x = b(c(x))
             return x
+        meta, params = self.meta_params()
+        return _BoardChain.apply(x, meta, self.relu_in, *params)
+
+    def fused_ok(self, x):
+        return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and tuple(x.shape[1:]) == (32, 3, 3)
+                and x.shape[0] > 0 and all(b.training and b.fused_relu for b in self.bns)
+                and torch.is_grad_enabled())
+
+    def meta_params(self):
+        """Advance the BatchNorms' batch counters (as their forward would) and collect the chain's arguments."""
         meta, params = [], []
-        for c, b in zip(convs, bns):
+        for c, b in zip(self.convs, self.bns):
             b.num_batches_tracked.add_(1)
             meta.append((b.running_mean, b.running_var, b.momentum, b.eps))
             params += [c.weight, b.weight, b.bias]
-        return _BoardChain.apply(x, meta, self.relu_in, *params)
+        return meta, params
+
+
+class _ChainHeads(nn.Module):
+    """A _ConvBNChain whose only consumer is the _FusedHeads pair, as one _ChainHeadsFn (fuse_bn_relu's
+    rewrite); anything the fused path does not take runs the two modules one after the other."""
+
+    def __init__(self, chain, heads):
+        super().__init__()
+        object.__setattr__(self, 'chain', chain)
+        object.__setattr__(self, 'heads', heads)
+
+    def forward(self, x):
+        if not self.chain.fused_ok(x):
+            return self.heads(self.chain(x))
+        (cp, fp), (cv, fv) = _board_head_spec(self.heads.head_p), _board_head_spec(self.heads.head_v)
+        meta, params = self.chain.meta_params()
+        return _ChainHeadsFn.apply(x, meta, self.chain.relu_in, cp.weight, cp.bias, cv.weight, cv.bias, fp.weight,
+                                   fv.weight, *params)
+
+
+def _fuse_chain_heads(gm):
+    """Merge a chain call whose only user is the fused heads call into one _ChainHeads call; 0 or 1."""
+    for node in list(gm.graph.nodes):
+        if node.op != 'call_module' or not isinstance(gm.get_submodule(node.target), _FusedHeads):
+            continue
+        src = node.args[0] if len(node.args) == 1 else None
+        if not (isinstance(src, torch.fx.Node) and src.op == 'call_module'
+                and isinstance(gm.get_submodule(src.target), _ConvBNChain) and len(src.users) == 1):
+            return 0
+        gm.add_submodule('_hrl_chain_heads', _ChainHeads(gm.get_submodule(src.target), gm.get_submodule(node.target)))
+        with gm.graph.inserting_before(src):
+            call = gm.graph.call_module('_hrl_chain_heads', src.args)
+        node.replace_all_uses_with(call)
+        gm.graph.erase_node(node)
+        gm.graph.erase_node(src)
+        return 1
+    return 0
 
 
 class _LeafTracer(torch.fx.Tracer):
@@ -1243,6 +1365,8 @@ def fuse_bn_relu(model, example=None):
             anchor = item
         merged += 1
     fused_heads = _fuse_heads(gm, heads) if heads else 0
+    if fused_heads:
+        fused_heads += _fuse_chain_heads(gm)
     if not pairs and not merged and not fused_heads:
         return 0
     gm.graph.lint()

@@ -186,7 +186,7 @@ def test_fx_fusion_in_learner(cuda):
     keys = list(net.state_dict())
     step = LearnerStep(net, default_args(9, 64), cuda)
     step.step(tictactoe_batch(64, 9, cuda, seed=0))
-    assert step.fused_pairs == 5   # three BN->ReLU folds + one conv-BN chain + the two heads as one kernel
+    assert step.fused_pairs == 6   # three BN->ReLU folds + one conv-BN chain + the two heads + chain and heads joined
     assert all(m.fused_relu for m in net.modules() if isinstance(m, BatchNorm2d))
     assert hasattr(step.net, '_hrl_heads') if hasattr(step.net, 'graph') else True
     assert list(net.state_dict()) == keys
