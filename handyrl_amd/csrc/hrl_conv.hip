@@ -445,6 +445,21 @@ __global__ void conv3x3_pack_kernel(const float *__restrict__ w, int flip, float
     wpk[i] = v;
 }
 
+// Both layouts of up to 8 weights in one launch: packed[(l*2 + flip) * kPack + i] (hrl_conv3x3_pack_n)
+constexpr int kPack = kTaps * 2 * kC * 16;
+struct WeightList {
+    const float *w[8];
+};
+__global__ void conv3x3_pack_n_kernel(WeightList wl, int n, float *__restrict__ packed) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * 2 * kPack) return;
+    const int l = i / (2 * kPack), flip = (i / kPack) & 1, e = i % kPack;
+    const int j = e % 16, k = (e / 16) % kC, ct = (e / (16 * kC)) % 2, tap = e / (16 * kC * 2);
+    const int out_c = ct * 16 + j, in_c = k;
+    const float *w = wl.w[l];
+    packed[i] = !flip ? w[(out_c * kC + in_c) * kTaps + tap] : w[(in_c * kC + out_c) * kTaps + (kTaps - 1 - tap)];
+}
+
 // One 4-wave workgroup per CU (LDS: 109 KB forward, 145 KB weight gradient);
 // the waves walk row tiles grid-stride so the next tile's loads overlap MFMAs.
 constexpr int kGrid = 256;
@@ -486,11 +501,14 @@ int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, con
     if (epilogue == 2 && (!ep_mean || !ep_alpha || !ep_beta)) return HRL_EINVAL;
     if (epilogue >= 2 && bias) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    float *wpk = static_cast<float *>(workspace);
-    hipLaunchKernelGGL(conv3x3_pack_kernel, dim3((kTaps * 2 * kC * 16 + 255) / 256), dim3(256), 0, s, weight, flip,
-                       wpk);
-    int rc = status();
-    if (rc) return rc;
+    const float *wpk = weight;   // flip & 2: `weight` is already in the packed layout (hrl_conv3x3_pack_n)
+    if (!(flip & 2)) {
+        float *dst = static_cast<float *>(workspace);
+        hipLaunchKernelGGL(conv3x3_pack_kernel, dim3((kPack + 255) / 256), dim3(256), 0, s, weight, flip & 1, dst);
+        const int rc = status();
+        if (rc) return rc;
+        wpk = dst;
+    }
     const dim3 grid(grid_for(M)), block(kThreads);
 #define HRL_CONV_LAUNCH(PRO, EPI)                                                                            \
     hipLaunchKernelGGL((conv3x3_kernel<PRO, EPI>), grid, block, 0, s, x, M, wpk, bias, in_alpha, in_beta, ref, \
@@ -503,6 +521,18 @@ int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, con
     default: if (pro) HRL_CONV_LAUNCH(true, 3); else HRL_CONV_LAUNCH(false, 3); break;
     }
 #undef HRL_CONV_LAUNCH
+    return status();
+}
+
+int hrl_conv3x3_pack_n(const float *const *weights, int n, float *packed, void *stream) {
+    if (n < 1 || n > 8 || !weights || !packed) return HRL_EINVAL;
+    WeightList wl{};
+    for (int i = 0; i < n; ++i) {
+        if (!weights[i]) return HRL_EINVAL;
+        wl.w[i] = weights[i];
+    }
+    hipLaunchKernelGGL(conv3x3_pack_n_kernel, dim3((n * 2 * kPack + 255) / 256), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), wl, n, packed);
     return status();
 }
 

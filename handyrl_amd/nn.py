@@ -1034,11 +1034,16 @@ def _chain_forward(h0, meta, relu_in, params, apply_out=True):
     x = h0
     a_prev, b_prev = (unit[0], unit[1]) if relu_in else (None, None)
     ys, coefs = [], []
+    # every conv's forward and input-gradient weight layouts in one launch (the backward reuses them)
+    weights = [params[3 * i].contiguous() for i in range(len(meta))]
+    packed = torch.empty(len(weights), 2, 9216, dtype=torch.float32, device=dev)
+    _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array(weights), len(weights), P(packed), stream),
+                  'hrl_conv3x3_pack_n')
     for i, (rm, rv, momentum, eps) in enumerate(meta):
         w, gamma, beta = params[3 * i:3 * i + 3]
         y = torch.empty_like(h0)
-        _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(a_prev), P(b_prev), P(w), None, 0, P(y), 1, None, None,
-                                                 None, None, P(part), P(ws), ws_bytes, stream),
+        _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(a_prev), P(b_prev), P(packed[i, 0]), None, 2, P(y), 1,
+                                                 None, None, None, None, P(part), P(ws), ws_bytes, stream),
                       'hrl_conv3x3_forward_ex')
         coef = torch.empty(4, 32, dtype=torch.float32, device=dev)   # mean, invstd, alpha, beta
         _native.check(lib.hrl_bn_finalize_stats(P(part), nblk, 32, M * 9, P(gamma), P(beta), P(rm), P(rv),
@@ -1051,10 +1056,10 @@ def _chain_forward(h0, meta, relu_in, params, apply_out=True):
     if apply_out:
         out = torch.empty_like(h0)
         _native.check(lib.hrl_bn_apply(P(x), M, 32, 9, P(a_prev), P(b_prev), 1, P(out), stream), 'hrl_bn_apply')
-    return out, ys, coefs, unit
+    return out, ys, coefs, unit, packed
 
 
-def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, part_in=None, nblk_in=0):
+def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, packed, part_in=None, nblk_in=0):
     """Backward of the chain from g = dL/d(chain output); with part_in the last BN's backward sums were already
     formed by the consumer (fused heads).  Returns (dL/dh0 | None, parameter gradients)."""
     lib = _native.load()
@@ -1100,14 +1105,15 @@ def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, pa
         grads[3 * i:3 * i + 3] = [_ret(bw), _ret(bgam), _ret(bbet)]
         if i > 0:   # dL/dh_i, and BN_{i-1}'s backward sums in the same launch
             g = torch.empty_like(h0)
-            _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g), 2, P(ys[i - 1]),
+            _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(packed[i, 1]), None, 3, P(g), 2,
+                                                     P(ys[i - 1]),
                                                      P(coefs[i - 1][0]), P(coefs[i - 1][2]),
                                                      P(coefs[i - 1][3]), P(part), P(ws), ws_bytes, stream),
                           'hrl_conv3x3_forward_ex(flip, bn sums)')
             sums, sums_n = part, nblk
         elif need_input_grad:
             g = torch.empty_like(h0)
-            _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(w), None, 1, P(g),
+            _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(packed[i, 1]), None, 3, P(g),
                                                      3 if relu_in else 0, P(h0) if relu_in else None,
                                                      None, None, None, None, P(ws), ws_bytes, stream),
                           'hrl_conv3x3_forward_ex(flip)')
@@ -1135,8 +1141,8 @@ class _BoardChain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h0, meta, relu_in, *params):
         h0 = h0.contiguous()
-        out, ys, coefs, unit = _chain_forward(h0, meta, relu_in, params)
-        ctx.save_for_backward(h0, *ys, *coefs, *params)
+        out, ys, coefs, unit, packed = _chain_forward(h0, meta, relu_in, params)
+        ctx.save_for_backward(h0, *ys, *coefs, packed, *params)
         ctx.n = len(meta)
         ctx.relu_in = relu_in
         return out
@@ -1145,9 +1151,9 @@ class _BoardChain(torch.autograd.Function):
     def backward(ctx, g):
         n = ctx.n
         t = ctx.saved_tensors
-        h0, ys, coefs, params = t[0], list(t[1:1 + n]), list(t[1 + n:1 + 2 * n]), t[1 + 2 * n:]
+        h0, ys, coefs, packed, params = t[0], list(t[1:1 + n]), list(t[1 + n:1 + 2 * n]), t[1 + 2 * n], t[2 + 2 * n:]
         unit = _unit_coefs(h0.device) if ctx.relu_in else None
-        g_in, grads = _chain_backward(h0, ys, coefs, unit, params, ctx.relu_in, g, ctx.needs_input_grad[0])
+        g_in, grads = _chain_backward(h0, ys, coefs, unit, params, ctx.relu_in, g, ctx.needs_input_grad[0], packed)
         return (g_in, None, None, *grads)
 
 
@@ -1159,7 +1165,7 @@ class _ChainHeadsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h0, meta, relu_in, w1p, b1p, w1v, b1v, wp, wv, *params):
         h0 = h0.contiguous()
-        _, ys, coefs, unit = _chain_forward(h0, meta, relu_in, params, apply_out=False)
+        _, ys, coefs, unit, packed = _chain_forward(h0, meta, relu_in, params, apply_out=False)
         y, coef = ys[-1], coefs[-1]
         N = h0.shape[0]
         dev = h0.device
@@ -1173,7 +1179,7 @@ class _ChainHeadsFn(torch.autograd.Function):
         _native.check(lib.hrl_heads_forward(P(y), N, P(w1p), P(b1p.contiguous()), P(w1v), P(b1v.contiguous()),
                                             P(wp), P(wv), P(coef[2]), P(coef[3]), P(a_p), P(a_v), P(p), P(v),
                                             _native.stream_of(dev)), 'hrl_heads_forward(bn)')
-        ctx.save_for_backward(h0, *ys, *coefs, a_p, a_v, w1p, w1v, wp, wv, *params)
+        ctx.save_for_backward(h0, *ys, *coefs, a_p, a_v, w1p, w1v, wp, wv, packed, *params)
         ctx.biases = (b1p, b1v)
         ctx.n = len(meta)
         ctx.relu_in = relu_in
@@ -1184,8 +1190,8 @@ class _ChainHeadsFn(torch.autograd.Function):
         n = ctx.n
         t = ctx.saved_tensors
         h0, ys, coefs = t[0], list(t[1:1 + n]), list(t[1 + n:1 + 2 * n])
-        a_p, a_v, w1p, w1v, wp, wv = t[1 + 2 * n:7 + 2 * n]
-        params = t[7 + 2 * n:]
+        a_p, a_v, w1p, w1v, wp, wv, packed = t[1 + 2 * n:8 + 2 * n]
+        params = t[8 + 2 * n:]
         b1p, b1v = ctx.biases
         N = h0.shape[0]
         dev = h0.device
@@ -1205,7 +1211,7 @@ class _ChainHeadsFn(torch.autograd.Function):
                                              P(db1p), P(dw1v), P(db1v), P(dwp), P(dwv), P(ws), ws_bytes,
                                              _native.stream_of(dev)), 'hrl_heads_backward(bn)')
         unit = _unit_coefs(dev) if ctx.relu_in else None
-        g_in, grads = _chain_backward(h0, ys, coefs, unit, params, ctx.relu_in, dh, ctx.needs_input_grad[0],
+        g_in, grads = _chain_backward(h0, ys, coefs, unit, params, ctx.relu_in, dh, ctx.needs_input_grad[0], packed,
                                       part_in=bn_part, nblk_in=nparts)
         return (g_in, None, None, *(_ret(b) for b in hbufs), *grads)
 
@@ -1249,9 +1255,9 @@ class _ConvBNChain(nn.Module):
 
     def meta_params(self):
         """Advance the BatchNorms' batch counters (as their forward would) and collect the chain's arguments."""
+        torch._foreach_add_([b.num_batches_tracked for b in self.bns], 1)   # one launch for all counters
         meta, params = [], []
         for c, b in zip(self.convs, self.bns):
-            b.num_batches_tracked.add_(1)
             meta.append((b.running_mean, b.running_var, b.momentum, b.eps))
             params += [c.weight, b.weight, b.bias]
         return meta, params

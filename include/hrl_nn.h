@@ -144,6 +144,10 @@ int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, 
  * hrl_conv3x3_forward / hrl_conv3x3_wgrad are these with nothing fused.
  */
 int64_t hrl_conv3x3_stats_blocks(int64_t M);
+/* Both packed layouts of n <= 8 weights (32, 32, 3, 3) in one launch: packed[(l*2 + f) * 9216], f = 0 forward,
+ * 1 input gradient (host array of device pointers).  hrl_conv3x3_forward_ex with flip | 2 takes `weight`
+ * as such a packed layout and skips its own packing launch. */
+int hrl_conv3x3_pack_n(const float *const *weights, int n, float *packed, void *stream);
 int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, const float *in_beta,
                            const float *weight, const float *bias, int flip, float *y, int epilogue,
                            const float *ref, const float *ep_mean, const float *ep_alpha, const float *ep_beta,
