@@ -53,10 +53,11 @@ struct Coef {
 
 // torch.max(a, b) on two tensors propagates NaN (losses.py:36).  Written as selects
 // (v_cndmask), not early returns: the branches the early-return form compiled to
-// (two exec-mask regions per time step) sat on the scan's serial chain.
+// (two exec-mask regions per time step) sat on the scan's serial chain.  x is the
+// carried v[t+1], known a step ahead, so its NaN test is off the chain; a NaN y fails
+// `x > y` and is selected as is.  Same result, payloads included, as testing both.
 __device__ __forceinline__ float max_nan(float x, float y) {
-    float m = x > y ? x : y;
-    m = (y != y) ? y : m;
+    const float m = x > y ? x : y;
     return (x != x) ? x : m;
 }
 
@@ -321,9 +322,8 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
 
     // One time step: the reference recurrences on the carry; results stay in registers (no LDS
     // traffic on the serial chain, so no lgkmcnt waits between steps).
-    auto one_step = [&](int tt, int t0, float v, float r, float rho, float cc, float ret_t, float &tgt_out,
-                        float &adv_out) {
-        const bool last = (t0 + tt == T - 1);
+    auto one_step = [&](bool last, float v, float r, float rho, float cc, float ret_t, float &tgt_out,
+                        float &adv_out) __attribute__((always_inline)) {
         float adv, adv_unused;
         Carry nx = s;
         if constexpr (TGT != kNone && TGT != ADV) {
@@ -364,6 +364,47 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
     // full vmcnt(0) -- draining the prefetched chunk -- in front of the recurrence.
     asm volatile("" : "+v"(boot));
 
+    // The recurrence over one chunk held in LDS.  TOP: the chunk holds t = T-1 (the bootstrap
+    // step).  Chunks are cut from t = 0, so only the top chunk can be partial; a FULL chunk
+    // has no per-step guards and a compile-time bootstrap test (tt == kTChunk-1 in a full top
+    // chunk, never elsewhere), so its serial chain has no compares, branches or spilled step
+    // indices.  Only a partial top chunk (T % kTChunk != 0) tests `last` at run time.
+    auto recur = [&](int tc, auto full, auto top) __attribute__((always_inline)) {
+        constexpr bool F = decltype(full)::value;
+        constexpr bool TOP = decltype(top)::value;
+        // every LDS read is issued ahead of the dependent chain (tc is wave-uniform, so the
+        // guards of a partial chunk are scalar branches)
+        float xv[kTChunk], xr[kTChunk], xrho[kTChunk], xc[kTChunk], xret[kTChunk];
+#pragma unroll
+        for (int tt = 0; tt < kTChunk; ++tt) {
+            if (F || tt < tc) {
+                const int iv = vbase + tt * C;
+                const int ir = rbase + tt * a.rhoC;
+                xv[tt] = t_v[iv];
+                xr[tt] = REW ? t_r[iv] : 0.f;
+                xrho[tt] = kRho ? t_rho[ir] : 0.f;
+                xc[tt] = kRho ? t_cs[ir] : 0.f;
+                xret[tt] = kRet ? t_ret[iv] : boot;
+            }
+        }
+        float ot[kTChunk], oa[kTChunk];
+#pragma unroll
+        for (int tt = kTChunk - 1; tt >= 0; --tt) {
+            if (F || tt < tc) {
+                const bool last = TOP && (F ? tt == kTChunk - 1 : tt == tc - 1);
+                one_step(last, xv[tt], xr[tt], xrho[tt], xc[tt], xret[tt], ot[tt], oa[tt]);
+            }
+        }
+#pragma unroll
+        for (int tt = 0; tt < kTChunk; ++tt) {
+            if (F || tt < tc) {
+                const int iv = vbase + tt * C;
+                if constexpr (TGT != kNone) t_tgt[iv] = ot[tt];
+                t_adv[iv] = oa[tt];
+            }
+        }
+    };
+
     auto process = [&](int ch, auto prefetch) {
         const int t0 = ch * kTChunk;
         const int tc = min(kTChunk, T - t0);
@@ -379,34 +420,9 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
         __syncthreads();
 
         if (active) {
-            // every LDS read is issued ahead of the dependent chain (tc is wave-uniform, so the
-            // guards of a partial chunk are scalar branches)
-            float xv[kTChunk], xr[kTChunk], xrho[kTChunk], xc[kTChunk], xret[kTChunk];
-#pragma unroll
-            for (int tt = 0; tt < kTChunk; ++tt) {
-                if (tt < tc) {
-                    const int iv = vbase + tt * C;
-                    const int ir = rbase + tt * a.rhoC;
-                    xv[tt] = t_v[iv];
-                    xr[tt] = REW ? t_r[iv] : 0.f;
-                    xrho[tt] = kRho ? t_rho[ir] : 0.f;
-                    xc[tt] = kRho ? t_cs[ir] : 0.f;
-                    xret[tt] = kRet ? t_ret[iv] : boot;
-                }
-            }
-            float ot[kTChunk], oa[kTChunk];
-#pragma unroll
-            for (int tt = kTChunk - 1; tt >= 0; --tt) {
-                if (tt < tc) one_step(tt, t0, xv[tt], xr[tt], xrho[tt], xc[tt], xret[tt], ot[tt], oa[tt]);
-            }
-#pragma unroll
-            for (int tt = 0; tt < kTChunk; ++tt) {
-                if (tt < tc) {
-                    const int iv = vbase + tt * C;
-                    if constexpr (TGT != kNone) t_tgt[iv] = ot[tt];
-                    t_adv[iv] = oa[tt];
-                }
-            }
+            if (ch != nchunks - 1) recur(tc, std::true_type{}, std::false_type{});
+            else if (tc == kTChunk) recur(tc, std::true_type{}, std::true_type{});
+            else recur(tc, std::false_type{}, std::true_type{});
         }
         __syncthreads();
 
