@@ -64,6 +64,41 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// ---- exact three-way bf16 split of fp32 operands (the SPLIT path) ----
+// x = h + m + l EXACTLY: h = x with the low 16 bits cleared (8 significant bits),
+// r = x - h is exact (<= 16 significant bits), m = r with the low 16 bits cleared,
+// l = r - m is exact and has <= 8 significant bits, so it is a bf16 as is.  A product
+// x*w keeps the six terms hh, hm, mh, hl, lh, mm; the dropped ml, lm, ll are below
+// 2^-23 |x w| together -- the size of one fp32 rounding.  Every bf16 x bf16 product is
+// exact in fp32 and the MFMA accumulates in fp32, so the result is fp32-accurate, at
+// 6/16 of the fp32 MFMA's cycles (gfx950: v_mfma_f32_16x16x4_f32 runs at 1/16 of the
+// bf16 rate, MI355X_MICROARCH.md).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(float x, uint32_t &h, uint32_t &m, uint32_t &l) {
+    const uint32_t xb = __float_as_uint(x);
+    const uint32_t hb = xb & 0xffff0000u;
+    const float r = x - __uint_as_float(hb);
+    const uint32_t rb = __float_as_uint(r);
+    const uint32_t mb = rb & 0xffff0000u;
+    const float lo = r - __uint_as_float(mb);
+    h = hb >> 16;
+    m = mb >> 16;
+    l = __float_as_uint(lo) >> 16;
+}
+
+// part 0/1/2 (h/m/l) of x as the 16 bf16 bits
+__device__ __forceinline__ uint32_t split_part(float x, int part) {
+    uint32_t h, m, l;
+    split3(x, h, m, l);
+    return part == 0 ? h : (part == 1 ? m : l);
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(const uint4 &a, const uint4 &b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                   c, 0, 0, 0);
+}
+
 // ------------------------------------------------------------------ forward / input gradient
 // x: (M, 288) rows; wpk: packed [tap][ct][ci][16] = W'[tap][ci][ct*16+j]; y: (M, 288)
 // Forward / input gradient.
@@ -89,7 +124,7 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 //   partials go to part[block][c][2] (fp64), the layout bn_finalize_kernel folds.
 //   ref tiles (EPI 2, 3) are loaded with the next input tile and transposed
 //   to the accumulator layout through the tile's LDS buffer.
-template <bool PRO, int EPI>
+template <bool PRO, int EPI, bool SPLIT>
 __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restrict__ x, int64_t M,
                                                            const float *__restrict__ wpk,
                                                            const float *__restrict__ bias,
@@ -102,18 +137,37 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
                                                            float *__restrict__ y, double *__restrict__ part) {
     constexpr bool kRef = EPI == 2 || EPI == 3;
     constexpr bool kSums = EPI == 1 || EPI == 2;
-    __shared__ float w_lds[kTaps * 2 * kC * 16];           // 36 KB
+    // fp32: packed [tap][ct][ci][16] (36 KB).  SPLIT: the B fragments of
+    // v_mfma_f32_16x16x32_bf16, [tap][ct][part h/m/l][lane] x 4 dwords (54 KB): lane l's
+    // 8 bf16 are W'[tap][ci = 8(l>>4) + e][co = 16ct + (l&15)], e = 0..7, one
+    // conflict-free ds_read_b128 per fragment.
+    constexpr int kWWords = SPLIT ? kTaps * 2 * 3 * 64 * 4 : kTaps * 2 * kC * 16;
+    __shared__ __attribute__((aligned(16))) uint32_t w_lds_u[kWWords];
     __shared__ float a_lds[kWaves][kTile * kStride];       // 4 x 18.1 KB
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < kTaps * 2 * kC * 16; i += kThreads) w_lds[i] = wpk[i];
-    // PRO: a lane's A fragments are input channels 4s + (lane>>4), s = 0..7
+    if constexpr (SPLIT) {
+        for (int i = threadIdx.x; i < kWWords; i += kThreads) {
+            const int d = i & 3, l = (i >> 2) & 63, f = i >> 8;      // f = (tap*2 + ct)*3 + part
+            const int part = f % 3, tc = f / 3;                      // tc = tap*2 + ct
+            const int ci = 8 * (l >> 4) + 2 * d, j = l & 15;
+            const float w0 = wpk[(tc * kC + ci) * 16 + j];
+            const float w1 = wpk[(tc * kC + ci + 1) * 16 + j];
+            w_lds_u[i] = split_part(w0, part) | (split_part(w1, part) << 16);
+        }
+    } else {
+        for (int i = threadIdx.x; i < kWWords; i += kThreads) w_lds_u[i] = __float_as_uint(wpk[i]);
+    }
+    const float *w_lds = reinterpret_cast<const float *>(w_lds_u);
+    // PRO: a lane's A fragments are input channels 4s + (lane>>4), s = 0..7 (fp32 path)
+    // or 8(lane>>4) + e, e = 0..7 (SPLIT)
     float pa[PRO ? kC / 4 : 1], pb[PRO ? kC / 4 : 1];
     if constexpr (PRO) {
 #pragma unroll
         for (int s = 0; s < kC / 4; ++s) {
-            pa[s] = in_alpha[4 * s + (lane >> 4)];
-            pb[s] = in_beta[4 * s + (lane >> 4)];
+            const int ci = SPLIT ? 8 * (lane >> 4) + s : 4 * s + (lane >> 4);
+            pa[s] = in_alpha[ci];
+            pb[s] = in_beta[ci];
         }
     }
     // epilogue: a lane's outputs are channels (lane & 15) and 16 + (lane & 15)
@@ -177,6 +231,79 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
         const int ak = lane >> 4;          // A/B k within the 4-wide step
         const float *arow = as + ar * kStride;
         const float *wl = w_lds + ak * 16 + (lane & 15);
+        if constexpr (SPLIT) {
+            const uint4 *wb = reinterpret_cast<const uint4 *>(w_lds_u) + lane;
+            // A fragment of cell p: row ar, input channels 8*ak + e (e = 0..7); the next cell's
+            // A reads are issued before this cell's MFMAs.
+            const float *acol = arow + 8 * ak * kCells;
+            float an[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) an[e] = acol[e * kCells];
+            auto cell = [&](int p) __attribute__((always_inline)) {
+                float av[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) av[e] = an[e];
+                if (p + 1 < kCells) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) an[e] = acol[e * kCells + p + 1];
+                }
+                uint32_t ah[4], am[4], al[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    float v[2];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int e = 2 * d + u;
+                        float a = av[e];
+                        if constexpr (PRO) {   // input channel 8ak+e: the previous block's BN+ReLU
+                            const float t = a * pa[e] + pb[e];
+                            a = t < 0.f ? 0.f : t;
+                        }
+                        v[u] = a;
+                    }
+                    uint32_t h0, m0, l0, h1, m1, l1;
+                    split3(v[0], h0, m0, l0);
+                    split3(v[1], h1, m1, l1);
+                    ah[d] = h0 | (h1 << 16);
+                    am[d] = m0 | (m1 << 16);
+                    al[d] = l0 | (l1 << 16);
+                }
+                const uint4 Ah = make_uint4(ah[0], ah[1], ah[2], ah[3]);
+                const uint4 Am = make_uint4(am[0], am[1], am[2], am[3]);
+                const uint4 Al = make_uint4(al[0], al[1], al[2], al[3]);
+                const int py = p / kBoard, px = p - py * kBoard;
+#pragma unroll
+                for (int q = 0; q < kCells; ++q) {
+                    // tap_of(p, q) with p uniform at run time: a scalar branch
+                    const int dy = py - q / kBoard + 1, dx = px - q % kBoard + 1;
+                    if (dy < 0 || dy > 2 || dx < 0 || dx > 2) continue;
+                    const int tap = dy * 3 + dx;
+#pragma unroll
+                    for (int ct = 0; ct < 2; ++ct) {
+                        const uint4 *wf = wb + (tap * 2 + ct) * 3 * 64;
+                        const uint4 Bh = wf[0], Bm = wf[64], Bl = wf[128];
+                        f32x4 c = acc[q][ct];
+                        c = mfma_bf16(Al, Bh, c);   // smallest terms first
+                        c = mfma_bf16(Am, Bm, c);
+                        c = mfma_bf16(Ah, Bl, c);
+                        c = mfma_bf16(Am, Bh, c);
+                        c = mfma_bf16(Ah, Bm, c);
+                        c = mfma_bf16(Ah, Bh, c);
+                        acc[q][ct] = c;
+                    }
+                }
+            };
+            if constexpr (kRef) {
+                // the reference tile's 72 staging registers leave no room for the unrolled form
+                // (every cell's fragments and B reads hoisted: spills), so the cell loop stays a
+                // loop and tap_of(p, q) a scalar branch
+#pragma unroll 1
+                for (int p = 0; p < kCells; ++p) cell(p);
+            } else {
+#pragma unroll
+                for (int p = 0; p < kCells; ++p) cell(p);
+            }
+        } else {
 #pragma unroll
         for (int p = 0; p < kCells; ++p) {
 #pragma unroll
@@ -194,6 +321,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
                     acc[q][1] = mfma(a, wl[((tap * 2 + 1) * kC) * 16 + s * 64], acc[q][1]);
                 }
             }
+        }
         }
 
         const int64_t valid = M - tile * kTile;          // rows of this tile inside the batch
@@ -460,6 +588,9 @@ __global__ void conv3x3_pack_n_kernel(WeightList wl, int n, float *__restrict__ 
     packed[i] = !flip ? w[(out_c * kC + in_c) * kTaps + tap] : w[(in_c * kC + out_c) * kTaps + (kTaps - 1 - tap)];
 }
 
+// Forward / input-gradient arithmetic: exact-split bf16 MFMA (1, default) or fp32 MFMA (0).
+int g_split = 1;
+
 // One 4-wave workgroup per CU (LDS: 109 KB forward, 145 KB weight gradient);
 // the waves walk row tiles grid-stride so the next tile's loads overlap MFMAs.
 constexpr int kGrid = 256;
@@ -488,6 +619,12 @@ int64_t hrl_conv3x3_workspace_bytes(int64_t M) {
 
 int64_t hrl_conv3x3_stats_blocks(int64_t M) { return M < 1 ? -1 : grid_for(M); }
 
+int hrl_conv3x3_set_split(int on) {
+    const int prev = g_split;
+    g_split = on ? 1 : 0;
+    return prev;
+}
+
 int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, const float *in_beta,
                            const float *weight, const float *bias, int flip, float *y, int epilogue,
                            const float *ref, const float *ep_mean, const float *ep_alpha, const float *ep_beta,
@@ -510,9 +647,15 @@ int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, con
         wpk = dst;
     }
     const dim3 grid(grid_for(M)), block(kThreads);
-#define HRL_CONV_LAUNCH(PRO, EPI)                                                                            \
-    hipLaunchKernelGGL((conv3x3_kernel<PRO, EPI>), grid, block, 0, s, x, M, wpk, bias, in_alpha, in_beta, ref, \
-                       ep_mean, ep_alpha, ep_beta, y, part)
+#define HRL_CONV_LAUNCH(PRO, EPI)                                                                             \
+    do {                                                                                                      \
+        if (g_split)                                                                                          \
+            hipLaunchKernelGGL((conv3x3_kernel<PRO, EPI, true>), grid, block, 0, s, x, M, wpk, bias, in_alpha, \
+                               in_beta, ref, ep_mean, ep_alpha, ep_beta, y, part);                            \
+        else                                                                                                  \
+            hipLaunchKernelGGL((conv3x3_kernel<PRO, EPI, false>), grid, block, 0, s, x, M, wpk, bias, in_alpha, \
+                               in_beta, ref, ep_mean, ep_alpha, ep_beta, y, part);                            \
+    } while (0)
     const bool pro = in_alpha != nullptr;
     switch (epilogue) {
     case 0: if (pro) HRL_CONV_LAUNCH(true, 0); else HRL_CONV_LAUNCH(false, 0); break;

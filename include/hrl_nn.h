@@ -144,6 +144,10 @@ int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, 
  * hrl_conv3x3_forward / hrl_conv3x3_wgrad are these with nothing fused.
  */
 int64_t hrl_conv3x3_stats_blocks(int64_t M);
+/* Arithmetic of the forward / input-gradient kernel: on != 0 (the default) an exact three-way bf16 split of
+ * both fp32 operands on v_mfma_f32_16x16x32_bf16 (six partial products, fp32 accumulation; error below one fp32
+ * rounding per product), 0 the fp32 v_mfma_f32_16x16x4_f32.  Process-wide; returns the previous setting. */
+int hrl_conv3x3_set_split(int on);
 /* Both packed layouts of n <= 8 weights (32, 32, 3, 3) in one launch: packed[(l*2 + f) * 9216], f = 0 forward,
  * 1 input gradient (host array of device pointers).  hrl_conv3x3_forward_ex with flip | 2 takes `weight`
  * as such a packed layout and skips its own packing launch. */

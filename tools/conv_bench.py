@@ -25,9 +25,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--M', type=int, default=131072)
     ap.add_argument('--iters', type=int, default=50)
+    ap.add_argument('--split', type=int, default=1, help='forward/input-gradient arithmetic: 1 split-bf16, 0 fp32 MFMA')
     opts = ap.parse_args()
     dev = torch.device('cuda', 0)
     lib = _native.load()
+    lib.hrl_conv3x3_set_split(opts.split)
     M = opts.M
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(M, 288, device=dev, generator=g)
@@ -80,7 +82,17 @@ def main():
     fwd()
     ref = torch.nn.functional.conv2d(x.view(M, 32, 3, 3), w, b, padding=1).view(M, 288)
     err = float((y - ref).abs().max())
-    res = {'M': M, 'fwd_max_abs_err': err}
+    # error against an fp64 reference, beside torch's own fp32 conv
+    r64 = torch.nn.functional.conv2d(x.view(M, 32, 3, 3).double(), w.double(), b.double(), padding=1).view(M, 288)
+    scale = float(r64.abs().max())
+    res = {'M': M, 'split': opts.split, 'fwd_max_abs_err_vs_torch32': err,
+           'fwd_max_err_vs_fp64_rel_to_max': float((y.double() - r64).abs().max()) / scale,
+           'torch32_max_err_vs_fp64_rel_to_max': float((ref.double() - r64).abs().max()) / scale,
+           'fwd_rms_rel_err_vs_fp64': float(((y.double() - r64).norm() / r64.norm())),
+           'torch32_rms_rel_err_vs_fp64': float(((ref.double() - r64).norm() / r64.norm()))}
+    dgrad()
+    d64 = torch.nn.grad.conv2d_input((M, 32, 3, 3), w.double(), dy.view(M, 32, 3, 3).double(), padding=1).view(M, 288)
+    res['dgrad_max_err_vs_fp64_rel_to_max'] = float((y.double() - d64).abs().max()) / float(d64.abs().max())
     for name, fn in (('fwd', fwd), ('dgrad', dgrad), ('wgrad', wgrad), ('fwd_pro_stats', fwd_pro_stats),
                      ('dgrad_bnred', dgrad_bnred), ('dgrad_mask', dgrad_mask), ('wgrad_pro', wgrad_pro),
                      ('fwd_again', fwd)):
