@@ -1,0 +1,87 @@
+"""Split-bf16 arithmetic of the board conv (csrc/hrl_conv.hip, hrl_conv3x3_set_split).
+
+The forward / input-gradient kernel splits both fp32 operands exactly into three bf16 parts and
+runs six partial products on v_mfma_f32_16x16x32_bf16 with fp32 accumulation.  Checked here:
+  * integer data (every product and partial sum exact in fp32) gives exactly the fp64 result,
+    so the bf16 fragment layouts (k order of A and B, both column tiles, every tap) are right;
+  * on random data the error against an fp64 reference is no larger than torch's own fp32
+    conv's error (tolerance: 2x torch-CPU fp32's max error, measured on the same data);
+  * the fp32-MFMA form (split off) gives the same results within the same bound.
+"""
+
+import pytest
+import torch
+
+from handyrl_amd import _native
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def cuda():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    return torch.device('cuda', 0)
+
+
+def _run(lib, dev, x, w, b, flip, split):
+    M = x.shape[0]
+    y = torch.empty_like(x)
+    ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    prev = lib.hrl_conv3x3_set_split(split)
+    try:
+        P = _native.ptr
+        _native.check(lib.hrl_conv3x3_forward(P(x), M, 32, 32, P(w), P(b) if b is not None else None, flip, P(y),
+                                              P(ws), ws_bytes, _native.stream_of(dev)), 'conv')
+        torch.cuda.synchronize(dev)
+    finally:
+        lib.hrl_conv3x3_set_split(prev)
+    return y
+
+
+def _ref64(x, w, b, flip):
+    M = x.shape[0]
+    x64, w64 = x.double().cpu().view(M, 32, 3, 3), w.double().cpu()
+    if flip:   # input gradient: the adjoint of the 'same' conv
+        return torch.nn.grad.conv2d_input((M, 32, 3, 3), w64, x64, padding=1).view(M, 288)
+    return torch.nn.functional.conv2d(x64, w64, None if b is None else b.double().cpu(), padding=1).view(M, 288)
+
+
+@pytest.mark.parametrize('flip', [0, 1])
+@pytest.mark.parametrize('split', [1, 0])
+def test_integer_data_is_exact(cuda, flip, split):
+    lib = _native.load()
+    g = torch.Generator().manual_seed(3 + flip)
+    M = 1000
+    x = torch.randint(-8, 9, (M, 288), generator=g).float()
+    w = torch.randint(-8, 9, (32, 32, 3, 3), generator=g).float()
+    b = None if flip else torch.randint(-8, 9, (32,), generator=g).float()
+    y = _run(lib, cuda, x.to(cuda), w.to(cuda), None if b is None else b.to(cuda), flip, split)
+    assert torch.equal(y.cpu().double(), _ref64(x, w, b, flip))
+
+
+@pytest.mark.parametrize('flip', [0, 1])
+@pytest.mark.parametrize('M', [17, 4099])
+def test_error_within_fp32_conv_error(cuda, flip, M):
+    lib = _native.load()
+    g = torch.Generator().manual_seed(M + flip)
+    # wide dynamic range: per-row scales over 2^-20 .. 2^20, a few exact zeros and negative zeros
+    x = torch.randn(M, 288, generator=g) * torch.exp2(torch.randint(-20, 21, (M, 1), generator=g).float())
+    x[::7, ::5] = 0.0
+    x[1::7, ::11] = -0.0
+    w = torch.randn(32, 32, 3, 3, generator=g) * 0.1
+    b = None if flip else torch.randn(32, generator=g)
+    ref = _ref64(x, w, b, flip)
+    M_ = x.shape[0]
+    if flip:
+        t32 = torch.nn.grad.conv2d_input((M_, 32, 3, 3), w, x.view(M_, 32, 3, 3), padding=1).view(M_, 288)
+    else:
+        t32 = torch.nn.functional.conv2d(x.view(M_, 32, 3, 3), w, b, padding=1).view(M_, 288)
+    # per-row error relative to the row's largest output (rows span 40 binades)
+    rowmax = ref.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+    bound = 2.0 * float(((t32.double() - ref).abs() / rowmax).max()) + 1e-7
+    for split in (1, 0):
+        y = _run(lib, cuda, x.to(cuda), w.to(cuda), None if b is None else b.to(cuda), flip, split).cpu().double()
+        err = float(((y - ref).abs() / rowmax).max())
+        assert err <= bound, (split, err, bound)
