@@ -57,6 +57,53 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Exact three-way bf16 split (x = h + m + l exactly; six partial products on
+// v_mfma_f32_16x16x32_bf16, fp32 accumulation): the arithmetic of hrl_conv.hip's
+// split path, see the error analysis there.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(float x, uint32_t &h, uint32_t &m, uint32_t &l) {
+    const uint32_t hb = __float_as_uint(x) & 0xffff0000u;
+    const float r = x - __uint_as_float(hb);
+    const uint32_t mb = __float_as_uint(r) & 0xffff0000u;
+    h = hb >> 16;
+    m = mb >> 16;
+    l = __float_as_uint(r - __uint_as_float(mb)) >> 16;
+}
+
+// 8 fp32 -> the h/m/l bf16x8 fragments
+__device__ __forceinline__ void split8(const float (&v)[8], uint4 &H, uint4 &M, uint4 &L) {
+    uint32_t h[4], m[4], l[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split3(v[2 * d], h0, m0, l0);
+        split3(v[2 * d + 1], h1, m1, l1);
+        h[d] = h0 | (h1 << 16);
+        m[d] = m0 | (m1 << 16);
+        l[d] = l0 | (l1 << 16);
+    }
+    H = make_uint4(h[0], h[1], h[2], h[3]);
+    M = make_uint4(m[0], m[1], m[2], m[3]);
+    L = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(const uint4 &a, const uint4 &b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                   c, 0, 0, 0);
+}
+
+// acc += A * B with both operands as exact splits (smallest terms first)
+__device__ __forceinline__ f32x4 mfma_split(const uint4 &Ah, const uint4 &Am, const uint4 &Al, const uint4 &Bh,
+                                            const uint4 &Bm, const uint4 &Bl, f32x4 c) {
+    c = mfma_bf16(Al, Bh, c);
+    c = mfma_bf16(Am, Bm, c);
+    c = mfma_bf16(Ah, Bl, c);
+    c = mfma_bf16(Am, Bh, c);
+    c = mfma_bf16(Ah, Bm, c);
+    return mfma_bf16(Ah, Bh, c);
+}
+
 __device__ __forceinline__ int torus_nbr(int q, int H, int W, int tap) {
     const int r = q / W, c = q - r * W;
     int rr = r + tap / 3 - 1, cc = c + tap % 3 - 1;
@@ -159,7 +206,7 @@ __device__ __forceinline__ void lds_fence() {
 // ------------------------------------------------------------------ forward / input gradient
 // x: (N, Cin, HW); wpk: [tap][KS][2][64]; y: (N, out_c, HW), out_c <= 32 (the first out_c channels of
 // the 32 computed); part: [grid][32][2] (STATS)
-template <int KS, bool VEC, bool STATS>
+template <int KS, bool VEC, bool STATS, bool SPLIT>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void torus_conv_kernel(const float *__restrict__ x, int64_t N, int Cin,
                                                               int H, int W, const float *__restrict__ wpk,
                                                               const float *__restrict__ bias, int out_c,
@@ -222,6 +269,41 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
         for (int mt = 0; mt < kMT; ++mt) acc[mt][0] = acc[mt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
         const float *wl = w_lds + lane;
+        if constexpr (SPLIT) {
+            // one k-step of 32 input channels per tap: lane l's A/B k are channels 8(l>>4) + e.
+            // nrow carries the fp32 mapping's channel offset (l>>4)*kS; move it to 8(l>>4)*kS.
+            const int cofs = 7 * (lane >> 4) * kS;
+#pragma unroll
+            for (int t = 0; t < kTaps; ++t) {
+                // B: W^T[ci][co = 16ct + (l&15)] from the packed [tap][s][ct][64] (ci = 4s + (l'>>4)),
+                // zero past the KS*4 packed channels
+                uint4 Bh[2], Bm[2], Bl[2];
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    float bv[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const int ci = 8 * (lane >> 4) + e;
+                        const int sk = ci >> 2;
+                        const float w = w_lds[((t * KS + min(sk, KS - 1)) * 2 + ct) * 64 + (ci & 3) * 16 + (lane & 15)];
+                        bv[e] = sk < KS ? w : 0.f;
+                    }
+                    split8(bv, Bh[ct], Bm[ct], Bl[ct]);
+                }
+#pragma unroll
+                for (int mt = 0; mt < kMT; ++mt) {
+                    const float *ap = tile + nrow[mt][t / 3] + ncol[mt][t % 3] + cofs;
+                    float av[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) av[e] = ap[e * kS];
+                    uint4 Ah, Am, Al;
+                    split8(av, Ah, Am, Al);
+#pragma unroll
+                    for (int ct = 0; ct < 2; ++ct)
+                        acc[mt][ct] = mfma_split(Ah, Am, Al, Bh[ct], Bm[ct], Bl[ct], acc[mt][ct]);
+                }
+            }
+        } else {
 #pragma unroll
         for (int t = 0; t < kTaps; ++t) {
 #pragma unroll
@@ -235,6 +317,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
                     acc[mt][1] = mfma(a, b1, acc[mt][1]);
                 }
             }
+        }
         }
         lds_fence();   // every lane's A reads done before the tile is overwritten
 
@@ -270,7 +353,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
                      add ? add_mask + ob : nullptr);
         lds_fence();
         // padding rows must read as zero again for the next sample (the output tile used them)
-        for (int i = in_elem / HW * kS + lane; i < KS * 4 * kS; i += 64) tile[i] = 0.f;
+        for (int i = in_elem / HW * kS + lane; i < (SPLIT ? kCo : KS * 4) * kS; i += 64) tile[i] = 0.f;
     }
     if constexpr (STATS) {
         // fold the 4 lanes sharing a channel and the 4 waves in a fixed order
@@ -462,9 +545,18 @@ bool shape_ok(int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W) {
 constexpr int64_t kPackFloats = kTaps * 8 * 2 * 64;
 constexpr int64_t kPartFloats = kTaps * kCo * kCo + kCo;
 
+// Forward / input-gradient arithmetic: exact-split bf16 MFMA (1, default) or fp32 MFMA (0).
+int g_split = 1;
+
 }  // namespace
 
 extern "C" {
+
+int hrl_torus_set_split(int on) {
+    const int prev = g_split;
+    g_split = on ? 1 : 0;
+    return prev;
+}
 
 int64_t hrl_torus_workspace_bytes(int64_t N) {
     if (N < 1) return -1;
@@ -496,8 +588,14 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
     const bool vec_out = (out_c * HW) % 4 == 0 && aligned16(y) && (!add || (aligned16(add) && aligned16(add_mask)));
     const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
 #define HRL_TORUS_LAUNCH(KS_, VEC_, ST_)                                                                           \
-    hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_>), grid, block, 0, s, x, N, in_c, (int)H, (int)W, wpk,    \
-                       bias, out_c, vec_out, y, part, add, add_mask)
+    do {                                                                                                         \
+        if (g_split)                                                                                             \
+            hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_, true>), grid, block, 0, s, x, N, in_c, (int)H,  \
+                               (int)W, wpk, bias, out_c, vec_out, y, part, add, add_mask);                       \
+        else                                                                                                     \
+            hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_, false>), grid, block, 0, s, x, N, in_c, (int)H, \
+                               (int)W, wpk, bias, out_c, vec_out, y, part, add, add_mask);                       \
+    } while (0)
     const bool st = part != nullptr;
     if (KS == 8) {
         if (vec) { if (st) HRL_TORUS_LAUNCH(8, true, true); else HRL_TORUS_LAUNCH(8, true, false); }

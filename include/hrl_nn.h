@@ -213,6 +213,9 @@ int hrl_hidden_update_backward(const float *const *dout, const float *mask, int6
  * workspace: hrl_torus_workspace_bytes(N) bytes.
  */
 int64_t hrl_torus_workspace_bytes(int64_t N);
+/* Arithmetic of the torus forward / input-gradient kernel, as hrl_conv3x3_set_split: on != 0 (default) the exact
+ * three-way bf16 split on v_mfma_f32_16x16x32_bf16, 0 fp32 MFMA.  Process-wide; returns the previous setting. */
+int hrl_torus_set_split(int on);
 int64_t hrl_torus_stats_blocks(int64_t N);
 int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
                            const float *weight, const float *bias, int flip, float *y, double *part,

@@ -1,4 +1,4 @@
-"""Time the torus-conv kernels (csrc/hrl_torus.hip) at the Geese learner size: python tools/torus_bench.py [N]."""
+"""Time the torus-conv kernels (csrc/hrl_torus.hip) at the Geese learner size: python tools/torus_bench.py [N] [split]."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -7,6 +7,7 @@ from handyrl_amd import _native
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 131072
 dev = torch.device('cuda', 0)
 lib = _native.load()
+lib.hrl_torus_set_split(int(sys.argv[2]) if len(sys.argv) > 2 else 1)
 P = _native.ptr
 g = torch.Generator(device=dev).manual_seed(0)
 x = torch.randn(N, 32, 7, 11, device=dev, generator=g)
