@@ -295,10 +295,13 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
             };
             if constexpr (kRef) {
                 // the reference tile's 72 staging registers leave no room for the unrolled form
-                // (every cell's fragments and B reads hoisted: spills), so the cell loop stays a
-                // loop and tap_of(p, q) a scalar branch
+                // (every cell's fragments and B reads hoisted: spills), so the board rows stay a
+                // loop (a row's three cells unrolled) and the row half of tap_of(p, q) a scalar branch
 #pragma unroll 1
-                for (int p = 0; p < kCells; ++p) cell(p);
+                for (int py = 0; py < kBoard; ++py) {
+#pragma unroll
+                    for (int px = 0; px < kBoard; ++px) cell(py * kBoard + px);
+                }
             } else {
 #pragma unroll
                 for (int p = 0; p < kCells; ++p) cell(p);
