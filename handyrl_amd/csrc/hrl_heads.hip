@@ -400,7 +400,11 @@ __global__ __launch_bounds__(256) void heads_reduce_kernel(const float *__restri
     }
 }
 
-constexpr int kGrid = 1024;
+// Workgroups (one wave each).  The backward's 51.9 KB of LDS lets 3 reside per CU, so 768 on the
+// 256 CUs run in one round: its former 1024 ran as 768 + a tail of 256 at a third of the
+// occupancy.  The forward (10.8 KB LDS, 230 VGPRs) keeps all 1024 resident.
+constexpr int kGridFwd = 1024;
+constexpr int kGridBwd = 768;
 
 int status() {
     const hipError_t e = hipGetLastError();
@@ -409,9 +413,9 @@ int status() {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-int grid_for(int64_t N) {
+int grid_for(int64_t N, int cap = kGridBwd) {
     const int64_t blocks = (N + 63) / 64;
-    return (int)(blocks < kGrid ? blocks : kGrid);
+    return (int)(blocks < cap ? blocks : cap);
 }
 
 }  // namespace
@@ -430,7 +434,7 @@ int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *
         return HRL_EINVAL;
     const Weights w{w1p, w1v, b1p, b1v, wp, wv};
     const BnIn bn{bn_alpha, bn_beta, nullptr, nullptr};
-    hipLaunchKernelGGL(heads_fwd_kernel, dim3(grid_for(N)), dim3(64), 0, static_cast<hipStream_t>(stream), h, N, w,
+    hipLaunchKernelGGL(heads_fwd_kernel, dim3(grid_for(N, kGridFwd)), dim3(64), 0, static_cast<hipStream_t>(stream), h, N, w,
                        bn, a_p, a_v, p_out, v_out);
     return status();
 }
