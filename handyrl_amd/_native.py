@@ -53,6 +53,10 @@ SIGNATURES = {
         _f32p, ctypes.c_void_p, _i64, _i64, _i64, _i64, _i64,
         _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _dbl, _dbl,
         ctypes.c_void_p, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_void_p]),
+    'hrl_output_mask_forward': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _f32p, _i64, _i64, _i64, _i64, _f32p,
+                                               _f32p, ctypes.c_void_p]),
+    'hrl_output_mask_backward': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _i64, _i64, _i64, _i64, _f32p, _f32p,
+                                                ctypes.c_void_p]),
     'hrl_board_weight': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _i64, _i64, _i64, _f32p, ctypes.c_void_p]),
     'hrl_board_fold': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _i64, _i64, _i64, _f32p, ctypes.c_void_p]),
     'hrl_board_bias': (ctypes.c_int, [_f32p, _i64, _i64, _f32p, ctypes.c_void_p]),

@@ -285,6 +285,72 @@ bool dims_ok(int64_t B, int64_t T, int64_t P, int64_t Pp, int64_t A, LossDims &d
     return d.BT < ((int64_t)1 << 40);
 }
 
+// ------------------------------------------------------------------ output masking
+// forward_prediction's post-processing of a feed-forward net's outputs (train.py:176-183):
+//   policy[bt, a] = sum_p o_pol[bt, p|0, a] * tmask[bt, p] - amask[bt, a]
+//   value[bt, p]  = o_val[bt, p|0] * omask[bt, p]
+// one launch each way instead of torch's mul / sum / sub / mul (and their backward mul / sum-to-size
+// pairs).  The float operations and the p order are torch's: products rounded, summed from 0 in p order.
+__global__ __launch_bounds__(kThreads) void out_mask_fwd_kernel(const float *__restrict__ opol,
+                                                                const float *__restrict__ oval,
+                                                                const float *__restrict__ tmask,
+                                                                const float *__restrict__ omask,
+                                                                const float *__restrict__ amask, int64_t BT, int P,
+                                                                int Pq, int A, float *__restrict__ pol,
+                                                                float *__restrict__ val) {
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const int64_t npol = BT * A;
+    if (i < npol) {
+        const int64_t bt = i / A;
+        const int a = (int)(i - bt * A);
+        float acc = 0.f;
+        for (int p = 0; p < P; ++p) acc += opol[(bt * Pq + (Pq == 1 ? 0 : p)) * A + a] * tmask[bt * P + p];
+        pol[i] = acc - amask[i];
+    } else if (oval && i < npol + BT * P) {
+        const int64_t j = i - npol;
+        const int64_t bt = j / P;
+        const int p = (int)(j - bt * P);
+        val[j] = oval[bt * Pq + (Pq == 1 ? 0 : p)] * omask[j];
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void out_mask_bwd_kernel(const float *__restrict__ gpol,
+                                                                const float *__restrict__ gval,
+                                                                const float *__restrict__ tmask,
+                                                                const float *__restrict__ omask, int64_t BT, int P,
+                                                                int Pq, int A, float *__restrict__ gopol,
+                                                                float *__restrict__ goval) {
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const int64_t npol = BT * Pq * A;
+    if (i < npol) {
+        const int64_t btq = i / A;
+        const int a = (int)(i - btq * A);
+        const int64_t bt = btq / Pq;
+        const int q = (int)(btq - bt * Pq);
+        const float g = gpol[bt * A + a];
+        float acc;
+        if (Pq == 1) {
+            acc = 0.f;
+            for (int p = 0; p < P; ++p) acc += g * tmask[bt * P + p];
+        } else {
+            acc = g * tmask[bt * P + q];
+        }
+        gopol[i] = acc;
+    } else if (gval && i < npol + BT * Pq) {
+        const int64_t btq = i - npol;
+        const int64_t bt = btq / Pq;
+        const int q = (int)(btq - bt * Pq);
+        float acc;
+        if (Pq == 1) {
+            acc = 0.f;
+            for (int p = 0; p < P; ++p) acc += gval[bt * P + p] * omask[bt * P + p];
+        } else {
+            acc = gval[bt * P + q] * omask[bt * P + q];
+        }
+        goval[btq] = acc;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -356,6 +422,34 @@ int hrl_loss_backward(const float *tpol, const int64_t *action, int64_t B, int64
     hipLaunchKernelGGL(loss_backward_kernel, dim3(w.nblocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream), a,
                        d, w);
     return status();
+}
+
+int hrl_output_mask_forward(const float *opol, const float *oval, const float *tmask, const float *omask,
+                            const float *amask, int64_t BT, int64_t P, int64_t Pq, int64_t A, float *pol,
+                            float *val, void *stream) {
+    if (BT < 1 || P < 1 || P > 64 || A < 1 || A > (1 << 20) || (Pq != 1 && Pq != P)) return HRL_EINVAL;
+    if (!opol || !tmask || !amask || !pol || (oval && (!omask || !val))) return HRL_EINVAL;
+    const int64_t n = BT * A + (oval ? BT * P : 0);
+    if (n > ((int64_t)1 << 40)) return HRL_EINVAL;
+    hipLaunchKernelGGL(out_mask_fwd_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), opol, oval, tmask, omask, amask, BT, (int)P, (int)Pq,
+                       (int)A, pol, val);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
+}
+
+int hrl_output_mask_backward(const float *gpol, const float *gval, const float *tmask, const float *omask,
+                             int64_t BT, int64_t P, int64_t Pq, int64_t A, float *gopol, float *goval,
+                             void *stream) {
+    if (BT < 1 || P < 1 || P > 64 || A < 1 || A > (1 << 20) || (Pq != 1 && Pq != P)) return HRL_EINVAL;
+    if (!gpol || !tmask || !gopol || (gval && (!omask || !goval))) return HRL_EINVAL;
+    const int64_t n = BT * Pq * A + (gval ? BT * Pq : 0);
+    if (n > ((int64_t)1 << 40)) return HRL_EINVAL;
+    hipLaunchKernelGGL(out_mask_bwd_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), gpol, gval, tmask, omask, BT, (int)P, (int)Pq, (int)A,
+                       gopol, goval);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
 }
 
 }  // extern "C"

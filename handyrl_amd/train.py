@@ -74,8 +74,13 @@ def forward_prediction(model, hidden, batch, args):
         outputs = {k: torch.stack(o, dim=1) for k, o in per_t.items() if o[0] is not None}
 
     result = {}
+    fused = _output_mask_fusable(outputs, batch, B, T)
+    if fused:
+        result['policy'], result['value'] = _OutputMask.apply(
+            outputs['policy'].view(B, T, -1, outputs['policy'].size(-1)),
+            outputs['value'].view(B, T, -1, 1), tmask, batch['observation_mask'], batch['action_mask'])
     for k, o in outputs.items():
-        if k == 'hidden' or o is None:
+        if k == 'hidden' or o is None or (fused and k in ('policy', 'value')):
             continue
         o = o.view(B, T, -1, o.size(-1))
         if k == 'policy':
@@ -83,6 +88,62 @@ def forward_prediction(model, hidden, batch, args):
         else:
             result[k] = o.mul(batch['observation_mask'])
     return result
+
+
+def _output_mask_fusable(outputs, batch, B, T):
+    """The common feed-forward case of the masking above, for _OutputMask: fp32 CUDA tensors, policy and
+    value P-extents 1 or P, masks (B, T, P, 1), action_mask (B, T, 1, A)."""
+    pol, val = outputs.get('policy'), outputs.get('value')
+    if pol is None or val is None or not pol.is_cuda or pol.dtype != torch.float32 or val.dtype != torch.float32:
+        return False
+    tmask, omask, amask = batch['turn_mask'], batch['observation_mask'], batch['action_mask']
+    if tmask.dim() != 4 or tmask.shape[-1] != 1 or omask.shape != tmask.shape:
+        return False
+    P, A = tmask.shape[2], pol.size(-1)
+    if pol.numel() % (B * T * A) or val.size(-1) != 1 or val.numel() % (B * T):
+        return False
+    if pol.numel() // (B * T * A) not in (1, P) or val.numel() // (B * T) not in (1, P):
+        return False
+    if pol.numel() // (B * T * A) != val.numel() // (B * T):
+        return False
+    if tuple(amask.shape) != (B, T, 1, A) or amask.dtype != torch.float32:
+        return False
+    return all(t.is_contiguous() for t in (pol, val, tmask, omask, amask))
+
+
+class _OutputMask(torch.autograd.Function):
+    """train.py:176-183 for policy and value as csrc/hrl_loss.hip's out_mask kernels (one launch each way)."""
+
+    @staticmethod
+    def forward(ctx, opol, oval, tmask, omask, amask):
+        B, T, Pq, A = opol.shape
+        P = tmask.shape[2]
+        pol = torch.empty(B, T, 1, A, dtype=opol.dtype, device=opol.device)
+        val = torch.empty(B, T, P, 1, dtype=oval.dtype, device=oval.device)
+        lib, p = _native.load(), _native.ptr
+        _native.check(lib.hrl_output_mask_forward(p(opol), p(oval), p(tmask), p(omask), p(amask), B * T, P, Pq, A,
+                                                  p(pol), p(val), _native.stream_of(opol.device)),
+                      'hrl_output_mask_forward')
+        ctx.save_for_backward(tmask, omask)
+        ctx.pq, ctx.a = Pq, A
+        return pol, val
+
+    @staticmethod
+    def backward(ctx, gpol, gval):
+        tmask, omask = ctx.saved_tensors
+        B, T, P = tmask.shape[:3]
+        A = ctx.a
+        gpol = torch.zeros(B, T, 1, A, dtype=tmask.dtype, device=tmask.device) if gpol is None else gpol.contiguous()
+        gval = gval.contiguous() if gval is not None else None
+        gopol = torch.empty(B, T, ctx.pq, A, dtype=gpol.dtype, device=gpol.device)
+        goval = torch.empty(B, T, ctx.pq, 1, dtype=gpol.dtype, device=gpol.device) if gval is not None else None
+        lib, p = _native.load(), _native.ptr
+        _native.check(lib.hrl_output_mask_backward(p(gpol), p(gval) if gval is not None else None, p(tmask),
+                                                   p(omask), B * T, P, ctx.pq, A, p(gopol),
+                                                   p(goval) if goval is not None else None,
+                                                   _native.stream_of(gpol.device)),
+                      'hrl_output_mask_backward')
+        return gopol, goval, None, None, None
 
 
 def _leaves(x):

@@ -58,6 +58,20 @@ int hrl_loss_backward(const float *tpol, const int64_t *action,
                       const void *workspace, int64_t workspace_bytes, const float *dlosses,
                       float *g_tpol, float *g_value, float *g_ret, void *stream);
 
+/*
+ * forward_prediction's masking of a feed-forward net's outputs (handyrl/train.py:176-183), one launch each way:
+ *   policy (BT, A)    = sum_p opol[bt, p|0, :] * tmask[bt, p] - amask[bt, :]   (opol (BT, Pq, A), amask (BT, 1, A))
+ *   value  (BT, P)    = oval[bt, p|0] * omask[bt, p]                          (oval (BT, Pq, 1); NULL: no value head)
+ * Pq = 1 or P; tmask, omask (BT, P).  The backward forms dL/dopol (BT, Pq, A) and dL/doval (BT, Pq) from
+ * dL/dpolicy and dL/dvalue (gval NULL: no value head).  Float operations and sum order as torch's.
+ */
+int hrl_output_mask_forward(const float *opol, const float *oval, const float *tmask, const float *omask,
+                            const float *amask, int64_t BT, int64_t P, int64_t Pq, int64_t A, float *pol,
+                            float *val, void *stream);
+int hrl_output_mask_backward(const float *gpol, const float *gval, const float *tmask, const float *omask,
+                             int64_t BT, int64_t P, int64_t Pq, int64_t A, float *gopol, float *goval,
+                             void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -174,3 +174,30 @@ def test_fused_loss_deterministic(cuda):
         losses['total'].backward()
         runs.append((torch.stack([losses[k] for k in ('p', 'v', 'ent', 'total')]).cpu(), net.p.grad.clone()))
     assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('Pq', [1, 2])
+def test_output_mask_kernels_match_torch(Pq):
+    """forward_prediction's masking (train.py:176-183) as one HIP launch each way (_OutputMask) vs the torch ops."""
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from handyrl_amd.train import _OutputMask
+    dev = torch.device('cuda', 0)
+    g = torch.Generator().manual_seed(Pq)
+    B, T, P, A = 37, 9, 2, 9
+    opol = torch.randn(B, T, Pq, A, generator=g)
+    oval = torch.randn(B, T, Pq, 1, generator=g)
+    tmask = (torch.rand(B, T, P, 1, generator=g) > 0.5).float()
+    omask = (torch.rand(B, T, P, 1, generator=g) > 0.3).float()
+    amask = (torch.rand(B, T, 1, A, generator=g) > 0.7).float() * 1e32
+    gp, gv = torch.randn(B, T, 1, A, generator=g), torch.randn(B, T, P, 1, generator=g)
+    ref_in = [opol.clone().requires_grad_(True), oval.clone().requires_grad_(True)]
+    rp = ref_in[0].mul(tmask).sum(2, keepdim=True) - amask
+    rv = ref_in[1].mul(omask)
+    torch.autograd.backward([rp, rv], [gp, gv])
+    hip_in = [opol.to(dev).requires_grad_(True), oval.to(dev).requires_grad_(True)]
+    hp, hv = _OutputMask.apply(hip_in[0], hip_in[1], tmask.to(dev), omask.to(dev), amask.to(dev))
+    torch.autograd.backward([hp, hv], [gp.to(dev), gv.to(dev)])
+    assert torch.equal(hp.detach().cpu(), rp.detach()) and torch.equal(hv.detach().cpu(), rv.detach())
+    assert torch.equal(hip_in[0].grad.cpu(), ref_in[0].grad) and torch.equal(hip_in[1].grad.cpu(), ref_in[1].grad)
