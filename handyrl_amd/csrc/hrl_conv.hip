@@ -37,6 +37,7 @@
 
 #include "../../include/hrl_nn.h"
 #include "../../include/hrl_targets.h"
+#include "hrl_split.h"
 
 namespace {
 
@@ -64,40 +65,11 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// ---- exact three-way bf16 split of fp32 operands (the SPLIT path) ----
-// x = h + m + l EXACTLY: h = x with the low 16 bits cleared (8 significant bits),
-// r = x - h is exact (<= 16 significant bits), m = r with the low 16 bits cleared,
-// l = r - m is exact and has <= 8 significant bits, so it is a bf16 as is.  A product
-// x*w keeps the six terms hh, hm, mh, hl, lh, mm; the dropped ml, lm, ll are below
-// 2^-23 |x w| together -- the size of one fp32 rounding.  Every bf16 x bf16 product is
-// exact in fp32 and the MFMA accumulates in fp32, so the result is fp32-accurate, at
-// 6/16 of the fp32 MFMA's cycles (gfx950: v_mfma_f32_16x16x4_f32 runs at 1/16 of the
-// bf16 rate, MI355X_MICROARCH.md).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ void split3(float x, uint32_t &h, uint32_t &m, uint32_t &l) {
-    const uint32_t xb = __float_as_uint(x);
-    const uint32_t hb = xb & 0xffff0000u;
-    const float r = x - __uint_as_float(hb);
-    const uint32_t rb = __float_as_uint(r);
-    const uint32_t mb = rb & 0xffff0000u;
-    const float lo = r - __uint_as_float(mb);
-    h = hb >> 16;
-    m = mb >> 16;
-    l = __float_as_uint(lo) >> 16;
-}
-
-// part 0/1/2 (h/m/l) of x as the 16 bf16 bits
-__device__ __forceinline__ uint32_t split_part(float x, int part) {
-    uint32_t h, m, l;
-    split3(x, h, m, l);
-    return part == 0 ? h : (part == 1 ? m : l);
-}
-
-__device__ __forceinline__ f32x4 mfma_bf16(const uint4 &a, const uint4 &b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
-                                                   c, 0, 0, 0);
-}
+// The SPLIT path: exact three-way bf16 split of both fp32 operands, six partial products on
+// v_mfma_f32_16x16x32_bf16 (hrl_split.h: error analysis and helpers).
+using hrl_split::split3;
+using hrl_split::split_part;
+using hrl_split::mfma_bf16;
 
 // ------------------------------------------------------------------ forward / input gradient
 // x: (M, 288) rows; wpk: packed [tap][ct][ci][16] = W'[tap][ci][ct*16+j]; y: (M, 288)
@@ -426,6 +398,10 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
 // ------------------------------------------------------------------ weight gradient
 // dW[tap][ci][co] = sum_rows sum_{(p,q): tap(p,q) = tap} x[row, ci, p] * dy[row, co, q]
 // MFMA C tile = 16 ci x 16 co; A[i = ci][k = row], B[k = row][j = co]
+// The weight gradient stays on fp32 MFMA.  A split form (contraction index = (pair of the tap, row),
+// two pairs x 16 rows per 32-deep bf16 k-step, every operand re-split per pair) was measured at
+// 274 us against this kernel's 140 us: the per-pair LDS gathers and splits cost more than the MFMA
+// cycles they save.
 template <bool PRO>
 __global__ __launch_bounds__(kThreads) void conv3x3_wgrad_kernel(const float *__restrict__ x,
                                                                  const float *__restrict__ in_alpha,

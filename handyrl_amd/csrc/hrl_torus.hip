@@ -38,6 +38,7 @@
 
 #include "../../include/hrl_nn.h"
 #include "../../include/hrl_targets.h"
+#include "hrl_split.h"
 
 namespace {
 
@@ -57,52 +58,9 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// Exact three-way bf16 split (x = h + m + l exactly; six partial products on
-// v_mfma_f32_16x16x32_bf16, fp32 accumulation): the arithmetic of hrl_conv.hip's
-// split path, see the error analysis there.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ void split3(float x, uint32_t &h, uint32_t &m, uint32_t &l) {
-    const uint32_t hb = __float_as_uint(x) & 0xffff0000u;
-    const float r = x - __uint_as_float(hb);
-    const uint32_t mb = __float_as_uint(r) & 0xffff0000u;
-    h = hb >> 16;
-    m = mb >> 16;
-    l = __float_as_uint(r - __uint_as_float(mb)) >> 16;
-}
-
-// 8 fp32 -> the h/m/l bf16x8 fragments
-__device__ __forceinline__ void split8(const float (&v)[8], uint4 &H, uint4 &M, uint4 &L) {
-    uint32_t h[4], m[4], l[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        uint32_t h0, m0, l0, h1, m1, l1;
-        split3(v[2 * d], h0, m0, l0);
-        split3(v[2 * d + 1], h1, m1, l1);
-        h[d] = h0 | (h1 << 16);
-        m[d] = m0 | (m1 << 16);
-        l[d] = l0 | (l1 << 16);
-    }
-    H = make_uint4(h[0], h[1], h[2], h[3]);
-    M = make_uint4(m[0], m[1], m[2], m[3]);
-    L = make_uint4(l[0], l[1], l[2], l[3]);
-}
-
-__device__ __forceinline__ f32x4 mfma_bf16(const uint4 &a, const uint4 &b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
-                                                   c, 0, 0, 0);
-}
-
-// acc += A * B with both operands as exact splits (smallest terms first)
-__device__ __forceinline__ f32x4 mfma_split(const uint4 &Ah, const uint4 &Am, const uint4 &Al, const uint4 &Bh,
-                                            const uint4 &Bm, const uint4 &Bl, f32x4 c) {
-    c = mfma_bf16(Al, Bh, c);
-    c = mfma_bf16(Am, Bm, c);
-    c = mfma_bf16(Ah, Bl, c);
-    c = mfma_bf16(Am, Bh, c);
-    c = mfma_bf16(Ah, Bm, c);
-    return mfma_bf16(Ah, Bh, c);
-}
+// The split path's helpers (exact three-way bf16 split, six partial products): hrl_split.h.
+using hrl_split::split8;
+using hrl_split::mfma_split;
 
 __device__ __forceinline__ int torus_nbr(int q, int H, int W, int tap) {
     const int r = q / W, c = q - r * W;
