@@ -52,7 +52,9 @@ def up_to_date():
 
 def _compile(src):
     obj = os.path.join(OBJ_DIR, os.path.basename(src) + '.o')
-    hdr_mtime = max(os.path.getmtime(os.path.join(INCLUDE, f)) for f in os.listdir(INCLUDE))
+    hdrs = [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)]
+    hdrs += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
+    hdr_mtime = max(os.path.getmtime(h) for h in hdrs)
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
         return obj
     cmd = [hipcc()] + HIPCC_FLAGS + ['-c', src, '-o', obj]
