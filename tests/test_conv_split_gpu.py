@@ -1,4 +1,4 @@
-"""Split-bf16 arithmetic of the board conv (csrc/hrl_conv.hip, hrl_conv3x3_set_split).
+"""Split-bf16 arithmetic of the board and torus convs (csrc/hrl_conv.hip, csrc/hrl_torus.hip; *_set_split).
 
 The forward / input-gradient kernel splits both fp32 operands exactly into three bf16 parts and
 runs six partial products on v_mfma_f32_16x16x32_bf16 with fp32 accumulation.  Checked here:
@@ -85,3 +85,51 @@ def test_error_within_fp32_conv_error(cuda, flip, M):
         y = _run(lib, cuda, x.to(cuda), w.to(cuda), None if b is None else b.to(cuda), flip, split).cpu().double()
         err = float(((y - ref).abs() / rowmax).max())
         assert err <= bound, (split, err, bound)
+
+
+def _torus64(x, w, b):
+    """GeeseNet's TorusConv2d (hungry_geese.py:30-35: wrap with two cats, 'valid' conv) in fp64."""
+    xp = torch.cat([x[:, :, -1:], x, x[:, :, :1]], dim=2)
+    xp = torch.cat([xp[:, :, :, -1:], xp, xp[:, :, :, :1]], dim=3)
+    return torch.nn.functional.conv2d(xp, w, b)
+
+
+@pytest.mark.parametrize('cin', [32, 17])
+@pytest.mark.parametrize('integer', [True, False])
+def test_torus_split_matches_fp64(cuda, cin, integer):
+    """csrc/hrl_torus.hip's split forward: exact on integer data (fragment layouts, the 17-channel stem's zero
+    padding to one 32-deep k-step), and within 2x torch fp32's error on random data; both arithmetics."""
+    lib = _native.load()
+    g = torch.Generator().manual_seed(cin + integer)
+    N, H, W = 300, 7, 11
+    if integer:
+        x = torch.randint(-8, 9, (N, cin, H, W), generator=g).float()
+        w = torch.randint(-8, 9, (32, cin, 3, 3), generator=g).float()
+        b = torch.randint(-8, 9, (32,), generator=g).float()
+    else:
+        x = torch.randn(N, cin, H, W, generator=g) * torch.exp2(torch.randint(-20, 21, (N, 1, 1, 1), generator=g).float())
+        w = torch.randn(32, cin, 3, 3, generator=g) * 0.1
+        b = torch.randn(32, generator=g)
+    ref = _torus64(x.double(), w.double(), b.double())
+    t32 = _torus64(x, w, b).double()
+    rowmax = ref.abs().flatten(1).amax(dim=1).clamp_min(1e-300).view(N, 1, 1, 1)
+    bound = 2.0 * float(((t32 - ref).abs() / rowmax).max()) + 1e-7
+    ws_bytes = lib.hrl_torus_workspace_bytes(N)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+    P = _native.ptr
+    for split in (1, 0):
+        xg, wg, bg = x.to(cuda), w.to(cuda), b.to(cuda)
+        y = torch.empty(N, 32, H, W, device=cuda)
+        prev = lib.hrl_torus_set_split(split)
+        try:
+            _native.check(lib.hrl_torus_conv_forward(P(xg), N, cin, 32, H, W, P(wg), P(bg), 0, P(y), None, None,
+                                                     None, P(ws), ws_bytes, _native.stream_of(cuda)), 'torus')
+            torch.cuda.synchronize(cuda)
+        finally:
+            lib.hrl_torus_set_split(prev)
+        yd = y.cpu().double()
+        if integer:
+            assert torch.equal(yd, ref), split
+        else:
+            err = float(((yd - ref).abs() / rowmax).max())
+            assert err <= bound, (split, err, bound)
