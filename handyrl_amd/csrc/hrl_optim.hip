@@ -42,7 +42,9 @@ __global__ __launch_bounds__(kThreads) void clip_kernel(float *__restrict__ g, i
         const float total = (float)sqrt(red[0]);
         total_out[0] = total;
         const float c = max_norm / (total + 1e-6f);
-        coef_s = c < 1.0f ? c : 1.0f;
+        // torch.clamp(c, max=1) propagates NaN: a NaN norm turns every gradient into NaN, as the
+        // reference's clip_grad_norm_ does (an inf norm gives c = 0: finite gradients become 0)
+        coef_s = (c < 1.0f || c != c) ? c : 1.0f;
     }
     __syncthreads();
     const float c = coef_s;

@@ -124,6 +124,8 @@ class GradAllReduce:
 
     def _make_hook(self, i):
         def hook(_param):
+            if not self.enabled:
+                return      # a probe or capture pass: nothing is counted (and nothing launched)
             b = self.param_bucket[i]
             self._pending[b] -= 1
             self._launch_ready()
@@ -133,11 +135,16 @@ class GradAllReduce:
 
     def mark_ready(self, params):
         """Params whose gradient was written outside autograd (nn.DeferredGrads.flush): count them
-        as accumulated, as their post-accumulate hook would."""
+        as accumulated, as their post-accumulate hook would.  Each parameter counts once, however
+        often it appears in ``params``."""
+        if not self.enabled:
+            return
         index = {id(p): i for i, p in enumerate(self.fg.params)}
+        seen = set()
         for p in params:
             i = index.get(id(p))
-            if i is not None:
+            if i is not None and i not in seen:
+                seen.add(i)
                 self._pending[self.param_bucket[i]] -= 1
         self._launch_ready()
 

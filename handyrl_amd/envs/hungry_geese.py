@@ -50,7 +50,8 @@ class TorusConv2d(nn.Module):
     use_hip = False   # set by nn.accelerate: the conv runs as csrc/hrl_torus.hip (no wrapped copy)
 
     def forward(self, x):
-        if self.use_hip:
+        # a CPU copy of an accelerated net (Trainer.train returns one for the workers) runs the torch form
+        if self.use_hip and x.is_cuda:
             from ..nn import torus_conv2d, torus_supported
             if not torus_supported(x, self.conv.weight):
                 raise RuntimeError('TorusConv2d: shape %s x %s is outside the HIP torus conv'
@@ -70,7 +71,7 @@ class GeeseNet(nn.Module):
         self.head_v = nn.Linear(filters * 2, 1, bias=False)
 
     def forward(self, x, _=None):
-        if self.training and self.conv0.use_hip and self.conv0.bn is not None:
+        if self.training and self.conv0.use_hip and self.conv0.bn is not None and x.is_cuda:
             # accelerated training step: each unit is one fused HIP Function (nn.torus_block)
             from ..nn import torus_block
             h = torus_block(x, self.conv0, residual=False)

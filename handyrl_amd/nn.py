@@ -65,8 +65,9 @@ class DeferredGrads:
 
     @torch.no_grad()
     def flush(self):
-        """Accumulate the deferred gradients into .grad; returns the parameters that got one."""
-        touched = []
+        """Accumulate the deferred gradients into .grad; returns the parameters that got one, each once
+        (a ConvLSTM h-conv weight is recorded once per input slice)."""
+        touched = {}
         for (w, b, sl, pad), rec in self.conv.items():
             X = torch.cat([r[0] for r in rec]) if len(rec) > 1 else rec[0][0]
             DY = torch.cat([r[1] for r in rec]) if len(rec) > 1 else rec[0][1]
@@ -75,20 +76,20 @@ class DeferredGrads:
                 DY, X, wv, [wv.shape[0]] if b is not None else None, [1, 1], list(pad), [1, 1], False, [0, 0], 1,
                 [False, True, b is not None])
             _add_grad(w, dw, sl)
-            touched.append(w)
+            touched[id(w)] = w
             if b is not None:
                 _add_grad(b, db, None)
-                touched.append(b)
+                touched[id(b)] = b
         for (w, b), rec in self.affine.items():
             if w is not None:
                 _add_grad(w, torch.stack([r[0] for r in rec]).sum(0), None)
-                touched.append(w)
+                touched[id(w)] = w
             if b is not None:
                 _add_grad(b, torch.stack([r[1] for r in rec]).sum(0), None)
-                touched.append(b)
+                touched[id(b)] = b
         self.conv.clear()
         self.affine.clear()
-        return touched
+        return list(touched.values())
 
 
 def _add_grad(p, g, sl):

@@ -53,7 +53,10 @@ class LearnerStep:
         if world_size > 1:
             self.reducer = hdist.GradAllReduce(self.grads, group=reduce_group, bucket_bytes=bucket_bytes)
         if lr is None:
-            lr = DEFAULT_LR * args['batch_size'] * args['forward_steps']
+            # train.py:318-321: lr = 3e-8 * batch_size * forward_steps for the batch ONE update sees.
+            # Here args['batch_size'] is the per-rank shard and the gradients are SUMmed over the ranks,
+            # so one update sees world_size * batch_size windows (nn.DataParallel's global batch).
+            lr = DEFAULT_LR * args['batch_size'] * world_size * args['forward_steps']
         # one fused multi-tensor Adam kernel on the GPU (train.py:322: Adam, weight_decay 1e-5)
         fused = device.type == 'cuda'
         if self.graph:
@@ -93,7 +96,7 @@ class LearnerStep:
         for p in self.params:
             p.grad = None
         if self.reducer is not None:
-            self.reducer.enabled = False
+            self.reducer.enabled = False    # its hooks neither count nor launch during the probe
         try:
             outputs = forward_prediction(self.net, small_hidden, small, self.args)
             losses, _ = self.loss_fn(outputs, small, self.args)
@@ -106,6 +109,7 @@ class LearnerStep:
                 b.copy_(saved)
             if self.reducer is not None:
                 self.reducer.enabled = True
+                self.reducer.reset()
         self.live = live
         if not all(live):
             kw = dict(self._opt_kwargs)
@@ -275,7 +279,8 @@ class Trainer:
         self.batcher = batcher
         self.device = device or torch.device('cuda', torch.cuda.current_device())
         self.default_lr = DEFAULT_LR
-        self.data_cnt_ema = args['batch_size'] * args['forward_steps']
+        # train.py:318: the EMA starts at the global batch's cell count (args['batch_size'] is per rank)
+        self.data_cnt_ema = args['batch_size'] * world_size * args['forward_steps']
         self.steps = 0
         self.update_flag = False
         self.shutdown_flag = False

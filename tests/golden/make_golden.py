@@ -27,6 +27,15 @@ Fixtures written
     TicTacToe / Geister self-play episodes in the four training modes; the
     episodes are stored decompressed and pickle-free (JSON structure + npz
     arrays, ``encode_episode``), the outputs as arrays.
+``geese_net.npz`` + ``geese_net.json``
+    GeeseNet (handyrl/envs/kaggle/hungry_geese.py:23-57, config C4) with
+    ``kaggle_environments`` stubbed in ``sys.modules`` (the module imports only
+    ``make`` from it, :18, and the net never uses it): seeded initial weights,
+    the train- and eval-mode forward, ``compute_loss`` in the solo layout
+    (turn_based_training=False, P = Pp = 1) with every parameter's gradient,
+    and three ``Trainer.train`` learner steps with the final state_dict.  The
+    batch is ``handyrl_amd.synthetic.geese_batch`` (no Hungry Geese rules here),
+    stored as input arrays.
 ``learner.npz`` + ``learner.json``
     Three learner steps of the TicTacToe ``SimpleConv2dModel`` exactly as
     ``Trainer.train`` runs them (train.py:375-385): loss, backward,
@@ -470,7 +479,92 @@ def geister_net_case():
     return arrays, meta
 
 
+# ---------------------------------------------------------------------------
+# 7. GeeseNet (torus convs, hungry_geese.py:23-57) with kaggle_environments stubbed
+# ---------------------------------------------------------------------------
+
+def geese_net_case():
+    import types
+    if 'kaggle_environments' not in sys.modules:
+        stub = types.ModuleType('kaggle_environments')
+
+        def make(*_a, **_k):
+            raise RuntimeError('kaggle_environments stub: the rules are not available')
+        stub.make = make
+        sys.modules['kaggle_environments'] = stub
+    from handyrl.envs.kaggle.hungry_geese import GeeseNet
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))   # the repo: its synthetic batch generator
+    from handyrl_amd.synthetic import geese_batch, geese_args
+
+    arrays, meta = {}, {'state': {}}
+    torch.manual_seed(21)
+    net = GeeseNet()
+    for k, v in net.state_dict().items():
+        vv = v.double()
+        meta['state'][k] = [list(v.shape), float(vv.sum()), float((vv * vv).sum())]
+
+    # forward: train mode (batch statistics; updates the running statistics), then eval mode
+    fwd = geese_batch(2, 5, torch.device('cpu'), seed=22)['observation'].reshape(10, 17, 7, 11)
+    arrays['fwd.x'] = _np(fwd)
+    net.train()
+    out = net(fwd)
+    arrays['fwd.train_policy'], arrays['fwd.train_value'] = _np(out['policy']), _np(out['value'])
+    net.eval()
+    with torch.no_grad():
+        out = net(fwd)
+    arrays['fwd.eval_policy'], arrays['fwd.eval_value'] = _np(out['policy']), _np(out['value'])
+    for k, v in net.state_dict().items():
+        if 'running' in k:
+            arrays['fwd.after.' + k] = _np(v)
+
+    # compute_loss (solo layout) and three learner steps from a fresh seeded net
+    B, T = 8, 6
+    args = geese_args(T, B)
+    batch = geese_batch(B, T, torch.device('cpu'), seed=23)
+    for k, v in batch.items():
+        arrays['batch.' + k] = _np(v)
+    torch.manual_seed(21)
+    net = GeeseNet()
+    model = ModelWrapper(net)
+    model.train()
+    losses, dcnt = ref_train.compute_loss(batch, model, None, args)
+    losses['total'].backward()
+    meta['loss'] = {'args': args, 'dcnt': dcnt, 'losses': {k: float(v.item()) for k, v in losses.items()}}
+    for n, p in net.named_parameters():
+        arrays['grad.' + n] = _np(p.grad)
+
+    torch.manual_seed(21)
+    net = GeeseNet()
+    model = ModelWrapper(net)
+    params = list(model.parameters())
+    lr = 3e-8 * B * T
+    opt = torch.optim.Adam(params, lr=lr, weight_decay=1e-5)
+    model.train()
+    steps = []
+    for s in range(3):
+        losses, dcnt = ref_train.compute_loss(batch, model, None, args)
+        opt.zero_grad()
+        losses['total'].backward()
+        gn = nn.utils.clip_grad_norm_(params, 4.0)
+        opt.step()
+        steps.append({k: float(v.item()) for k, v in losses.items()})
+        steps[-1]['grad_norm'] = float(gn)
+        steps[-1]['dcnt'] = dcnt
+    for k, v in net.state_dict().items():
+        arrays['final.' + k] = _np(v)
+    meta['learner'] = {'B': B, 'T': T, 'lr': lr, 'steps': steps}
+    return arrays, meta
+
+
 def main():
+    only = sys.argv[1:]
+    if only == ['geese']:
+        arr, meta = geese_net_case()
+        np.savez_compressed(os.path.join(OUT, 'geese_net.npz'), **arr)
+        with open(os.path.join(OUT, 'geese_net.json'), 'w') as f:
+            json.dump(meta, f, indent=1)
+        print('geese net: %d tensors' % len(meta['state']))
+        return
     arr, man = target_cases()
     np.savez_compressed(os.path.join(OUT, 'targets.npz'), **arr)
     with open(os.path.join(OUT, 'targets.json'), 'w') as f:
@@ -507,6 +601,12 @@ def main():
     with open(os.path.join(OUT, 'geister_net.json'), 'w') as f:
         json.dump(meta, f, indent=1)
     print('geister net: %d tensors' % len(meta['state']))
+
+    arr, meta = geese_net_case()
+    np.savez_compressed(os.path.join(OUT, 'geese_net.npz'), **arr)
+    with open(os.path.join(OUT, 'geese_net.json'), 'w') as f:
+        json.dump(meta, f, indent=1)
+    print('geese net: %d tensors' % len(meta['state']))
 
     arr, meta = learner_case()
     np.savez_compressed(os.path.join(OUT, 'learner.npz'), **arr)

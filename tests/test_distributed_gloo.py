@@ -36,6 +36,21 @@ class SmallNet(nn.Module):
         return {'policy': self.fc_p(h), 'value': torch.tanh(self.fc_v(h))}
 
 
+class HeadsFirstNet(SmallNet):
+    """The same net with its heads registered before its convs: registration order is not backward
+    order, so the first gradient hook lands in a later bucket than the first backward-order one."""
+
+    def __init__(self):
+        nn.Module.__init__(self)
+        self.fc_p = nn.Linear(72, 9)
+        self.fc_v = nn.Linear(72, 1)
+        self.conv = nn.Conv2d(3, 8, 3, padding=1)
+        self.conv2 = nn.Conv2d(8, 8, 3, padding=1)
+
+
+NETS = {'SmallNet': SmallNet, 'HeadsFirstNet': HeadsFirstNet}
+
+
 def oracle_loss(outputs, batch, args):
     from oracle.learner import loss_from_outputs
     losses, dcnt = loss_from_outputs(outputs, batch, args)
@@ -56,7 +71,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, out_path, steps, bucket_bytes):
+def _rank_main(rank, world, port, out_path, steps, bucket_bytes, net_name='SmallNet'):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -67,9 +82,9 @@ def _rank_main(rank, world, port, out_path, steps, bucket_bytes):
     B = batch['value'].size(0)
     shard = {k: v[rank * B // world:(rank + 1) * B // world] for k, v in batch.items()}
     torch.manual_seed(0)
-    net = SmallNet()
+    net = NETS[net_name]()
     step = LearnerStep(net, args, torch.device('cpu'), world_size=world, loss_fn=oracle_loss,
-                       bucket_bytes=bucket_bytes)
+                       bucket_bytes=bucket_bytes, lr=1e-3)
     assert len(step.reducer.buckets) >= 1
     for _ in range(steps):
         step.step(shard)
@@ -84,26 +99,28 @@ def _rank_main(rank, world, port, out_path, steps, bucket_bytes):
     dist.destroy_process_group()
 
 
-def _single_process(steps):
+def _single_process(steps, net_name='SmallNet'):
     from handyrl_amd.trainer import LearnerStep
     batch, args = make_batch_and_args()
     torch.manual_seed(0)
-    net = SmallNet()
-    step = LearnerStep(net, args, torch.device('cpu'), loss_fn=oracle_loss)
+    net = NETS[net_name]()
+    step = LearnerStep(net, args, torch.device('cpu'), loss_fn=oracle_loss, lr=1e-3)
     for _ in range(steps):
         step.step(batch)
     sums, _ = step.pop_stats()
     return torch.cat([p.detach().reshape(-1) for p in net.parameters()]).numpy(), sums
 
 
-@pytest.mark.parametrize('bucket_bytes', [256 * 1024, 1024])   # one bucket / several hook-launched buckets
-def test_two_rank_sum_allreduce_matches_full_batch(bucket_bytes):
+@pytest.mark.parametrize('bucket_bytes,net_name', [(256 * 1024, 'SmallNet'),   # one bucket
+                                                    (1024, 'SmallNet'),         # several hook-launched buckets
+                                                    (1024, 'HeadsFirstNet')])   # registration != backward order
+def test_two_rank_sum_allreduce_matches_full_batch(bucket_bytes, net_name):
     steps = 3
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, 'r0.pt')
-        mp.spawn(_rank_main, args=(2, _free_port(), out, steps, bucket_bytes), nprocs=2, join=True)
+        mp.spawn(_rank_main, args=(2, _free_port(), out, steps, bucket_bytes, net_name), nprocs=2, join=True)
         res = torch.load(out, weights_only=True)
-    ref_params, ref_sums = _single_process(steps)
+    ref_params, ref_sums = _single_process(steps, net_name)
     p0, p1 = (p.numpy() for p in res['params'])
     np.testing.assert_array_equal(p0, p1)                        # replicas stay identical
     np.testing.assert_allclose(p0, ref_params, rtol=1e-5, atol=1e-7)
@@ -111,6 +128,18 @@ def test_two_rank_sum_allreduce_matches_full_batch(bucket_bytes):
         assert abs(res['sums'][k] - ref_sums[k]) <= 1e-4 * max(1.0, abs(ref_sums[k])), k
     if bucket_bytes == 1024:
         assert res['buckets'] > 1
+
+
+def test_data_parallel_lr_is_the_global_batch_lr():
+    """args['batch_size'] is the per-rank shard; one update SUMs the gradients of world_size shards,
+    so the lr is the reference's for the global batch: 3e-8 * world_size * B * T (train.py:318-322)."""
+    from handyrl_amd.trainer import LearnerStep, Trainer
+    _, args = make_batch_and_args(B=8, T=9)
+    step = LearnerStep(SmallNet(), args, torch.device('cpu'), world_size=4)
+    assert step.optimizer.param_groups[0]['lr'] == pytest.approx(3e-8 * 4 * 8 * 9, rel=1e-12)
+    tr = Trainer(args, SmallNet(), batcher=None, device=torch.device('cpu'), world_size=4)
+    assert tr.data_cnt_ema == 4 * 8 * 9
+    assert tr.learner.optimizer.param_groups[0]['lr'] == pytest.approx(3e-8 * 4 * 8 * 9, rel=1e-12)
 
 
 def test_bucket_layout_covers_flat_buffer():
@@ -136,6 +165,7 @@ def _gpu_rank_main(rank, world, port, out_path, steps, graph=False):
     batch = {k: v.to(dev) for k, v in batch.items()}
     B = batch['value'].size(0)
     shard = {k: v[rank * B // world:(rank + 1) * B // world].contiguous() for k, v in batch.items()}
+    args = dict(args, batch_size=B // world)   # per-rank shard; LearnerStep's lr is the global batch's
     torch.manual_seed(0)
     net = SmallNet()
     step = LearnerStep(net, args, dev, world_size=world, bucket_bytes=1024, graph=graph)
@@ -194,7 +224,8 @@ def _rccl_rank_main(rank, world, port, out_path, steps):
     args = default_args(T, B)
     batch = tictactoe_batch(B, T, dev, seed=4)
     torch.manual_seed(0)
-    step = LearnerStep(SimpleConv2dModel(), args, dev, graph=True, world_size=2)
+    # world_size 2 on a one-rank communicator: pin the lr to the single-GPU step's (train.py:318)
+    step = LearnerStep(SimpleConv2dModel(), args, dev, graph=True, world_size=2, lr=3e-8 * B * T)
     assert step.reducer is not None
     for _ in range(steps):
         step.step(batch)

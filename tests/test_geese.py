@@ -1,13 +1,9 @@
 """GeeseNet (config C4, handyrl/envs/kaggle/hungry_geese.py:23-57) and its HIP torus convolution.
 
-Parity status: the reference module imports kaggle_environments at its top
-(hungry_geese.py:18), which is not installed here, so the reference GeeseNet
-cannot run in this container.  The restatement is pinned to the reference
-SOURCE (module order, state_dict keys, the 116,928 parameters counted in
-SURVEY.md §8e); its torch-CPU forward is the oracle for the HIP path, and the
-learner step is checked against the CPU oracle learner (oracle/learner.py,
-itself pinned to reference goldens).  Reference-output parity for GeeseNet is
-unpinned.
+Parity status: the reference GeeseNet's own outputs are pinned in
+tests/test_geese_golden.py (fixtures made with kaggle_environments stubbed).
+This file covers the HIP torus kernels against torch fp32 on many shapes and
+the learner at a second batch against the CPU oracle learner.
 """
 
 import pytest
@@ -131,8 +127,9 @@ def test_geese_learner_matches_cpu_oracle(cuda, graph):
         r = oracle.step(cpu_batch)
         out = step.step(batch)
         for k in ('p', 'v', 'ent', 'total'):
-            assert abs(float(out[k]) - r[k]) <= 1e-4 * max(1.0, abs(r[k])), (i, k, float(out[k]), r[k])
-        assert abs(float(out['grad_norm']) - r['grad_norm']) <= 1e-3 * max(1e-3, r['grad_norm']), i
+            assert abs(float(out[k]) - r[k]) <= 1e-5 * max(1.0, abs(r[k])), (i, k, float(out[k]), r[k])
+        assert abs(float(out['grad_norm']) - r['grad_norm']) <= 1e-5 * max(1e-3, r['grad_norm']), \
+            (i, float(out['grad_norm']), r['grad_norm'])
     got = dict(step.net.named_parameters())
     for n, p in ref.named_parameters():
         if n.endswith('conv.bias'):

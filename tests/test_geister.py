@@ -133,7 +133,7 @@ def test_gpu_rnn_compute_loss_matches_reference(golden, cuda):
     losses, dcnt = compute_loss(batch, net, hidden, meta['loss']['args'])
     losses['total'].backward()
     grads = {n: float((p.grad.double() ** 2).sum()) for n, p in net.named_parameters() if p.grad is not None}
-    check_loss(losses, dcnt, grads, meta, rtol=1e-4)
+    check_loss(losses, dcnt, grads, meta, rtol=1e-5)
 
 
 @pytest.mark.gpu
@@ -225,8 +225,10 @@ def test_gpu_recurrent_learner_matches_cpu_oracle(cuda, graph):
     for i in range(3):
         r = oracle.step(cpu_batch, zeros('cpu'))
         out = step.step(batch, zeros(cuda))
-        assert abs(float(out['total']) - r['total']) <= 1e-4 * max(1.0, abs(r['total'])), (i, float(out['total']), r)
-        assert abs(float(out['grad_norm']) - r['grad_norm']) <= 1e-3 * max(1e-3, r['grad_norm']), i
+        for k in ('p', 'v', 'r', 'ent', 'total'):
+            assert abs(float(out[k]) - r[k]) <= 1e-5 * max(1.0, abs(r[k])), (i, k, float(out[k]), r[k])
+        assert abs(float(out['grad_norm']) - r['grad_norm']) <= 1e-5 * max(1e-3, r['grad_norm']), \
+            (i, float(out['grad_norm']), r['grad_norm'])
     dead = [n for (n, _), live in zip(step.net.named_parameters(), step.live) if not live]
     assert sorted(dead) == sorted('body.blocks.%d.conv.%s' % (i, k) for i in (0, 1) for k in ('weight', 'bias'))
     got = dict(step.net.named_parameters())
