@@ -7,19 +7,19 @@ it is named either by a registry key or by its import path
 the learner trains (forward(x, hidden) -> {'policy', 'value'[, 'return'][,
 'hidden']}, optional init_hidden(batch_size)).
 
-Registry entries point at this package's own env modules where one exists;
-any other module path (e.g. ``handyrl.envs.geister`` from a HandyRL checkout
-on ``sys.path``) is imported as given.
+Every registry key resolves to this package's own env module; any other
+module path (e.g. a user's ``my_envs.go`` or ``handyrl.envs.geister`` from a
+HandyRL checkout on ``sys.path``) is imported as given.
 """
 
 import importlib
 
-ENVS = {
+ENVS = {   # environment.py:9-15, every key resolved inside this package
     'TicTacToe': 'handyrl_amd.envs.tictactoe',
-    'Geister': 'handyrl.envs.geister',
-    'CIGeister': 'handyrl.envs.ci_geister',
-    'ParallelTicTacToe': 'handyrl.envs.parallel_tictactoe',
-    'HungryGeese': 'handyrl.envs.kaggle.hungry_geese',
+    'Geister': 'handyrl_amd.envs.geister',
+    'CIGeister': 'handyrl_amd.envs.ci_geister',
+    'ParallelTicTacToe': 'handyrl_amd.envs.parallel_tictactoe',
+    'HungryGeese': 'handyrl_amd.envs.hungry_geese',
 }
 
 

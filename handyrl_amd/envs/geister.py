@@ -18,7 +18,9 @@ bit for bit (pinned by tests/golden/geister_net.json):
 
 ``GeisterBatch`` restates the rules (geister.py:170-541) as tensor ops over
 E concurrent games for device self-play (rollout.DeviceGenerator); the
-per-game CPU plugin stays the reference's Environment.  Observation format
+per-game plugin ``Environment`` (the reference's API, geister.py:170-541) is
+one such game on the CPU, so both share one statement of the rules.
+Observation format
 {'board': (7, 6, 6), 'scalar': (18,)}, 214 actions.
 """
 
@@ -26,6 +28,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ..environment import BaseEnvironment
 
 BOARD = (6, 6)
 BOARD_PLANES = 7
@@ -312,8 +316,11 @@ class GeisterBatch:
         draw = moving & (self.turn_count >= self.MAX_MOVES) & (win < 0)
         self.win = torch.where(draw, torch.full_like(win, 2), win)
 
-    def observation(self, player):
-        """{'board': (E,7,6,6), 'scalar': (E,18)} seen by `player` (E,) (geister.py:495-535, player given)."""
+    COMPLETE_INFO = False   # CIGeister (ci_geister.py:520-568) shows the opponent's colours in every view
+
+    def observation(self, player, full=False):
+        """{'board': (E,7,6,6), 'scalar': (E,18)} seen by `player` (E,) (geister.py:495-535, player given);
+        ``full``: the reference's ``observation(None)`` view, which also shows the opponent's colours."""
         turn_view = player == self.color
         me = torch.where(turn_view, self.color, 1 - self.color)
         opp = 1 - me
@@ -327,8 +334,11 @@ class GeisterBatch:
         red_c = b == (me * 2 + 1).view(-1, 1)
         own_all = blue_c | red_c
         opp_all = (b >= 0) & ~own_all
-        zero = torch.zeros_like(own_all)
-        planes = torch.stack([torch.ones_like(own_all), own_all, opp_all, blue_c, red_c, zero, zero], 1).float()
+        if full or self.COMPLETE_INFO:
+            blue_o, red_o = b == (opp * 2).view(-1, 1), b == (opp * 2 + 1).view(-1, 1)
+        else:
+            blue_o = red_o = torch.zeros_like(own_all)
+        planes = torch.stack([torch.ones_like(own_all), own_all, opp_all, blue_c, red_c, blue_o, red_o], 1).float()
         planes = torch.where((me == 1).view(-1, 1, 1), planes.flip(-1), planes)   # white: rotate 180 degrees
         return {'board': planes.view(-1, BOARD_PLANES, *BOARD), 'scalar': scalar}
 
@@ -340,3 +350,96 @@ class GeisterBatch:
         """(E, 2): +1/-1 for the winning colour, 0/0 for a draw (geister.py:431-438)."""
         w = torch.where(self.win == 0, 1.0, torch.where(self.win == 1, -1.0, 0.0))
         return torch.stack([w, -w], dim=1)
+
+
+class Environment(BaseEnvironment):
+    """One Geister game behind the reference plugin API (geister.py:170-541).
+
+    The state is a one-game ``GeisterBatch`` on the CPU, so the rules are the
+    same tensor code the device self-play runs (pinned to the reference env by
+    tests/test_geister_rules.py).  Actions and observations are the
+    reference's: 214 labels, ``{'board': (7, 6, 6), 'scalar': (18,)}`` numpy
+    arrays; ``observation(None)`` is the turn player's view with the
+    opponent's colours shown, ``observation(p)`` hides them.
+    """
+
+    BATCH = GeisterBatch
+    X, Y = 'ABCDEF', '123456'
+
+    def __init__(self, args=None):
+        super().__init__(args)
+        self.game = self.BATCH(1, torch.device('cpu'))
+        self.reset()
+
+    def reset(self, args=None):
+        self.game.reset()
+        self.record = []
+
+    def __str__(self):
+        b = self.game.board[0].view(6, 6).tolist()
+        marks = {-1: '_', 0: 'B', 1: 'R', 2: 'b', 3: 'r'}
+        rows = ['  ' + ' '.join(self.Y)] + [self.X[i] + ' ' + ' '.join(marks[v] for v in b[i]) for i in range(6)]
+        return '\n'.join(rows) + '\ncolor = ' + 'BW'[self.turn()] + '\nrecord = ' + ' '.join(
+            self.action2str(a, i % 2) for i, a in enumerate(self.record))
+
+    def play(self, action, _=None):
+        self.game.step(torch.tensor([int(action)]), torch.tensor([True]))
+        self.record.append(int(action))
+
+    def turn(self):
+        return int(self.game.color[0])
+
+    def terminal(self):
+        return bool(self.game.win[0] >= 0)
+
+    def reward(self):
+        return {p: -0.01 for p in self.players()}
+
+    def outcome(self):
+        o = self.game.outcome()[0].tolist()
+        return {0: o[0], 1: o[1]}
+
+    def legal_actions(self, _=None):
+        return torch.nonzero(self.game.legal()[0]).view(-1).tolist()
+
+    def action_length(self):
+        return ACTIONS
+
+    def players(self):
+        return [0, 1]
+
+    def observation(self, player=None):
+        who = self.turn() if player is None else player
+        obs = self.game.observation(torch.tensor([who]), full=player is None)
+        return {'scalar': obs['scalar'][0].numpy(), 'board': obs['board'][0].numpy()}
+
+    def net(self):
+        return GeisterNet
+
+    # -- move notation (geister.py:263-330): 'B2C2' from/to in absolute squares, '**' = off the board by
+    # a goal, 's<k>' = initial layout k; white's labels are in its 180-degree rotated frame
+    def _square(self, x, y):
+        return self.X[x] + self.Y[y] if 0 <= x < 6 and 0 <= y < 6 else '**'
+
+    def action2str(self, a, player):
+        a = int(a)
+        if a >= GeisterBatch.MOVES:
+            return 's' + str(a - GeisterBatch.MOVES)
+        d, x, y = a // 36, (a % 36) // 6, a % 6
+        if player == 1:
+            d, x, y = 3 - d, 5 - x, 5 - y
+        dx, dy = GeisterBatch.DIRS[d]
+        return self._square(x, y) + self._square(x + dx, y + dy)
+
+    def str2action(self, s, player):
+        if s[0] == 's':
+            return GeisterBatch.MOVES + int(s[1:])
+        x, y = self.X.index(s[0]), self.Y.index(s[1])
+        if s[2:] == '**':
+            d = next(d for d, (dx, dy) in enumerate(GeisterBatch.DIRS) if (x + dx, y + dy) in GeisterBatch.GOALS[player])
+        else:
+            tx, ty = self.X.index(s[2]), self.Y.index(s[3])
+            d = GeisterBatch.DIRS.index((tx - x, ty - y))
+        if player == 1:
+            d, x, y = 3 - d, 5 - x, 5 - y
+        return d * 36 + x * 6 + y

@@ -273,7 +273,7 @@ class Trainer:
     dict (host or device tensors); ``model`` is the env's network.
     """
 
-    def __init__(self, args, model, batcher, device=None, graph=False, world_size=1, group=None):
+    def __init__(self, args, model, batcher, device=None, graph=False, world_size=1, group=None, loss_fn=None):
         self.args = args
         self.model = model
         self.batcher = batcher
@@ -285,14 +285,10 @@ class Trainer:
         self.update_flag = False
         self.shutdown_flag = False
         self.learner = LearnerStep(model, args, self.device, lr=self.default_lr * self.data_cnt_ema,
-                                   graph=graph, reduce_group=group, world_size=world_size)
+                                   graph=graph, reduce_group=group, world_size=world_size, loss_fn=loss_fn)
 
     def _to_device(self, batch):
-        def mv(x):
-            if isinstance(x, dict):
-                return {k: mv(v) for k, v in x.items()}
-            return x.to(self.device, non_blocking=True) if x is not None else None
-        return mv(batch)
+        return map_r(batch, lambda x: x.to(self.device, non_blocking=True) if x is not None else None)
 
     def train(self, max_steps=None):
         """One epoch: step until update_flag / shutdown (or max_steps); returns a CPU model copy."""
@@ -312,7 +308,8 @@ class Trainer:
         sums.pop('grad_norm', None)
         print('loss = %s' % ' '.join('%s:%.3f' % (k, v / max(data_cnt, 1e-9)) for k, v in sums.items()))
         self.data_cnt_ema = self.data_cnt_ema * 0.8 + data_cnt / (1e-2 + batch_cnt) * 0.2
-        self.learner.set_lr(self.default_lr * self.data_cnt_ema / (1 + self.steps * 1e-5))
+        self.lr = self.default_lr * self.data_cnt_ema / (1 + self.steps * 1e-5)
+        self.learner.set_lr(self.lr)
         model = copy.deepcopy(self.model).cpu()
         model.eval()
         return model

@@ -36,6 +36,12 @@ Fixtures written
     and three ``Trainer.train`` learner steps with the final state_dict.  The
     batch is ``handyrl_amd.synthetic.geese_batch`` (no Hungry Geese rules here),
     stored as input arrays.
+``trainer.npz`` + ``trainer.json``
+    ``Trainer.train`` (train.py:312-401) for two epochs of 2 and 3 batches
+    over fixed TicTacToe ``make_batch`` batches (the batcher replaced by a
+    list that raises ``update_flag`` at the epoch's last batch): the lr and
+    ``data_cnt_ema`` after each epoch (the epoch-end schedule, :396-398) and
+    the final weights.
 ``learner.npz`` + ``learner.json``
     Three learner steps of the TicTacToe ``SimpleConv2dModel`` exactly as
     ``Trainer.train`` runs them (train.py:375-385): loss, backward,
@@ -556,8 +562,62 @@ def geese_net_case():
     return arrays, meta
 
 
+# ---------------------------------------------------------------------------
+# 8. Trainer.train epochs: lr schedule and data-count EMA (train.py:312-401)
+# ---------------------------------------------------------------------------
+
+def trainer_case():
+    from handyrl.envs.tictactoe import SimpleConv2dModel
+    B, T = 16, 9
+    eps = gen_episodes('TicTacToe', 32, False, seed=41, net_cls=SimpleConv2dModel)
+    args = {'turn_based_training': True, 'observation': False, 'forward_steps': T, 'compress_steps': 4,
+            'lambda': 0.7, 'gamma': 0.8, 'policy_target': 'UPGO', 'value_target': 'VTRACE',
+            'entropy_regularization': 0.1, 'entropy_regularization_decay': 0.1, 'batch_size': B,
+            'maximum_episodes': 1000, 'num_batchers': 1}
+    batches = [ref_train.make_batch(select_windows(eps, B, T, 4, seed=60 + i), args) for i in range(5)]
+    arrays = {}
+    for i, b in enumerate(batches):
+        for k, v in b.items():
+            arrays['batch%d.%s' % (i, k)] = _np(v)
+    torch.manual_seed(2025)
+    net = SimpleConv2dModel()
+    real_batcher = ref_train.Batcher
+    ref_train.Batcher = lambda *a, **k: None       # no batcher processes: batches come from the list
+    try:
+        trainer = ref_train.Trainer(args, net)
+    finally:
+        ref_train.Batcher = real_batcher
+
+    class ListBatcher:
+        def __init__(self, items):
+            self.items = list(items)
+
+        def batch(self):
+            b = self.items.pop(0)
+            if not self.items:
+                trainer.update_flag = True     # the epoch ends after this batch (train.py:372)
+            return b
+    epochs = []
+    for lo, hi in ((0, 2), (2, 5)):
+        trainer.update_flag = False
+        trainer.batcher = ListBatcher(batches[lo:hi])
+        trainer.train()
+        epochs.append({'batches': [lo, hi], 'lr': trainer.optimizer.param_groups[0]['lr'],
+                       'data_cnt_ema': trainer.data_cnt_ema, 'steps': trainer.steps})
+    for k, v in trainer.model.state_dict().items():
+        arrays['final.' + k] = _np(v)
+    return arrays, {'args': args, 'epochs': epochs, 'seed': 2025}
+
+
 def main():
     only = sys.argv[1:]
+    if only == ['trainer']:
+        arr, meta = trainer_case()
+        np.savez_compressed(os.path.join(OUT, 'trainer.npz'), **arr)
+        with open(os.path.join(OUT, 'trainer.json'), 'w') as f:
+            json.dump(meta, f, indent=1)
+        print('trainer: %d epochs' % len(meta['epochs']))
+        return
     if only == ['geese']:
         arr, meta = geese_net_case()
         np.savez_compressed(os.path.join(OUT, 'geese_net.npz'), **arr)
@@ -607,6 +667,12 @@ def main():
     with open(os.path.join(OUT, 'geese_net.json'), 'w') as f:
         json.dump(meta, f, indent=1)
     print('geese net: %d tensors' % len(meta['state']))
+
+    arr, meta = trainer_case()
+    np.savez_compressed(os.path.join(OUT, 'trainer.npz'), **arr)
+    with open(os.path.join(OUT, 'trainer.json'), 'w') as f:
+        json.dump(meta, f, indent=1)
+    print('trainer: %d epochs' % len(meta['epochs']))
 
     arr, meta = learner_case()
     np.savez_compressed(os.path.join(OUT, 'learner.npz'), **arr)
