@@ -165,8 +165,11 @@ def pmc_traffic(B, T):
     return None
 
 
-def cpu_baseline(B=2048, T=32, steps=6):
-    """The CPU learner oracle on this host, 1 thread (train.py as shipped: model.py:8)."""
+def cpu_baseline(B=4096, T=32, steps=3):
+    """The CPU learner oracle on this host, 1 thread (train.py as shipped: model.py:8), at the metric's
+    B=4096 T=32 (about 4 s per step on the GPU box's host cores).  Calibrated against the reference
+    itself in the build container by tools/calibrate_cpu.py (profiles/r02_cpu_calibration.json: the
+    port runs at 0.91-1.07x the reference's time)."""
     from oracle.learner import CpuLearner
     threads = torch.get_num_threads()
     torch.set_num_threads(1)
