@@ -398,10 +398,7 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
 // ------------------------------------------------------------------ weight gradient
 // dW[tap][ci][co] = sum_rows sum_{(p,q): tap(p,q) = tap} x[row, ci, p] * dy[row, co, q]
 // MFMA C tile = 16 ci x 16 co; A[i = ci][k = row], B[k = row][j = co]
-// The weight gradient stays on fp32 MFMA.  A split form (contraction index = (pair of the tap, row),
-// two pairs x 16 rows per 32-deep bf16 k-step, every operand re-split per pair) was measured at
-// 274 us against this kernel's 140 us: the per-pair LDS gathers and splits cost more than the MFMA
-// cycles they save.
+// fp32 MFMA form (hrl_conv3x3_set_split(0)); the default is conv3x3_wgrad_split_kernel below.
 template <bool PRO>
 __global__ __launch_bounds__(kThreads) void conv3x3_wgrad_kernel(const float *__restrict__ x,
                                                                  const float *__restrict__ in_alpha,
@@ -505,6 +502,135 @@ __global__ __launch_bounds__(kThreads) void conv3x3_wgrad_kernel(const float *__
                     const int co = jt * 16 + (lane & 15);
                     red[wave * kW + (t * kC + ci) * kC + co] = acc[t][it][jt][r];
                 }
+    __syncthreads();
+    float *out = partial + (int64_t)blockIdx.x * kW;
+    for (int i = threadIdx.x; i < kW; i += kThreads)
+        out[i] = ((red[i] + red[kW + i]) + red[2 * kW + i]) + red[3 * kW + i];
+}
+
+// Weight gradient on the exact bf16 split (default; hrl_conv3x3_set_split).  One tap's dW is a 32x32
+// (ci, co) matrix, i.e. exactly one v_mfma_f32_32x32x16_bf16 tile, and a 16-row tile is one K=16 step:
+//   dW[tap] += X_p^T (32 ci x 16 rows) . dY_q (16 rows x 32 co)   for every (p, q) with tap(p, q) = tap,
+// six partial products per pair (hrl_split.h), 49 pairs x 6 = 294 MFMAs of 32 cycles per tile against
+// 784 fp32 16x16x4 MFMAs of 32 cycles.  Both operands are split ONCE per tile: the nine dY_q fragments
+// are split up front and held in registers, X_p is split as the p loop reaches it (a former split form
+// re-split every operand per (p, q) pair and ran at 274 us).  Lane l = (r = l & 31, h = l >> 5) holds
+// rows 8h..8h+7 of channel r of a cell: A[i = ci = r][k = row], B[k = row][j = co = r].  The tiles sit in
+// LDS with a row stride of 292 floats (16-byte aligned rows, so tiles are written with ds_write_b128;
+// 8 x 292 == 32 (mod 64), so the two lane halves' column reads do not collide).  Waves fold in a fixed
+// order: deterministic.
+constexpr int kStrideW = kRow + 4;   // 292
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma32(const uint4 &a, const uint4 &b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+
+template <bool PRO>
+__global__ __launch_bounds__(kThreads) void conv3x3_wgrad_split_kernel(const float *__restrict__ x,
+                                                                       const float *__restrict__ in_alpha,
+                                                                       const float *__restrict__ in_beta,
+                                                                       const float *__restrict__ dy, int64_t M,
+                                                                       float *__restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float lds[2 * kWaves * kTile * kStrideW];   // 149.5 KB
+    static_assert(2 * kWaves * kTile * kStrideW >= kWaves * kTaps * kC * kC, "fold buffer");
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    float *xs = lds + wave * kTile * kStrideW;
+    float *gs = lds + (kWaves + wave) * kTile * kStrideW;
+    const int r = lane & 31, h = lane >> 5;
+    float pa = 1.f, pb = 0.f;
+    if constexpr (PRO) {   // x is a raw conv output read as relu(x*alpha + beta); A rows are channel r
+        pa = in_alpha[r];
+        pb = in_beta[r];
+    }
+    const int64_t ntiles = (M + kTile - 1) / kTile;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    const int64_t lim = M * kRow;
+
+    f32x16 acc[kTaps];
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+
+    for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < ntiles; tile += stride) {
+        {
+            const int64_t base = tile * kTile * kRow;
+            float4 sx[kVec], sg[kVec];
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                const int64_t e = base + (int64_t)(k * 64 + lane) * 4;
+                const int64_t ec = e < lim ? e : lim - 4;
+                sx[k] = *reinterpret_cast<const float4 *>(x + ec);
+                sg[k] = *reinterpret_cast<const float4 *>(dy + ec);
+            }
+#pragma unroll
+            for (int k = 0; k < kVec; ++k) {
+                const int e = (k * 64 + lane) * 4;
+                const int row = e / kRow, c = e - row * kRow;
+                const bool ok = base + e < lim;   // ragged tile: zero gradient rows
+                *reinterpret_cast<float4 *>(xs + row * kStrideW + c) = sx[k];
+                *reinterpret_cast<float4 *>(gs + row * kStrideW + c) = ok ? sg[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes done
+        __builtin_amdgcn_wave_barrier();
+
+        // the nine dY_q fragments, split once
+        uint4 Bh[kCells], Bm[kCells], Bl[kCells];
+        const float *gcol = gs + (8 * h) * kStrideW + r * kCells;
+#pragma unroll
+        for (int q = 0; q < kCells; ++q) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = gcol[j * kStrideW + q];
+            hrl_split::split8(v, Bh[q], Bm[q], Bl[q]);
+        }
+        const float *xcol = xs + (8 * h) * kStrideW + r * kCells;
+#pragma unroll
+        for (int p = 0; p < kCells; ++p) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float a = xcol[j * kStrideW + p];
+                if constexpr (PRO) {   // bn_apply_kernel's float operations
+                    const float t = a * pa + pb;
+                    a = t < 0.f ? 0.f : t;
+                }
+                v[j] = a;
+            }
+            uint4 Ah, Am, Al;
+            hrl_split::split8(v, Ah, Am, Al);
+#pragma unroll
+            for (int q = 0; q < kCells; ++q) {
+                const int tap = tap_of(p, q);
+                if (tap < 0) continue;
+                f32x16 c = acc[tap];
+                c = mfma32(Al, Bh[q], c);   // smallest terms first
+                c = mfma32(Am, Bm[q], c);
+                c = mfma32(Ah, Bl[q], c);
+                c = mfma32(Am, Bh[q], c);
+                c = mfma32(Ah, Bm[q], c);
+                c = mfma32(Ah, Bh[q], c);
+                acc[tap] = c;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    // fold the block's 4 wave partials in a fixed order: partial[block][tap][ci][co]
+    __syncthreads();
+    float *red = lds;
+    constexpr int kW = kTaps * kC * kC;
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int ci = (i & 3) + 8 * (i >> 2) + 4 * h;   // C/D: col = lane & 31, row = (reg&3) + 8(reg>>2) + 4h
+            red[wave * kW + (t * kC + ci) * kC + r] = acc[t][i];
+        }
     __syncthreads();
     float *out = partial + (int64_t)blockIdx.x * kW;
     for (int i = threadIdx.x; i < kW; i += kThreads)
@@ -674,12 +800,20 @@ int hrl_conv3x3_wgrad_ex(const float *x, const float *in_alpha, const float *in_
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int grid = grid_for(M);
     float *partial = static_cast<float *>(workspace) + kTaps * 2 * kC * 16 * 2;
-    if (in_alpha)
+    if (g_split) {
+        if (in_alpha)
+            hipLaunchKernelGGL((conv3x3_wgrad_split_kernel<true>), dim3(grid), dim3(kThreads), 0, s, x, in_alpha,
+                               in_beta, dy, M, partial);
+        else
+            hipLaunchKernelGGL((conv3x3_wgrad_split_kernel<false>), dim3(grid), dim3(kThreads), 0, s, x, in_alpha,
+                               in_beta, dy, M, partial);
+    } else if (in_alpha) {
         hipLaunchKernelGGL((conv3x3_wgrad_kernel<true>), dim3(grid), dim3(kThreads), 0, s, x, in_alpha, in_beta, dy,
                            M, partial);
-    else
+    } else {
         hipLaunchKernelGGL((conv3x3_wgrad_kernel<false>), dim3(grid), dim3(kThreads), 0, s, x, in_alpha, in_beta,
                            dy, M, partial);
+    }
     int rc = status();
     if (rc) return rc;
     hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, partial, grid,

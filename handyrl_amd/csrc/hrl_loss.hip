@@ -1,18 +1,16 @@
 // hrl_loss.hip — fused learner loss for HandyRL on MI355X (gfx950).
 //
 // One learner step's loss after the network forward, train.py:220-258 and
-// compose_losses train.py:188-215, as five launches instead of ~60 small
+// compose_losses train.py:188-215, as two launches instead of ~60 small
 // PyTorch kernels (log_softmax x2, gather x2, exp, clamp x2, stack/neg/div
 // for the zero-sum symmetrisation, 2-4 target scans, the advantage
 // composition, five masked reductions, Categorical entropy, ...):
 //
-//   prep   (one thread per (b,t)): log-softmax + gather of the behaviour and
-//          target policies, rho = exp(lt - lb), clipped rho, entropy of the
-//          target policy, zero-sum value symmetrisation and outcome padding
-//   scan x2 (hrl_targets.hip): value head (value_target targets +
-//          policy_target advantages) and return head, one launch each
-//   terms  (one thread per (b,t)): turn advantages, the five loss sums and
-//          dcnt as fp64 per-block partials
+//   fused  (one wave per G trajectories, LDS tiles of 32 time steps): the IS
+//          ratios, the target policy's entropy, the value preparation, the
+//          value- and return-head scans of hrl_scan.h (value_target targets +
+//          policy_target advantages), the turn advantages and the five loss
+//          sums and dcnt as fp64 per-wave partials
 //   reduce (one workgroup): fixed-order fold of the partials -> 6 floats
 //
 // and the backward as ONE launch of closed-form gradients w.r.t. the target
@@ -25,10 +23,17 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/hrl_loss.h"
 #include "../../include/hrl_targets.h"
+#include "hrl_scan.h"
 
 namespace {
+
+using hrl_scan::Coef;
+
+HRL_STAMP_DECL
 
 constexpr int kThreads = 256;
 constexpr int kTerms = 6;   // p, v (before /2), r, ent, ent weighted by progress, dcnt
@@ -42,8 +47,11 @@ struct LossDims {
 struct Ws {
     float *lt, *crho, *ent, *vprep, *tv, *advv, *tr, *advr, *turn;
     double *part;
-    int nblocks;
+    int nblocks;   // 256-thread blocks over B*T (backward)
+    int nparts;    // waves of the fused forward, one fp64 partial set each
 };
+
+int fused_G(int64_t B, int P);
 
 __host__ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
@@ -63,13 +71,21 @@ __host__ __device__ inline Ws carve(void *base, const LossDims &d) {
     const int64_t off = align16((int64_t)((char *)f - (char *)base));
     w.part = reinterpret_cast<double *>((char *)base + off);
     w.nblocks = (int)((d.BT + kThreads - 1) / kThreads);
+    const int G = fused_G(d.B, d.P);
+    w.nparts = (int)((d.B + G - 1) / G);
     return w;
 }
 
 int64_t ws_bytes(const LossDims &d) {
     const int64_t floats = 3 * d.BT * d.Pp + 5 * d.BT * d.P + d.BT;
-    const int64_t nblocks = (d.BT + kThreads - 1) / kThreads;
-    return align16(floats * 4) + nblocks * kTerms * 8 + 64;
+    const int G = fused_G(d.B, d.P);
+    const int64_t nparts = (d.B + G - 1) / G;
+    return align16(floats * 4) + nparts * kTerms * 8 + 64;
+}
+
+int status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
 }
 
 struct FwdArgs {
@@ -88,109 +104,349 @@ __device__ __forceinline__ void row_stats(const float *z, int A, float &m, float
     for (int a = 0; a < A; ++a) s += expf(z[a] - m);
 }
 
-// ---- prep: IS ratios, entropy, value preparation -----------------------------------------------
-__global__ __launch_bounds__(kThreads) void loss_prep_kernel(FwdArgs a, LossDims d, Ws w) {
-    const int64_t bt = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (bt >= d.BT) return;
-    const int64_t b = bt / d.T;
-    const float em = a.emask[bt];
-    for (int pp = 0; pp < d.Pp; ++pp) {
-        const int64_t row = bt * d.Pp + pp;
-        const float *zt = a.tpol + row * d.A;
-        const float *zb = a.bpol + row * d.A;
-        const int64_t act = a.action[row];
-        float mt, st, mb, sb;
-        row_stats(zt, d.A, mt, st);
-        row_stats(zb, d.A, mb, sb);
+// One policy row (train.py:224-231): lt = log_softmax(target)[act] * emask, the clipped IS ratio
+// clamp(exp(lt - lb), 0, 1) and the target policy's entropy.  AK > 0: the row has exactly AK actions
+// (compile time) and sits in registers, so its loads issue at once and no per-action guard exists;
+// AK = 0: any A, one action per loop trip.  Same float operations in the same order either way.
+template <int AK>
+__device__ __forceinline__ void policy_row(const float *zt, const float *zb, int A, int act, float em, float &lt,
+                                           float &crho, float &ent) {
+    float mt, st, mb, sb;
+    float h = 0.f;
+    if constexpr (AK > 0) {
+        float xt[AK], xb[AK], et[AK];
+#pragma unroll
+        for (int q = 0; q < AK; ++q) {
+            xt[q] = zt[q];
+            xb[q] = zb[q];
+        }
+        mt = xt[0];
+        mb = xb[0];
+#pragma unroll
+        for (int q = 1; q < AK; ++q) {
+            mt = fmaxf(mt, xt[q]);
+            mb = fmaxf(mb, xb[q]);
+        }
+        st = 0.f;
+        sb = 0.f;
+        float zta = xt[0], zba = xb[0];
+#pragma unroll
+        for (int q = 0; q < AK; ++q) {
+            et[q] = expf(xt[q] - mt);
+            st += et[q];
+            sb += expf(xb[q] - mb);
+            zta = q == act ? xt[q] : zta;
+            zba = q == act ? xb[q] : zba;
+        }
+        lt = ((zta - mt) - logf(st)) * em;                                  // train.py:224-225
+        const float lb = ((zba - mb) - logf(sb)) * em;
+        const float lse = mt + logf(st);
+#pragma unroll
+        for (int q = 0; q < AK; ++q) h += (xt[q] - lse) * (et[q] / st);
+        crho = fminf(fmaxf(expf(lt - lb), 0.f), 1.f);                        // train.py:228-231
+    } else {
+        row_stats(zt, A, mt, st);
+        row_stats(zb, A, mb, sb);
         // F.log_softmax(x)[act] = (x - max) - log(sum exp(x - max))      (train.py:224-225)
-        const float lt = ((zt[act] - mt) - logf(st)) * em;
+        lt = ((zt[act] - mt) - logf(st)) * em;
         const float lb = ((zb[act] - mb) - logf(sb)) * em;
-        const float rho = expf(lt - lb);                                    // train.py:228-229
-        w.lt[row] = lt;
-        w.crho[row] = fminf(fmaxf(rho, 0.f), 1.f);                          // train.py:230-231
         // Categorical(logits).entropy(): logits normalised by logsumexp = m + log(s)
         const float lse = mt + logf(st);
-        float h = 0.f;
-        for (int q = 0; q < d.A; ++q) {
-            const float la = zt[q] - lse;
-            h += la * (expf(zt[q] - mt) / st);
-        }
-        w.ent[row] = -h;
+        for (int q = 0; q < A; ++q) h += (zt[q] - lse) * (expf(zt[q] - mt) / st);
+        crho = fminf(fmaxf(expf(lt - lb), 0.f), 1.f);                        // train.py:228-231
     }
-    if (a.value) {                                                          // train.py:234-239
-        const float *v = a.value + bt * d.P;
-        const float *om = a.omask + bt * d.P;
-        for (int p = 0; p < d.P; ++p) {
-            float vp = v[p];
-            if (a.symmetrize) {   // two-player zero-sum: (v - swap(v)) / (sum omask + 1e-8)
-                vp = (v[p] + (-v[1 - p])) / ((om[0] + om[1]) + 1e-8f);
+    ent = -h;
+}
+
+// action counts with a register-resident specialisation of the fused loss (TicTacToe 9, Hungry Geese 4);
+// any other A runs the loop form
+
+// ---- fused forward: prep + both target scans + loss terms, one wave per G trajectories ------------
+//
+// A wave owns G consecutive trajectories and walks them in LDS tiles of up to kLossTile time steps,
+// top tile first (the scans run backwards in time).  Per tile:
+//   1. prep (lanes over the tile's (g, t, pp) rows): log-softmax + gather of both policies, the IS
+//      ratio and its clip, the target policy's entropy (train.py:224-231); the zero-sum value
+//      preparation with outcome padding (train.py:234-239) and the return head's inputs, all into
+//      LDS tiles laid out as the scans read them;
+//   2. the value- and return-head recurrences (hrl_scan.h), lane (g, c) per column, straight from
+//      and back into LDS: the 4-5 MB round trip of the former prep -> scan -> terms launches is gone;
+//   3. terms (lanes over (g, t)): the turn advantages and the five loss sums and dcnt, accumulated
+//      in fp64 per lane (train.py:202-213, 248-256); turn, the targets and the entropy go to the
+//      workspace for the backward.
+// The wave folds its partials in a fixed shuffle tree, so the sums are deterministic.
+constexpr int kLossTile = 32;   // time steps per LDS tile (two register-resident recurrence chunks)
+
+struct FusedArgs {
+    FwdArgs a;
+    LossDims d;
+    Ws w;
+    Coef kv;   // value head: gamma = 1 (train.py:245)
+    Coef kr;   // return head: gamma (train.py:246)
+    int G;     // trajectories per wave
+};
+
+// trajectories per wave: G*P <= 64 scan lanes, at most 8 (so a tile's prep/terms rows stay a few
+// per lane), fewer at small B so the launch still has ~2048 waves: two per SIMD, so one wave's
+// loads overlap the other's recurrence (B=4096: G=2, one prep row per lane at T=32)
+int fused_G(int64_t B, int P) {
+    const int gmax = min(8, hrl_scan::kWave / P);
+    int g = 1;
+    while (g * 2 <= gmax && B / (g * 2) >= 2048) g *= 2;
+    return g;
+}
+
+size_t fused_lds_bytes(const LossDims &d, int G, bool hv, bool hr, bool vt_mc, bool pt_mc) {
+    const int TT = d.T < kLossTile ? (int)d.T : kLossTile;
+    const size_t vt = (size_t)G * hrl_scan::padded_row(TT * d.P, d.P);
+    const size_t rt = (size_t)G * hrl_scan::padded_row(TT * d.Pp, 1);
+    const int ntiles = (hv ? 2 + (vt_mc ? 0 : 1) : 0) + (hr ? 3 + (pt_mc ? 1 : 0) + (vt_mc ? 0 : 1) : 0);
+    return sizeof(float) * (3 * rt + ntiles * vt);
+}
+
+template <int VT, int PT, bool HV, bool HR, int AK>
+__global__ __launch_bounds__(hrl_scan::kWave) void loss_fused_kernel(FusedArgs f) {
+    using namespace hrl_scan;
+    constexpr int TGT = VT == HRL_ALG_MC ? kNone : VT;            // MC targets are the returns as given
+    constexpr bool kRho = (TGT == HRL_ALG_VTRACE) || (PT == HRL_ALG_VTRACE);
+    constexpr bool kRetT = PT == HRL_ALG_MC;                      // return-head MC reads ret at every t
+    extern __shared__ float lds[];
+    const FwdArgs &a = f.a;
+    const LossDims &d = f.d;
+    const Ws &w = f.w;
+    const int lane = threadIdx.x;
+    const int P = d.P, Pp = d.Pp, A = AK > 0 ? AK : d.A, T = (int)d.T;
+    const int C = P, rhoC = Pp, rhoDiv = P / Pp;
+    const int G = f.G;
+    const int TT = T < kLossTile ? T : kLossTile;
+    const int Lpv = padded_row(TT * C, C), Lpr = padded_row(TT * rhoC, 1);
+    const int64_t b0 = (int64_t)blockIdx.x * G;
+    const int ntraj = (int)min<int64_t>(G, d.B - b0);
+
+    const int vt = G * Lpv, rt = G * Lpr;
+    float *p = lds;
+    float *t_rho = p; p += rt;
+    float *t_lt = p; p += rt;
+    float *t_ent = p; p += rt;
+    float *t_v = p; p += HV ? vt : 0;
+    float *t_tv = p; p += (HV && TGT != kNone) ? vt : 0;
+    float *t_advv = p; p += HV ? vt : 0;
+    float *t_rv = p; p += HR ? vt : 0;
+    float *t_rr = p; p += HR ? vt : 0;
+    float *t_rret = p; p += (HR && kRetT) ? vt : 0;
+    float *t_tr = p; p += (HR && TGT != kNone) ? vt : 0;
+    float *t_advr = p;
+
+    const int g = lane / C;                 // scan lane (g, c)
+    const int c = lane - g * C;
+    const bool active = lane < G * C && g < ntraj;
+    float boot_v = 0.f, boot_r = 0.f;
+    if (active) {
+        if constexpr (HV) boot_v = a.outcome[(b0 + g) * P + c];
+        if constexpr (HR) boot_r = a.ret[((b0 + g) * d.T + (T - 1)) * P + c];
+    }
+    Carry sv{0.f, 0.f, 0.f, 0.f, 0.f}, sr{0.f, 0.f, 0.f, 0.f, 0.f};
+    double acc[kTerms] = {0, 0, 0, 0, 0, 0};
+    HRL_STAMP_WALL(14);
+    HRL_STAMP(0);
+
+    const int ntile = (T + kLossTile - 1) / kLossTile;
+    for (int tile = ntile - 1; tile >= 0; --tile) {
+        const int t0 = tile * kLossTile;
+        const int tc = min(kLossTile, T - t0);
+
+        // 1. prep: policy rows (g, t, pp)
+        {
+            const int per = tc * Pp;
+            const float inv_per = 1.0f / (float)per, inv_pp = 1.0f / (float)Pp;
+            for (int e = lane; e < ntraj * per; e += kWave) {
+                const int gg = fdiv(e, inv_per);
+                const int rem = e - gg * per;
+                const int tt = fdiv(rem, inv_pp);
+                const int pp = rem - tt * Pp;
+                const int64_t bt = (b0 + gg) * d.T + t0 + tt;
+                const int64_t row = bt * Pp + pp;
+                const float em = a.emask[bt];
+                const int64_t act = a.action[row];
+                float lt, crho, ent;
+                policy_row<AK>(a.tpol + row * A, a.bpol + row * A, A, (int)act, em, lt, crho, ent);
+                const int slot = gg * Lpr + tt * rhoC + pp;
+                t_rho[slot] = crho;
+                t_lt[slot] = lt;
+                t_ent[slot] = ent;
             }
-            const float oc = a.outcome[b * d.P + p];
-            w.vprep[bt * d.P + p] = vp * em + oc * (1.f - em);
-            if (a.value_mc) w.tv[bt * d.P + p] = oc;     // MC value target = outcome (losses.py:17)
         }
+        HRL_STAMP(1);
+        // 1b. value-shaped inputs (g, t, p): prepared values (train.py:234-239), return-head inputs
+        if constexpr (HV || HR) {
+            const int per = tc * P;
+            const float inv_per = 1.0f / (float)per, inv_p = 1.0f / (float)P;
+            for (int e = lane; e < ntraj * per; e += kWave) {
+                const int gg = fdiv(e, inv_per);
+                const int rem = e - gg * per;
+                const int tt = fdiv(rem, inv_p);
+                const int q = rem - tt * P;
+                const int64_t b = b0 + gg;
+                const int64_t bt = b * d.T + t0 + tt;
+                const int64_t i = bt * P + q;
+                const int slot = gg * Lpv + tt * C + q;
+                if constexpr (HV) {
+                    const float em = a.emask[bt];
+                    const float *v = a.value + bt * P;
+                    float vp = v[q];
+                    if (a.symmetrize) {   // two-player zero-sum: (v - swap(v)) / (sum omask + 1e-8)
+                        const float *om = a.omask + bt * P;
+                        vp = (v[q] + (-v[1 - q])) / ((om[0] + om[1]) + 1e-8f);
+                    }
+                    t_v[slot] = vp * em + a.outcome[b * P + q] * (1.f - em);
+                }
+                if constexpr (HR) {
+                    t_rv[slot] = a.ret_out[i];
+                    t_rr[slot] = a.reward[i];
+                    if constexpr (kRetT) t_rret[slot] = a.ret[i];
+                }
+            }
+        }
+        __syncthreads();
+        HRL_STAMP(2);
+
+        // 2. the scans: value head (returns = outcome, no rewards, gamma 1) and return head
+        if (active) {
+            const int nsub = (tc + kTChunk - 1) / kTChunk;
+            for (int sc = nsub - 1; sc >= 0; --sc) {
+                const int tcs = min(kTChunk, tc - sc * kTChunk);
+                const bool top = tile == ntile - 1 && sc == nsub - 1;
+                const int vofs = g * Lpv + sc * kTChunk * C + c;
+                const int rofs = g * Lpr + sc * kTChunk * rhoC + c / rhoDiv;
+                auto run = [&](auto full, auto topc) __attribute__((always_inline)) {
+                    constexpr bool F = decltype(full)::value, TOP = decltype(topc)::value;
+                    if constexpr (HV)
+                        recur_chunk<TGT, PT, false, kRho, false, F, TOP, true>(sv, boot_v, f.kv, tcs, C, rhoC, t_v,
+                                                                         nullptr, nullptr, t_rho, t_rho, vofs,
+                                                                         rofs, t_tv, t_advv);
+                    if constexpr (HR)
+                        recur_chunk<TGT, PT, true, kRho, kRetT, F, TOP>(sr, boot_r, f.kr, tcs, C, rhoC, t_rv,
+                                                                        t_rr, t_rret, t_rho, t_rho, vofs, rofs,
+                                                                        t_tr, t_advr);
+                };
+                // only the top chunk of the top tile can be partial (tiles and chunks are cut from t = 0)
+                if (!top) run(std::true_type{}, std::false_type{});
+                else if (tcs == kTChunk) run(std::true_type{}, std::true_type{});
+                else run(std::false_type{}, std::true_type{});
+            }
+        }
+        __syncthreads();
+        HRL_STAMP(3);
+
+        // 3. terms: turn advantages and the loss sums (train.py:202-213, 248-256)
+        {
+            const float inv_tc = 1.0f / (float)tc;
+            for (int e = lane; e < ntraj * tc; e += kWave) {
+                const int gg = fdiv(e, inv_tc);
+                const int tt = e - gg * tc;
+                const int64_t b = b0 + gg;
+                const int64_t bt = b * d.T + t0 + tt;
+                const float *tm = a.tmask + bt * P;
+                const float *om = a.omask + bt * P;
+                const int vrow = gg * Lpv + tt * C, rrow = gg * Lpr + tt * rhoC;
+                // total_advantages = clipped_rhos * (adv_value + adv_return); turn sum under turn_mask
+                float turn = 0.f;
+                for (int q = 0; q < P; ++q) {
+                    const int pp = Pp == 1 ? 0 : q;
+                    float s = 0.f;
+                    if constexpr (HV) s = s + t_advv[vrow + q];
+                    if constexpr (HR) s = s + t_advr[vrow + q];
+                    turn += (t_rho[rrow + pp] * s) * tm[q];
+                }
+                w.turn[bt] = turn;
+                for (int pp = 0; pp < Pp; ++pp) {
+                    acc[0] += (double)(-t_lt[rrow + pp] * turn);
+                    w.ent[bt * Pp + pp] = t_ent[rrow + pp];
+                }
+                const float prog = 1.f - a.progress[bt] * (1.f - a.ent_decay);
+                for (int q = 0; q < P; ++q) {
+                    const int pp = Pp == 1 ? 0 : q;
+                    const int64_t i = bt * P + q;
+                    if constexpr (HV) {
+                        const float tv = TGT == kNone ? a.outcome[b * P + q] : t_tv[vrow + q];
+                        const float e2 = a.value[i] - tv;
+                        acc[1] += (double)((e2 * e2) * om[q]);
+                        w.tv[i] = tv;
+                    }
+                    if constexpr (HR) {
+                        const float tr = TGT == kNone ? a.ret[i] : t_tr[vrow + q];
+                        const float x = a.ret_out[i] - tr;
+                        const float ax = fabsf(x);
+                        const float l = ax < 1.f ? 0.5f * x * x : ax - 0.5f;
+                        acc[2] += (double)(l * om[q]);
+                        w.tr[i] = tr;
+                    }
+                    const float ent = t_ent[rrow + pp] * tm[q];
+                    acc[3] += (double)ent;
+                    acc[4] += (double)(ent * prog);
+                    acc[5] += (double)tm[q];
+                }
+            }
+        }
+        __syncthreads();   // the next tile's prep rewrites the tiles
+        HRL_STAMP(4);
     }
-    if (a.ret_out && a.value_mc) {                       // MC return target = batch['return']
-        for (int p = 0; p < d.P; ++p) w.tr[bt * d.P + p] = a.ret[bt * d.P + p];
+
+    // 4. fixed-order fold of the wave's partials (shuffle tree), lane 0 writes them
+#pragma unroll
+    for (int k = 0; k < kTerms; ++k) {
+        double v = acc[k];
+        for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_down(v, off, kWave);
+        acc[k] = v;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < kTerms; ++k) w.part[(int64_t)blockIdx.x * kTerms + k] = acc[k];
+    }
+    HRL_STAMP(5);
+    HRL_STAMP_WALL(15);
+}
+
+template <int VT, int PT, bool HV, bool HR>
+int launch_fused(const FusedArgs &f, hipStream_t s) {
+    const size_t lds = fused_lds_bytes(f.d, f.G, HV, HR, VT == HRL_ALG_MC, PT == HRL_ALG_MC);
+    const dim3 grid((unsigned)f.w.nparts), block(hrl_scan::kWave);
+    if (f.d.A == 9) hipLaunchKernelGGL((loss_fused_kernel<VT, PT, HV, HR, 9>), grid, block, lds, s, f);
+    else if (f.d.A == 4) hipLaunchKernelGGL((loss_fused_kernel<VT, PT, HV, HR, 4>), grid, block, lds, s, f);
+    else hipLaunchKernelGGL((loss_fused_kernel<VT, PT, HV, HR, 0>), grid, block, lds, s, f);
+    return status();
+}
+
+template <int VT, int PT>
+int launch_fused_heads(const FusedArgs &f, bool hv, bool hr, hipStream_t s) {
+    if (hv) return hr ? launch_fused<VT, PT, true, true>(f, s) : launch_fused<VT, PT, true, false>(f, s);
+    return hr ? launch_fused<VT, PT, false, true>(f, s) : launch_fused<VT, PT, false, false>(f, s);
+}
+
+template <int VT>
+int launch_fused_pt(int pt, const FusedArgs &f, bool hv, bool hr, hipStream_t s) {
+    switch (pt) {
+        case HRL_ALG_MC: return launch_fused_heads<VT, HRL_ALG_MC>(f, hv, hr, s);
+        case HRL_ALG_TD: return launch_fused_heads<VT, HRL_ALG_TD>(f, hv, hr, s);
+        case HRL_ALG_UPGO: return launch_fused_heads<VT, HRL_ALG_UPGO>(f, hv, hr, s);
+        default: return launch_fused_heads<VT, HRL_ALG_VTRACE>(f, hv, hr, s);
     }
 }
 
-// ---- terms: advantages, loss partial sums --------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void loss_terms_kernel(FwdArgs a, LossDims d, Ws w, int has_ret) {
-    __shared__ double red[kTerms][kThreads];
-    const int64_t bt = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    double acc[kTerms] = {0, 0, 0, 0, 0, 0};
-    if (bt < d.BT) {
-        const float *tm = a.tmask + bt * d.P;
-        const float *om = a.omask + bt * d.P;
-        // total_advantages = clipped_rhos * (adv_value + adv_return); turn sum under turn_mask
-        float turn = 0.f;
-        for (int p = 0; p < d.P; ++p) {
-            const int pp = d.Pp == 1 ? 0 : p;
-            float s = 0.f;
-            if (a.value) s = s + w.advv[bt * d.P + p];
-            if (has_ret) s = s + w.advr[bt * d.P + p];
-            turn += (w.crho[bt * d.Pp + pp] * s) * tm[p];
-        }
-        w.turn[bt] = turn;
-        for (int pp = 0; pp < d.Pp; ++pp) acc[0] += (double)(-w.lt[bt * d.Pp + pp] * turn);
-        const float prog = 1.f - a.progress[bt] * (1.f - a.ent_decay);
-        for (int p = 0; p < d.P; ++p) {
-            const int pp = d.Pp == 1 ? 0 : p;
-            if (a.value) {
-                const float e = a.value[bt * d.P + p] - w.tv[bt * d.P + p];
-                acc[1] += (double)((e * e) * om[p]);
-            }
-            if (has_ret) {
-                const float x = a.ret_out[bt * d.P + p] - w.tr[bt * d.P + p];
-                const float ax = fabsf(x);
-                const float l = ax < 1.f ? 0.5f * x * x : ax - 0.5f;
-                acc[2] += (double)(l * om[p]);
-            }
-            const float ent = w.ent[bt * d.Pp + pp] * tm[p];
-            acc[3] += (double)ent;
-            acc[4] += (double)(ent * prog);
-            acc[5] += (double)tm[p];
-        }
+int launch_fused_all(int vt, int pt, const FusedArgs &f, bool hv, bool hr, hipStream_t s) {
+    switch (vt) {
+        case HRL_ALG_MC: return launch_fused_pt<HRL_ALG_MC>(pt, f, hv, hr, s);
+        case HRL_ALG_TD: return launch_fused_pt<HRL_ALG_TD>(pt, f, hv, hr, s);
+        case HRL_ALG_UPGO: return launch_fused_pt<HRL_ALG_UPGO>(pt, f, hv, hr, s);
+        default: return launch_fused_pt<HRL_ALG_VTRACE>(pt, f, hv, hr, s);
     }
-#pragma unroll
-    for (int k = 0; k < kTerms; ++k) red[k][threadIdx.x] = acc[k];
-    __syncthreads();
-    for (int s = kThreads / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-#pragma unroll
-            for (int k = 0; k < kTerms; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x < kTerms) w.part[(int64_t)blockIdx.x * kTerms + threadIdx.x] = red[threadIdx.x][0];
 }
 
 // ---- reduce: fixed-order fold of the block partials -> p, v, r, ent, total, dcnt ---------------
 __global__ __launch_bounds__(kThreads) void loss_reduce_kernel(Ws w, float ent_coef, float *losses) {
     __shared__ double red[kTerms][kThreads];
     double acc[kTerms] = {0, 0, 0, 0, 0, 0};
-    for (int i = threadIdx.x; i < w.nblocks; i += kThreads) {
+    for (int i = threadIdx.x; i < w.nparts; i += kThreads) {
 #pragma unroll
         for (int k = 0; k < kTerms; ++k) acc[k] += w.part[(int64_t)i * kTerms + k];
     }
@@ -229,6 +485,7 @@ struct BwdArgs {
     float ent_coef, ent_decay;
 };
 
+template <int AK>
 __global__ __launch_bounds__(kThreads) void loss_backward_kernel(BwdArgs a, LossDims d, Ws w) {
     const int64_t bt = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (bt >= d.BT) return;
@@ -251,16 +508,36 @@ __global__ __launch_bounds__(kThreads) void loss_backward_kernel(BwdArgs a, Loss
             }
         }
         const float ce = de * wsum + dt * (-a.ent_coef) * wdec;
-        float m, s;
-        row_stats(z, d.A, m, s);
-        const float lse = m + logf(s);
         const float h = w.ent[row];
         const int64_t act = a.action[row];
-        for (int q = 0; q < d.A; ++q) {
-            const float pq = expf(z[q] - m) / s;
-            const float la = z[q] - lse;
-            const float onehot = (q == act) ? 1.f : 0.f;
-            g[q] = cp * (onehot - pq) + ce * (-pq * (la + h));    // dH/dz = -p (log p + H)
+        if constexpr (AK > 0) {   // the row in registers: its loads issue at once (same float operations)
+            float x[AK];
+#pragma unroll
+            for (int q = 0; q < AK; ++q) x[q] = z[q];
+            float m = x[0];
+#pragma unroll
+            for (int q = 1; q < AK; ++q) m = fmaxf(m, x[q]);
+            float s = 0.f;
+#pragma unroll
+            for (int q = 0; q < AK; ++q) s += expf(x[q] - m);
+            const float lse = m + logf(s);
+#pragma unroll
+            for (int q = 0; q < AK; ++q) {
+                const float pq = expf(x[q] - m) / s;
+                const float la = x[q] - lse;
+                const float onehot = (q == act) ? 1.f : 0.f;
+                g[q] = cp * (onehot - pq) + ce * (-pq * (la + h));    // dH/dz = -p (log p + H)
+            }
+        } else {
+            float m, s;
+            row_stats(z, d.A, m, s);
+            const float lse = m + logf(s);
+            for (int q = 0; q < d.A; ++q) {
+                const float pq = expf(z[q] - m) / s;
+                const float la = z[q] - lse;
+                const float onehot = (q == act) ? 1.f : 0.f;
+                g[q] = cp * (onehot - pq) + ce * (-pq * (la + h));    // dH/dz = -p (log p + H)
+            }
         }
     }
     for (int p = 0; p < d.P; ++p) {
@@ -272,11 +549,6 @@ __global__ __launch_bounds__(kThreads) void loss_backward_kernel(BwdArgs a, Loss
             a.g_ret[i] = (dr + dt) * sl * om[p];
         }
     }
-}
-
-int status() {
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
 }
 
 bool dims_ok(int64_t B, int64_t T, int64_t P, int64_t Pp, int64_t A, LossDims &d) {
@@ -355,6 +627,10 @@ __global__ __launch_bounds__(kThreads) void out_mask_bwd_kernel(const float *__r
 
 extern "C" {
 
+#ifdef HRL_STAMPS
+int hrl_debug_set_stamps_loss(void *buf) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_hrl_stamps), &buf, sizeof(buf)); }
+#endif
+
 int64_t hrl_loss_workspace_bytes(int64_t B, int64_t T, int64_t P, int64_t Pp) {
     LossDims d;
     if (!dims_ok(B, T, P, Pp, 1, d)) return -1;
@@ -382,26 +658,10 @@ int hrl_loss_forward(const float *tpol, const float *bpol, const int64_t *action
     Ws w = carve(workspace, d);
     FwdArgs a{tpol, bpol, action, emask, tmask, omask, progress, value, outcome, ret_out, ret, reward,
               value_target == HRL_ALG_MC, symmetrize, (float)ent_coef, (float)ent_decay};
-    const dim3 grid(w.nblocks), block(kThreads);
-    hipLaunchKernelGGL(loss_prep_kernel, grid, block, 0, s, a, d, w);
-    int rc = status();
+    FusedArgs f{a, d, w, hrl_scan::make_coef(lmb, 1.0), hrl_scan::make_coef(lmb, gamma), fused_G(B, (int)P)};
+    int rc = launch_fused_all(value_target, policy_target, f, value != nullptr, ret_out != nullptr, s);
     if (rc) return rc;
-    const int64_t rho_div = P / Pp;
-    const bool mc = value_target == HRL_ALG_MC;
-    if (value) {   // value head: returns = outcome (T-extent 1), no rewards, gamma = 1 (train.py:245)
-        rc = hrl_compute_targets_fused(value_target, policy_target, w.vprep, outcome, nullptr, w.crho, w.crho, B, T,
-                                       P, 1, Pp, rho_div, lmb, 1.0, mc ? nullptr : w.tv, w.advv, stream);
-        if (rc) return rc;
-    }
-    if (ret_out) {  // return head: returns = batch['return'], rewards, gamma (train.py:246)
-        rc = hrl_compute_targets_fused(value_target, policy_target, ret_out, ret, reward, w.crho, w.crho, B, T, P, T,
-                                       Pp, rho_div, lmb, gamma, mc ? nullptr : w.tr, w.advr, stream);
-        if (rc) return rc;
-    }
-    hipLaunchKernelGGL(loss_terms_kernel, grid, block, 0, s, a, d, w, ret_out != nullptr ? 1 : 0);
-    rc = status();
-    if (rc) return rc;
-    hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), block, 0, s, w, (float)ent_coef, losses);
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(kThreads), 0, s, w, (float)ent_coef, losses);
     return status();
 }
 
@@ -419,8 +679,11 @@ int hrl_loss_backward(const float *tpol, const int64_t *action, int64_t B, int64
     Ws w = carve(const_cast<void *>(workspace), d);
     BwdArgs a{tpol, action, emask, tmask, omask, progress, value, ret_out, dlosses, g_tpol, g_value, g_ret,
               (float)ent_coef, (float)ent_decay};
-    hipLaunchKernelGGL(loss_backward_kernel, dim3(w.nblocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream), a,
-                       d, w);
+    const dim3 grid(w.nblocks), block(kThreads);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (A == 9) hipLaunchKernelGGL(loss_backward_kernel<9>, grid, block, 0, s, a, d, w);
+    else if (A == 4) hipLaunchKernelGGL(loss_backward_kernel<4>, grid, block, 0, s, a, d, w);
+    else hipLaunchKernelGGL(loss_backward_kernel<0>, grid, block, 0, s, a, d, w);
     return status();
 }
 

@@ -34,48 +34,17 @@
 #include <type_traits>
 
 #include "../../include/hrl_targets.h"
+#include "hrl_scan.h"
 
 namespace {
 
-constexpr int kWave = 64;
-constexpr int kTChunk = 16;                          // time steps per LDS pass
+using namespace hrl_scan;
+
+HRL_STAMP_DECL
+
 constexpr int kMaxTile = kTChunk * kWave;            // floats of one tensor chunk
 constexpr int kMaxVec = kMaxTile / 4 / kWave;        // float4 loads per lane (8)
 constexpr int kMaxScalar = kMaxTile / kWave;         // scalar loads per lane (32)
-constexpr int kNone = -1;
-
-struct Coef {
-    float a;   // (float)(1 - lmb)
-    float l;   // (float)lmb
-    float g;   // (float)gamma
-    float gl;  // (float)(gamma * lmb)
-};
-
-// torch.max(a, b) on two tensors propagates NaN (losses.py:36).  Written as selects
-// (v_cndmask), not early returns: the branches the early-return form compiled to
-// (two exec-mask regions per time step) sat on the scan's serial chain.  x is the
-// carried v[t+1], known a step ahead, so its NaN test is off the chain; a NaN y fails
-// `x > y` and is selected as is.  Same result, payloads included, as testing both.
-__device__ __forceinline__ float max_nan(float x, float y) {
-    const float m = x > y ? x : y;
-    return (x != x) ? x : m;
-}
-
-// floor(e / d) for 0 <= e < 2^20 and d >= 1, given inv = 1.0f / d: the exact
-// quotient of (e + 0.5) / d sits at least 0.5/d away from an integer, far more
-// than the float32 rounding error at these magnitudes, so no integer divide.
-__device__ __forceinline__ int fdiv(int e, float inv) {
-    return (int)(((float)e + 0.5f) * inv);
-}
-
-// LDS row stride for rows of L floats read column-wise by lanes (g, c), c < Cx:
-// the smallest Lp >= L with Lp == Cx (mod 32) makes g*Lp + c distinct modulo
-// 32 over each 32-lane half when Cx divides 32 (conflict-free ds_read_b32).
-__host__ __device__ __forceinline__ int padded_row(int L, int Cx) {
-    const int m = 32;
-    const int want = Cx % m;
-    return L + ((want - L % m) % m + m) % m;
-}
 
 // One chunk of one (B, T, Cx) tensor for the wave's trajectories.
 //   global: trajectory b0+g, time t0+tt, column cx at (b0+g)*R + t0*Cx + tt*Cx + cx
@@ -234,47 +203,6 @@ struct Args {
     Coef k;
 };
 
-// Carried state of every recurrence for one column, walking t = T-1 .. 0.
-struct Carry {
-    float v_next;    // values[t+1]
-    float tv_td;     // TD target at t+1
-    float tv_up;     // UPGO target at t+1
-    float acc;       // V-trace (vs - v) at t+1
-    float vs_next;   // V-trace vs at t+1
-};
-
-// One time step of algorithm ALG for one column: reads the carry `s` of step
-// t+1, writes this algorithm's fields of the carry `nx` for step t, returns
-// the target and writes the advantage.
-template <int ALG>
-__device__ __forceinline__ float step(const Carry &s, Carry &nx, bool last, float v, float r, float rho,
-                                      float c, float ret_t, float boot, const Coef &k, float &adv) {
-    if constexpr (ALG == HRL_ALG_MC) {                       // losses.py:16-17
-        adv = ret_t - v;
-        return ret_t;
-    } else if constexpr (ALG == HRL_ALG_TD) {                // losses.py:20-28
-        const float tv = last ? boot : r + k.g * (k.a * s.v_next + k.l * s.tv_td);
-        nx.tv_td = tv;
-        adv = tv - v;
-        return tv;
-    } else if constexpr (ALG == HRL_ALG_UPGO) {              // losses.py:31-40
-        const float tv = last ? boot : r + k.g * max_nan(s.v_next, k.a * s.v_next + k.l * s.tv_up);
-        nx.tv_up = tv;
-        adv = tv - v;
-        return tv;
-    } else {                                                 // losses.py:43-58
-        const float v1 = last ? boot : s.v_next;
-        const float delta = rho * ((r + k.g * v1) - v);
-        const float acc = last ? delta : delta + (k.gl * c) * s.acc;   // vs_minus_v_xs, carried as is
-        const float vs = acc + v;
-        const float vs1 = last ? boot : s.vs_next;
-        nx.acc = acc;
-        nx.vs_next = vs;
-        adv = (r + k.g * vs1) - v;
-        return vs;
-    }
-}
-
 // TGT: algorithm whose target is written (kNone: no target output).
 // ADV: algorithm whose advantages are written.
 // REW: rewards present.  RETT: MC reads returns at every t (ret_T == T).
@@ -312,6 +240,8 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
     const int vbase = g * Lpv + c;                     // + tt*C
     const int rbase = g * Lpr + c / a.rhoDiv;          // + tt*rhoC
 
+    HRL_STAMP_WALL(14);
+    HRL_STAMP(0);
     float boot = 0.f;
     if (active) {
         boot = a.returns[(b0 + g) * (int64_t)a.retT * C + (int64_t)(a.retT - 1) * C + c];
@@ -319,23 +249,6 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
 
     Carry s{0.f, 0.f, 0.f, 0.f, 0.f};
     const int nchunks = (T + kTChunk - 1) / kTChunk;
-
-    // One time step: the reference recurrences on the carry; results stay in registers (no LDS
-    // traffic on the serial chain, so no lgkmcnt waits between steps).
-    auto one_step = [&](bool last, float v, float r, float rho, float cc, float ret_t, float &tgt_out,
-                        float &adv_out) __attribute__((always_inline)) {
-        float adv, adv_unused;
-        Carry nx = s;
-        if constexpr (TGT != kNone && TGT != ADV) {
-            tgt_out = step<TGT>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv_unused);
-            step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
-        } else {
-            tgt_out = step<ADV>(s, nx, last, v, r, rho, cc, ret_t, boot, a.k, adv);
-        }
-        adv_out = adv;
-        nx.v_next = v;
-        s = nx;
-    };
 
     // Software pipeline over chunks (walking time backwards): chunk ch's inputs
     // arrive in registers one iteration ahead, so the global-load latency of
@@ -363,6 +276,7 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
     // load); afterwards `boot` is a plain register, so the waitcnt pass does not put a
     // full vmcnt(0) -- draining the prefetched chunk -- in front of the recurrence.
     asm volatile("" : "+v"(boot));
+    HRL_STAMP(1);
 
     // The recurrence over one chunk held in LDS.  TOP: the chunk holds t = T-1 (the bootstrap
     // step).  Chunks are cut from t = 0, so only the top chunk can be partial; a FULL chunk
@@ -370,39 +284,8 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
     // chunk, never elsewhere), so its serial chain has no compares, branches or spilled step
     // indices.  Only a partial top chunk (T % kTChunk != 0) tests `last` at run time.
     auto recur = [&](int tc, auto full, auto top) __attribute__((always_inline)) {
-        constexpr bool F = decltype(full)::value;
-        constexpr bool TOP = decltype(top)::value;
-        // every LDS read is issued ahead of the dependent chain (tc is wave-uniform, so the
-        // guards of a partial chunk are scalar branches)
-        float xv[kTChunk], xr[kTChunk], xrho[kTChunk], xc[kTChunk], xret[kTChunk];
-#pragma unroll
-        for (int tt = 0; tt < kTChunk; ++tt) {
-            if (F || tt < tc) {
-                const int iv = vbase + tt * C;
-                const int ir = rbase + tt * a.rhoC;
-                xv[tt] = t_v[iv];
-                xr[tt] = REW ? t_r[iv] : 0.f;
-                xrho[tt] = kRho ? t_rho[ir] : 0.f;
-                xc[tt] = kRho ? t_cs[ir] : 0.f;
-                xret[tt] = kRet ? t_ret[iv] : boot;
-            }
-        }
-        float ot[kTChunk], oa[kTChunk];
-#pragma unroll
-        for (int tt = kTChunk - 1; tt >= 0; --tt) {
-            if (F || tt < tc) {
-                const bool last = TOP && (F ? tt == kTChunk - 1 : tt == tc - 1);
-                one_step(last, xv[tt], xr[tt], xrho[tt], xc[tt], xret[tt], ot[tt], oa[tt]);
-            }
-        }
-#pragma unroll
-        for (int tt = 0; tt < kTChunk; ++tt) {
-            if (F || tt < tc) {
-                const int iv = vbase + tt * C;
-                if constexpr (TGT != kNone) t_tgt[iv] = ot[tt];
-                t_adv[iv] = oa[tt];
-            }
-        }
+        recur_chunk<TGT, ADV, REW, kRho, kRet, decltype(full)::value, decltype(top)::value>(
+            s, boot, a.k, tc, C, a.rhoC, t_v, t_r, t_ret, t_rho, t_cs, vbase, rbase, t_tgt, t_adv);
     };
 
     auto process = [&](int ch, auto prefetch) {
@@ -418,6 +301,7 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
         // instantiation, so no register phi forces an early wait on them)
         if constexpr (decltype(prefetch)::value) setup_and_load(ch - 1);
         __syncthreads();
+        HRL_STAMP(2 + 3 * (nchunks - 1 - ch));
 
         if (active) {
             if (ch != nchunks - 1) recur(tc, std::true_type{}, std::false_type{});
@@ -425,13 +309,16 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
             else recur(tc, std::false_type{}, std::true_type{});
         }
         __syncthreads();
+        HRL_STAMP(3 + 3 * (nchunks - 1 - ch));
 
         const int64_t off = b0 * (int64_t)T * C + (int64_t)t0 * C;
         if constexpr (TGT != kNone) store_chunk<VEC>(out, t_tgt, a.targets + off);
         store_chunk<VEC>(out, t_adv, a.advantages + off);
+        HRL_STAMP(4 + 3 * (nchunks - 1 - ch));
     };
     for (int ch = nchunks - 1; ch > 0; --ch) process(ch, std::true_type{});
     process(0, std::false_type{});
+    HRL_STAMP_WALL(15);
 }
 
 template <int TGT, int ADV, bool REW, bool RETT, bool VEC>
@@ -519,10 +406,7 @@ int prepare(int target_alg, int adv_alg, const float *values, const float *retur
     a.values = values; a.returns = returns; a.rewards = rewards; a.rhos = rhos; a.cs = cs;
     a.targets = targets; a.advantages = advantages;
     a.B = B; a.T = (int)T; a.C = (int)C; a.retT = (int)ret_T; a.rhoC = (int)rho_C; a.rhoDiv = (int)rho_div;
-    a.k.a = (float)(1.0 - lmb);
-    a.k.l = (float)lmb;
-    a.k.g = (float)gamma;
-    a.k.gl = (float)(gamma * lmb);
+    a.k = make_coef(lmb, gamma);
     // Waves per launch: a wave's trajectories are walked by one serial chain, so at small B
     // spread them over at least ~1024 waves (one per SIMD) instead of filling every lane.
     {
@@ -540,6 +424,12 @@ int prepare(int target_alg, int adv_alg, const float *values, const float *retur
 }  // namespace
 
 extern "C" {
+
+#ifdef HRL_STAMPS
+int hrl_debug_set_stamps_targets(void *buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_hrl_stamps), &buf, sizeof(buf));
+}
+#endif
 
 int hrl_abi_version(void) { return 9; }
 

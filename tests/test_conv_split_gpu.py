@@ -133,3 +133,64 @@ def test_torus_split_matches_fp64(cuda, cin, integer):
         else:
             err = float(((yd - ref).abs() / rowmax).max())
             assert err <= bound, (split, err, bound)
+
+
+def _wgrad(lib, dev, x, dy, split, alpha=None, beta=None):
+    M = x.shape[0]
+    dw = torch.empty(32, 32, 3, 3, device=dev)
+    ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    prev = lib.hrl_conv3x3_set_split(split)
+    try:
+        P = _native.ptr
+        _native.check(lib.hrl_conv3x3_wgrad_ex(P(x), P(alpha) if alpha is not None else None,
+                                               P(beta) if beta is not None else None, P(dy), M, P(dw), P(ws),
+                                               ws_bytes, _native.stream_of(dev)), 'wgrad')
+        torch.cuda.synchronize(dev)
+    finally:
+        lib.hrl_conv3x3_set_split(prev)
+    return dw
+
+
+def _wgrad_ref64(x, dy, alpha=None, beta=None):
+    M = x.shape[0]
+    x64 = x.double().cpu().view(M, 32, 3, 3)
+    if alpha is not None:   # the fused prologue: relu(x*alpha + beta) per input channel
+        x64 = torch.relu(x64 * alpha.double().cpu().view(1, 32, 1, 1) + beta.double().cpu().view(1, 32, 1, 1))
+    return torch.nn.grad.conv2d_weight(x64, (32, 32, 3, 3), dy.double().cpu().view(M, 32, 3, 3), padding=1)
+
+
+@pytest.mark.parametrize('pro', [False, True])
+@pytest.mark.parametrize('split', [1, 0])
+@pytest.mark.parametrize('M', [1000, 4099])
+def test_wgrad_integer_data_is_exact(cuda, pro, split, M):
+    """conv3x3_wgrad_split_kernel (32x32x16 bf16 MFMA, one tap = one tile): exact on integer data, so the
+    A/B/C fragment layouts, every tap and the ragged last row tile are right; the fp32 form likewise."""
+    lib = _native.load()
+    g = torch.Generator().manual_seed(11 + M)
+    x = torch.randint(-4, 5, (M, 288), generator=g).float()
+    dy = torch.randint(-4, 5, (M, 288), generator=g).float()
+    alpha = beta = None
+    if pro:
+        alpha = torch.randint(1, 3, (32,), generator=g).float()
+        beta = torch.randint(-2, 3, (32,), generator=g).float()
+    dw = _wgrad(lib, cuda, x.to(cuda), dy.to(cuda), split, None if alpha is None else alpha.to(cuda),
+                None if beta is None else beta.to(cuda))
+    assert torch.equal(dw.cpu().double(), _wgrad_ref64(x, dy, alpha, beta))
+
+
+def test_wgrad_error_within_fp32_error(cuda):
+    """On random data the split weight gradient's error against fp64 is within 2x torch-CPU fp32's."""
+    lib = _native.load()
+    g = torch.Generator().manual_seed(5)
+    M = 8192
+    x = torch.randn(M, 288, generator=g)
+    dy = torch.randn(M, 288, generator=g) * torch.exp(torch.randn(M, 1, generator=g) * 3)
+    ref = _wgrad_ref64(x, dy)
+    t32 = torch.nn.grad.conv2d_weight(x.view(M, 32, 3, 3), (32, 32, 3, 3), dy.view(M, 32, 3, 3), padding=1)
+    scale = ref.abs().max()
+    bound = 2 * float((t32.double() - ref).abs().max() / scale)
+    for split in (1, 0):
+        dw = _wgrad(lib, cuda, x.to(cuda), dy.to(cuda), split).cpu().double()
+        err = float((dw - ref).abs().max() / scale)
+        assert err <= bound, (split, err, bound)
