@@ -16,6 +16,8 @@ import os
 import torch  # noqa: F401  (must precede loading libhrl.so, see module doc)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libhrl.so')
+# diagnostic builds (tools/*): HRL_LIB_PATH names another build of the same sources
+LIB_PATH = os.environ.get('HRL_LIB_PATH', LIB_PATH)
 
 HRL_OK = 0
 HRL_EINVAL = -22
@@ -85,6 +87,10 @@ SIGNATURES = {
                                                 _f32p, _f32p, ctypes.c_void_p]),
     'hrl_bn_backward_apply': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p,
                                              ctypes.c_int, _f32p, _f32p, _f32p, ctypes.c_void_p]),
+    'hrl_conv3x3_block_backward': (ctypes.c_int, [_f32p, _f32p, _i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
+                                                  _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, ctypes.c_int, _f32p,
+                                                  _f32p, _f32p, ctypes.c_void_p, ctypes.c_void_p, _i64,
+                                                  ctypes.c_void_p]),
     'hrl_conv3x3_wgrad_ex': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _i64, _f32p, ctypes.c_void_p, _i64,
                                             ctypes.c_void_p]),
     'hrl_hidden_gather': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, ctypes.c_int, ctypes.c_void_p,

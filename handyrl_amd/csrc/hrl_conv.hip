@@ -38,8 +38,11 @@
 #include "../../include/hrl_nn.h"
 #include "../../include/hrl_targets.h"
 #include "hrl_split.h"
+#include "hrl_stamps.h"
 
 namespace {
+
+HRL_STAMP_DECL
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -70,6 +73,92 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 using hrl_split::split3;
 using hrl_split::split_part;
 using hrl_split::mfma_bf16;
+
+// The split (exact bf16, six partial products) MFMA loop of conv3x3_kernel over one wave's 16-row A tile
+// in LDS (rows of stride kStride): acc[q][ct] += sum_p A_p . W'[tap(p, q)][ct] on v_mfma_f32_16x16x32_bf16.
+//  * the B fragments (split weights) are [tap][ct][part h/m/l][lane] x 4 dwords in LDS;
+//  * A fragment of cell p: row lane & 15, input channels 8*(lane >> 4) + e (e = 0..7), read as
+//    relu(a*pa[e] + pb[e]) when PRO; the next cell's A reads are issued before this cell's MFMAs;
+//  * ROWLOOP: the board rows stay a loop (a row's three cells unrolled), for callers whose live
+//    registers leave no room for the fully unrolled form (every cell's fragments and B reads hoisted).
+template <bool PRO, bool ROWLOOP>
+__device__ __forceinline__ void split_tile_mfma(const float *as, const uint32_t *w_lds_u, int lane, const float *pa,
+                                                const float *pb, f32x4 (&acc)[kCells][2]) {
+    const int ar = lane & 15;          // A row (sample within the tile)
+    const int ak = lane >> 4;          // A k group
+    const float *arow = as + ar * kStride;
+    const uint4 *wb = reinterpret_cast<const uint4 *>(w_lds_u) + lane;
+    // A fragment of cell p: row ar, input channels 8*ak + e (e = 0..7); the next cell's
+    // A reads are issued before this cell's MFMAs.
+    const float *acol = arow + 8 * ak * kCells;
+    float an[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) an[e] = acol[e * kCells];
+    auto cell = [&](int p) __attribute__((always_inline)) {
+        float av[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) av[e] = an[e];
+        if (p + 1 < kCells) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) an[e] = acol[e * kCells + p + 1];
+        }
+        uint32_t ah[4], am[4], al[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            float v[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = 2 * d + u;
+                float a = av[e];
+                if constexpr (PRO) {   // input channel 8ak+e: the previous block's BN+ReLU
+                    const float t = a * pa[e] + pb[e];
+                    a = t < 0.f ? 0.f : t;
+                }
+                v[u] = a;
+            }
+            uint32_t h0, m0, l0, h1, m1, l1;
+            split3(v[0], h0, m0, l0);
+            split3(v[1], h1, m1, l1);
+            ah[d] = h0 | (h1 << 16);
+            am[d] = m0 | (m1 << 16);
+            al[d] = l0 | (l1 << 16);
+        }
+        const uint4 Ah = make_uint4(ah[0], ah[1], ah[2], ah[3]);
+        const uint4 Am = make_uint4(am[0], am[1], am[2], am[3]);
+        const uint4 Al = make_uint4(al[0], al[1], al[2], al[3]);
+        const int py = p / kBoard, px = p - py * kBoard;
+#pragma unroll
+        for (int q = 0; q < kCells; ++q) {
+            // tap_of(p, q) with p uniform at run time: a scalar branch
+            const int dy = py - q / kBoard + 1, dx = px - q % kBoard + 1;
+            if (dy < 0 || dy > 2 || dx < 0 || dx > 2) continue;
+            const int tap = dy * 3 + dx;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const uint4 *wf = wb + (tap * 2 + ct) * 3 * 64;
+                const uint4 Bh = wf[0], Bm = wf[64], Bl = wf[128];
+                f32x4 c = acc[q][ct];
+                c = mfma_bf16(Al, Bh, c);   // smallest terms first
+                c = mfma_bf16(Am, Bm, c);
+                c = mfma_bf16(Ah, Bl, c);
+                c = mfma_bf16(Am, Bh, c);
+                c = mfma_bf16(Ah, Bm, c);
+                c = mfma_bf16(Ah, Bh, c);
+                acc[q][ct] = c;
+            }
+        }
+    };
+    if constexpr (ROWLOOP) {
+#pragma unroll 1
+        for (int py = 0; py < kBoard; ++py) {
+#pragma unroll
+            for (int px = 0; px < kBoard; ++px) cell(py * kBoard + px);
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < kCells; ++p) cell(p);
+    }
+}
 
 // ------------------------------------------------------------------ forward / input gradient
 // x: (M, 288) rows; wpk: packed [tap][ct][ci][16] = W'[tap][ci][ct*16+j]; y: (M, 288)
@@ -204,80 +293,8 @@ __global__ __launch_bounds__(kThreads) void conv3x3_kernel(const float *__restri
         const float *arow = as + ar * kStride;
         const float *wl = w_lds + ak * 16 + (lane & 15);
         if constexpr (SPLIT) {
-            const uint4 *wb = reinterpret_cast<const uint4 *>(w_lds_u) + lane;
-            // A fragment of cell p: row ar, input channels 8*ak + e (e = 0..7); the next cell's
-            // A reads are issued before this cell's MFMAs.
-            const float *acol = arow + 8 * ak * kCells;
-            float an[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) an[e] = acol[e * kCells];
-            auto cell = [&](int p) __attribute__((always_inline)) {
-                float av[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) av[e] = an[e];
-                if (p + 1 < kCells) {
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) an[e] = acol[e * kCells + p + 1];
-                }
-                uint32_t ah[4], am[4], al[4];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    float v[2];
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const int e = 2 * d + u;
-                        float a = av[e];
-                        if constexpr (PRO) {   // input channel 8ak+e: the previous block's BN+ReLU
-                            const float t = a * pa[e] + pb[e];
-                            a = t < 0.f ? 0.f : t;
-                        }
-                        v[u] = a;
-                    }
-                    uint32_t h0, m0, l0, h1, m1, l1;
-                    split3(v[0], h0, m0, l0);
-                    split3(v[1], h1, m1, l1);
-                    ah[d] = h0 | (h1 << 16);
-                    am[d] = m0 | (m1 << 16);
-                    al[d] = l0 | (l1 << 16);
-                }
-                const uint4 Ah = make_uint4(ah[0], ah[1], ah[2], ah[3]);
-                const uint4 Am = make_uint4(am[0], am[1], am[2], am[3]);
-                const uint4 Al = make_uint4(al[0], al[1], al[2], al[3]);
-                const int py = p / kBoard, px = p - py * kBoard;
-#pragma unroll
-                for (int q = 0; q < kCells; ++q) {
-                    // tap_of(p, q) with p uniform at run time: a scalar branch
-                    const int dy = py - q / kBoard + 1, dx = px - q % kBoard + 1;
-                    if (dy < 0 || dy > 2 || dx < 0 || dx > 2) continue;
-                    const int tap = dy * 3 + dx;
-#pragma unroll
-                    for (int ct = 0; ct < 2; ++ct) {
-                        const uint4 *wf = wb + (tap * 2 + ct) * 3 * 64;
-                        const uint4 Bh = wf[0], Bm = wf[64], Bl = wf[128];
-                        f32x4 c = acc[q][ct];
-                        c = mfma_bf16(Al, Bh, c);   // smallest terms first
-                        c = mfma_bf16(Am, Bm, c);
-                        c = mfma_bf16(Ah, Bl, c);
-                        c = mfma_bf16(Am, Bh, c);
-                        c = mfma_bf16(Ah, Bm, c);
-                        c = mfma_bf16(Ah, Bh, c);
-                        acc[q][ct] = c;
-                    }
-                }
-            };
-            if constexpr (kRef) {
-                // the reference tile's 72 staging registers leave no room for the unrolled form
-                // (every cell's fragments and B reads hoisted: spills), so the board rows stay a
-                // loop (a row's three cells unrolled) and the row half of tap_of(p, q) a scalar branch
-#pragma unroll 1
-                for (int py = 0; py < kBoard; ++py) {
-#pragma unroll
-                    for (int px = 0; px < kBoard; ++px) cell(py * kBoard + px);
-                }
-            } else {
-#pragma unroll
-                for (int p = 0; p < kCells; ++p) cell(p);
-            }
+            // kRef: the reference tile's 72 staging registers leave no room for the unrolled form
+            split_tile_mfma<PRO, kRef>(as, w_lds_u, lane, pa, pb, acc);
         } else {
 #pragma unroll
         for (int p = 0; p < kCells; ++p) {
@@ -637,6 +654,306 @@ __global__ __launch_bounds__(kThreads) void conv3x3_wgrad_split_kernel(const flo
         out[i] = ((red[i] + red[kW + i]) + red[2 * kW + i]) + red[3 * kW + i];
 }
 
+// ------------------------------------------------------------------ one chain block's backward, fused
+// For a chain block y_i = conv_i(x'), out_i = relu(BN_i(y_i)) with x' = relu(x*in_alpha + in_beta) (or x), from
+// g = dL/d out_i in ONE launch:
+//   dY   = BN_i's input gradient, bn_bwd_apply_kernel's float operations (hrl_bn.hip), in registers;
+//   dW  += x'^T dY, the weight gradient of conv3x3_wgrad_split_kernel (32x32x16 bf16, exact split);
+//   gin  = conv_i^T(dY), conv3x3_kernel's split input-gradient loop on dY staged in LDS, with the
+//          epilogue of hrl_conv3x3_forward_ex: 2 = BN_{i-1}'s backward sums (ref = x), 3 = x > 0 mask.
+// It replaces bn_bwd_apply (reads g, y; writes dY), the weight gradient (reads x, dY) and the input gradient
+// (reads dY, x): 1.2 GB of a B=4096 T=32 step's block traffic becomes 604 MB (reads g, y, x; writes gin; the
+// epilogue's second read of x hits L2), and neither dY nor x' reaches HBM.
+// Data layout: lane l = (r = l & 31, h = l >> 5) owns channel r of rows 8h..8h+7 of a 16-row tile, i.e. the
+// wgrad operand layout, so BN_i's, the prologue's and the epilogue's per-channel constants are registers and
+// the loads are 36-byte runs (three buffer_load_dwordx3 per row; the descriptor's range check zeroes rows past
+// the batch and drops their stores).
+struct BlockBwdArgs {
+    const float *g, *y;                                          // dL/d out_i, y_i: (M, 288)
+    const float *bn_w, *bn_b, *bn_mean, *bn_invstd, *bn_k, *bn_gm;   // BN_i (hrl_bn_backward_apply's arguments)
+    const float *x, *in_alpha, *in_beta;                         // conv_i's input (raw), its prologue
+    const float *wpk;                                            // packed input-gradient weights (flip layout)
+    const float *ep_mean, *ep_alpha, *ep_beta;                   // epilogue 2: BN_{i-1}
+    float *gin;                                                  // dL/dx' masked per the epilogue (DG)
+    double *part;                                                // epilogue 2 sums [block][32][2]
+    float *wpart;                                                // weight-gradient partials [block][tap][ci][co]
+    int64_t M;
+};
+
+typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+
+// buffer descriptor over `bytes` bytes at `base`; the inputs are made provably wave-uniform so the compiler
+// keeps the descriptor in SGPRs (no waterfall loops around the buffer ops)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void *base, uint32_t bytes) {
+    const uint64_t p = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, (int)n,
+                                             0x00020000);
+}
+
+// the 9 cells of one channel of one row (36 bytes at byte offset off)
+__device__ __forceinline__ void load_cells(__amdgpu_buffer_rsrc_t rs, int off, float (&d)[kCells]) {
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, off + 12 * m, 0, 0);
+        d[3 * m + 0] = __uint_as_float(v.x);
+        d[3 * m + 1] = __uint_as_float(v.y);
+        d[3 * m + 2] = __uint_as_float(v.z);
+    }
+}
+
+__device__ __forceinline__ void store_cells(__amdgpu_buffer_rsrc_t rs, int off, const float (&d)[kCells]) {
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+        u32x3 v;
+        v.x = __float_as_uint(d[3 * m + 0]);
+        v.y = __float_as_uint(d[3 * m + 1]);
+        v.z = __float_as_uint(d[3 * m + 2]);
+        __builtin_amdgcn_raw_buffer_store_b96(v, rs, off + 12 * m, 0, 0);
+    }
+}
+
+template <bool PRO, int EPI, bool DG>
+__global__ __launch_bounds__(kThreads) void conv3x3_block_bwd_kernel(BlockBwdArgs a) {
+    constexpr int kWWords = kTaps * 2 * 3 * 64 * 4;            // split input-gradient weights (54 KB)
+    constexpr int kTileF = kTile * kStride;                    // one wave's dY / output tile (18.1 KB)
+    constexpr int kW = kTaps * kC * kC;
+    constexpr int kFoldF = (kWaves - 1) * kW;                  // waves 1..3's weight-gradient partials
+    constexpr int kUseF = DG ? kWWords + kWaves * kTileF : 0;
+    constexpr int kSmemF = kUseF > kFoldF ? kUseF : kFoldF;
+    __shared__ __attribute__((aligned(16))) float smem[kSmemF];
+    uint32_t *w_lds_u = reinterpret_cast<uint32_t *>(smem);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    float *as = smem + kWWords + wave * kTileF;
+    if constexpr (DG) {
+        for (int i = threadIdx.x; i < kWWords; i += kThreads) {
+            const int d = i & 3, l = (i >> 2) & 63, f = i >> 8;      // f = (tap*2 + ct)*3 + part
+            const int part = f % 3, tc = f / 3;
+            const int ci = 8 * (l >> 4) + 2 * d, j = l & 15;
+            const float w0 = a.wpk[(tc * kC + ci) * 16 + j];
+            const float w1 = a.wpk[(tc * kC + ci + 1) * 16 + j];
+            w_lds_u[i] = split_part(w0, part) | (split_part(w1, part) << 16);
+        }
+    }
+    const int r = lane & 31, h = lane >> 5;
+    // BN_i's backward apply for channel r (bn_bwd_apply_kernel's per-channel values)
+    const float mu = a.bn_mean[r], kk = a.bn_k[r], gmn = a.bn_gm[r], is = a.bn_invstd[r];
+    const float ww = a.bn_w ? a.bn_w[r] : 1.0f;
+    const float al = is * ww;
+    const float be = (a.bn_b ? a.bn_b[r] : 0.0f) - mu * al;
+    float pa = 1.f, pb = 0.f;
+    if constexpr (PRO) {
+        pa = a.in_alpha[r];
+        pb = a.in_beta[r];
+    }
+    float em = 0.f, ea = 1.f, eb = 0.f;
+    if constexpr (DG && EPI == 2) {
+        em = a.ep_mean[r];
+        ea = a.ep_alpha[r];
+        eb = a.ep_beta[r];
+    }
+    double s1 = 0.0, s2 = 0.0;
+    f32x16 wacc[kTaps];
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wacc[t][i] = 0.f;
+    if constexpr (DG) __syncthreads();   // weights in LDS
+
+    const int64_t ntiles = (a.M + kTile - 1) / kTile;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    const int off0 = ((8 * h) * kRow + r * kCells) * 4;         // byte offset of this lane's first run
+    HRL_STAMP_WALL(14);
+    int st_it = 0;   // stamps: the first two tiles of wave 0, slots 0..11
+    for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < ntiles; tile += stride, ++st_it) {
+        if (st_it < 2) HRL_STAMP(6 * st_it + 0);
+        const int64_t row0 = tile * kTile;
+        const int rows = (int)min<int64_t>(kTile, a.M - row0);
+        const uint32_t bytes = (uint32_t)rows * kRow * 4;
+        const int64_t eofs = row0 * kRow;
+        const __amdgpu_buffer_rsrc_t rg = wave_rsrc(a.g + eofs, bytes);
+        const __amdgpu_buffer_rsrc_t ry = wave_rsrc(a.y + eofs, bytes);
+        const __amdgpu_buffer_rsrc_t rx = wave_rsrc(a.x + eofs, bytes);
+        float G[8][kCells], X[8][kCells];
+        {
+            float Y[8][kCells];
+            // dY = BN_i backward apply; rows past the batch are zero (their zero inputs would not give 0)
+            auto bn_apply = [&]() __attribute__((always_inline)) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const bool valid = 8 * h + j < rows;
+#pragma unroll
+                    for (int c = 0; c < kCells; ++c) {
+                        const float yv = Y[j][c];
+                        float gv = G[j][c];
+                        if (!(yv * al + be > 0.f)) gv = 0.f;
+                        const float t = (yv - mu) * kk;
+                        const float d = (((gv - gmn) - t) * is) * ww;
+                        G[j][c] = valid ? d : 0.f;
+                    }
+                }
+            };
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                load_cells(rg, off0 + j * kRow * 4, G[j]);
+                load_cells(ry, off0 + j * kRow * 4, Y[j]);
+                load_cells(rx, off0 + j * kRow * 4, X[j]);
+            }
+            bn_apply();
+        }
+        if (st_it < 2) HRL_STAMP(6 * st_it + 1);
+        if constexpr (DG) {   // dY -> this wave's LDS tile, the input gradient's A operand
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int c = 0; c < kCells; ++c) as[(8 * h + j) * kStride + r * kCells + c] = G[j][c];
+        }
+        // weight gradient: the nine dY_q fragments split once, x'_p split as the p loop reaches it
+        {
+            uint4 Bh[kCells], Bm[kCells], Bl[kCells];
+#pragma unroll
+            for (int q = 0; q < kCells; ++q) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = G[j][q];
+                hrl_split::split8(v, Bh[q], Bm[q], Bl[q]);
+            }
+#pragma unroll
+            for (int p = 0; p < kCells; ++p) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float xv = X[j][p];
+                    if constexpr (PRO) {   // bn_apply_kernel's float operations
+                        const float t = xv * pa + pb;
+                        xv = t < 0.f ? 0.f : t;
+                    }
+                    v[j] = xv;
+                }
+                uint4 Ah, Am, Al;
+                hrl_split::split8(v, Ah, Am, Al);
+#pragma unroll
+                for (int q = 0; q < kCells; ++q) {
+                    const int tap = tap_of(p, q);
+                    if (tap < 0) continue;
+                    f32x16 c = wacc[tap];
+                    c = mfma32(Al, Bh[q], c);   // smallest terms first
+                    c = mfma32(Am, Bm[q], c);
+                    c = mfma32(Ah, Bl[q], c);
+                    c = mfma32(Am, Bh[q], c);
+                    c = mfma32(Ah, Bm[q], c);
+                    c = mfma32(Ah, Bh[q], c);
+                    wacc[tap] = c;
+                }
+            }
+        }
+        if (st_it < 2) HRL_STAMP(6 * st_it + 2);
+        if constexpr (DG) {
+            // the epilogue's reference (x itself) is read again rather than held through the weight gradient
+            // (registers); the tile was read a few microseconds ago, so these loads hit L2.  Issued before the
+            // MFMAs, they land during them.
+            float R[8][kCells];
+            if constexpr (EPI == 2 || EPI == 3) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) load_cells(rx, off0 + j * kRow * 4, R[j]);
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the dY tile is in LDS
+            __builtin_amdgcn_wave_barrier();
+            f32x4 acc[kCells][2];
+#pragma unroll
+            for (int q = 0; q < kCells; ++q) acc[q][0] = acc[q][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            split_tile_mfma<false, true>(as, w_lds_u, lane, nullptr, nullptr, acc);
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            if (st_it < 2) HRL_STAMP(6 * st_it + 3);
+            // accumulators -> the tile [row][c*9 + q] -> this lane's channel-r runs, epilogue, stores
+#pragma unroll
+            for (int q = 0; q < kCells; ++q)
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = (lane >> 4) * 4 + rr;   // C/D: row = (lane>>4)*4 + reg, col = lane & 15
+                        const int co = ct * 16 + (lane & 15);
+                        as[row * kStride + co * kCells + q] = acc[q][ct][rr];
+                    }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            const __amdgpu_buffer_rsrc_t ro = wave_rsrc(a.gin + eofs, bytes);
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const bool valid = 8 * h + j < rows;
+                float o[kCells];
+#pragma unroll
+                for (int c = 0; c < kCells; ++c) {
+                    float v = as[(8 * h + j) * kStride + r * kCells + c];
+                    const float rv = (EPI == 2 || EPI == 3) ? R[j][c] : 0.f;
+                    if constexpr (EPI == 3) {
+                        if (!(rv > 0.f)) v = 0.f;
+                    } else if constexpr (EPI == 2) {   // bn_bwd_reduce_kernel's mask and sums
+                        const float gm = (rv * ea + eb > 0.f && valid) ? v : 0.f;
+                        t1 += gm;
+                        t2 += gm * (rv - em);
+                    }
+                    o[c] = v;
+                }
+                store_cells(ro, off0 + j * kRow * 4, o);
+            }
+            if constexpr (EPI == 2) {
+                s1 += (double)t1;
+                s2 += (double)t2;
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // this tile's LDS reads are done before the next tile's writes
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (st_it < 2) HRL_STAMP(6 * st_it + 4);
+    }
+    HRL_STAMP(12);
+    // weight-gradient partials: waves 1..3 through LDS, wave 0 folds ((w0 + w1) + w2) + w3 and writes
+    // partial[block][tap][ci][co] (C/D layout of 32x32x16: col = co = r, row = ci = (i&3) + 8(i>>2) + 4h)
+    __syncthreads();
+    float *red = smem;
+    if (wave > 0) {
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int ci = (i & 3) + 8 * (i >> 2) + 4 * h;
+                red[(wave - 1) * kW + (t * kC + ci) * kC + r] = wacc[t][i];
+            }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        float *out = a.wpart + (int64_t)blockIdx.x * kW;
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int idx = (t * kC + (i & 3) + 8 * (i >> 2) + 4 * h) * kC + r;
+                out[idx] = ((wacc[t][i] + red[idx]) + red[kW + idx]) + red[2 * kW + idx];
+            }
+    }
+    if constexpr (DG && EPI == 2) {   // BN_{i-1}'s sums: lanes (h, r) of the 4 waves, fixed order
+        __syncthreads();
+        double *dred = reinterpret_cast<double *>(smem);
+        dred[((wave * 2 + h) * kC + r) * 2 + 0] = s1;
+        dred[((wave * 2 + h) * kC + r) * 2 + 1] = s2;
+        __syncthreads();
+        if (threadIdx.x < 2 * kC) {
+            const int c = threadIdx.x >> 1, k = threadIdx.x & 1;
+            double t = 0.0;
+            for (int i = 0; i < 2 * kWaves; ++i) t += dred[(i * kC + c) * 2 + k];
+            a.part[((int64_t)blockIdx.x * kC + c) * 2 + k] = t;
+        }
+    }
+    HRL_STAMP(13);
+    HRL_STAMP_WALL(15);
+}
+
 // fold per-workgroup partials into dW[co][ci][3][3]: a workgroup owns 64 consecutive
 // outputs; its 4 waves take every 4th partial (4 independent sums in flight per
 // thread) and combine in a fixed order -> deterministic.
@@ -716,6 +1033,10 @@ int grid_for(int64_t M) {
 }  // namespace
 
 extern "C" {
+
+#ifdef HRL_STAMPS
+int hrl_debug_set_stamps_conv(void *buf) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_hrl_stamps), &buf, sizeof(buf)); }
+#endif
 
 int64_t hrl_conv3x3_workspace_bytes(int64_t M) {
     if (M < 1) return -1;
@@ -817,6 +1138,43 @@ int hrl_conv3x3_wgrad_ex(const float *x, const float *in_alpha, const float *in_
     int rc = status();
     if (rc) return rc;
     hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, partial, grid,
+                       dweight);
+    return status();
+}
+
+int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const float *bn_weight,
+                               const float *bn_bias, const float *save_mean, const float *save_invstd,
+                               const float *kcoef, const float *gmean, const float *x, const float *in_alpha,
+                               const float *in_beta, const float *packed_flip, float *dweight, float *gin,
+                               int epilogue, const float *ep_mean, const float *ep_alpha, const float *ep_beta,
+                               double *part, void *workspace, int64_t workspace_bytes, void *stream) {
+    if (M < 1 || !g || !y || !save_mean || !save_invstd || !kcoef || !gmean || !x || !dweight || !workspace)
+        return HRL_EINVAL;
+    if ((in_alpha == nullptr) != (in_beta == nullptr)) return HRL_EINVAL;
+    if (workspace_bytes < hrl_conv3x3_workspace_bytes(M) || M * kRow * 4 > 0xffffffffLL) return HRL_EINVAL;
+    if (gin && (!packed_flip || epilogue < 0 || epilogue == 1 || epilogue > 3)) return HRL_EINVAL;
+    if (gin && epilogue == 2 && (!ep_mean || !ep_alpha || !ep_beta || !part)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int grid = grid_for(M);
+    float *wpart = static_cast<float *>(workspace) + kTaps * 2 * kC * 16 * 2;
+    BlockBwdArgs a{g, y, bn_weight, bn_bias, save_mean, save_invstd, kcoef, gmean, x, in_alpha, in_beta, packed_flip,
+                   ep_mean, ep_alpha, ep_beta, gin, part, wpart, M};
+    const bool pro = in_alpha != nullptr;
+#define HRL_BLOCK_LAUNCH(PRO, EPI, DG) \
+    hipLaunchKernelGGL((conv3x3_block_bwd_kernel<PRO, EPI, DG>), dim3(grid), dim3(kThreads), 0, s, a)
+    if (!gin) {
+        if (pro) HRL_BLOCK_LAUNCH(true, 0, false); else HRL_BLOCK_LAUNCH(false, 0, false);
+    } else if (epilogue == 2) {
+        if (pro) HRL_BLOCK_LAUNCH(true, 2, true); else HRL_BLOCK_LAUNCH(false, 2, true);
+    } else if (epilogue == 3) {
+        if (pro) HRL_BLOCK_LAUNCH(true, 3, true); else HRL_BLOCK_LAUNCH(false, 3, true);
+    } else {
+        if (pro) HRL_BLOCK_LAUNCH(true, 0, true); else HRL_BLOCK_LAUNCH(false, 0, true);
+    }
+#undef HRL_BLOCK_LAUNCH
+    int rc = status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, wpart, grid,
                        dweight);
     return status();
 }

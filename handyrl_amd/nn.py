@@ -1081,26 +1081,38 @@ def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, pa
     for i in reversed(range(n)):
         w, gamma, beta = params[3 * i:3 * i + 3]
         mean, invstd = coefs[i][0], coefs[i][1]
-        dy = torch.empty_like(h0)
         bw, bgam, bbet = _grad_buffer(w), _grad_buffer(gamma), _grad_buffer(beta)
         dgam, dbet = bgam[0], bbet[0]
-        if sums is not None:
-            kg = torch.empty(2, 32, dtype=torch.float32, device=dev)
-            _native.check(lib.hrl_bn_finalize_backward(P(sums), sums_n, 32, M * 9, P(gamma), P(invstd), P(dgam),
-                                                       P(dbet), P(kg[0]), P(kg[1]), stream),
-                          'hrl_bn_finalize_backward')
-            _native.check(lib.hrl_bn_backward_apply(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(mean),
-                                                    P(invstd), 1, P(kg[0]), P(kg[1]), P(dy), stream),
-                          'hrl_bn_backward_apply')
-        else:
-            _native.check(lib.hrl_bn_backward(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(mean), P(invstd),
-                                              1, P(dy), P(dgam), P(dbet), P(bn_ws), bn_ws_bytes, stream),
-                          'hrl_bn_backward')
         if i == 0:
             x, a, b = h0, (unit[0] if unit is not None else None), (unit[1] if unit is not None else None)
         else:
             x, a, b = ys[i - 1], coefs[i - 1][2], coefs[i - 1][3]
         dw = bw[0]
+        if sums is not None:
+            # BN_i's backward sums are formed (by the consumer or block i+1's input-gradient epilogue): the block's
+            # BN backward apply, weight gradient and input gradient run as ONE launch (conv3x3_block_bwd_kernel)
+            kg = torch.empty(2, 32, dtype=torch.float32, device=dev)
+            _native.check(lib.hrl_bn_finalize_backward(P(sums), sums_n, 32, M * 9, P(gamma), P(invstd), P(dgam),
+                                                       P(dbet), P(kg[0]), P(kg[1]), stream),
+                          'hrl_bn_finalize_backward')
+            gin, epi, ep = None, 0, (None, None, None)
+            if i > 0:
+                gin, epi, ep = torch.empty_like(h0), 2, (coefs[i - 1][0], coefs[i - 1][2], coefs[i - 1][3])
+            elif need_input_grad:
+                gin, epi = torch.empty_like(h0), (3 if relu_in else 0)
+            _native.check(lib.hrl_conv3x3_block_backward(
+                P(g), P(ys[i]), M, P(gamma), P(beta), P(mean), P(invstd), P(kg[0]), P(kg[1]), P(x), P(a), P(b),
+                P(packed[i, 1]), P(dw), P(gin), epi, P(ep[0]), P(ep[1]), P(ep[2]), P(part) if i > 0 else None,
+                P(ws), ws_bytes, stream), 'hrl_conv3x3_block_backward')
+            grads[3 * i:3 * i + 3] = [_ret(bw), _ret(bgam), _ret(bbet)]
+            g = gin
+            if i > 0:
+                sums, sums_n = part, nblk   # read by the next block's finalize before its launch rewrites part
+            continue
+        dy = torch.empty_like(h0)
+        _native.check(lib.hrl_bn_backward(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(mean), P(invstd),
+                                          1, P(dy), P(dgam), P(dbet), P(bn_ws), bn_ws_bytes, stream),
+                      'hrl_bn_backward')
         _native.check(lib.hrl_conv3x3_wgrad_ex(P(x), P(a), P(b), P(dy), M, P(dw), P(ws), ws_bytes, stream),
                       'hrl_conv3x3_wgrad_ex')
         grads[3 * i:3 * i + 3] = [_ret(bw), _ret(bgam), _ret(bbet)]

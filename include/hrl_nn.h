@@ -160,6 +160,26 @@ int hrl_conv3x3_wgrad_ex(const float *x, const float *in_alpha, const float *in_
                          float *dweight, void *workspace, int64_t workspace_bytes, void *stream);
 
 /*
+ * One conv -> BN -> ReLU chain block's whole backward in one launch (conv3x3_block_bwd_kernel), replacing
+ * hrl_bn_backward_apply + hrl_conv3x3_wgrad_ex + hrl_conv3x3_forward_ex(flip) of that block:
+ *   dY      = hrl_bn_backward_apply(y, g; bn_weight, bn_bias, save_mean, save_invstd, relu=1, kcoef, gmean),
+ *             formed in registers (never stored);
+ *   dweight = the weight gradient of conv(x') with x' = relu(x*in_alpha + in_beta) (or x; both or neither);
+ *   gin     = (gin != NULL) the input gradient conv^T(dY) from packed_flip (hrl_conv3x3_pack_n's f = 1 layout)
+ *             with the epilogue of hrl_conv3x3_forward_ex and ref = x: 0 none, 2 BN_{i-1}'s backward sums
+ *             into part (ep_mean, ep_alpha, ep_beta), 3 gin *= [x > 0].
+ * g, y, x, gin: (M, 288) rows; M * 1152 bytes < 4 GiB.  workspace: hrl_conv3x3_workspace_bytes(M) bytes;
+ * part: hrl_conv3x3_stats_blocks(M) x 32 x 2 doubles.  Replaces, for the TicTacToe body
+ * (tictactoe.py:57-65), the autograd backward of conv -> BatchNorm2d -> ReLU per block.
+ */
+int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const float *bn_weight,
+                               const float *bn_bias, const float *save_mean, const float *save_invstd,
+                               const float *kcoef, const float *gmean, const float *x, const float *in_alpha,
+                               const float *in_beta, const float *packed_flip, float *dweight, float *gin,
+                               int epilogue, const float *ep_mean, const float *ep_alpha, const float *ep_beta,
+                               double *part, void *workspace, int64_t workspace_bytes, void *stream);
+
+/*
  * Fused ConvLSTM cell gates (GeisterNet DRC, handyrl/envs/geister.py:48-63;
  * replaces the split/sigmoid/tanh/mul/add chain of ConvLSTMCell.forward and
  * its autograd backward).  Gate pre-activations z = zx + zh in channel order

@@ -350,3 +350,62 @@ def test_stem_conv_matches_torch_cpu(cuda, N, cin, bias):
     np.testing.assert_allclose(hip.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-5, atol=tol)
     if bias:
         np.testing.assert_allclose(hip.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-5, atol=tol)
+
+
+@pytest.mark.parametrize('M', [37, 4099])
+@pytest.mark.parametrize('epi', [0, 2, 3, None])
+@pytest.mark.parametrize('pro', [False, True])
+def test_block_backward_matches_unfused_launches(cuda, M, epi, pro):
+    """hrl_conv3x3_block_backward (BN backward apply + weight gradient + input gradient of one chain block in
+    one launch) vs the three launches it replaces on the same inputs: the weight gradient and the input
+    gradient are bit-identical (same split MFMA order on the same dY), the epilogue-2 BatchNorm sums equal
+    to fp64 rounding of a different fp32 summation order.  epi None: no input gradient.  M = 37 leaves a
+    ragged last row tile (rows past the batch must contribute nothing)."""
+    from handyrl_amd import _native
+    lib = _native.load()
+    P = _native.ptr
+    stream = _native.stream_of(cuda)
+    g0 = torch.Generator(device=cuda).manual_seed(M + (epi or 7))
+    rnd = lambda *s: torch.randn(*s, device=cuda, generator=g0)   # noqa: E731
+    g, y, x = rnd(M, 288), rnd(M, 288), rnd(M, 288)
+    w = rnd(32, 32, 3, 3) * 0.1
+    gamma, beta = rnd(32).abs() + 0.5, rnd(32) * 0.2
+    mean, invstd = rnd(32) * 0.1, rnd(32).abs() + 0.5
+    kcoef, gmean = rnd(32) * 0.1, rnd(32) * 0.1
+    alpha, bet = (rnd(32).abs() + 0.5, rnd(32) * 0.3) if pro else (None, None)
+    em, ea, eb = rnd(32) * 0.1, rnd(32).abs() + 0.5, rnd(32) * 0.3
+    packed = torch.empty(1, 2, 9216, device=cuda)
+    _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array([w]), 1, P(packed), stream), 'pack')
+    ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+    nblk = lib.hrl_conv3x3_stats_blocks(M)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+    # the three launches
+    dy = torch.empty_like(g)
+    _native.check(lib.hrl_bn_backward_apply(P(y), P(g), M, 32, 9, P(gamma), P(beta), P(mean), P(invstd), 1,
+                                            P(kcoef), P(gmean), P(dy), stream), 'apply')
+    dw0 = torch.empty(32, 32, 3, 3, device=cuda)
+    _native.check(lib.hrl_conv3x3_wgrad_ex(P(x), P(alpha), P(bet), P(dy), M, P(dw0), P(ws), ws_bytes, stream), 'wg')
+    gin0, part0 = torch.empty_like(g), torch.zeros(nblk * 64, dtype=torch.float64, device=cuda)
+    if epi is not None:
+        _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(packed[0, 1]), None, 3, P(gin0), epi,
+                                                 P(x) if epi else None, P(em), P(ea), P(eb),
+                                                 P(part0) if epi == 2 else None, P(ws), ws_bytes, stream), 'dg')
+    # one launch
+    dw1 = torch.empty_like(dw0)
+    gin1, part1 = torch.empty_like(g), torch.zeros_like(part0)
+    _native.check(lib.hrl_conv3x3_block_backward(
+        P(g), P(y), M, P(gamma), P(beta), P(mean), P(invstd), P(kcoef), P(gmean), P(x), P(alpha), P(bet),
+        P(packed[0, 1]), P(dw1), P(gin1) if epi is not None else None, epi or 0, P(em), P(ea), P(eb),
+        P(part1) if epi == 2 else None, P(ws), ws_bytes, stream), 'block')
+    torch.cuda.synchronize(cuda)
+    assert torch.equal(dw1, dw0)
+    if epi is not None:
+        assert torch.equal(gin1, gin0)
+    if epi == 2:   # both against the fp64 sums: sum g*m and sum g*m*(x - mean), m = [x*alpha + beta > 0]
+        xg, gg = x.double().view(M, 32, 9), gin0.double().view(M, 32, 9)
+        m = (x.view(M, 32, 9) * ea.view(1, 32, 1) + eb.view(1, 32, 1) > 0).double()
+        ref = torch.stack([(gg * m).sum((0, 2)), (gg * m * (xg - em.double().view(1, 32, 1))).sum((0, 2))], 1)
+        scale = float((gg.abs() * (1 + xg.abs())).sum((0, 2)).max())
+        err0 = float((part0.view(nblk, 32, 2).sum(0) - ref).abs().max()) / scale
+        err1 = float((part1.view(nblk, 32, 2).sum(0) - ref).abs().max()) / scale
+        assert err1 <= max(2 * err0, 1e-7), (err1, err0)

@@ -15,7 +15,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, 'tools', 'micro', 'libhrl_stamps.so')
-SRCS = ['hrl_targets.hip', 'hrl_loss.hip']
+SRCS = ['hrl_targets.hip', 'hrl_loss.hip', 'hrl_conv.hip']
 
 
 def build():
@@ -118,11 +118,61 @@ def main():
                   ['prep: policy rows', 'prep: values + barrier', 'scans + barrier', 'terms + barrier',
                    'wave fold + partial store'])
 
-    run_scan(4096, 32)
-    run_scan(4096, 9)
-    run_scan(1 << 18, 9)
-    run_loss(4096, 32)
-    run_loss(4096, 9)
+    def run_block(M=131072):
+        lib.hrl_conv3x3_workspace_bytes.restype = i64
+        lib.hrl_conv3x3_workspace_bytes.argtypes = [i64]
+        lib.hrl_conv3x3_stats_blocks.restype = i64
+        lib.hrl_conv3x3_stats_blocks.argtypes = [i64]
+        lib.hrl_conv3x3_pack_n.argtypes = [vp, ctypes.c_int, vp, vp]
+        lib.hrl_conv3x3_block_backward.argtypes = [vp, vp, i64] + [vp] * 12 + [ctypes.c_int, vp, vp, vp, vp, vp,
+                                                                            i64, vp]
+        r = lambda *sh: torch.randn(*sh, device=dev, generator=g)   # noqa: E731
+        gg, y, x = r(M, 288), r(M, 288), r(M, 288)
+        w = r(32, 32, 3, 3) * 0.1
+        c = [r(32).abs() + 0.5 for _ in range(11)]
+        packed = torch.empty(1, 2, 9216, device=dev)
+        wp = (ctypes.c_void_p * 1)(w.data_ptr())
+        assert lib.hrl_conv3x3_pack_n(wp, 1, p(packed), stream) == 0
+        wsb = lib.hrl_conv3x3_workspace_bytes(M)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        part = torch.empty(lib.hrl_conv3x3_stats_blocks(M) * 64, dtype=torch.float64, device=dev)
+        dw, gin = torch.empty(32, 32, 3, 3, device=dev), torch.empty_like(gg)
+        buf = torch.zeros(256 * 16 + 16, dtype=torch.int64, device=dev)
+        for it in range(3):
+            buf.zero_()
+            lib.hrl_debug_set_stamps_conv(p(buf))
+            rc = lib.hrl_conv3x3_block_backward(p(gg), p(y), M, *[p(t) for t in c[:6]], p(x), p(c[6]), p(c[7]),
+                                                p(packed[0, 1]), p(dw), p(gin), 2, p(c[8]), p(c[9]), p(c[10]),
+                                                p(part), p(ws), wsb, stream)
+            assert rc == 0, rc
+            torch.cuda.synchronize(dev)
+        st = buf.view(-1, 16).cpu().numpy()
+        st = st[st[:, 15] != 0]
+        import numpy as np
+        st = st.astype(np.int64)
+        labels = ['loads + BN apply (dY)', 'weight gradient (dY split, 294 MFMA32)', 'dY to LDS wait + input-grad MFMA',
+                  'epilogue: stage, sums, stores']
+        wall = (st[:, 15] - st[:, 14]) * 10.0
+        print('block backward M=%d: %d workgroups, wave-0 wall median %.1f us' % (M, len(st), np.median(wall) / 1e3))
+        for t in range(2):
+            for k in range(4):
+                d = st[:, 6 * t + k + 1] - st[:, 6 * t + k]
+                print('   tile %d %-42s median %7.0f cyc  p90 %7.0f' % (t, labels[k], np.median(d), np.percentile(d, 90)))
+        d = st[:, 12] - st[:, 0]
+        print('   all tiles (stamped, drained)                      median %7.0f cyc' % np.median(d))
+        d = st[:, 13] - st[:, 12]
+        print('   final folds                                       median %7.0f cyc' % np.median(d))
+
+    which = sys.argv[1:] or ['scan', 'loss', 'block']
+    if 'scan' in which:
+        run_scan(4096, 32)
+        run_scan(4096, 9)
+        run_scan(1 << 18, 9)
+    if 'loss' in which:
+        run_loss(4096, 32)
+        run_loss(4096, 9)
+    if 'block' in which:
+        run_block()
 
 
 if __name__ == '__main__':
