@@ -190,6 +190,12 @@ class GradAllReduce:
         (the graph-captured step: between the backward graph and the clip/Adam graph)."""
         dist.all_reduce(self.fg.flat, op=dist.ReduceOp.SUM, group=self.group)
 
+    def all_reduce_ranges(self, ranges):
+        """Asynchronous SUM all-reduce of element ranges of the flat buffer (one message each), ordered
+        after the work already enqueued on the current stream; returns the work handles."""
+        return [dist.all_reduce(self.fg.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                for lo, hi in ranges]
+
     def remove(self):
         for h in self._hooks:
             h.remove()

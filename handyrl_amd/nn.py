@@ -1409,6 +1409,7 @@ def fuse_bn_relu(model, example=None):
     for bn in bns:
         bn.fused_relu = True
     model.forward = gm.forward
+    object.__setattr__(model, '_hrl_graph', gm)   # the rewritten graph, unregistered: state_dict unchanged
     return len(pairs) + merged + chains + fused_heads
 
 
@@ -1504,6 +1505,7 @@ def unfuse(model):
     """Undo fuse_bn_relu (e.g. before pickling the model for CPU workers)."""
     if 'forward' in model.__dict__:
         del model.forward
+    model.__dict__.pop('_hrl_graph', None)
     for m in model.modules():
         if isinstance(m, BatchNorm2d):
             m.fused_relu = False

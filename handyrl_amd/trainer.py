@@ -36,7 +36,7 @@ DEFAULT_LR = 3e-8  # train.py:318
 
 class LearnerStep:
     def __init__(self, net, args, device, lr=None, graph=False, reduce_group=None, world_size=1,
-                 bucket_bytes=256 * 1024, hip_layers=True, loss_fn=None):
+                 bucket_bytes=256 * 1024, hip_layers=True, loss_fn=None, segment_backward=True):
         self.net = net.to(device)
         self._fuse_pending = False
         if hip_layers and device.type == 'cuda':
@@ -68,7 +68,12 @@ class LearnerStep:
         self.live = None        # params that receive a gradient (set on the first batch)
         self.defer = hip_layers and device.type == 'cuda'   # batched weight gradients for recurrent steps
         self._graph = None
+        self._graph_seg2 = None     # data parallel: the backward below the cut (second segment)
         self._graph_update = None
+        self.segments = None        # data parallel: [(flat-buffer ranges, params)] per backward segment
+        self.segment_error = None   # why the step stayed one backward graph
+        self.segment_backward = segment_backward
+        self._cut = None            # forward pre-hook state: the fused chain's input (the segment cut)
         self._static = None
         self._static_out = None
         self.stats = None
@@ -182,9 +187,20 @@ class LearnerStep:
                     bimap_r(self._static_hidden, hidden, lambda dst, src: dst.copy_(src, non_blocking=True))
             self._graph.replay()
             if self._graph_update is not None:
-                # data parallel: the gradient exchange runs between the two graphs (eager RCCL
-                # all-reduce of the flat buffer, one message), then clip + Adam replay
-                self.reducer.all_reduce_flat()
+                if self._graph_seg2 is not None:
+                    # data parallel, two backward segments: the upper segment's gradients are complete
+                    # when its graph has run, so their all-reduce is enqueued (RCCL stream, eager) before
+                    # the lower segment's graph and runs while it does; then the lower segment's bucket
+                    works = [self.reducer.all_reduce_ranges(self.segments[0][0])]
+                    self._graph_seg2.replay()
+                    works.append(self.reducer.all_reduce_ranges(self.segments[1][0]))
+                    for w in works:
+                        for x in w:
+                            x.wait()
+                else:
+                    # data parallel: the gradient exchange runs between the two graphs (eager RCCL
+                    # all-reduce of the flat buffer, one message), then clip + Adam replay
+                    self.reducer.all_reduce_flat()
                 self._graph_update.replay()
             out = self._static_out
         else:
@@ -213,6 +229,8 @@ class LearnerStep:
         with torch.cuda.stream(side):
             for _ in range(3):
                 self._body(batch, hidden)
+            if self.reducer is not None and hidden is None and self.segment_backward:
+                self._try_plan_segments(batch)   # its forward's BatchNorm updates are undone below
         torch.cuda.current_stream(self.device).wait_stream(side)
         with torch.no_grad():
             for p, v in zip(params, saved_p):
@@ -230,17 +248,120 @@ class LearnerStep:
             return
         torch.cuda.synchronize(self.device)
         self.reducer.enabled = False     # no collective inside a capture
+        seg2 = None
         try:
             grads_graph, update_graph = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             # thread-local capture: the process group's watchdog thread may query its events meanwhile
-            with torch.cuda.graph(grads_graph, capture_error_mode='thread_local'):
-                losses, dcnt = self._grads(batch, hidden)
+            if self.segments is not None:
+                seg2 = torch.cuda.CUDAGraph()
+                handle = self._cut_module().register_forward_pre_hook(self._grab_cut)
+                try:
+                    with direct_grads():
+                        with torch.cuda.graph(grads_graph, capture_error_mode='thread_local'):
+                            self.grads.zero()
+                            outputs = forward_prediction(self.net, hidden, batch, self.args)
+                            losses, dcnt = self.loss_fn(outputs, batch, self.args)
+                            cut, upper, lower = self._cut, self.segments[0][1], self.segments[1][1]
+                            torch.autograd.backward(losses['total'], inputs=[cut] + upper, retain_graph=True)
+                        with torch.cuda.graph(seg2, capture_error_mode='thread_local'):
+                            torch.autograd.backward(cut, grad_tensors=cut.grad, inputs=lower)
+                finally:
+                    handle.remove()
+                    self._cut = None
+            else:
+                with torch.cuda.graph(grads_graph, capture_error_mode='thread_local'):
+                    losses, dcnt = self._grads(batch, hidden)
             with torch.cuda.graph(update_graph, capture_error_mode='thread_local'):
                 self._static_out = self._update(losses, dcnt)
         finally:
             self.reducer.enabled = True
             self.reducer.reset()
-        self._graph, self._graph_update = grads_graph, update_graph
+        self._graph, self._graph_update, self._graph_seg2 = grads_graph, update_graph, seg2
+
+    # -- data parallel: two backward segments ------------------------------------------------------
+    def _cut_module(self):
+        """The fused conv chain (nn._ChainHeads / nn._ConvBNChain): the backward is cut at its input,
+        the upper segment (loss, heads, chain) holds nearly all of the step's backward, the lower one
+        the layers in front of the chain (the stem).  None: the step stays one backward graph."""
+        from .nn import _ChainHeads, _ConvBNChain
+        gm = getattr(self.net, '_hrl_graph', None)   # fuse_bn_relu's rewritten forward holds the chain
+        if gm is None:
+            return None
+        for node in gm.graph.nodes:                  # the first one the forward CALLS (a chain merged into
+            if node.op == 'call_module':             # _ChainHeads stays registered but is not called)
+                m = gm.get_submodule(node.target)
+                if isinstance(m, (_ChainHeads, _ConvBNChain)):
+                    return m
+        return None
+
+    def _grab_cut(self, _module, args):
+        """The chain gets a view of its input, and that view is the cut: for a non-leaf `inputs=` tensor
+        the autograd engine still runs the tensor's own grad_fn in the first segment, which must not be
+        the stem's HIP Function (its backward writes the stem's weight gradient in place; the second
+        segment would then add it again)."""
+        cut = args[0].view_as(args[0])
+        self._cut = cut
+        return (cut,) + tuple(args[1:])
+
+    def _try_plan_segments(self, batch):
+        """Eager dry run (forward + loss) that finds the segment cut and splits the parameters; leaves
+        self.segments None when the net has no fused chain or its parameters do not split cleanly."""
+        mod = self._cut_module()
+        if mod is None:
+            self.segment_error = 'no fused conv chain in the net'
+            return
+        handle = mod.register_forward_pre_hook(self._grab_cut)
+        try:
+            with direct_grads():
+                outputs = forward_prediction(self.net, None, batch, self.args)
+                losses, _ = self.loss_fn(outputs, batch, self.args)
+                self._plan_segments(losses['total'])
+        except RuntimeError as e:
+            self.segments = None
+            self.segment_error = str(e)
+        finally:
+            handle.remove()
+            self._cut = None
+
+    def _plan_segments(self, loss):
+        """Split the live parameters at the cut tensor by walking the autograd graph: `upper` are reached
+        from the loss without passing the cut's node, `lower` from the cut.  Both sets disjoint and each a
+        few contiguous ranges of the flat buffer, one bucket per segment (self.segments)."""
+        cut = self._cut
+        if cut is None or not cut.requires_grad or cut.grad_fn is None:
+            raise RuntimeError('segmented capture: the chain input was not seen or does not require grad')
+
+        def reach(root, stop):
+            seen, params, todo = set(), set(), [root]
+            while todo:
+                fn = todo.pop()
+                if fn is None or fn in seen or fn is stop:
+                    continue
+                seen.add(fn)
+                var = getattr(fn, 'variable', None)
+                if var is not None:
+                    params.add(id(var))
+                todo.extend(f for f, _ in fn.next_functions)
+            return params
+        up = reach(loss.grad_fn, cut.grad_fn)
+        low = reach(cut.grad_fn, None)
+        live = self.live or [True] * len(self.params)
+        upper = [p for p, l in zip(self.params, live) if l and id(p) in up]
+        lower = [p for p, l in zip(self.params, live) if l and id(p) in low]
+        if set(map(id, upper)) & set(map(id, lower)) or len(upper) + len(lower) != sum(live):
+            raise RuntimeError('segmented capture: parameters shared across the cut')
+        index = {id(p): i for i, p in enumerate(self.params)}
+
+        def ranges(ps):
+            out = []
+            for off, n in sorted(self.grads.slices[index[id(p)]] for p in ps):
+                if out and out[-1][1] == off:
+                    out[-1][1] = off + n
+                else:
+                    out.append([off, off + n])
+            return [tuple(r) for r in out]
+        self.segments = [(ranges(upper), upper), (ranges(lower), lower)]
+        return cut, upper, lower
 
     def load_batch(self, batch):
         """Copy a new batch into the captured graph's static input tensors."""
