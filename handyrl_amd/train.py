@@ -211,9 +211,16 @@ def _unroll_flat_hidden(model, hidden, batch, args):
 def compose_losses(outputs, log_selected_policies, total_advantages, targets, batch, args):
     """Summed policy / value / return / entropy losses (train.py:188-215).
 
-    Returns ``(losses, dcnt)`` with ``dcnt`` a 0-d device tensor (the
-    reference returns ``tmasks.sum().item()``; ``compute_loss`` converts).
+    Returns ``(losses, dcnt)`` with ``dcnt`` a Python float, as the reference
+    (``tmasks.sum().item()``, train.py:199); the learner's sync-free path uses
+    ``_compose_losses``, whose ``dcnt`` stays a 0-d device tensor.
     """
+    losses, dcnt = _compose_losses(outputs, log_selected_policies, total_advantages, targets, batch, args)
+    return losses, dcnt.item()
+
+
+def _compose_losses(outputs, log_selected_policies, total_advantages, targets, batch, args):
+    """compose_losses with ``dcnt`` as a 0-d device tensor (no host sync)."""
     tmasks = batch['turn_mask']
     omasks = batch['observation_mask']
 
@@ -357,7 +364,7 @@ def loss_terms_composed(outputs, batch, args):
         nograd.get('return'), batch['return'], batch['reward'], lmb, gamma, clipped_rhos, cs)
 
     total_advantages = clipped_rhos * sum(advantages.values())
-    return compose_losses(outputs, log_sel_t, total_advantages, targets, batch, args)
+    return _compose_losses(outputs, log_sel_t, total_advantages, targets, batch, args)
 
 
 def compute_loss(batch, model, hidden, args):
