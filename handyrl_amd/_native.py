@@ -127,9 +127,16 @@ SIGNATURES = {
                                               _f32p, _f32p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_torus_conv_wgrad': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, _i64, _i64, _f32p, _f32p,
                                             ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_torus_unit_forward': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p,
+                                              _f32p, ctypes.c_void_p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_torus_unit_input_grad': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, _f32p,
+                                                 _f32p, _f32p, ctypes.c_void_p, ctypes.c_void_p, _i64,
+                                                 ctypes.c_void_p]),
+    'hrl_bn_backward_apply_masked': (ctypes.c_int, [_f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p,
+                                                    _f32p, _f32p, _f32p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lib = None
 

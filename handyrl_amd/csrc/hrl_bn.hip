@@ -630,6 +630,23 @@ int hrl_bn_apply_residual(const float *x, const float *res, int64_t N, int64_t C
     return launch_status();
 }
 
+int hrl_bn_backward_apply_masked(const float *x, const float *dy, const float *out, int64_t N, int64_t C, int64_t HW,
+                                 const float *weight, const float *save_mean, const float *save_invstd,
+                                 const float *kcoef, const float *gmean, float *dx, void *stream) {
+    if (!x || !dy || !out || !dx || !save_mean || !save_invstd || !kcoef || !gmean || dx == dy) return HRL_EINVAL;
+    const bool vec = (C * HW) % 4 == 0 && aligned16(x) && aligned16(dy) && aligned16(dx) && aligned16(out);
+    Geo g;
+    if (!make_geo(N, C, HW, vec ? 4 : 1, g)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 grid(g.nblocks), block(kThreads);
+    const float *nul = nullptr;
+    if (vec) hipLaunchKernelGGL((bn_bwd_apply_kernel<4, false, 2>), grid, block, 0, s, x, dy, g, save_mean, save_invstd,
+                                weight, kcoef, gmean, nul, dx, out);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<1, false, 2>), grid, block, 0, s, x, dy, g, save_mean, save_invstd,
+                            weight, kcoef, gmean, nul, dx, out);
+    return launch_status();
+}
+
 int hrl_bn_backward_masked(const float *x, const float *dy, const float *out, int64_t N, int64_t C, int64_t HW,
                            const float *weight, const float *save_mean, const float *save_invstd, float *dx,
                            float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream) {

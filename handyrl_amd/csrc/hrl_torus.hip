@@ -73,9 +73,29 @@ __device__ __forceinline__ int torus_nbr(int q, int H, int W, int tap) {
 // floor(e / d) for 0 <= e < 2^20 given inv = 1/d (exact: see hrl_targets.hip fdiv)
 __device__ __forceinline__ int fdiv(int e, float inv) { return (int)(((float)e + 0.5f) * inv); }
 
+// An index the compiler cannot see through: the per-element tile / coefficient addresses of the staging
+// loops are sample-invariant, and hoisting all of them out of the sample loop spills (40-80 registers).
+__device__ __forceinline__ int opaque(int i) {
+    asm volatile("" : "+v"(i));
+    return i;
+}
+
+// The LDS tile slots of the float4 at element 4i of a [c][cell] sample: channel c0 = floor(4i / HW) (one
+// division per float4) and cell r0; element 4i+j is in channel c0 + wrap_j, wrap_j = [r0 + j >= HW].
+struct Quad {
+    int c0, base, r0;
+    __device__ __forceinline__ Quad(int i, int HW, float inv_hw) {
+        c0 = fdiv(4 * i, inv_hw);
+        r0 = 4 * i - c0 * HW;
+        base = c0 * kS + r0;
+    }
+    __device__ __forceinline__ bool wrap(int j, int HW) const { return r0 + j >= HW; }
+    __device__ __forceinline__ int slot(int j, int HW) const { return base + j + (wrap(j, HW) ? kS - HW : 0); }
+};
+
 // ------------------------------------------------------------------ sample staging
 // One sample's n_elem = C*HW floats: global (contiguous) -> registers -> LDS [c][cell] rows.
-template <bool VEC, int NLD>
+template <bool VEC, int NLD, bool OPQ = false>
 struct Stage {
     float4 v[VEC ? NLD : 1];
     float s[VEC ? 1 : NLD];
@@ -98,21 +118,18 @@ struct Stage {
             const int nv = n_elem >> 2;
 #pragma unroll
             for (int k = 0; k < NLD; ++k) {
-                const int i = k * 64 + lane;
+                const int i = OPQ ? opaque(k * 64 + lane) : k * 64 + lane;
                 if (i < nv) {
                     const float x4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+                    const Quad q(i, HW, inv_hw);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int e = 4 * i + j;
-                        const int c = fdiv(e, inv_hw);
-                        tile[c * kS + (e - c * HW)] = x4[j];
-                    }
+                    for (int j = 0; j < 4; ++j) tile[q.slot(j, HW)] = x4[j];
                 }
             }
         } else {
 #pragma unroll
             for (int k = 0; k < NLD; ++k) {
-                const int e = k * 64 + lane;
+                const int e = OPQ ? opaque(k * 64 + lane) : k * 64 + lane;
                 if (e < n_elem) {
                     const int c = fdiv(e, inv_hw);
                     tile[c * kS + (e - c * HW)] = s[k];
@@ -130,12 +147,9 @@ __device__ __forceinline__ void store_sample(const float *tile, float *dst, int 
         const int nv = n_elem >> 2;
         for (int i = lane; i < nv; i += 64) {
             float x4[4];
+            const Quad q(i, HW, inv_hw);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int e = 4 * i + j;
-                const int c = fdiv(e, inv_hw);
-                x4[j] = tile[c * kS + (e - c * HW)];
-            }
+            for (int j = 0; j < 4; ++j) x4[j] = tile[q.slot(j, HW)];
             if (add) {
                 const float4 a = reinterpret_cast<const float4 *>(add)[i];
                 const float4 m = reinterpret_cast<const float4 *>(mask)[i];
@@ -163,19 +177,127 @@ __device__ __forceinline__ void lds_fence() {
 
 // ------------------------------------------------------------------ forward / input gradient
 // x: (N, Cin, HW); wpk: [tap][KS][2][64]; y: (N, out_c, HW), out_c <= 32 (the first out_c channels of
-// the 32 computed); part: [grid][32][2] (STATS)
-template <int KS, bool VEC, bool STATS, bool SPLIT>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void torus_conv_kernel(const float *__restrict__ x, int64_t N, int Cin,
-                                                              int H, int W, const float *__restrict__ wpk,
-                                                              const float *__restrict__ bias, int out_c,
-                                                              bool vec_out, float *__restrict__ y,
-                                                              double *__restrict__ part,
-                                                              const float *__restrict__ add,
-                                                              const float *__restrict__ add_mask) {
+// the 32 computed); part: [grid][32][2] (STATS, SUMS)
+struct ConvArgs {
+    const float *x;
+    int64_t N;
+    int Cin, H, W;
+    const float *wpk, *bias;
+    int out_c;
+    bool vec_out;
+    float *y;
+    double *part;
+    const float *add, *add_mask;   // out = conv + add * [add_mask > 0]
+    // PRO: x is the previous unit's conv output; the conv input is h = relu([res +] x*alpha[c] + beta[c])
+    // (bn_apply_kernel / bn_res_apply_kernel arithmetic), also written to hout
+    const float *res, *alpha, *beta;
+    float *hout;
+    // SUMS: with v the stored output and m = [hmask > 0], per channel sum(v m) and sum(v m (yprev - mean))
+    // (bn_bwd_reduce_kernel<MASK = 2> of the previous unit)
+    const float *hmask, *yprev, *mean;
+};
+
+__device__ __forceinline__ float relu(float v) { return v < 0.f ? 0.f : v; }   // NaN stays NaN
+
+// PRO prologue: the staged previous conv output (and residual) -> h in the LDS tile and in global memory
+template <int PRO, int NLD>
+__device__ __forceinline__ void pro_to_lds(const Stage<true, NLD, true> &sx, const Stage<true, NLD, true> &sr, float *tile,
+                                           float *hout, int n_elem, int HW, float inv_hw, int lane,
+                                           const float *al, const float *be) {
+    const int nv = n_elem >> 2;
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+        const int i = opaque(k * 64 + lane);
+        if (i < nv) {
+            const float x4[4] = {sx.v[k].x, sx.v[k].y, sx.v[k].z, sx.v[k].w};
+            const float r4[4] = {sr.v[k].x, sr.v[k].y, sr.v[k].z, sr.v[k].w};
+            float o[4];
+            const Quad q(i, HW, inv_hw);
+            const float a0 = al[q.c0], a1 = al[q.c0 + 1], b0 = be[q.c0], b1 = be[q.c0 + 1];   // coef_s has 33+ rows
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool w = q.wrap(j, HW);
+                float v = x4[j] * (w ? a1 : a0) + (w ? b1 : b0);
+                if constexpr (PRO == 2) v = r4[j] + v;
+                v = relu(v);
+                tile[q.slot(j, HW)] = v;
+                o[j] = v;
+            }
+            reinterpret_cast<float4 *>(hout)[i] = make_float4(o[0], o[1], o[2], o[3]);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one float4 at a time: hoisting every coefficient read spills
+    }
+}
+
+// SUMS epilogue, after the output tile is complete (vec layout only): store out = tile + add*[mask > 0],
+// then the per-channel sums of out*[hmask > 0] (s1) and out*[hmask > 0]*(yprev - mean) (s2) in fp64.
+// Lane l owns channel l & 31 and half (l >> 5) of the cells; its masked values wait in registers while
+// the tile is refilled with yprev - mean.
+__device__ __forceinline__ void store_sample_sums(float *tile, float *dst, int n_elem, int HW, float inv_hw,
+                                                  int lane, const float *add, const float *mask,
+                                                  const float *hmask, const float *yprev, const float *mean_s,
+                                                  double &s1, double &s2) {
+    const int nv = n_elem >> 2;
+    for (int i = lane; i < nv; i += 64) {
+        const float4 a = reinterpret_cast<const float4 *>(add)[i];
+        const float4 m = reinterpret_cast<const float4 *>(mask)[i];
+        const float4 hm = reinterpret_cast<const float4 *>(hmask)[i];
+        const float a4[4] = {a.x, a.y, a.z, a.w}, m4[4] = {m.x, m.y, m.z, m.w}, h4[4] = {hm.x, hm.y, hm.z, hm.w};
+        float x4[4];
+        const Quad q(i, HW, inv_hw);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float *slot = tile + q.slot(j, HW);
+            x4[j] = *slot + (m4[j] > 0.f ? a4[j] : 0.f);
+            *slot = h4[j] > 0.f ? x4[j] : 0.f;
+        }
+        reinterpret_cast<float4 *>(dst)[i] = make_float4(x4[0], x4[1], x4[2], x4[3]);
+    }
+    lds_fence();
+    constexpr int kHalf = kMaxCells / 2;
+    const int c = lane & 31, c0 = (lane >> 5) * kHalf;
+    float gm[kHalf];
+    float t1 = 0.f, t2 = 0.f;   // fp32 within the sample, fp64 across samples (as the STATS epilogue)
+#pragma unroll
+    for (int j = 0; j < kHalf; ++j) {
+        gm[j] = c0 + j < HW ? tile[c * kS + c0 + j] : 0.f;
+        t1 += gm[j];
+    }
+    s1 += (double)t1;
+    lds_fence();
+    for (int i = lane; i < nv; i += 64) {
+        const float4 yv = reinterpret_cast<const float4 *>(yprev)[i];
+        const float y4[4] = {yv.x, yv.y, yv.z, yv.w};
+        const Quad q(i, HW, inv_hw);
+        const float mu0 = mean_s[q.c0], mu1 = mean_s[q.c0 + 1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tile[q.slot(j, HW)] = y4[j] - (q.wrap(j, HW) ? mu1 : mu0);
+    }
+    lds_fence();
+#pragma unroll
+    for (int j = 0; j < kHalf; ++j)
+        if (c0 + j < HW) t2 += gm[j] * tile[c * kS + c0 + j];
+    s2 += (double)t2;
+}
+
+template <int KS, bool VEC, bool STATS, bool SPLIT, int PRO = 0, bool SUMS = false>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void torus_conv_kernel(ConvArgs a) {
+    static_assert(VEC || (PRO == 0 && !SUMS), "the prologue / sums forms need the float4 layout");
+    const float *__restrict__ x = a.x;
+    const int64_t N = a.N;
+    const int Cin = a.Cin, H = a.H, W = a.W, out_c = a.out_c;
+    const float *__restrict__ wpk = a.wpk;
+    const float *__restrict__ bias = a.bias;
+    float *__restrict__ y = a.y;
+    const bool vec_out = a.vec_out;
+    double *__restrict__ part = a.part;
+    const float *__restrict__ add = a.add;
+    const float *__restrict__ add_mask = a.add_mask;
     constexpr int kNW = kTaps * KS * 2 * 64;
     constexpr int kNLd = VEC ? (KS * 4 * kMaxCells / 4 + 63) / 64 : (KS * 4 * kMaxCells + 63) / 64;
     __shared__ float w_lds[kNW];
     __shared__ float tiles[kWaves * kTile];
+    __shared__ float coef_s[2 * kCo + 2];   // PRO: alpha[32], beta[32]; SUMS: mean[32]; +1 read past the last channel
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int HW = H * W;
@@ -184,12 +306,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
     float *tile = tiles + wave * kTile;
 
     for (int i = threadIdx.x; i < kNW; i += kThreads) w_lds[i] = wpk[i];
+    if constexpr (PRO != 0) {
+        if (threadIdx.x < 2 * kCo) coef_s[threadIdx.x] = threadIdx.x < kCo ? a.alpha[threadIdx.x] : a.beta[threadIdx.x - kCo];
+    }
+    if constexpr (SUMS) {
+        if (threadIdx.x < kCo) coef_s[threadIdx.x] = a.mean[threadIdx.x];
+    }
     // channel rows Cin .. 4*KS-1 stay zero (their packed weights are zero too; no NaN * 0)
     for (int i = lane; i < kTile; i += 64) tile[i] = 0.f;
 
     // the lane's A-fragment cells: q = mt*16 + (lane & 15); cells past the board read cell q - HW.
-    // nbr(q, tap) = row part (ky) + column part (kx): 30 registers instead of 45.
-    int nrow[kMT][3], ncol[kMT][3];
+    // nbr(q, tap) = row part (ky) + column part (kx), packed as row | column << 16: 15 registers instead
+    // of 45 (the kernel sits at the 256-register limit of 2 waves per SIMD)
+    uint32_t nbp[kMT][3];
 #pragma unroll
     for (int mt = 0; mt < kMT; ++mt) {
         int q = mt * 16 + (lane & 15);
@@ -200,10 +329,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
             int rr = r + d - 1, cc = c + d - 1;
             rr = rr < 0 ? rr + H : (rr >= H ? rr - H : rr);
             cc = cc < 0 ? cc + W : (cc >= W ? cc - W : cc);
-            nrow[mt][d] = rr * W + (lane >> 4) * kS;
-            ncol[mt][d] = cc;
+            nbp[mt][d] = (uint32_t)(rr * W + (lane >> 4) * kS) | ((uint32_t)cc << 16);
         }
     }
+    auto nbr_ofs = [&](int mt, int t) -> int { return (int)(nbp[mt][t / 3] & 0xffffu) + (int)(nbp[mt][t % 3] >> 16); };
     float bias_v[2] = {0.f, 0.f};
     if (bias) {
         bias_v[0] = bias[lane & 15];
@@ -213,12 +342,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
 
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int64_t n = (int64_t)blockIdx.x * kWaves + wave;
-    Stage<VEC, kNLd> st;
-    if (n < N) st.load(x + n * in_elem, in_elem, lane);
-    __syncthreads();   // weights in LDS, tiles zeroed
+    Stage<VEC, kNLd, true> st;
+    Stage<VEC, kNLd, true> sr;   // PRO == 2: the residual input
+    if (n < N) {
+        st.load(x + n * in_elem, in_elem, lane);
+        if constexpr (PRO == 2) sr.load(a.res + n * in_elem, in_elem, lane);
+    }
+    __syncthreads();   // weights (and coefficients) in LDS, tiles zeroed
 
     for (; n < N; n += stride) {
-        st.to_lds(tile, in_elem, HW, inv_hw, lane);
+        if constexpr (PRO != 0)
+            pro_to_lds<PRO>(st, sr, tile, a.hout + n * in_elem, in_elem, HW, inv_hw, lane, coef_s, coef_s + kCo);
+        else
+            st.to_lds(tile, in_elem, HW, inv_hw, lane);
         lds_fence();
         const int64_t next = n + stride;
         if (next < N) st.load(x + next * in_elem, in_elem, lane);   // in flight during the MFMAs
@@ -250,7 +386,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
                 }
 #pragma unroll
                 for (int mt = 0; mt < kMT; ++mt) {
-                    const float *ap = tile + nrow[mt][t / 3] + ncol[mt][t % 3] + cofs;
+                    const float *ap = tile + nbr_ofs(mt, t) + cofs;
                     float av[8];
 #pragma unroll
                     for (int e = 0; e < 8; ++e) av[e] = ap[e * kS];
@@ -270,7 +406,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
                 const float b1 = wl[((t * KS + s) * 2 + 1) * 64];
 #pragma unroll
                 for (int mt = 0; mt < kMT; ++mt) {
-                    const float a = tile[nrow[mt][t / 3] + ncol[mt][t % 3] + s * 4 * kS];
+                    const float a = tile[nbr_ofs(mt, t) + s * 4 * kS];
                     acc[mt][0] = mfma(a, b0, acc[mt][0]);
                     acc[mt][1] = mfma(a, b1, acc[mt][1]);
                 }
@@ -278,6 +414,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
         }
         }
         lds_fence();   // every lane's A reads done before the tile is overwritten
+        if constexpr (PRO == 2) {
+            if (next < N) sr.load(a.res + next * in_elem, in_elem, lane);   // in flight during the epilogue
+        }
 
         // accumulators (cell = mt*16 + (lane>>4)*4 + r, co = ct*16 + (lane&15)) -> tile [co][cell]
         float t1[2] = {0.f, 0.f}, t2[2] = {0.f, 0.f};
@@ -307,8 +446,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
         }
         lds_fence();
         const int64_t ob = n * (out_c * HW);
-        store_sample(tile, y + ob, out_c * HW, vec_out, HW, inv_hw, lane, add ? add + ob : nullptr,
-                     add ? add_mask + ob : nullptr);
+        if constexpr (SUMS)
+            store_sample_sums(tile, y + ob, out_c * HW, HW, inv_hw, lane, add + ob, add_mask + ob, a.hmask + ob,
+                              a.yprev + ob, coef_s, s1[0], s2[0]);
+        else
+            store_sample(tile, y + ob, out_c * HW, vec_out, HW, inv_hw, lane, add ? add + ob : nullptr,
+                         add ? add_mask + ob : nullptr);
         lds_fence();
         // padding rows must read as zero again for the next sample (the output tile used them)
         for (int i = in_elem / HW * kS + lane; i < (SPLIT ? kCo : KS * 4) * kS; i += 64) tile[i] = 0.f;
@@ -329,6 +472,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
             const int co = threadIdx.x >> 1, k = threadIdx.x & 1;
             double t = 0.0;
             for (int i = 0; i < kWaves * 4; ++i) t += red[(i * kCo + co) * 2 + k];
+            part[((int64_t)blockIdx.x * kCo + co) * 2 + k] = t;
+        }
+    }
+    if constexpr (SUMS) {
+        // lane l holds channel l & 31 over half l >> 5 of the cells: fold halves and waves in a fixed order
+        __syncthreads();
+        double *red = reinterpret_cast<double *>(tiles);   // [wave][half][32][2]
+        red[((wave * 2 + (lane >> 5)) * kCo + (lane & 31)) * 2 + 0] = s1[0];
+        red[((wave * 2 + (lane >> 5)) * kCo + (lane & 31)) * 2 + 1] = s2[0];
+        __syncthreads();
+        if (threadIdx.x < 2 * kCo) {
+            const int co = threadIdx.x >> 1, k = threadIdx.x & 1;
+            double t = 0.0;
+            for (int i = 0; i < kWaves * 2; ++i) t += red[(i * kCo + co) * 2 + k];
             part[((int64_t)blockIdx.x * kCo + co) * 2 + k] = t;
         }
     }
@@ -542,17 +699,18 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
     int rc = status();
     if (rc) return rc;
     const int HW = (int)(H * W);
-    const bool vec = (in_c * HW) % 4 == 0 && aligned16(x);
-    const bool vec_out = (out_c * HW) % 4 == 0 && aligned16(y) && (!add || (aligned16(add) && aligned16(add_mask)));
+    // float4 staging: a float4 spans at most two channels, so boards of at least 4 cells
+    const bool vec = HW >= 4 && (in_c * HW) % 4 == 0 && aligned16(x);
+    const bool vec_out = HW >= 4 && (out_c * HW) % 4 == 0 && aligned16(y) &&
+                         (!add || (aligned16(add) && aligned16(add_mask)));
+    ConvArgs a{};
+    a.x = x; a.N = N; a.Cin = in_c; a.H = (int)H; a.W = (int)W; a.wpk = wpk; a.bias = bias; a.out_c = out_c;
+    a.vec_out = vec_out; a.y = y; a.part = part; a.add = add; a.add_mask = add_mask;
     const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
 #define HRL_TORUS_LAUNCH(KS_, VEC_, ST_)                                                                           \
     do {                                                                                                         \
-        if (g_split)                                                                                             \
-            hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_, true>), grid, block, 0, s, x, N, in_c, (int)H,  \
-                               (int)W, wpk, bias, out_c, vec_out, y, part, add, add_mask);                       \
-        else                                                                                                     \
-            hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_, false>), grid, block, 0, s, x, N, in_c, (int)H, \
-                               (int)W, wpk, bias, out_c, vec_out, y, part, add, add_mask);                       \
+        if (g_split) hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_, true>), grid, block, 0, s, a);        \
+        else hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_, false>), grid, block, 0, s, a);               \
     } while (0)
     const bool st = part != nullptr;
     if (KS == 8) {
@@ -565,13 +723,68 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
     return status();
 }
 
+int hrl_torus_unit_forward(const float *y_prev, const float *res, const float *alpha, const float *beta, float *h,
+                           int64_t N, int64_t H, int64_t W, const float *weight, const float *bias, float *y,
+                           double *part, void *workspace, int64_t workspace_bytes, void *stream) {
+    if (!shape_ok(N, kCo, kCo, H, W) || !y_prev || !alpha || !beta || !h || !weight || !y || !part || !workspace)
+        return HRL_EINVAL;
+    if (workspace_bytes < hrl_torus_workspace_bytes(N)) return HRL_EINVAL;
+    if (H * W < 4 || (kCo * H * W) % 4 != 0 || !aligned16(y_prev) || !aligned16(h) || !aligned16(y) || (res && !aligned16(res)))
+        return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    float *wpk = static_cast<float *>(workspace);
+    hipLaunchKernelGGL(torus_pack_kernel, dim3((kTaps * 8 * 128 + 255) / 256), dim3(256), 0, s, weight, (int)kCo, 8, 0,
+                       wpk);
+    int rc = status();
+    if (rc) return rc;
+    ConvArgs a{};
+    a.x = y_prev; a.N = N; a.Cin = kCo; a.H = (int)H; a.W = (int)W; a.wpk = wpk; a.bias = bias; a.out_c = kCo;
+    a.vec_out = true; a.y = y; a.part = part; a.res = res; a.alpha = alpha; a.beta = beta; a.hout = h;
+    const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
+    if (res) {
+        if (g_split) hipLaunchKernelGGL((torus_conv_kernel<8, true, true, true, 2>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((torus_conv_kernel<8, true, true, false, 2>), grid, block, 0, s, a);
+    } else {
+        if (g_split) hipLaunchKernelGGL((torus_conv_kernel<8, true, true, true, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((torus_conv_kernel<8, true, true, false, 1>), grid, block, 0, s, a);
+    }
+    return status();
+}
+
+int hrl_torus_unit_input_grad(const float *dy, int64_t N, int64_t H, int64_t W, const float *weight, const float *g,
+                              const float *out, float *dh, const float *h_mask, const float *y_prev,
+                              const float *mean_prev, double *part, void *workspace, int64_t workspace_bytes,
+                              void *stream) {
+    if (!shape_ok(N, kCo, kCo, H, W) || !dy || !weight || !g || !out || !dh || !h_mask || !y_prev || !mean_prev ||
+        !part || !workspace)
+        return HRL_EINVAL;
+    if (workspace_bytes < hrl_torus_workspace_bytes(N)) return HRL_EINVAL;
+    if (H * W < 4 || (kCo * H * W) % 4 != 0) return HRL_EINVAL;
+    for (const void *p : {(const void *)dy, (const void *)g, (const void *)out, (const void *)dh, (const void *)h_mask,
+                          (const void *)y_prev})
+        if (!aligned16(p)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    float *wpk = static_cast<float *>(workspace);
+    hipLaunchKernelGGL(torus_pack_kernel, dim3((kTaps * 8 * 128 + 255) / 256), dim3(256), 0, s, weight, (int)kCo, 8, 1,
+                       wpk);
+    int rc = status();
+    if (rc) return rc;
+    ConvArgs a{};
+    a.x = dy; a.N = N; a.Cin = kCo; a.H = (int)H; a.W = (int)W; a.wpk = wpk; a.out_c = kCo; a.vec_out = true;
+    a.y = dh; a.part = part; a.add = g; a.add_mask = out; a.hmask = h_mask; a.yprev = y_prev; a.mean = mean_prev;
+    const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
+    if (g_split) hipLaunchKernelGGL((torus_conv_kernel<8, true, false, true, 0, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((torus_conv_kernel<8, true, false, false, 0, true>), grid, block, 0, s, a);
+    return status();
+}
+
 int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
                          float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream) {
     if (!shape_ok(N, Cin, Cout, H, W) || !x || !dy || !dweight || !workspace) return HRL_EINVAL;
     if (workspace_bytes < hrl_torus_workspace_bytes(N)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int HW = (int)(H * W);
-    const bool vec = (Cin * HW) % 4 == 0 && (kCo * HW) % 4 == 0 && aligned16(x) && aligned16(dy);
+    const bool vec = HW >= 4 && (Cin * HW) % 4 == 0 && (kCo * HW) % 4 == 0 && aligned16(x) && aligned16(dy);
     const int grid = grid_for(N, kGridWgrad);
     float *partial = static_cast<float *>(workspace) + kPackFloats;
     if (Cin == kCo) {

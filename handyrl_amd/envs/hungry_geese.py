@@ -72,11 +72,9 @@ class GeeseNet(nn.Module):
 
     def forward(self, x, _=None):
         if self.training and self.conv0.use_hip and self.conv0.bn is not None and x.is_cuda:
-            # accelerated training step: each unit is one fused HIP Function (nn.torus_block)
-            from ..nn import torus_block
-            h = torus_block(x, self.conv0, residual=False)
-            for block in self.blocks:
-                h = torus_block(h, block, residual=True)
+            # accelerated training step: the unit chain is one HIP Function (nn.torus_tower)
+            from ..nn import torus_tower
+            h = torus_tower(x, [self.conv0, *self.blocks])
         else:
             h = F.relu(self.conv0(x))
             for block in self.blocks:

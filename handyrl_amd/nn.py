@@ -550,6 +550,147 @@ def torus_block(h, unit, residual):
                                bn.running_var if bn.track_running_stats else None, momentum, bn.eps, residual)
 
 
+class _TorusTower(torch.autograd.Function):
+    """GeeseNet's unit chain in training mode (hungry_geese.py:48-51): the stem h_1 = relu(bn_0(conv_0(x)))
+    and h_{i+1} = relu(h_i + bn_i(conv_i(h_i))), with every BatchNorm pass but one folded into a conv:
+
+    forward : stem conv (+ BN statistics) -> finalize; unit i's conv builds its input h_i from the previous
+              unit's conv output in its prologue (hrl_torus_unit_forward) -> finalize; one residual apply for
+              the last unit's output;
+    backward: the last unit's masked BN backward; per unit: weight gradient -> input gradient whose epilogue
+              adds the residual branch and sums the previous unit's masked BN backward terms
+              (hrl_torus_unit_input_grad) -> finalize -> masked BN backward apply.
+    Per unit only h_i and y_i reach HBM (as with the per-unit Functions); the residual-apply and masked
+    reduce passes of nn.torus_block are gone.  ``units`` carries each BatchNorm's running statistics,
+    momentum and eps; ``params`` is (conv weight, conv bias, bn weight, bn bias) per unit.
+    """
+
+    @staticmethod
+    def forward(ctx, x, units, *params):
+        x = x.contiguous()
+        N, Cin, H, W = x.shape
+        HW = H * W
+        dev = x.device
+        lib = _native.load()
+        stream = _native.stream_of(dev)
+        n = len(units)
+        ws_bytes = max(lib.hrl_torus_workspace_bytes(N), lib.hrl_bn_workspace_bytes(N, 32, HW))
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        nparts = lib.hrl_torus_stats_blocks(N)
+        part = torch.empty(nparts * 64, dtype=torch.float64, device=dev)
+        coef = torch.empty(n, 4, 32, device=dev, dtype=x.dtype)   # per unit: save_mean, save_invstd, alpha, beta
+        ws_ = (_native.ptr(ws), ws_bytes, stream)
+        P = _native.ptr
+        weights = [params[4 * i].contiguous() for i in range(n)]
+        ys, hs = [], [x]
+        for i in range(n):
+            w, b, gamma, beta = weights[i], params[4 * i + 1], params[4 * i + 2], params[4 * i + 3]
+            y = torch.empty(N, 32, H, W, device=dev, dtype=x.dtype)
+            if i == 0:
+                _native.check(lib.hrl_torus_conv_forward(P(x), N, Cin, 32, H, W, P(w), P(b), 0, P(y), P(part), None,
+                                                         None, *ws_), 'hrl_torus_conv_forward(stats)')
+            else:
+                h = torch.empty(N, 32, H, W, device=dev, dtype=x.dtype)
+                _native.check(lib.hrl_torus_unit_forward(P(ys[-1]), P(hs[-1]) if i >= 2 else None, P(coef[i - 1, 2]),
+                                                         P(coef[i - 1, 3]), P(h), N, H, W, P(w), P(b), P(y), P(part),
+                                                         *ws_), 'hrl_torus_unit_forward')
+                hs.append(h)
+            rm, rv, momentum, eps = units[i]
+            _native.check(lib.hrl_bn_finalize_stats(P(part), nparts, 32, N * HW, P(gamma), P(beta), P(rm), P(rv),
+                                                    momentum, eps, P(coef[i, 0]), P(coef[i, 1]), P(coef[i, 2]),
+                                                    P(coef[i, 3]), stream), 'hrl_bn_finalize_stats')
+            ys.append(y)
+        out = torch.empty_like(ys[-1])
+        _native.check(lib.hrl_bn_apply_residual(P(ys[-1]), P(hs[-1]) if n >= 2 else None, N, 32, HW,
+                                                P(coef[n - 1, 2]), P(coef[n - 1, 3]), P(out), stream),
+                      'hrl_bn_apply_residual')
+        gammas = [params[4 * i + 2] for i in range(n)]
+        ctx.save_for_backward(out, coef, *weights, *gammas, *ys, *hs)
+        ctx.n = n
+        ctx.has_bias = [params[4 * i + 1] is not None for i in range(n)]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        n = ctx.n
+        saved = ctx.saved_tensors
+        out, coef = saved[0], saved[1]
+        weights, gammas = saved[2:2 + n], saved[2 + n:2 + 2 * n]
+        ys, hs = saved[2 + 2 * n:2 + 3 * n], saved[2 + 3 * n:]
+        g = g.contiguous()
+        x = hs[0]
+        N, Cin, H, W = x.shape
+        HW = H * W
+        dev = x.device
+        lib = _native.load()
+        stream = _native.stream_of(dev)
+        P = _native.ptr
+        bn_ws_bytes = lib.hrl_bn_workspace_bytes(N, 32, HW)
+        ws_bytes = max(lib.hrl_torus_workspace_bytes(N), bn_ws_bytes)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        nparts = lib.hrl_torus_stats_blocks(N)
+        part = torch.empty(nparts * 64, dtype=torch.float64, device=dev)
+        kg = torch.empty(2, 32, device=dev, dtype=g.dtype)   # k, mean(dy) of the unit being applied
+        grads = [None] * (4 * n)
+        for i in range(n):
+            grads[4 * i + 2] = torch.empty(32, device=dev, dtype=g.dtype)
+            grads[4 * i + 3] = torch.empty(32, device=dev, dtype=g.dtype)
+        dy = torch.empty_like(ys[-1])
+        _native.check(lib.hrl_bn_backward_masked(P(ys[-1]), P(g), P(out), N, 32, HW, P(gammas[-1]),
+                                                 P(coef[n - 1, 0]), P(coef[n - 1, 1]), P(dy), P(grads[4 * n - 2]),
+                                                 P(grads[4 * n - 1]), P(ws), bn_ws_bytes, stream),
+                      'hrl_bn_backward_masked')
+        g_cur = g
+        dx = None
+        for i in range(n - 1, -1, -1):
+            dw = torch.empty_like(weights[i])
+            db = torch.empty(32, device=dev, dtype=g.dtype) if ctx.has_bias[i] else None
+            cin = Cin if i == 0 else 32
+            _native.check(lib.hrl_torus_conv_wgrad(P(hs[i]), P(dy), N, cin, 32, H, W, P(dw), P(db), P(ws), ws_bytes,
+                                                   stream), 'hrl_torus_conv_wgrad')
+            grads[4 * i], grads[4 * i + 1] = dw, db
+            if i == 0:
+                if ctx.needs_input_grad[0]:
+                    dx = torch.empty_like(x)
+                    _native.check(lib.hrl_torus_conv_forward(P(dy), N, Cin, 32, H, W, P(weights[0]), None, 1, P(dx),
+                                                             None, None, None, P(ws), ws_bytes, stream),
+                                  'hrl_torus_conv_forward(flip)')
+                break
+            out_i = hs[i + 1] if i + 1 < n else out
+            g_prev = torch.empty_like(g_cur)
+            _native.check(lib.hrl_torus_unit_input_grad(P(dy), N, H, W, P(weights[i]), P(g_cur), P(out_i), P(g_prev),
+                                                        P(hs[i]), P(ys[i - 1]), P(coef[i - 1, 0]), P(part), P(ws),
+                                                        ws_bytes, stream), 'hrl_torus_unit_input_grad')
+            _native.check(lib.hrl_bn_finalize_backward(P(part), nparts, 32, N * HW, P(gammas[i - 1]),
+                                                       P(coef[i - 1, 1]), P(grads[4 * i - 2]), P(grads[4 * i - 1]),
+                                                       P(kg[0]), P(kg[1]), stream), 'hrl_bn_finalize_backward')
+            dy = torch.empty_like(dy)
+            _native.check(lib.hrl_bn_backward_apply_masked(P(ys[i - 1]), P(g_prev), P(hs[i]), N, 32, HW,
+                                                           P(gammas[i - 1]), P(coef[i - 1, 0]), P(coef[i - 1, 1]),
+                                                           P(kg[0]), P(kg[1]), P(dy), stream),
+                          'hrl_bn_backward_apply_masked')
+            g_cur = g_prev
+        return (dx, None, *grads)
+
+
+def torus_tower(x, units):
+    """The chain relu(bn(conv(x))) -> relu(h + bn(conv(h))) ... over training-mode TorusConv2d ``units``
+    (GeeseNet's conv0 and blocks, hungry_geese.py:48-51) as one HIP Function (_TorusTower); each
+    BatchNorm module's batch counter and running statistics advance as in its forward."""
+    meta, params = [], []
+    for unit in units:
+        bn = unit.bn
+        momentum = 0.0 if bn.momentum is None else bn.momentum
+        if bn.track_running_stats and bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+            if bn.momentum is None:
+                momentum = 1.0 / float(bn.num_batches_tracked.item())
+        meta.append((bn.running_mean if bn.track_running_stats else None,
+                     bn.running_var if bn.track_running_stats else None, momentum, bn.eps))
+        params += [unit.conv.weight, unit.conv.bias, bn.weight, bn.bias]
+    return _TorusTower.apply(x, meta, *params)
+
+
 def _board_head_spec(m):
     """(conv, fc) of a TicTacToe-style Head (tictactoe.py:35-49): 1x1 conv with bias and no BatchNorm ->
     LeakyReLU(0.1) -> flatten -> bias-free Linear; None for anything else.  Matches the reference's Head

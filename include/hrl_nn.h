@@ -90,6 +90,11 @@ int hrl_bn_apply_residual(const float *x, const float *res, int64_t N, int64_t C
 int hrl_bn_backward_masked(const float *x, const float *dy, const float *out, int64_t N, int64_t C, int64_t HW,
                            const float *weight, const float *save_mean, const float *save_invstd, float *dx,
                            float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream);
+/* The apply half of hrl_bn_backward_masked with the coefficients of hrl_bn_finalize_backward
+ * (sums from hrl_torus_unit_input_grad). */
+int hrl_bn_backward_apply_masked(const float *x, const float *dy, const float *out, int64_t N, int64_t C, int64_t HW,
+                                 const float *weight, const float *save_mean, const float *save_invstd,
+                                 const float *kcoef, const float *gmean, float *dx, void *stream);
 
 /*
  * Tiny-board convolution as one dense matrix (handyrl_amd/nn.py BoardConv2d):
@@ -243,6 +248,29 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
                            void *stream);
 int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
                          float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream);
+
+/*
+ * The GeeseNet unit chain (hungry_geese.py:48-51, h_{i+1} = relu(h_i + bn_i(conv_i(h_i)))) with the
+ * BatchNorm passes folded into the torus convs:
+ * hrl_torus_unit_forward: unit i's conv (32 -> 32, with the BN statistics in part) whose input
+ *   h = relu([res +] y_prev*alpha[c] + beta[c]) is built in the prologue from the previous unit's conv
+ *   output y_prev, its residual input res (NULL for the unit after the stem) and BN coefficients
+ *   (hrl_bn_finalize_stats alpha/beta); h is also written (N, 32, H, W).  Same arithmetic as
+ *   hrl_bn_apply_residual + hrl_torus_conv_forward, one pass less.
+ * hrl_torus_unit_input_grad: dh = conv^T(dy) + g*[out > 0] (unit i's input gradient, the residual
+ *   branch added) and, in the same pass, the previous unit's masked BatchNorm backward sums
+ *   part[block][c] = (sum dh*[h_mask > 0], sum dh*[h_mask > 0]*(y_prev - mean_prev[c])) over
+ *   hrl_torus_stats_blocks(N) blocks -> hrl_bn_finalize_backward -> hrl_bn_backward_apply_masked.
+ *   h_mask is unit i's input (= unit i-1's output), y_prev unit i-1's conv output.
+ * Both: float4-aligned tensors, workspace hrl_torus_workspace_bytes(N).
+ */
+int hrl_torus_unit_forward(const float *y_prev, const float *res, const float *alpha, const float *beta, float *h,
+                           int64_t N, int64_t H, int64_t W, const float *weight, const float *bias, float *y,
+                           double *part, void *workspace, int64_t workspace_bytes, void *stream);
+int hrl_torus_unit_input_grad(const float *dy, int64_t N, int64_t H, int64_t W, const float *weight, const float *g,
+                              const float *out, float *dh, const float *h_mask, const float *y_prev,
+                              const float *mean_prev, double *part, void *workspace, int64_t workspace_bytes,
+                              void *stream);
 
 /*
  * The TicTacToe net's two output heads fused (handyrl/envs/tictactoe.py:35-49, 59-60;

@@ -169,3 +169,48 @@ def test_fused_torus_block_matches_torch(cuda, residual, cin, N):
         torch.testing.assert_close(q.grad.cpu(), p.grad, rtol=1e-4, atol=tol, msg=n)
     for n in ('running_mean', 'running_var', 'num_batches_tracked'):
         torch.testing.assert_close(getattr(unit.bn, n).cpu(), getattr(ref.bn, n), rtol=1e-5, atol=1e-6, msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N', [41, 1500])
+def test_torus_tower_matches_unit_chain(cuda, N):
+    """nn.torus_tower (BN apply folded into the next conv's prologue, the previous unit's masked BN
+    reduce folded into the input gradient's epilogue) vs the per-unit Functions (nn.torus_block):
+    the forward, the hidden states and the running statistics are bit-identical (same arithmetic,
+    one pass less); the backward's BN sums are folded in another order, so gradients agree to
+    fp32 rounding."""
+    from handyrl_amd.nn import torus_block, torus_tower
+    torch.manual_seed(N)
+    ref_units = [TorusConv2d(17, 32, (3, 3), True)] + [TorusConv2d(32, 32, (3, 3), True) for _ in range(3)]
+    for u in ref_units:
+        with torch.no_grad():
+            u.bn.weight.uniform_(0.5, 1.5)
+            u.bn.bias.uniform_(-0.2, 0.2)
+    units_a = [u.to(cuda) for u in ref_units]
+    units_b = [TorusConv2d(u.conv.in_channels, 32, (3, 3), True).to(cuda) for u in ref_units]
+    for a, b in zip(units_a, units_b):
+        b.load_state_dict(a.state_dict())
+    for u in units_a + units_b:
+        u.use_hip = True
+    x = torch.randn(N, 17, 7, 11, device=cuda)
+    g = torch.randn(N, 32, 7, 11, device=cuda)
+    xa = x.clone().requires_grad_(True)
+    h = torus_block(xa, units_a[0], residual=False)
+    for u in units_a[1:]:
+        h = torus_block(h, u, residual=True)
+    h.backward(g)
+    xb = x.clone().requires_grad_(True)
+    hb = torus_tower(xb, units_b)
+    hb.backward(g)
+    assert torch.equal(hb.detach(), h.detach())
+    for a, b in zip(units_a, units_b):
+        for k in ('running_mean', 'running_var', 'num_batches_tracked'):
+            assert torch.equal(getattr(b.bn, k), getattr(a.bn, k)), k
+    torch.testing.assert_close(xb.grad, xa.grad, rtol=1e-4, atol=1e-5)
+    for a, b in zip(units_a, units_b):
+        wscale = a.conv.weight.grad.abs().max().item()
+        for (name, p), q in zip(a.named_parameters(), b.parameters()):
+            # the conv bias feeds a training-mode BatchNorm: its exact gradient is zero and both sides hold
+            # rounding noise, compared at the weight gradient's scale
+            scale = wscale if name == 'conv.bias' else p.grad.abs().max().item()
+            assert (q.grad - p.grad).abs().max().item() <= 1e-4 * scale + 1e-6, (name, scale)
