@@ -132,6 +132,9 @@ SIGNATURES = {
     'hrl_torus_unit_input_grad': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, _f32p,
                                                  _f32p, _f32p, ctypes.c_void_p, ctypes.c_void_p, _i64,
                                                  ctypes.c_void_p]),
+    'hrl_torus_head_pool': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, _i64, _f32p, _f32p, ctypes.c_void_p]),
+    'hrl_torus_head_unpool': (ctypes.c_int, [_f32p, _f32p, _f32p, _i64, _i64, _i64, _i64, _f32p,
+                                             ctypes.c_void_p]),
     'hrl_bn_backward_apply_masked': (ctypes.c_int, [_f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p,
                                                     _f32p, _f32p, _f32p, ctypes.c_void_p]),
 }

@@ -620,6 +620,168 @@ __global__ __launch_bounds__(kThreads) void torus_wgrad_kernel(const float *__re
     }
 }
 
+// Weight gradient on the exact bf16 split (default with hrl_torus_set_split; Cin = 32, float4 layout).
+// Per tap dW[tap] (co x ci) is one v_mfma_f32_32x32x16_bf16 tile: dW[tap] += dY (co x 16 cells) .
+// X_tap (16 cells x ci) over the 5 k-steps of a sample (80 cells, dY zero past the board), six partial
+// products per k-step (hrl_split.h), 270 MFMAs of 32 cycles per sample against the fp32 kernel's 720
+// 16x16x4 MFMAs of 32 cycles.  Lane l = (r = l & 31, h = l >> 5) holds cells 8h..8h+7 of the k-step:
+// A[co = r][cell] from the fp32 dY tile (two ds_read_b128: rows of kSG = 84 floats), split once per k-step
+// and reused by the 9 taps; B[cell][ci = r] = X[r][nbr(cell, tap)] gathered from X split ONCE per sample
+// into LDS as (hi | mid << 16) words and lo halves (a gather is a b32 + a u16 read, three permutes build
+// the fragments).  The bias gradient sums the A values.  Waves fold in a fixed order: deterministic.
+constexpr int kSG = 84;   // dY tile row stride: 16-byte aligned rows, conflict-free ds_read_b128
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma32(const uint4 &a, const uint4 &b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(kThreads) void torus_wgrad_split_kernel(const float *__restrict__ x,
+                                                                     const float *__restrict__ dy, int64_t N, int H,
+                                                                     int W, float *__restrict__ partial) {
+    constexpr int kNLd = (kCo * kMaxCells / 4 + 63) / 64;   // float4 per lane per sample tensor
+    constexpr int kPart = kTaps * kCo * kCo + kCo;
+    constexpr int kHalf = kMaxCells / 2;
+    __shared__ __attribute__((aligned(16))) float gs_all[kWaves][kCo * kSG];   // dY [co][cell]
+    __shared__ uint32_t xhm_all[kWaves][kCo * kS];                              // X (hi | mid << 16) [ci][cell]
+    __shared__ uint16_t xl_all[kWaves][kCo * kS];                               // X lo [ci][cell]
+    __shared__ int nbr_tab[kMaxCells * kTaps];
+    static_assert(sizeof(gs_all) + sizeof(xhm_all) >= (kPart + kWaves * 2 * kCo) * sizeof(float), "fold buffer");
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int HW = H * W;
+    const float inv_hw = 1.0f / (float)HW;
+    const int n_elem = kCo * HW, nv = n_elem / 4;
+    float *gs = gs_all[wave];
+    uint32_t *xhm = xhm_all[wave];
+    uint16_t *xl = xl_all[wave];
+    for (int i = threadIdx.x; i < kMaxCells * kTaps; i += kThreads) {
+        const int q = i / kTaps, t = i - q * kTaps;
+        nbr_tab[i] = q < HW ? torus_nbr(q, H, W, t) : 0;   // cells past the board: dY is zero there
+    }
+    for (int i = lane; i < kCo * kSG; i += 64) gs[i] = 0.f;
+    for (int i = lane; i < kCo * kS; i += 64) { xhm[i] = 0u; xl[i] = 0; }
+    __syncthreads();
+
+    f32x16 acc[kTaps];
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    float bsum = 0.f;
+    const int r = lane & 31, h = lane >> 5;
+
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    int64_t n = (int64_t)blockIdx.x * kWaves + wave;
+    float4 sx[kNLd], sg[kNLd];
+    auto load = [&](int64_t m) {
+        const float4 *xp = reinterpret_cast<const float4 *>(x + m * n_elem);
+        const float4 *gp = reinterpret_cast<const float4 *>(dy + m * n_elem);
+#pragma unroll
+        for (int k = 0; k < kNLd; ++k) {
+            const int i = min(k * 64 + lane, nv - 1);
+            sx[k] = xp[i];
+            sg[k] = gp[i];
+        }
+    };
+    if (n < N) load(n);
+    for (; n < N; n += stride) {
+#pragma unroll
+        for (int k = 0; k < kNLd; ++k) {
+            const int i = k * 64 + lane;
+            if (i < nv) {
+                const Quad q(i, HW, inv_hw);
+                const float x4[4] = {sx[k].x, sx[k].y, sx[k].z, sx[k].w};
+                const float g4[4] = {sg[k].x, sg[k].y, sg[k].z, sg[k].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bool w = q.wrap(j, HW);
+                    const int c = q.c0 + (w ? 1 : 0), cell = q.r0 + j - (w ? HW : 0);
+                    uint32_t hb, mb, lb;
+                    hrl_split::split3(x4[j], hb, mb, lb);
+                    xhm[c * kS + cell] = hb | (mb << 16);
+                    xl[c * kS + cell] = (uint16_t)lb;
+                    gs[c * kSG + cell] = g4[j];
+                }
+            }
+        }
+        lds_fence();
+        if (n + stride < N) load(n + stride);   // in flight during the MFMAs
+
+#pragma unroll 1
+        for (int ks = 0; ks < kMaxCells / 16; ++ks) {
+            const int cell0 = ks * 16 + 8 * h;
+            const float4 g0 = *reinterpret_cast<const float4 *>(gs + r * kSG + cell0);
+            const float4 g1 = *reinterpret_cast<const float4 *>(gs + r * kSG + cell0 + 4);
+            const float av[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bsum += av[j];
+            uint4 Ah, Am, Al;
+            hrl_split::split8(av, Ah, Am, Al);
+            const int *nb = nbr_tab + cell0 * kTaps;
+#pragma unroll
+            for (int t = 0; t < kTaps; ++t) {
+                uint32_t hm[8], lo[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int p = r * kS + nb[j * kTaps + t];
+                    hm[j] = xhm[p];
+                    lo[j] = xl[p];
+                }
+                uint32_t bh[4], bm[4], bl[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    bh[d] = __builtin_amdgcn_perm(hm[2 * d + 1], hm[2 * d], 0x05040100u);   // hi(e0) | hi(e1) << 16
+                    bm[d] = __builtin_amdgcn_perm(hm[2 * d + 1], hm[2 * d], 0x07060302u);   // mid(e0) | mid(e1) << 16
+                    bl[d] = lo[2 * d] | (lo[2 * d + 1] << 16);
+                }
+                const uint4 Bh = make_uint4(bh[0], bh[1], bh[2], bh[3]);
+                const uint4 Bm = make_uint4(bm[0], bm[1], bm[2], bm[3]);
+                const uint4 Bl = make_uint4(bl[0], bl[1], bl[2], bl[3]);
+                f32x16 c = acc[t];
+                c = mfma32(Al, Bh, c);   // smallest terms first
+                c = mfma32(Am, Bm, c);
+                c = mfma32(Ah, Bl, c);
+                c = mfma32(Am, Bh, c);
+                c = mfma32(Ah, Bm, c);
+                c = mfma32(Ah, Bh, c);
+                acc[t] = c;
+            }
+        }
+        lds_fence();   // the tiles are rewritten for the next sample
+    }
+    (void)kHalf;
+    // fold the 4 waves in a fixed order ((w0 + w1) + w2) + w3: red[tap][ci][co], then db per (wave, half)
+    float *red = reinterpret_cast<float *>(gs_all);
+    float *bred = red + kPart;
+    __syncthreads();
+#pragma unroll 1
+    for (int w = 0; w < kWaves; ++w) {
+        if (wave == w) {
+#pragma unroll
+            for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    // C/D: col = lane & 31 (ci), row = (reg & 3) + 8 (reg >> 2) + 4h (co)
+                    const int co = (i & 3) + 8 * (i >> 2) + 4 * h;
+                    float *d = red + (t * kCo + r) * kCo + co;
+                    *d = w == 0 ? acc[t][i] : *d + acc[t][i];
+                }
+            bred[(wave * 2 + h) * kCo + r] = bsum;
+        }
+        __syncthreads();
+    }
+    float *out = partial + (int64_t)blockIdx.x * kPart;
+    for (int i = threadIdx.x; i < kTaps * kCo * kCo; i += kThreads) out[i] = red[i];
+    if (threadIdx.x < kCo) {
+        float b = 0.f;
+        for (int i = 0; i < kWaves * 2; ++i) b += bred[i * kCo + threadIdx.x];
+        out[kTaps * kCo * kCo + threadIdx.x] = b;
+    }
+}
+
 // fold per-workgroup partials (fixed order, fp64) into dW (32, Cin, 3, 3) and db (32)
 __global__ __launch_bounds__(256) void torus_wgrad_reduce_kernel(const float *__restrict__ partial, int nparts,
                                                                  int Cin, float *__restrict__ dw,
@@ -634,6 +796,75 @@ __global__ __launch_bounds__(256) void torus_wgrad_reduce_kernel(const float *__
         if (ci < Cin) dw[(co * Cin + ci) * kTaps + tap] = (float)s;
     } else if (db) {
         db[i - kTaps * kCo * kCo] = (float)s;
+    }
+}
+
+// ------------------------------------------------------------------ GeeseNet head pooling
+// hungry_geese.py:52-53: head[n, c] = sum_q h[n, c, q] * x[n, 0, q], avg[n, c] = mean_q h[n, c, q].
+// One wave per sample: the sample is staged [c][cell] in LDS (coalesced float4 loads), then lane l sums
+// channel l & 31 over the cells, lanes 0-31 the x-weighted sum and 32-63 the mean (sum / HW, as the
+// reference's CPU mean: sum then divide).
+__global__ __launch_bounds__(kThreads) void torus_head_pool_kernel(const float *__restrict__ h,
+                                                                   const float *__restrict__ x, int64_t N, int HW,
+                                                                   int64_t x_stride, float *__restrict__ head,
+                                                                   float *__restrict__ avg) {
+    __shared__ float tiles[kWaves * kTile];
+    __shared__ float x0s[kWaves][kMaxCells];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float *tile = tiles + wave * kTile;
+    float *x0 = x0s[wave];
+    const float inv_hw = 1.0f / (float)HW;
+    const int nv = kCo * HW / 4;
+    const int c = lane & 31;
+    for (int64_t n = (int64_t)blockIdx.x * kWaves + wave; n < N; n += (int64_t)gridDim.x * kWaves) {
+        const float4 *src = reinterpret_cast<const float4 *>(h + n * (kCo * HW));
+        for (int i = lane; i < nv; i += 64) {
+            const float4 v = src[i];
+            const float v4[4] = {v.x, v.y, v.z, v.w};
+            const Quad q(i, HW, inv_hw);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) tile[q.slot(j, HW)] = v4[j];
+        }
+        for (int q = lane; q < HW; q += 64) x0[q] = x[n * x_stride + q];
+        lds_fence();
+        float acc = 0.f;
+        if (lane < 32) {
+            for (int q = 0; q < HW; ++q) acc += tile[c * kS + q] * x0[q];
+            head[n * kCo + c] = acc;
+        } else {
+            for (int q = 0; q < HW; ++q) acc += tile[c * kS + q];
+            avg[n * kCo + c] = acc / (float)HW;
+        }
+        lds_fence();
+    }
+}
+
+// the backward of both poolings as CPU autograd computes it (mul backward dhead*x0, mean backward davg / HW,
+// summed):
+// g[n, c, q] = dhead[n, c] * x[n, 0, q] + davg[n, c] / HW; one wave per sample, float4 stores
+__global__ __launch_bounds__(kThreads) void torus_head_unpool_kernel(const float *__restrict__ dhead,
+                                                                     const float *__restrict__ davg,
+                                                                     const float *__restrict__ x, int64_t N, int HW,
+                                                                     int64_t x_stride, float *__restrict__ g) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const float inv_hw = 1.0f / (float)HW;
+    const float fhw = (float)HW;
+    const int nv = kCo * HW / 4;
+    for (int64_t n = (int64_t)blockIdx.x * kWaves + wave; n < N; n += (int64_t)gridDim.x * kWaves) {
+        const float *x0 = x + n * x_stride;
+        float4 *dst = reinterpret_cast<float4 *>(g + n * (kCo * HW));
+        for (int i = lane; i < nv; i += 64) {
+            const Quad q(i, HW, inv_hw);
+            float o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool w = q.wrap(j, HW);
+                const int c = q.c0 + (w ? 1 : 0);
+                const int cell = q.r0 + j - (w ? HW : 0);
+                o[j] = dhead[n * kCo + c] * x0[cell] + davg[n * kCo + c] / fhw;
+            }
+            dst[i] = make_float4(o[0], o[1], o[2], o[3]);
+        }
     }
 }
 
@@ -787,7 +1018,9 @@ int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin
     const bool vec = HW >= 4 && (Cin * HW) % 4 == 0 && (kCo * HW) % 4 == 0 && aligned16(x) && aligned16(dy);
     const int grid = grid_for(N, kGridWgrad);
     float *partial = static_cast<float *>(workspace) + kPackFloats;
-    if (Cin == kCo) {
+    if (Cin == kCo && vec && g_split) {
+        hipLaunchKernelGGL(torus_wgrad_split_kernel, dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)H, (int)W, partial);
+    } else if (Cin == kCo) {
         if (vec)
             hipLaunchKernelGGL((torus_wgrad_kernel<8, true>), dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)Cin,
                                (int)H, (int)W, partial);
@@ -802,6 +1035,25 @@ int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin
     if (rc) return rc;
     hipLaunchKernelGGL(torus_wgrad_reduce_kernel, dim3((int)((kPartFloats + 255) / 256)), dim3(256), 0, s, partial,
                        grid, (int)Cin, dweight, dbias);
+    return status();
+}
+
+int hrl_torus_head_pool(const float *h, const float *x, int64_t N, int64_t H, int64_t W, int64_t x_stride,
+                        float *head, float *avg, void *stream) {
+    const int64_t HW = H * W;
+    if (N < 1 || HW < 4 || HW > kMaxCells || !h || !x || !head || !avg || x_stride < HW || !aligned16(h)) return HRL_EINVAL;
+    hipLaunchKernelGGL(torus_head_pool_kernel, dim3(grid_for(N, 2048)), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), h, x, N, (int)HW, x_stride, head, avg);
+    return status();
+}
+
+int hrl_torus_head_unpool(const float *dhead, const float *davg, const float *x, int64_t N, int64_t H, int64_t W,
+                          int64_t x_stride, float *g, void *stream) {
+    const int64_t HW = H * W;
+    if (N < 1 || HW < 4 || HW > kMaxCells || !dhead || !davg || !x || !g || x_stride < HW || !aligned16(g))
+        return HRL_EINVAL;
+    hipLaunchKernelGGL(torus_head_unpool_kernel, dim3(grid_for(N, 2048)), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), dhead, davg, x, N, (int)HW, x_stride, g);
     return status();
 }
 

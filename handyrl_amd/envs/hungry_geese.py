@@ -80,8 +80,12 @@ class GeeseNet(nn.Module):
             for block in self.blocks:
                 h = F.relu(h + block(h))
         n, c = h.size(0), h.size(1)
-        h_head = (h * x[:, :1]).view(n, c, -1).sum(-1)
-        h_avg = h.view(n, c, -1).mean(-1)
+        if self.conv0.use_hip and h.is_cuda:
+            from ..nn import geese_pool
+            h_head, h_avg = geese_pool(h, x)   # one HIP pass each way
+        else:
+            h_head = (h * x[:, :1]).view(n, c, -1).sum(-1)
+            h_avg = h.view(n, c, -1).mean(-1)
         p = self.head_p(h_head)
         v = torch.tanh(self.head_v(torch.cat([h_head, h_avg], 1)))
         return {'policy': p, 'value': v}

@@ -691,6 +691,48 @@ def torus_tower(x, units):
     return _TorusTower.apply(x, meta, *params)
 
 
+class _GeesePool(torch.autograd.Function):
+    """GeeseNet's head pooling (hungry_geese.py:52-53): h_head = sum over cells of h * x[:, :1],
+    h_avg = mean over cells of h, as csrc/hrl_torus.hip head_pool / head_unpool (one pass each way).
+    x is the net's input (data): no gradient flows to it."""
+
+    @staticmethod
+    def forward(ctx, h, x):
+        h = h.contiguous()
+        x = x.contiguous()
+        N, C, H, W = h.shape
+        lib = _native.load()
+        head = torch.empty(N, C, device=h.device, dtype=h.dtype)
+        avg = torch.empty(N, C, device=h.device, dtype=h.dtype)
+        _native.check(lib.hrl_torus_head_pool(_native.ptr(h), _native.ptr(x), N, H, W, x.shape[1] * H * W,
+                                              _native.ptr(head), _native.ptr(avg), _native.stream_of(h.device)),
+                      'hrl_torus_head_pool')
+        ctx.save_for_backward(x)
+        ctx.hshape = h.shape
+        return head, avg
+
+    @staticmethod
+    def backward(ctx, dhead, davg):
+        x, = ctx.saved_tensors
+        N, C, H, W = ctx.hshape
+        lib = _native.load()
+        dhead = torch.zeros(N, C, device=x.device, dtype=x.dtype) if dhead is None else dhead.contiguous()
+        davg = torch.zeros(N, C, device=x.device, dtype=x.dtype) if davg is None else davg.contiguous()
+        g = torch.empty(N, C, H, W, device=x.device, dtype=x.dtype)
+        _native.check(lib.hrl_torus_head_unpool(_native.ptr(dhead), _native.ptr(davg), _native.ptr(x), N, H, W,
+                                                x.shape[1] * H * W, _native.ptr(g), _native.stream_of(x.device)),
+                      'hrl_torus_head_unpool')
+        return g, None
+
+
+def geese_pool(h, x):
+    """(h_head, h_avg) of GeeseNet's heads on the GPU (HIP, one pass each way); h (N, 32, H, W)."""
+    if h.shape[1] != 32 or h.dtype != torch.float32 or x.dtype != torch.float32:
+        raise RuntimeError('geese_pool: expects float32 h with 32 channels, got %s %s'
+                           % (tuple(h.shape), h.dtype))
+    return _GeesePool.apply(h, x)
+
+
 def _board_head_spec(m):
     """(conv, fc) of a TicTacToe-style Head (tictactoe.py:35-49): 1x1 conv with bias and no BatchNorm ->
     LeakyReLU(0.1) -> flatten -> bias-free Linear; None for anything else.  Matches the reference's Head

@@ -267,6 +267,13 @@ int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin
 int hrl_torus_unit_forward(const float *y_prev, const float *res, const float *alpha, const float *beta, float *h,
                            int64_t N, int64_t H, int64_t W, const float *weight, const float *bias, float *y,
                            double *part, void *workspace, int64_t workspace_bytes, void *stream);
+/* GeeseNet's head pooling (hungry_geese.py:52-53) on h (N, 32, H, W) and the net input x (its plane 0,
+ * samples x_stride floats apart): head[n, c] = sum_q h[n, c, q] * x[n, 0, q], avg[n, c] = mean_q h[n, c, q]
+ * (both (N, 32)); hrl_torus_head_unpool: the gradient w.r.t. h, g = dhead * x0 + davg / (H*W). */
+int hrl_torus_head_pool(const float *h, const float *x, int64_t N, int64_t H, int64_t W, int64_t x_stride,
+                        float *head, float *avg, void *stream);
+int hrl_torus_head_unpool(const float *dhead, const float *davg, const float *x, int64_t N, int64_t H, int64_t W,
+                          int64_t x_stride, float *g, void *stream);
 int hrl_torus_unit_input_grad(const float *dy, int64_t N, int64_t H, int64_t W, const float *weight, const float *g,
                               const float *out, float *dh, const float *h_mask, const float *y_prev,
                               const float *mean_prev, double *part, void *workspace, int64_t workspace_bytes,

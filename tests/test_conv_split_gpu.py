@@ -194,3 +194,34 @@ def test_wgrad_error_within_fp32_error(cuda):
         dw = _wgrad(lib, cuda, x.to(cuda), dy.to(cuda), split).cpu().double()
         err = float((dw - ref).abs().max() / scale)
         assert err <= bound, (split, err, bound)
+
+
+@pytest.mark.parametrize('split', [1, 0])
+@pytest.mark.parametrize('N,H,W', [(300, 7, 11), (57, 4, 5), (33, 8, 10)])
+def test_torus_wgrad_integer_data_is_exact(cuda, split, N, H, W):
+    """torus_wgrad_split_kernel (32x32x16 bf16, X split once per sample into LDS, one tap = one tile) and the
+    fp32 form: exact on integer data against fp64, so the fragment layouts, the neighbour gathers, the cells
+    past the board and the bias sum are right."""
+    lib = _native.load()
+    g = torch.Generator().manual_seed(N + H)
+    x = torch.randint(-4, 5, (N, 32, H, W), generator=g).float()
+    dy = torch.randint(-4, 5, (N, 32, H, W), generator=g).float()
+    xr = x.double().requires_grad_(False)
+    w64 = torch.zeros(32, 32, 3, 3, dtype=torch.float64, requires_grad=True)
+    b64 = torch.zeros(32, dtype=torch.float64, requires_grad=True)
+    _torus64(xr, w64, b64).backward(dy.double())
+    ws_bytes = lib.hrl_torus_workspace_bytes(N)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+    dw = torch.empty(32, 32, 3, 3, device=cuda)
+    db = torch.empty(32, device=cuda)
+    P = _native.ptr
+    xg, dyg = x.to(cuda), dy.to(cuda)   # held: a temporary's block could be reused by the next copy
+    prev = lib.hrl_torus_set_split(split)
+    try:
+        _native.check(lib.hrl_torus_conv_wgrad(P(xg), P(dyg), N, 32, 32, H, W, P(dw), P(db), P(ws),
+                                               ws_bytes, _native.stream_of(cuda)), 'torus wgrad')
+        torch.cuda.synchronize(cuda)
+    finally:
+        lib.hrl_torus_set_split(prev)
+    assert torch.equal(dw.cpu().double(), w64.grad)
+    assert torch.equal(db.cpu().double(), b64.grad)

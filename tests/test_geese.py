@@ -214,3 +214,27 @@ def test_torus_tower_matches_unit_chain(cuda, N):
             # rounding noise, compared at the weight gradient's scale
             scale = wscale if name == 'conv.bias' else p.grad.abs().max().item()
             assert (q.grad - p.grad).abs().max().item() <= 1e-4 * scale + 1e-6, (name, scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N', [1, 37, 3000])
+def test_geese_pool_matches_torch(cuda, N):
+    """nn.geese_pool (HIP head pooling) vs the reference's torch expressions (hungry_geese.py:52-53) on the
+    CPU, where the reference learner runs: pooled features to fp32 summation-order rounding, the gradient
+    w.r.t. h bit-exact (the same products and quotient as CPU autograd's mul / mean backward; torch on the
+    GPU multiplies by 1/HW instead)."""
+    from handyrl_amd.nn import geese_pool
+    torch.manual_seed(N)
+    x = (torch.rand(N, 17, 7, 11) > 0.7).float()
+    h = torch.randn(N, 32, 7, 11)
+    dh, da = torch.randn(N, 32), torch.randn(N, 32)
+    h1 = h.clone().requires_grad_(True)
+    head1 = (h1 * x[:, :1]).view(N, 32, -1).sum(-1)
+    avg1 = h1.view(N, 32, -1).mean(-1)
+    (head1 * dh + avg1 * da).sum().backward()
+    h2 = h.to(cuda).requires_grad_(True)
+    head2, avg2 = geese_pool(h2, x.to(cuda))
+    (head2 * dh.to(cuda) + avg2 * da.to(cuda)).sum().backward()
+    torch.testing.assert_close(head2.detach().cpu(), head1.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(avg2.detach().cpu(), avg1.detach(), rtol=1e-5, atol=1e-6)
+    assert torch.equal(h2.grad.cpu(), h1.grad)
