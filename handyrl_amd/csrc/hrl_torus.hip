@@ -627,8 +627,10 @@ __global__ __launch_bounds__(kThreads) void torus_wgrad_kernel(const float *__re
 // 16x16x4 MFMAs of 32 cycles.  Lane l = (r = l & 31, h = l >> 5) holds cells 8h..8h+7 of the k-step:
 // A[co = r][cell] from the fp32 dY tile (two ds_read_b128: rows of kSG = 84 floats), split once per k-step
 // and reused by the 9 taps; B[cell][ci = r] = X[r][nbr(cell, tap)] gathered from X split ONCE per sample
-// into LDS as (hi | mid << 16) words and lo halves (a gather is a b32 + a u16 read, three permutes build
-// the fragments).  The bias gradient sums the A values.  Waves fold in a fixed order: deterministic.
+// into LDS as 64-bit slots (hi | mid << 16, lo): a gather is one ds_read_b64 (row stride 162 dwords: a
+// half-wave's 32 rows cover the 64 banks once), three permutes build the fragments.  A cell's
+// neighbours come from three packed (row part | column part << 16) words.  The bias gradient sums the
+// A values.  Waves fold in a fixed order: deterministic.
 constexpr int kSG = 84;   // dY tile row stride: 16-byte aligned rows, conflict-free ds_read_b128
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -645,24 +647,30 @@ __global__ __launch_bounds__(kThreads) void torus_wgrad_split_kernel(const float
     constexpr int kPart = kTaps * kCo * kCo + kCo;
     constexpr int kHalf = kMaxCells / 2;
     __shared__ __attribute__((aligned(16))) float gs_all[kWaves][kCo * kSG];   // dY [co][cell]
-    __shared__ uint32_t xhm_all[kWaves][kCo * kS];                              // X (hi | mid << 16) [ci][cell]
-    __shared__ uint16_t xl_all[kWaves][kCo * kS];                               // X lo [ci][cell]
-    __shared__ int nbr_tab[kMaxCells * kTaps];
-    static_assert(sizeof(gs_all) + sizeof(xhm_all) >= (kPart + kWaves * 2 * kCo) * sizeof(float), "fold buffer");
+    __shared__ uint2 xs_all[kWaves][kCo * kS];                                  // X (hi | mid << 16, lo) [ci][cell]
+    __shared__ uint32_t nbp_tab[kMaxCells * 3];   // per cell and d: (row (r + d - 1) * W) | (column (c + d - 1)) << 16
+    static_assert(sizeof(gs_all) + sizeof(xs_all) >= (kPart + kWaves * 2 * kCo) * sizeof(float), "fold buffer");
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int HW = H * W;
     const float inv_hw = 1.0f / (float)HW;
     const int n_elem = kCo * HW, nv = n_elem / 4;
     float *gs = gs_all[wave];
-    uint32_t *xhm = xhm_all[wave];
-    uint16_t *xl = xl_all[wave];
-    for (int i = threadIdx.x; i < kMaxCells * kTaps; i += kThreads) {
-        const int q = i / kTaps, t = i - q * kTaps;
-        nbr_tab[i] = q < HW ? torus_nbr(q, H, W, t) : 0;   // cells past the board: dY is zero there
+    uint2 *xs = xs_all[wave];
+    for (int i = threadIdx.x; i < kMaxCells * 3; i += kThreads) {
+        const int q = i / 3, d = i - q * 3;
+        uint32_t v = 0u;   // cells past the board: dY is zero there, any cell will do
+        if (q < HW) {
+            const int r = q / W, c = q - r * W;
+            int rr = r + d - 1, cc = c + d - 1;
+            rr = rr < 0 ? rr + H : (rr >= H ? rr - H : rr);
+            cc = cc < 0 ? cc + W : (cc >= W ? cc - W : cc);
+            v = (uint32_t)(rr * W) | ((uint32_t)cc << 16);
+        }
+        nbp_tab[i] = v;
     }
     for (int i = lane; i < kCo * kSG; i += 64) gs[i] = 0.f;
-    for (int i = lane; i < kCo * kS; i += 64) { xhm[i] = 0u; xl[i] = 0; }
+    for (int i = lane; i < kCo * kS; i += 64) xs[i] = make_uint2(0u, 0u);
     __syncthreads();
 
     f32x16 acc[kTaps];
@@ -701,8 +709,7 @@ __global__ __launch_bounds__(kThreads) void torus_wgrad_split_kernel(const float
                     const int c = q.c0 + (w ? 1 : 0), cell = q.r0 + j - (w ? HW : 0);
                     uint32_t hb, mb, lb;
                     hrl_split::split3(x4[j], hb, mb, lb);
-                    xhm[c * kS + cell] = hb | (mb << 16);
-                    xl[c * kS + cell] = (uint16_t)lb;
+                    xs[c * kS + cell] = make_uint2(hb | (mb << 16), lb);
                     gs[c * kSG + cell] = g4[j];
                 }
             }
@@ -720,15 +727,20 @@ __global__ __launch_bounds__(kThreads) void torus_wgrad_split_kernel(const float
             for (int j = 0; j < 8; ++j) bsum += av[j];
             uint4 Ah, Am, Al;
             hrl_split::split8(av, Ah, Am, Al);
-            const int *nb = nbr_tab + cell0 * kTaps;
+            uint32_t nbp[8][3];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int d = 0; d < 3; ++d) nbp[j][d] = nbp_tab[(cell0 + j) * 3 + d];
+            const uint2 *xrow = xs + r * kS;
 #pragma unroll
             for (int t = 0; t < kTaps; ++t) {
                 uint32_t hm[8], lo[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const int p = r * kS + nb[j * kTaps + t];
-                    hm[j] = xhm[p];
-                    lo[j] = xl[p];
+                    const uint2 v = xrow[(nbp[j][t / 3] & 0xffffu) + (nbp[j][t % 3] >> 16)];
+                    hm[j] = v.x;
+                    lo[j] = v.y;
                 }
                 uint32_t bh[4], bm[4], bl[4];
 #pragma unroll
