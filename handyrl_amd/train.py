@@ -327,8 +327,30 @@ def loss_terms(outputs, batch, args):
     if with_ret:
         losses['r'] = vec[2]
     losses['ent'] = vec[3]
-    losses['total'] = vec[4]
+    total = vec[4]
+    total._hrl_loss_vec = vec   # backward_total seeds the vector itself
+    losses['total'] = total
     return losses, vec[5].detach()
+
+
+_SEEDS = {}
+
+
+def backward_total(losses, inputs=None, retain_graph=None):
+    """``losses['total'].backward()``.  For the fused loss (loss_terms) the backward starts at the loss
+    vector with a persistent one-hot seed on its total: autograd's ones fill for the scalar and the
+    select backward's zeros fill and copy (three launches per step) do not run."""
+    total = losses['total']
+    vec = getattr(total, '_hrl_loss_vec', None)
+    if vec is None:
+        torch.autograd.backward(total, inputs=inputs, retain_graph=retain_graph)
+        return
+    seed = _SEEDS.get(vec.device)
+    if seed is None:   # made once, in the eager warm-up before any graph capture
+        seed = torch.zeros(6, dtype=vec.dtype, device=vec.device)
+        seed[4] = 1.0
+        _SEEDS[vec.device] = seed
+    torch.autograd.backward(vec, grad_tensors=seed, inputs=inputs, retain_graph=retain_graph)
 
 
 def loss_terms_composed(outputs, batch, args):

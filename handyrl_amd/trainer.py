@@ -28,7 +28,7 @@ import torch.nn as nn
 
 from . import distributed as hdist
 from .nn import accelerate, fuse_bn_relu, deferred_weight_grads, direct_grads
-from .train import forward_prediction, loss_terms
+from .train import backward_total, forward_prediction, loss_terms
 from .util import map_r, bimap_r
 
 DEFAULT_LR = 3e-8  # train.py:318
@@ -105,7 +105,7 @@ class LearnerStep:
         try:
             outputs = forward_prediction(self.net, small_hidden, small, self.args)
             losses, _ = self.loss_fn(outputs, small, self.args)
-            losses['total'].backward()
+            backward_total(losses)
             live = [p.grad is not None for p in self.params]
         finally:
             for p, v in zip(self.params, views):
@@ -138,7 +138,7 @@ class LearnerStep:
             with deferred_weight_grads() as deferred:
                 outputs = forward_prediction(self.net, hidden, batch, self.args)
                 losses, dcnt = self.loss_fn(outputs, batch, self.args)
-                losses['total'].backward()
+                backward_total(losses)
             touched = deferred.flush()
             if self.reducer is not None:
                 self.reducer.mark_ready(touched)
@@ -148,7 +148,7 @@ class LearnerStep:
             with direct_grads():
                 outputs = forward_prediction(self.net, hidden, batch, self.args)
                 losses, dcnt = self.loss_fn(outputs, batch, self.args)
-                losses['total'].backward()
+                backward_total(losses)
         return losses, dcnt
 
     def _update(self, losses, dcnt):
@@ -262,7 +262,7 @@ class LearnerStep:
                             outputs = forward_prediction(self.net, hidden, batch, self.args)
                             losses, dcnt = self.loss_fn(outputs, batch, self.args)
                             cut, upper, lower = self._cut, self.segments[0][1], self.segments[1][1]
-                            torch.autograd.backward(losses['total'], inputs=[cut] + upper, retain_graph=True)
+                            backward_total(losses, inputs=[cut] + upper, retain_graph=True)
                         with torch.cuda.graph(seg2, capture_error_mode='thread_local'):
                             torch.autograd.backward(cut, grad_tensors=cut.grad, inputs=lower)
                 finally:
