@@ -118,10 +118,10 @@ SIGNATURES = {
     'hrl_heads_workspace_bytes': (ctypes.c_int64, [_i64]),
     'hrl_heads_bn_parts': (ctypes.c_int64, [_i64]),
     'hrl_heads_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
-                                         _f32p, _f32p, _f32p, _f32p, ctypes.c_void_p]),
+                                         _f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_void_p]),
     'hrl_heads_backward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
                                           ctypes.c_void_p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
-                                          _f32p, _f32p, _f32p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
+                                          _f32p, _f32p, _f32p, _f32p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_bn_apply_residual': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_bn_backward_masked': (ctypes.c_int, [_f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p,
                                               _f32p, _f32p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
@@ -139,7 +139,7 @@ SIGNATURES = {
                                                     _f32p, _f32p, _f32p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _lib = None
 

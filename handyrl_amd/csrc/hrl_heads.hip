@@ -114,7 +114,8 @@ __device__ __forceinline__ void slice_to_lds(const float4 (&st)[kSV], float *til
 // ------------------------------------------------------------------ forward
 __global__ __launch_bounds__(64) void heads_fwd_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
                                                        float *__restrict__ a_p, float *__restrict__ a_v,
-                                                       float *__restrict__ p_out, float *__restrict__ v_out) {
+                                                       float *__restrict__ p_out, float *__restrict__ v_out,
+                                                       bool tanh_v) {
     __shared__ float tile[64 * kTS];
     __shared__ float sw1[kM * kC], sb1[kM], swp[kOP * kZP], swv[kHW], sal[kC], sbe[kC];
     const int lane = threadIdx.x;
@@ -177,7 +178,7 @@ __global__ __launch_bounds__(64) void heads_fwd_kernel(const float *__restrict__
             for (int q = 0; q < kHW; ++q) v += swv[q] * a[kZP + q];
 #pragma unroll
             for (int k = 0; k < kOP; ++k) p_out[n * kOP + k] = p[k];
-            v_out[n] = v;
+            v_out[n] = tanh_v ? tanhf(v) : v;   // the model's torch.tanh on the value head, folded
             if (a_p) {
 #pragma unroll
                 for (int j = 0; j < kZP; ++j) a_p[n * kZP + j] = a[j];
@@ -199,7 +200,8 @@ __device__ __forceinline__ float wave_sum(float v) {
 __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
                                                        const float *__restrict__ a_p, const float *__restrict__ a_v,
                                                        const float *__restrict__ dp, const float *__restrict__ dv,
-                                                       float *__restrict__ dh, float *__restrict__ part) {
+                                                       const float *__restrict__ vt, float *__restrict__ dh,
+                                                       float *__restrict__ part) {
     __shared__ float tile[64 * kTS];
     __shared__ float sw1[kM * kC], swp[kOP * kZP], swv[kHW], sal[kC], sbe[kC], smu[kC];
     __shared__ float gw1[kM * kC * 64];   // per-lane conv weight-gradient accumulators [m*32 + c][lane]
@@ -236,6 +238,7 @@ __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__
 #pragma unroll
         for (int k = 0; k < kOP; ++k) g[k] = valid ? dp[n * kOP + k] : 0.f;
         gv = valid ? dv[n] : 0.f;
+        if (vt) gv = gv * (1.f - vt[n] * vt[n]);   // tanh backward (grad * (1 - y*y), as torch's CPU kernel)
         // the activation gradient (the fc weight gradients are dp^T a_p, dv^T a_v: host side)
         float dz[kZ];
 #pragma unroll
@@ -343,7 +346,8 @@ __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__
 // its row range (rows in order) into partial row b, columns kGWP.. (one thread per weight)
 __global__ __launch_bounds__(256) void fc_grad_kernel(const float *__restrict__ a_p, const float *__restrict__ a_v,
                                                       const float *__restrict__ dp, const float *__restrict__ dv,
-                                                      int64_t N, int64_t rows_per_block, float *__restrict__ part) {
+                                                      const float *__restrict__ vt, int64_t N,
+                                                      int64_t rows_per_block, float *__restrict__ part) {
     const int t = threadIdx.x;
     if (t >= kOP * kZP + kHW) return;
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
@@ -357,13 +361,16 @@ __global__ __launch_bounds__(256) void fc_grad_kernel(const float *__restrict__ 
         float x[8], y[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            x[u] = pol ? dp[(n + u) * kOP + k] : dv[n + u];
+            x[u] = pol ? dp[(n + u) * kOP + k] : (vt ? dv[n + u] * (1.f - vt[n + u] * vt[n + u]) : dv[n + u]);
             y[u] = pol ? a_p[(n + u) * kZP + j] : a_v[(n + u) * kHW + j];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc += x[u] * y[u];
     }
-    for (; n < r1; ++n) acc += pol ? dp[n * kOP + k] * a_p[n * kZP + j] : dv[n] * a_v[n * kHW + j];
+    for (; n < r1; ++n) {
+        const float x = pol ? dp[n * kOP + k] : (vt ? dv[n] * (1.f - vt[n] * vt[n]) : dv[n]);
+        acc += x * (pol ? a_p[n * kZP + j] : a_v[n * kHW + j]);
+    }
     part[(int64_t)blockIdx.x * kGN + kGWP + t] = acc;
 }
 
@@ -428,21 +435,21 @@ int64_t hrl_heads_bn_parts(int64_t N) { return N < 1 ? -1 : grid_for(N); }
 
 int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *b1p, const float *w1v,
                       const float *b1v, const float *wp, const float *wv, const float *bn_alpha, const float *bn_beta,
-                      float *a_p, float *a_v, float *p_out, float *v_out, void *stream) {
+                      float *a_p, float *a_v, float *p_out, float *v_out, int tanh_v, void *stream) {
     if (N < 1 || !h || !w1p || !b1p || !w1v || !b1v || !wp || !wv || !p_out || !v_out) return HRL_EINVAL;
     if ((a_p == nullptr) != (a_v == nullptr) || (bn_alpha == nullptr) != (bn_beta == nullptr) || !aligned16(h))
         return HRL_EINVAL;
     const Weights w{w1p, w1v, b1p, b1v, wp, wv};
     const BnIn bn{bn_alpha, bn_beta, nullptr, nullptr};
     hipLaunchKernelGGL(heads_fwd_kernel, dim3(grid_for(N, kGridFwd)), dim3(64), 0, static_cast<hipStream_t>(stream), h, N, w,
-                       bn, a_p, a_v, p_out, v_out);
+                       bn, a_p, a_v, p_out, v_out, tanh_v != 0);
     return status();
 }
 
 int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float *w1v, const float *wp,
                        const float *wv, const float *bn_alpha, const float *bn_beta, const float *bn_mean,
                        double *bn_part, const float *a_p, const float *a_v, const float *dp, const float *dv,
-                       float *dh, float *dw1p, float *db1p, float *dw1v, float *db1v, float *dwp, float *dwv,
+                       const float *v_tanh, float *dh, float *dw1p, float *db1p, float *dw1v, float *db1v, float *dwp, float *dwv,
                        void *workspace, int64_t workspace_bytes, void *stream) {
     if (N < 1 || !h || !w1p || !w1v || !wp || !wv || !a_p || !a_v || !dp || !dv || !dh || !workspace)
         return HRL_EINVAL;
@@ -454,11 +461,11 @@ int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float 
     const BnIn bn{bn_alpha, bn_beta, bn_mean, bn_part};
     const int grid = grid_for(N);
     float *part = static_cast<float *>(workspace);
-    hipLaunchKernelGGL(heads_bwd_kernel, dim3(grid), dim3(64), 0, s, h, N, w, bn, a_p, a_v, dp, dv, dh, part);
+    hipLaunchKernelGGL(heads_bwd_kernel, dim3(grid), dim3(64), 0, s, h, N, w, bn, a_p, a_v, dp, dv, v_tanh, dh, part);
     int rc = status();
     if (rc) return rc;
     const int64_t rows = (N + grid - 1) / grid;
-    hipLaunchKernelGGL(fc_grad_kernel, dim3(grid), dim3(256), 0, s, a_p, a_v, dp, dv, N, rows, part);
+    hipLaunchKernelGGL(fc_grad_kernel, dim3(grid), dim3(256), 0, s, a_p, a_v, dp, dv, v_tanh, N, rows, part);
     rc = status();
     if (rc) return rc;
     hipLaunchKernelGGL(heads_reduce_kernel, dim3(kGN), dim3(256), 0, s, part, grid, dw1p, dw1v, db1p, db1v, dwp,

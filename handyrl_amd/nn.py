@@ -782,7 +782,7 @@ class _BoardHeadsFn(torch.autograd.Function):
         P = _native.ptr
         w1p, w1v, wp, wv = w1p.contiguous(), w1v.contiguous(), wp.contiguous(), wv.contiguous()
         _native.check(lib.hrl_heads_forward(P(h), N, P(w1p), P(b1p.contiguous()), P(w1v), P(b1v.contiguous()),
-                                            P(wp), P(wv), None, None, P(a_p), P(a_v), P(p), P(v),
+                                            P(wp), P(wv), None, None, P(a_p), P(a_v), P(p), P(v), 0,
                                             _native.stream_of(dev)), 'hrl_heads_forward')
         ctx.save_for_backward(h, w1p, w1v, wp, wv, a_p, a_v)
         ctx.biases = (b1p, b1v)
@@ -803,7 +803,7 @@ class _BoardHeadsFn(torch.autograd.Function):
         P = _native.ptr
         dw1p, db1p, dw1v, db1v, dwp, dwv = (b[0] for b in bufs)
         _native.check(lib.hrl_heads_backward(P(h), N, P(w1p), P(w1v), P(wp), P(wv), None, None, None, None, P(a_p),
-                                             P(a_v), P(dp), P(dv), P(dh), P(dw1p), P(db1p), P(dw1v), P(db1v), P(dwp),
+                                             P(a_v), P(dp), P(dv), None, P(dh), P(dw1p), P(db1p), P(dw1v), P(db1v), P(dwp),
                                              P(dwv), P(ws), ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward')
         return (dh, *(_ret(b) for b in bufs))
 
@@ -834,7 +834,7 @@ class _FusedHeads(nn.Module):
         _native.check(_native.load().hrl_heads_forward(P(x), N, P(cp.weight.contiguous()), P(cp.bias.contiguous()),
                                                        P(cv.weight.contiguous()), P(cv.bias.contiguous()),
                                                        P(fp.weight.contiguous()), P(fv.weight.contiguous()), None,
-                                                       None, None, None, P(p), P(v), _native.stream_of(x.device)),
+                                                       None, None, None, P(p), P(v), 0, _native.stream_of(x.device)),
                       'hrl_heads_forward')
         return p, v
 
@@ -1359,7 +1359,7 @@ class _ChainHeadsFn(torch.autograd.Function):
     the heads backward also forms that BN's backward sums, so the chain backward needs no reduce pass."""
 
     @staticmethod
-    def forward(ctx, h0, meta, relu_in, w1p, b1p, w1v, b1v, wp, wv, *params):
+    def forward(ctx, h0, meta, relu_in, tanh_v, w1p, b1p, w1v, b1v, wp, wv, *params):
         h0 = h0.contiguous()
         _, ys, coefs, unit, packed = _chain_forward(h0, meta, relu_in, params, apply_out=False)
         y, coef = ys[-1], coefs[-1]
@@ -1374,8 +1374,9 @@ class _ChainHeadsFn(torch.autograd.Function):
         w1p, w1v, wp, wv = w1p.contiguous(), w1v.contiguous(), wp.contiguous(), wv.contiguous()
         _native.check(lib.hrl_heads_forward(P(y), N, P(w1p), P(b1p.contiguous()), P(w1v), P(b1v.contiguous()),
                                             P(wp), P(wv), P(coef[2]), P(coef[3]), P(a_p), P(a_v), P(p), P(v),
-                                            _native.stream_of(dev)), 'hrl_heads_forward(bn)')
-        ctx.save_for_backward(h0, *ys, *coefs, a_p, a_v, w1p, w1v, wp, wv, packed, *params)
+                                            int(tanh_v), _native.stream_of(dev)), 'hrl_heads_forward(bn)')
+        ctx.save_for_backward(h0, *ys, *coefs, a_p, a_v, w1p, w1v, wp, wv, packed, v, *params)
+        ctx.tanh_v = tanh_v
         ctx.biases = (b1p, b1v)
         ctx.n = len(meta)
         ctx.relu_in = relu_in
@@ -1386,8 +1387,8 @@ class _ChainHeadsFn(torch.autograd.Function):
         n = ctx.n
         t = ctx.saved_tensors
         h0, ys, coefs = t[0], list(t[1:1 + n]), list(t[1 + n:1 + 2 * n])
-        a_p, a_v, w1p, w1v, wp, wv, packed = t[1 + 2 * n:8 + 2 * n]
-        params = t[8 + 2 * n:]
+        a_p, a_v, w1p, w1v, wp, wv, packed, v = t[1 + 2 * n:9 + 2 * n]
+        params = t[9 + 2 * n:]
         b1p, b1v = ctx.biases
         N = h0.shape[0]
         dev = h0.device
@@ -1403,13 +1404,14 @@ class _ChainHeadsFn(torch.autograd.Function):
         bn_part = torch.empty(nparts * 64, dtype=torch.float64, device=dev)
         dw1p, db1p, dw1v, db1v, dwp, dwv = (b[0] for b in hbufs)
         _native.check(lib.hrl_heads_backward(P(y), N, P(w1p), P(w1v), P(wp), P(wv), P(coef[2]), P(coef[3]),
-                                             P(coef[0]), P(bn_part), P(a_p), P(a_v), P(dp), P(dv), P(dh), P(dw1p),
+                                             P(coef[0]), P(bn_part), P(a_p), P(a_v), P(dp), P(dv),
+                                             P(v) if ctx.tanh_v else None, P(dh), P(dw1p),
                                              P(db1p), P(dw1v), P(db1v), P(dwp), P(dwv), P(ws), ws_bytes,
                                              _native.stream_of(dev)), 'hrl_heads_backward(bn)')
         unit = _unit_coefs(dev) if ctx.relu_in else None
         g_in, grads = _chain_backward(h0, ys, coefs, unit, params, ctx.relu_in, dh, ctx.needs_input_grad[0], packed,
                                       part_in=bn_part, nblk_in=nparts)
-        return (g_in, None, None, *(_ret(b) for b in hbufs), *grads)
+        return (g_in, None, None, None, *(_ret(b) for b in hbufs), *grads)
 
 
 class _ConvBNChain(nn.Module):
@@ -1467,14 +1469,16 @@ class _ChainHeads(nn.Module):
         super().__init__()
         object.__setattr__(self, 'chain', chain)
         object.__setattr__(self, 'heads', heads)
+        self.tanh_v = False   # the model's torch.tanh on the value output, folded in by _fuse_chain_heads
 
     def forward(self, x):
         if not self.chain.fused_ok(x):
-            return self.heads(self.chain(x))
+            p, v = self.heads(self.chain(x))
+            return p, (torch.tanh(v) if self.tanh_v else v)
         (cp, fp), (cv, fv) = _board_head_spec(self.heads.head_p), _board_head_spec(self.heads.head_v)
         meta, params = self.chain.meta_params()
-        return _ChainHeadsFn.apply(x, meta, self.chain.relu_in, cp.weight, cp.bias, cv.weight, cv.bias, fp.weight,
-                                   fv.weight, *params)
+        return _ChainHeadsFn.apply(x, meta, self.chain.relu_in, self.tanh_v, cp.weight, cp.bias, cv.weight, cv.bias,
+                                   fp.weight, fv.weight, *params)
 
 
 def _fuse_chain_heads(gm):
@@ -1486,12 +1490,22 @@ def _fuse_chain_heads(gm):
         if not (isinstance(src, torch.fx.Node) and src.op == 'call_module'
                 and isinstance(gm.get_submodule(src.target), _ConvBNChain) and len(src.users) == 1):
             return 0
-        gm.add_submodule('_hrl_chain_heads', _ChainHeads(gm.get_submodule(src.target), gm.get_submodule(node.target)))
+        fused = _ChainHeads(gm.get_submodule(src.target), gm.get_submodule(node.target))
+        gm.add_submodule('_hrl_chain_heads', fused)
         with gm.graph.inserting_before(src):
             call = gm.graph.call_module('_hrl_chain_heads', src.args)
         node.replace_all_uses_with(call)
         gm.graph.erase_node(node)
         gm.graph.erase_node(src)
+        # value = torch.tanh(heads[1]) as the value output's only use (tictactoe.py:62): the kernels apply it
+        for item in list(call.users):
+            if item.op == 'call_function' and item.target is operator.getitem and item.args[1] == 1 \
+                    and len(item.users) == 1:
+                user = next(iter(item.users))
+                if _is_tanh(user, item):
+                    user.replace_all_uses_with(item)
+                    gm.graph.erase_node(user)
+                    fused.tanh_v = True
         return 1
     return 0
 
@@ -1506,6 +1520,14 @@ class _LeafTracer(torch.fx.Tracer):
     def is_leaf_module(self, m, qualname):
         return isinstance(m, (BatchNorm2d, BoardConv2d, Linear, _MultiBoardConv, _ConvBNChain)) or \
             id(m) in self.extra or super().is_leaf_module(m, qualname)
+
+
+def _is_tanh(node, arg):
+    if node.op == 'call_function' and node.target in (torch.tanh, torch.nn.functional.tanh):
+        return node.args == (arg,) and not node.kwargs
+    if node.op == 'call_method' and node.target == 'tanh':
+        return node.args == (arg,) and not node.kwargs
+    return False
 
 
 def _is_relu(gm, node):

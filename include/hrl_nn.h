@@ -284,11 +284,13 @@ int hrl_torus_unit_input_grad(const float *dy, int64_t N, int64_t H, int64_t W, 
  * csrc/hrl_heads.hip): on h (N, 32, 3, 3),
  *   a_p = leaky_relu(conv1x1(h; w1p (2, 32), b1p (2)), 0.1)  (N, 18);  p = a_p @ wp^T, wp (9, 18)
  *   a_v = leaky_relu(conv1x1(h; w1v (1, 32), b1v (1)), 0.1)  (N, 9);   v = a_v @ wv^T, wv (1, 9)
- * hrl_heads_forward writes p (N, 9), v (N, 1) (the value before the model's tanh) and,
- * when a_p / a_v are non-NULL, the activations the backward needs.
+ * hrl_heads_forward writes p (N, 9), v (N, 1) (the value before the model's tanh; tanh_v != 0: after it,
+ * the model's torch.tanh folded in) and, when a_p / a_v are non-NULL, the activations the backward needs.
  * bn_alpha / bn_beta (32 each, both or neither): the input is the raw input y of the body's last
  * BatchNorm and the heads read h = relu(y*bn_alpha + bn_beta) (hrl_bn_finalize_stats' coefficients).
- * hrl_heads_backward: from dp (N, 9), dv (N, 1): dh (N, 288) = dL/dh and every parameter gradient
+ * hrl_heads_backward: from dp (N, 9), dv (N, 1): dh (N, 288) = dL/dh and every parameter gradient;
+ * v_tanh != NULL: dv is the gradient of tanh(v) and v_tanh that forward output (tanh_v = 1), the tanh
+ * backward dv * (1 - v_tanh^2) is applied in the kernels
  * (deterministic); with bn_part (needs bn_alpha/beta and bn_mean) also that BatchNorm's backward sums
  * (sum dh*m, sum dh*m*(y - bn_mean)), m = [y*bn_alpha + bn_beta > 0], as fp64 partials
  * bn_part[hrl_heads_bn_parts(N)][32][2] -> hrl_bn_finalize_backward.
@@ -298,11 +300,11 @@ int64_t hrl_heads_workspace_bytes(int64_t N);
 int64_t hrl_heads_bn_parts(int64_t N);
 int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *b1p, const float *w1v,
                       const float *b1v, const float *wp, const float *wv, const float *bn_alpha, const float *bn_beta,
-                      float *a_p, float *a_v, float *p_out, float *v_out, void *stream);
+                      float *a_p, float *a_v, float *p_out, float *v_out, int tanh_v, void *stream);
 int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float *w1v, const float *wp,
                        const float *wv, const float *bn_alpha, const float *bn_beta, const float *bn_mean,
                        double *bn_part, const float *a_p, const float *a_v, const float *dp, const float *dv,
-                       float *dh, float *dw1p, float *db1p, float *dw1v, float *db1v, float *dwp, float *dwv,
+                       const float *v_tanh, float *dh, float *dw1p, float *db1p, float *dw1v, float *db1v, float *dwp, float *dwv,
                        void *workspace, int64_t workspace_bytes, void *stream);
 
 /* The 3x3-board stem conv, Cin <= 3 -> 32 channels, with bias (TicTacToe, tictactoe.py:57), as fp32

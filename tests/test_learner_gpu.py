@@ -62,6 +62,9 @@ def test_learner_steps_golden(cuda, golden_learner):
         assert out['dcnt'].item() == ref['dcnt']
     for k, v in net.state_dict().items():
         np.testing.assert_allclose(v.cpu().numpy(), arrays['final.' + k], rtol=1e-5, atol=1e-6, err_msg=k)
+    # the rewritten forward ran the chain + heads as one Function with the value head's tanh in its kernels
+    gm = getattr(net, '_hrl_graph', None)
+    assert gm is not None and gm.get_submodule('_hrl_chain_heads').tanh_v
 
 
 def test_graph_step_equals_eager(cuda):
