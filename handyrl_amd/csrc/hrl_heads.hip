@@ -200,8 +200,8 @@ __device__ __forceinline__ float wave_sum(float v) {
 __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
                                                        const float *__restrict__ a_p, const float *__restrict__ a_v,
                                                        const float *__restrict__ dp, const float *__restrict__ dv,
-                                                       const float *__restrict__ vt, float *__restrict__ dh,
-                                                       float *__restrict__ part) {
+                                                       const float *__restrict__ vt, float *__restrict__ dv_raw,
+                                                       float *__restrict__ dh, float *__restrict__ part) {
     __shared__ float tile[64 * kTS];
     __shared__ float sw1[kM * kC], swp[kOP * kZP], swv[kHW], sal[kC], sbe[kC], smu[kC];
     __shared__ float gw1[kM * kC * 64];   // per-lane conv weight-gradient accumulators [m*32 + c][lane]
@@ -238,7 +238,10 @@ __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__
 #pragma unroll
         for (int k = 0; k < kOP; ++k) g[k] = valid ? dp[n * kOP + k] : 0.f;
         gv = valid ? dv[n] : 0.f;
-        if (vt) gv = gv * (1.f - vt[n] * vt[n]);   // tanh backward (grad * (1 - y*y), as torch's CPU kernel)
+        if (vt) {   // tanh backward (grad * (1 - y*y), as torch's CPU kernel), kept for fc_grad_kernel
+            gv = gv * (1.f - vt[n] * vt[n]);
+            if (valid) dv_raw[n] = gv;
+        }
         // the activation gradient (the fc weight gradients are dp^T a_p, dv^T a_v: host side)
         float dz[kZ];
 #pragma unroll
@@ -346,8 +349,7 @@ __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__
 // its row range (rows in order) into partial row b, columns kGWP.. (one thread per weight)
 __global__ __launch_bounds__(256) void fc_grad_kernel(const float *__restrict__ a_p, const float *__restrict__ a_v,
                                                       const float *__restrict__ dp, const float *__restrict__ dv,
-                                                      const float *__restrict__ vt, int64_t N,
-                                                      int64_t rows_per_block, float *__restrict__ part) {
+                                                      int64_t N, int64_t rows_per_block, float *__restrict__ part) {
     const int t = threadIdx.x;
     if (t >= kOP * kZP + kHW) return;
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
@@ -361,16 +363,13 @@ __global__ __launch_bounds__(256) void fc_grad_kernel(const float *__restrict__ 
         float x[8], y[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            x[u] = pol ? dp[(n + u) * kOP + k] : (vt ? dv[n + u] * (1.f - vt[n + u] * vt[n + u]) : dv[n + u]);
+            x[u] = pol ? dp[(n + u) * kOP + k] : dv[n + u];
             y[u] = pol ? a_p[(n + u) * kZP + j] : a_v[(n + u) * kHW + j];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc += x[u] * y[u];
     }
-    for (; n < r1; ++n) {
-        const float x = pol ? dp[n * kOP + k] : (vt ? dv[n] * (1.f - vt[n] * vt[n]) : dv[n]);
-        acc += x * (pol ? a_p[n * kZP + j] : a_v[n * kHW + j]);
-    }
+    for (; n < r1; ++n) acc += pol ? dp[n * kOP + k] * a_p[n * kZP + j] : dv[n] * a_v[n * kHW + j];
     part[(int64_t)blockIdx.x * kGN + kGWP + t] = acc;
 }
 
@@ -429,7 +428,8 @@ int grid_for(int64_t N, int cap = kGridBwd) {
 
 extern "C" {
 
-int64_t hrl_heads_workspace_bytes(int64_t N) { return N < 1 ? -1 : (int64_t)grid_for(N) * kGN * 4; }
+// workspace: the per-workgroup partials, then dv through the folded tanh's backward (N floats)
+int64_t hrl_heads_workspace_bytes(int64_t N) { return N < 1 ? -1 : ((int64_t)grid_for(N) * kGN + N) * 4; }
 
 int64_t hrl_heads_bn_parts(int64_t N) { return N < 1 ? -1 : grid_for(N); }
 
@@ -461,11 +461,13 @@ int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float 
     const BnIn bn{bn_alpha, bn_beta, bn_mean, bn_part};
     const int grid = grid_for(N);
     float *part = static_cast<float *>(workspace);
-    hipLaunchKernelGGL(heads_bwd_kernel, dim3(grid), dim3(64), 0, s, h, N, w, bn, a_p, a_v, dp, dv, v_tanh, dh, part);
+    float *dv_raw = part + (int64_t)grid * kGN;
+    hipLaunchKernelGGL(heads_bwd_kernel, dim3(grid), dim3(64), 0, s, h, N, w, bn, a_p, a_v, dp, dv, v_tanh, dv_raw, dh,
+                       part);
     int rc = status();
     if (rc) return rc;
     const int64_t rows = (N + grid - 1) / grid;
-    hipLaunchKernelGGL(fc_grad_kernel, dim3(grid), dim3(256), 0, s, a_p, a_v, dp, dv, v_tanh, N, rows, part);
+    hipLaunchKernelGGL(fc_grad_kernel, dim3(grid), dim3(256), 0, s, a_p, a_v, dp, v_tanh ? dv_raw : dv, N, rows, part);
     rc = status();
     if (rc) return rc;
     hipLaunchKernelGGL(heads_reduce_kernel, dim3(kGN), dim3(256), 0, s, part, grid, dw1p, dw1v, db1p, db1v, dwp,

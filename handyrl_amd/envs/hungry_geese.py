@@ -14,8 +14,9 @@ initial weights as the reference module would):
   tanh(Linear(64, 1)), both bias-free.  116,928 parameters.
 
 The rules live in kaggle_environments, which is not installed here, so this
-module has no batched rules; ``Environment`` gates on the import exactly as
-the reference module does (hungry_geese.py:18).  The learner trains GeeseNet
+module has no batched rules; ``Environment`` is the reference plugin's
+environment (with this net) where kaggle_environments and a HandyRL checkout
+are importable, and raises the reference module's ImportError otherwise.  The learner trains GeeseNet
 on make_batch-layout batches (solo training, turn_based_training=False:
 P = Pp = 1, train.py:57-58), see synthetic.geese_batch.
 
@@ -92,15 +93,26 @@ class GeeseNet(nn.Module):
 
 
 class Environment:
-    """The reference's rules wrap kaggle_environments (hungry_geese.py:18, :60-230): gated on that import."""
+    """Hungry Geese rules.  The reference's rules wrap kaggle_environments (hungry_geese.py:18, :60-230);
+    they are not restated here.  With kaggle_environments and a HandyRL checkout on ``sys.path``,
+    ``Environment(args)`` is the reference plugin's environment with ``net()`` returning this module's
+    GeeseNet (same modules and state_dict keys, HIP torus convs after ``nn.accelerate``); without them it
+    raises the ImportError the reference module would."""
 
-    def __init__(self, args=None):
+    def __new__(cls, args=None):
         try:
             import kaggle_environments  # noqa: F401
         except ImportError as e:
             raise ImportError('Hungry Geese rules need kaggle_environments, which is not installed; '
                               'GeeseNet trains on make_batch-layout batches without it') from e
-        raise NotImplementedError('Hungry Geese rules: use handyrl.envs.kaggle.hungry_geese (reference plugin)')
+        try:
+            from handyrl.envs.kaggle import hungry_geese as reference
+        except ImportError as e:
+            raise ImportError('Hungry Geese rules: the reference plugin handyrl.envs.kaggle.hungry_geese '
+                              '(a HandyRL checkout on sys.path) provides them') from e
+        env = reference.Environment(args or {})
+        env.net = cls.net.__get__(env)
+        return env
 
     def net(self):
         return GeeseNet

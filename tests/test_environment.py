@@ -62,6 +62,36 @@ def test_hungry_geese_rules_need_kaggle():
     assert Environment.net(None).__name__ == 'GeeseNet'
 
 
+def test_hungry_geese_delegates_to_reference_plugin(monkeypatch):
+    """With kaggle_environments and the reference plugin importable (stand-ins here), make_env returns the
+    plugin's environment, its net() this package's GeeseNet."""
+    import sys
+    import types
+    calls = []
+
+    class PluginEnv:
+        def __init__(self, args):
+            calls.append(args)
+
+        def net(self):
+            return None
+
+    plugin = types.ModuleType('handyrl.envs.kaggle.hungry_geese')
+    plugin.Environment = PluginEnv
+    pkgs = {name: types.ModuleType(name) for name in ('handyrl', 'handyrl.envs', 'handyrl.envs.kaggle')}
+    pkgs['handyrl'].envs = pkgs['handyrl.envs']
+    pkgs['handyrl.envs'].kaggle = pkgs['handyrl.envs.kaggle']
+    pkgs['handyrl.envs.kaggle'].hungry_geese = plugin
+    monkeypatch.setitem(sys.modules, 'kaggle_environments', types.ModuleType('kaggle_environments'))
+    for name, m in pkgs.items():
+        monkeypatch.setitem(sys.modules, name, m)
+    monkeypatch.setitem(sys.modules, 'handyrl.envs.kaggle.hungry_geese', plugin)
+    env = make_env({'env': 'HungryGeese', 'x': 1})
+    assert isinstance(env, PluginEnv) and calls == [{'env': 'HungryGeese', 'x': 1}]
+    from handyrl_amd.envs.hungry_geese import GeeseNet
+    assert env.net() is GeeseNet
+
+
 def test_geister_plugin_replays_reference_games(games):   # noqa: F811
     from handyrl_amd.envs.geister import Environment
     env = Environment()
