@@ -22,6 +22,8 @@
 // dx = ((dy - mean(dy)) - (x-mean)*k) * invstd * w with k = dot*invstd^2/M.
 
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <math.h>
 #include <stdint.h>
 
@@ -438,9 +440,12 @@ bool make_geo(int64_t N, int64_t C, int64_t HW, int VW, Geo &g) {
         g.kc = (g.ncol + kThreads - 1) / kThreads;
         if (g.kc > kMaxSlots) return false;
     }
-    // ~16K floats per workgroup, at most kMaxBlocks workgroups
+    // ~16K floats per workgroup, at most kMaxBlocks workgroups; small tensors (a recurrent learner's
+    // per-step BatchNorm, 256 x 1152 floats) get down to ~2K floats per workgroup instead of a handful of
+    // workgroups each walking its rows serially (18 workgroups: 20 us for a 1.2 MB reduce)
     const int64_t total = N * S;
     int64_t nb = (total + 16383) / 16384;
+    if (nb < 256) nb = std::min<int64_t>(256, (total + 2047) / 2048);
     nb = nb < 1 ? 1 : (nb > kMaxBlocks ? kMaxBlocks : nb);
     if (nb > N) nb = N;
     g.rows_per_block = (int)((N + nb - 1) / nb);
