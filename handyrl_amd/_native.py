@@ -45,6 +45,13 @@ SIGNATURES = {
     'hrl_bn_backward': (ctypes.c_int, [
         _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_int, _f32p, _f32p, _f32p,
         ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_bn_workspace_bytes_grouped': (ctypes.c_int64, [_i64, _i64, _i64, _i64]),
+    'hrl_bn_forward_train_grouped': (ctypes.c_int, [
+        _f32p, _i64, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, _dbl, _dbl, ctypes.c_int, _f32p, _f32p, _f32p,
+        ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_bn_backward_grouped': (ctypes.c_int, [
+        _f32p, _f32p, _i64, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_int, _f32p, _f32p, _f32p,
+        ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_loss_workspace_bytes': (ctypes.c_int64, [_i64, _i64, _i64, _i64]),
     'hrl_loss_forward': (ctypes.c_int, [
         _f32p, _f32p, ctypes.c_void_p, _i64, _i64, _i64, _i64, _i64,
@@ -139,7 +146,7 @@ SIGNATURES = {
                                                     _f32p, _f32p, _f32p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _lib = None
 

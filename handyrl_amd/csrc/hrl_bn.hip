@@ -45,7 +45,20 @@ struct Geo {
     int kc;            // column slots per thread (ncol > 256)
     int rows_per_block;
     int nblocks;
+    // groups (a recurrent net's time steps run as one launch): rows [g*Ng, (g+1)*Ng) are group g, whose
+    // statistics and coefficients are its own; nbg blocks per group, a block never straddles two
+    int64_t Ng;
+    int G, nbg;
 };
+
+// This block's rows [r0, r1) and group.
+__device__ __forceinline__ void block_rows(const Geo &g, int64_t &r0, int64_t &r1, int &grp) {
+    grp = (int)(blockIdx.x / (unsigned)g.nbg);
+    const int lb = (int)blockIdx.x - grp * g.nbg;
+    const int64_t gb = (int64_t)grp * g.Ng;
+    r0 = gb + (int64_t)lb * g.rows_per_block;
+    r1 = min(gb + g.Ng, r0 + g.rows_per_block);
+}
 
 template <int VW>
 struct VecT;
@@ -142,8 +155,9 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const float *__restr
 #pragma unroll
         for (int j = 0; j < VW; ++j) a[k][j] = b[k][j] = 0.0;
 
-    const int64_t r0 = (int64_t)blockIdx.x * g.rows_per_block;
-    const int64_t r1 = min(g.N, r0 + g.rows_per_block);
+    int64_t r0, r1;
+    int grp;
+    block_rows(g, r0, r1, grp);
     const int step = (g.ncol <= kThreads) ? g.rp : 1;
     for (int64_t r = r0 + ln.ro; r < r1; r += step) {
         const float *row = x + r * g.S;
@@ -167,53 +181,68 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const float *__restr
 // ---- fold the per-block partials of each channel (one workgroup per channel) ----
 // mode 0 (forward):  (sum x, sum x^2) -> mean, invstd, running stats, alpha/beta
 // mode 1 (backward): (sum dy, sum dy*(x-mean)) -> dweight, dbias, k, mean(dy)
+// With G groups the blocks [g*nbg, (g+1)*nbg) are group g: its statistics and coefficients land at
+// [g*C + c]; the groups are visited in order, so the running statistics advance exactly as G sequential
+// calls would, and dweight / dbias are the groups' sums.
 __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
     int mode, const double *__restrict__ part, int nblocks, int C, double M, const float *__restrict__ weight,
     const float *__restrict__ bias, float *running_mean, float *running_var, float momentum, double eps,
-    float *save_mean, float *save_invstd, float *coef_a, float *coef_b, float *dweight, float *dbias) {
+    float *save_mean, float *save_invstd, float *coef_a, float *coef_b, float *dweight, float *dbias, int G) {
     __shared__ double red[2][kThreads];
     const int c = blockIdx.x;
-    double s0 = 0.0, s1 = 0.0;
-    for (int i = threadIdx.x; i < nblocks; i += kThreads) {
-        s0 += part[((int64_t)i * C + c) * 2 + 0];
-        s1 += part[((int64_t)i * C + c) * 2 + 1];
-    }
-    red[0][threadIdx.x] = s0;
-    red[1][threadIdx.x] = s1;
-    __syncthreads();
-    for (int w = kThreads / 2; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) {
-            red[0][threadIdx.x] += red[0][threadIdx.x + w];
-            red[1][threadIdx.x] += red[1][threadIdx.x + w];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x != 0) return;
-    const double S0 = red[0][0], S1 = red[1][0];
+    const int nbg = nblocks / G;
     const float w = weight ? weight[c] : 1.0f;
-    if (mode == 0) {
-        const double mean = S0 / M;
-        double var = S1 / M - mean * mean;
-        if (var < 0.0) var = 0.0;
-        const float meanf = (float)mean;
-        const float invstd = (float)(1.0 / sqrt(var + eps));
-        save_mean[c] = meanf;
-        save_invstd[c] = invstd;
-        const float alpha = invstd * w;
-        coef_a[c] = alpha;
-        coef_b[c] = (bias ? bias[c] : 0.0f) - meanf * alpha;
-        if (running_mean) running_mean[c] = momentum * meanf + (1.0f - momentum) * running_mean[c];
-        if (running_var) {
-            const float unbiased = (float)(M > 1.0 ? var * M / (M - 1.0) : var);
-            running_var[c] = momentum * unbiased + (1.0f - momentum) * running_var[c];
+    float dw = 0.f, db = 0.f;
+    for (int grp = 0; grp < G; ++grp) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int i = threadIdx.x; i < nbg; i += kThreads) {
+            const int64_t b = (int64_t)grp * nbg + i;
+            s0 += part[(b * C + c) * 2 + 0];
+            s1 += part[(b * C + c) * 2 + 1];
         }
-    } else {
-        const float invstd = save_invstd[c];
-        const float sum_dy = (float)S0, dot = (float)S1;
-        if (dweight) dweight[c] = dot * invstd;
-        if (dbias) dbias[c] = sum_dy;
-        coef_a[c] = dot * invstd * invstd / (float)M;   // k
-        coef_b[c] = sum_dy / (float)M;                   // mean(dy)
+        red[0][threadIdx.x] = s0;
+        red[1][threadIdx.x] = s1;
+        __syncthreads();
+        for (int wd = kThreads / 2; wd > 0; wd >>= 1) {
+            if ((int)threadIdx.x < wd) {
+                red[0][threadIdx.x] += red[0][threadIdx.x + wd];
+                red[1][threadIdx.x] += red[1][threadIdx.x + wd];
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            const double S0 = red[0][0], S1 = red[1][0];
+            const int gc = grp * C + c;
+            if (mode == 0) {
+                const double mean = S0 / M;
+                double var = S1 / M - mean * mean;
+                if (var < 0.0) var = 0.0;
+                const float meanf = (float)mean;
+                const float invstd = (float)(1.0 / sqrt(var + eps));
+                save_mean[gc] = meanf;
+                save_invstd[gc] = invstd;
+                const float alpha = invstd * w;
+                coef_a[gc] = alpha;
+                coef_b[gc] = (bias ? bias[c] : 0.0f) - meanf * alpha;
+                if (running_mean) running_mean[c] = momentum * meanf + (1.0f - momentum) * running_mean[c];
+                if (running_var) {
+                    const float unbiased = (float)(M > 1.0 ? var * M / (M - 1.0) : var);
+                    running_var[c] = momentum * unbiased + (1.0f - momentum) * running_var[c];
+                }
+            } else {
+                const float invstd = save_invstd[gc];
+                const float sum_dy = (float)S0, dot = (float)S1;
+                dw = grp == 0 ? dot * invstd : dw + dot * invstd;
+                db = grp == 0 ? sum_dy : db + sum_dy;
+                coef_a[gc] = dot * invstd * invstd / (float)M;   // k
+                coef_b[gc] = sum_dy / (float)M;                   // mean(dy)
+            }
+        }
+        __syncthreads();   // red is reused by the next group
+    }
+    if (mode == 1 && threadIdx.x == 0) {
+        if (dweight) dweight[c] = dw;
+        if (dbias) dbias[c] = db;
     }
 }
 
@@ -239,6 +268,11 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float *__restr
                                                             const float *__restrict__ beta, float *__restrict__ y) {
     Lane ln;
     ln.init(g);
+    int64_t r0, r1;
+    int grp;
+    block_rows(g, r0, r1, grp);
+    alpha += grp * g.C;   // this block's group's coefficients
+    beta += grp * g.C;
     float al[kMaxSlots][VW], be[kMaxSlots][VW];
 #pragma unroll
     for (int k = 0; k < kMaxSlots; ++k)
@@ -248,8 +282,6 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const float *__restr
             al[k][j] = alpha[ch];
             be[k][j] = beta[ch];
         }
-    const int64_t r0 = (int64_t)blockIdx.x * g.rows_per_block;
-    const int64_t r1 = min(g.N, r0 + g.rows_per_block);
     const int step = (g.ncol <= kThreads) ? g.rp : 1;
     for (int64_t r = r0 + ln.ro; r < r1; r += step) {
 #pragma unroll
@@ -278,6 +310,11 @@ __global__ __launch_bounds__(kThreads) void bn_res_apply_kernel(const float *__r
                                                                 float *__restrict__ y) {
     Lane ln;
     ln.init(g);
+    int64_t r0, r1;
+    int grp;
+    block_rows(g, r0, r1, grp);
+    alpha += grp * g.C;
+    beta += grp * g.C;
     float al[kMaxSlots][VW], be[kMaxSlots][VW];
 #pragma unroll
     for (int k = 0; k < kMaxSlots; ++k)
@@ -287,8 +324,6 @@ __global__ __launch_bounds__(kThreads) void bn_res_apply_kernel(const float *__r
             al[k][j] = alpha[ch];
             be[k][j] = beta[ch];
         }
-    const int64_t r0 = (int64_t)blockIdx.x * g.rows_per_block;
-    const int64_t r1 = min(g.N, r0 + g.rows_per_block);
     const int step = (g.ncol <= kThreads) ? g.rp : 1;
     for (int64_t r = r0 + ln.ro; r < r1; r += step) {
 #pragma unroll
@@ -324,6 +359,11 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const float *__
     extern __shared__ double sh[];
     Lane ln;
     ln.init(g);
+    int64_t r0, r1;
+    int grp;
+    block_rows(g, r0, r1, grp);
+    mean += grp * g.C;     // this block's group's statistics
+    invstd += grp * g.C;
     float mu[kMaxSlots][VW], al[kMaxSlots][VW], be[kMaxSlots][VW];
     double a[kMaxSlots][VW], b[kMaxSlots][VW];
 #pragma unroll
@@ -337,8 +377,6 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const float *__
             al[k][j] = RELU ? invstd[ch] * (weight ? weight[ch] : 1.0f) : 0.f;
             be[k][j] = RELU ? (bias ? bias[ch] : 0.0f) - mean[ch] * al[k][j] : 0.f;
         }
-    const int64_t r0 = (int64_t)blockIdx.x * g.rows_per_block;
-    const int64_t r1 = min(g.N, r0 + g.rows_per_block);
     const int step = (g.ncol <= kThreads) ? g.rp : 1;
     for (int64_t r = r0 + ln.ro; r < r1; r += step) {
 #pragma unroll
@@ -380,6 +418,13 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float *__r
                                                                 const float *__restrict__ mo) {
     Lane ln;
     ln.init(g);
+    int64_t r0, r1;
+    int grp;
+    block_rows(g, r0, r1, grp);
+    mean += grp * g.C;     // this block's group's statistics and backward coefficients
+    invstd += grp * g.C;
+    kcoef += grp * g.C;
+    gmean += grp * g.C;
     float mu[kMaxSlots][VW], kk[kMaxSlots][VW], gm[kMaxSlots][VW], is[kMaxSlots][VW], ww[kMaxSlots][VW];
     float al[kMaxSlots][VW], be[kMaxSlots][VW];
 #pragma unroll
@@ -395,8 +440,6 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float *__r
             al[k][j] = RELU ? is[k][j] * ww[k][j] : 0.f;
             be[k][j] = RELU ? (bias ? bias[ch] : 0.0f) - mu[k][j] * al[k][j] : 0.f;
         }
-    const int64_t r0 = (int64_t)blockIdx.x * g.rows_per_block;
-    const int64_t r1 = min(g.N, r0 + g.rows_per_block);
     const int step = (g.ncol <= kThreads) ? g.rp : 1;
     for (int64_t r = r0 + ln.ro; r < r1; r += step) {
 #pragma unroll
@@ -426,8 +469,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const float *__r
 
 // ---------------------------------------------------------------- host side
 
-bool make_geo(int64_t N, int64_t C, int64_t HW, int VW, Geo &g) {
-    if (N < 1 || C < 1 || HW < 1) return false;
+bool make_geo(int64_t N, int64_t C, int64_t HW, int VW, Geo &g, int64_t G = 1) {
+    if (N < 1 || C < 1 || HW < 1 || G < 1 || N % G != 0 || G > kMaxBlocks) return false;
     const int64_t S = C * HW;
     if (S > kMaxRowFloats || S % VW != 0) return false;
     g.N = N; g.C = (int)C; g.HW = (int)HW; g.S = (int)S;
@@ -447,16 +490,24 @@ bool make_geo(int64_t N, int64_t C, int64_t HW, int VW, Geo &g) {
     int64_t nb = (total + 16383) / 16384;
     if (nb < 256) nb = std::min<int64_t>(256, (total + 2047) / 2048);
     nb = nb < 1 ? 1 : (nb > kMaxBlocks ? kMaxBlocks : nb);
-    if (nb > N) nb = N;
-    g.rows_per_block = (int)((N + nb - 1) / nb);
-    g.nblocks = (int)((N + g.rows_per_block - 1) / g.rows_per_block);
+    // per group: a share of the blocks, whole rows, never straddling groups
+    const int64_t Ng = N / G;
+    int64_t nbg = (nb + G - 1) / G;
+    if (nbg > Ng) nbg = Ng;
+    if (nbg * G > kMaxBlocks) nbg = kMaxBlocks / G;
+    if (nbg < 1) nbg = 1;
+    g.rows_per_block = (int)((Ng + nbg - 1) / nbg);
+    g.nbg = (int)((Ng + g.rows_per_block - 1) / g.rows_per_block);
+    g.Ng = Ng;
+    g.G = (int)G;
+    g.nblocks = g.nbg * g.G;
     return true;
 }
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// workspace layout: part[nblocks][C][2] doubles | coef_a[C] | coef_b[C] floats
-int64_t ws_bytes(const Geo &g) { return (int64_t)g.nblocks * g.C * 16 + 2 * (int64_t)g.C * 4 + 64; }
+// workspace layout: part[nblocks][C][2] doubles | coef_a[G*C] | coef_b[G*C] floats
+int64_t ws_bytes(const Geo &g) { return (int64_t)g.nblocks * g.C * 16 + 2 * (int64_t)g.G * g.C * 4 + 64; }
 
 int launch_status() {
     const hipError_t err = hipGetLastError();
@@ -498,32 +549,46 @@ int64_t hrl_bn_workspace_bytes(int64_t N, int64_t C, int64_t HW) {
     return -1;
 }
 
-int hrl_bn_forward_train(const float *x, int64_t N, int64_t C, int64_t HW, const float *weight, const float *bias,
-                         float *running_mean, float *running_var, double momentum, double eps, int relu, float *y,
-                         float *save_mean, float *save_invstd, void *workspace, int64_t workspace_bytes,
-                         void *stream) {
+int64_t hrl_bn_workspace_bytes_grouped(int64_t N, int64_t C, int64_t HW, int64_t G) {
+    Geo g;
+    if (make_geo(N, C, HW, 4, g, G) || make_geo(N, C, HW, 1, g, G)) return ws_bytes(g);
+    return -1;
+}
+
+int hrl_bn_forward_train_grouped(const float *x, int64_t N, int64_t C, int64_t HW, int64_t G, const float *weight,
+                                 const float *bias, float *running_mean, float *running_var, double momentum,
+                                 double eps, int relu, float *y, float *save_mean, float *save_invstd,
+                                 void *workspace, int64_t workspace_bytes, void *stream) {
     if (!x || !y || !save_mean || !save_invstd || !workspace) return HRL_EINVAL;
     const bool vec = (C * HW) % 4 == 0 && aligned16(x) && aligned16(y);
     Geo g;
-    if (!make_geo(N, C, HW, vec ? 4 : 1, g)) return HRL_EINVAL;
+    if (!make_geo(N, C, HW, vec ? 4 : 1, g, G)) return HRL_EINVAL;
     if (workspace_bytes < ws_bytes(g)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     double *part = static_cast<double *>(workspace);
     float *coef_a = reinterpret_cast<float *>(part + (int64_t)g.nblocks * g.C * 2);
-    float *coef_b = coef_a + g.C;
+    float *coef_b = coef_a + g.G * g.C;
     const size_t lds = sizeof(double) * 2 * g.S;
     if (vec) hipLaunchKernelGGL(bn_stats_kernel<4>, dim3(g.nblocks), dim3(kThreads), lds, s, x, g, part);
     else hipLaunchKernelGGL(bn_stats_kernel<1>, dim3(g.nblocks), dim3(kThreads), lds, s, x, g, part);
     int rc = launch_status();
     if (rc) return rc;
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(g.C), dim3(kThreads), 0, s, 0, part, g.nblocks, g.C,
-                       (double)N * (double)HW, weight, bias, running_mean, running_var, (float)momentum, eps,
-                       save_mean, save_invstd, coef_a, coef_b, (float *)nullptr, (float *)nullptr);
+                       (double)g.Ng * (double)HW, weight, bias, running_mean, running_var, (float)momentum, eps,
+                       save_mean, save_invstd, coef_a, coef_b, (float *)nullptr, (float *)nullptr, g.G);
     rc = launch_status();
     if (rc) return rc;
     if (vec) relu ? launch_apply<4, true>(g, s, x, coef_a, coef_b, y) : launch_apply<4, false>(g, s, x, coef_a, coef_b, y);
     else relu ? launch_apply<1, true>(g, s, x, coef_a, coef_b, y) : launch_apply<1, false>(g, s, x, coef_a, coef_b, y);
     return launch_status();
+}
+
+int hrl_bn_forward_train(const float *x, int64_t N, int64_t C, int64_t HW, const float *weight, const float *bias,
+                         float *running_mean, float *running_var, double momentum, double eps, int relu, float *y,
+                         float *save_mean, float *save_invstd, void *workspace, int64_t workspace_bytes,
+                         void *stream) {
+    return hrl_bn_forward_train_grouped(x, N, C, HW, 1, weight, bias, running_mean, running_var, momentum, eps, relu,
+                                        y, save_mean, save_invstd, workspace, workspace_bytes, stream);
 }
 
 int hrl_bn_finalize_stats(const double *part, int64_t nparts, int64_t C, int64_t count, const float *weight,
@@ -533,7 +598,8 @@ int hrl_bn_finalize_stats(const double *part, int64_t nparts, int64_t C, int64_t
         return HRL_EINVAL;
     hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)C), dim3(kThreads), 0, static_cast<hipStream_t>(stream), 0,
                        part, (int)nparts, (int)C, (double)count, weight, bias, running_mean, running_var,
-                       (float)momentum, eps, save_mean, save_invstd, alpha, beta, (float *)nullptr, (float *)nullptr);
+                       (float)momentum, eps, save_mean, save_invstd, alpha, beta, (float *)nullptr, (float *)nullptr,
+                       1);
     return launch_status();
 }
 
@@ -569,7 +635,7 @@ int hrl_bn_finalize_backward(const double *part, int64_t nparts, int64_t C, int6
     hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)C), dim3(kThreads), 0, static_cast<hipStream_t>(stream), 1,
                        part, (int)nparts, (int)C, (double)count, weight, (const float *)nullptr, (float *)nullptr,
                        (float *)nullptr, 0.f, 0.0, (float *)nullptr, const_cast<float *>(save_invstd), kcoef, gmean,
-                       dweight, dbias);
+                       dweight, dbias, 1);
     return launch_status();
 }
 
@@ -591,18 +657,19 @@ int hrl_bn_backward_apply(const float *x, const float *dy, int64_t N, int64_t C,
     return launch_status();
 }
 
-int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW, const float *weight,
-                    const float *bias, const float *save_mean, const float *save_invstd, int relu, float *dx,
-                    float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream) {
+int hrl_bn_backward_grouped(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW, int64_t G,
+                            const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
+                            int relu, float *dx, float *dweight, float *dbias, void *workspace,
+                            int64_t workspace_bytes, void *stream) {
     if (!x || !dy || !dx || !save_mean || !save_invstd || !workspace || dx == dy) return HRL_EINVAL;
     const bool vec = (C * HW) % 4 == 0 && aligned16(x) && aligned16(dy) && aligned16(dx);
     Geo g;
-    if (!make_geo(N, C, HW, vec ? 4 : 1, g)) return HRL_EINVAL;
+    if (!make_geo(N, C, HW, vec ? 4 : 1, g, G)) return HRL_EINVAL;
     if (workspace_bytes < ws_bytes(g)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     double *part = static_cast<double *>(workspace);
     float *kcoef = reinterpret_cast<float *>(part + (int64_t)g.nblocks * g.C * 2);
-    float *gmean = kcoef + g.C;
+    float *gmean = kcoef + g.G * g.C;
     const size_t lds = sizeof(double) * 2 * g.S;
     if (vec) relu ? launch_bwd<4, true>(g, s, lds, x, dy, save_mean, save_invstd, weight, bias, part)
                   : launch_bwd<4, false>(g, s, lds, x, dy, save_mean, save_invstd, weight, bias, part);
@@ -611,8 +678,9 @@ int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64
     int rc = launch_status();
     if (rc) return rc;
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(g.C), dim3(kThreads), 0, s, 1, part, g.nblocks, g.C,
-                       (double)N * (double)HW, weight, (const float *)nullptr, (float *)nullptr, (float *)nullptr,
-                       0.0f, 0.0, (float *)nullptr, const_cast<float *>(save_invstd), kcoef, gmean, dweight, dbias);
+                       (double)g.Ng * (double)HW, weight, (const float *)nullptr, (float *)nullptr, (float *)nullptr,
+                       0.0f, 0.0, (float *)nullptr, const_cast<float *>(save_invstd), kcoef, gmean, dweight, dbias,
+                       g.G);
     rc = launch_status();
     if (rc) return rc;
     if (vec) relu ? launch_bwd_apply<4, true>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx)
@@ -620,6 +688,13 @@ int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64
     else relu ? launch_bwd_apply<1, true>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx)
               : launch_bwd_apply<1, false>(g, s, x, dy, save_mean, save_invstd, weight, kcoef, gmean, bias, dx);
     return launch_status();
+}
+
+int hrl_bn_backward(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW, const float *weight,
+                    const float *bias, const float *save_mean, const float *save_invstd, int relu, float *dx,
+                    float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream) {
+    return hrl_bn_backward_grouped(x, dy, N, C, HW, 1, weight, bias, save_mean, save_invstd, relu, dx, dweight, dbias,
+                                   workspace, workspace_bytes, stream);
 }
 
 int hrl_bn_apply_residual(const float *x, const float *res, int64_t N, int64_t C, int64_t HW, const float *alpha,
@@ -675,7 +750,8 @@ int hrl_bn_backward_masked(const float *x, const float *dy, const float *out, in
     if (rc) return rc;
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(g.C), dim3(kThreads), 0, s, 1, part, g.nblocks, g.C,
                        (double)N * (double)HW, weight, (const float *)nullptr, (float *)nullptr, (float *)nullptr,
-                       0.0f, 0.0, (float *)nullptr, const_cast<float *>(save_invstd), kcoef, gmean, dweight, dbias);
+                       0.0f, 0.0, (float *)nullptr, const_cast<float *>(save_invstd), kcoef, gmean, dweight, dbias,
+                       1);
     rc = launch_status();
     if (rc) return rc;
     if (vec) hipLaunchKernelGGL((bn_bwd_apply_kernel<4, false, 2>), grid, block, 0, s, x, dy, g, save_mean, save_invstd,

@@ -97,14 +97,18 @@ class DRC(nn.Module):
         kernel adds the two (nn.lstm_gates).  A third fewer cell FLOPs, no
         concatenation, one gate launch per cell and direction.
         """
+        return self.step_hip(self.x_halves(x), hs, cs, num_repeats)
+
+    def x_halves(self, x):
+        """conv_x(x) + bias of every cell (the part of conv([x, h]) that does not depend on the state); x may
+        hold the encoder outputs of every time step of an unroll at once (GeisterNet.sequence_begin)."""
         from .. import nn as hnn
-        from ..nn import lstm_gates, conv2d
+        from ..nn import conv2d
         cin = x.shape[-3]
         ws = [blk.conv.weight for blk in self.blocks]
         bias = [blk.conv.bias for blk in self.blocks]
         pad = self.blocks[0].conv.padding
         n = len(self.blocks)
-        c_all = ws[0].shape[1]
         deferred = hnn._DEFER is not None   # LearnerStep batches the weight gradients over the unroll
 
         def x_half(layers):
@@ -117,9 +121,18 @@ class DRC(nn.Module):
             # Only the last layer reaches the output (every cell reads x and its own state), so the
             # others must stay outside its autograd graph: their weights then get no gradient at
             # all, as with the reference's cells, and the optimizer leaves them alone.
-            zx = x_half(list(range(n - 1))) + x_half([n - 1])
-        else:
-            zx = x_half(list(range(n)))
+            return list(x_half(list(range(n - 1))) + x_half([n - 1]))
+        return list(x_half(list(range(n))))
+
+    def step_hip(self, zx, hs, cs, num_repeats):
+        """One time step of the cells given their x halves zx (DRC.forward's repeats and layers)."""
+        from .. import nn as hnn
+        from ..nn import lstm_gates, conv2d
+        ws = [blk.conv.weight for blk in self.blocks]
+        pad = self.blocks[0].conv.padding
+        c_all = ws[0].shape[1]
+        cin = c_all - self.blocks[0].hidden_dim
+        deferred = hnn._DEFER is not None
         w_h = None if deferred else [w[:, cin:].contiguous() for w in ws]
         for _ in range(num_repeats):
             for i in range(len(self.blocks)):
@@ -186,6 +199,55 @@ class GeisterNet(nn.Module):
         policy = torch.cat([self.head_p_move(h), self.head_p_set(scalar[:, :1])], dim=-1)
         return {'policy': policy, 'value': torch.tanh(self.head_v(h)), 'return': self.head_r(h),
                 'hidden': hidden}
+
+    # ---- the learner's unroll in three parts (train._unroll_sequence) ----
+    # forward_prediction runs the net once per time step (train.py:155-174).  Only the cells depend on
+    # the state, so on the HIP path the stem, the cells' x halves and the heads run once over all T
+    # steps (rows time-major, T*N), with every BatchNorm normalising each step's rows with that step's
+    # own statistics and advancing its running statistics once per step, in order
+    # (nn.batch_norm_train(groups=T)): the same results as T calls of forward, in far fewer launches.
+
+    def _sequence_bns(self):
+        return (self.bn1, self.head_p_move.bn, self.head_v.bn, self.head_r.bn)
+
+    def sequence_ok(self, x):
+        from .. import nn as hnn
+        return (self.training and self.body.use_hip and torch.is_grad_enabled() and x['board'].is_cuda
+                and x['board'].dtype == torch.float32
+                and all(isinstance(b, hnn.BatchNorm2d) and b.momentum is not None and b.track_running_stats
+                        and b.affine for b in self._sequence_bns()))
+
+    @staticmethod
+    def _bn_steps(bn, y, T):
+        """relu(bn(y)) for T time steps' rows (time-major) with per-step statistics."""
+        from ..nn import batch_norm_train
+        bn.num_batches_tracked.add_(T)
+        return batch_norm_train(y, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
+                                relu=True, groups=T)
+
+    def sequence_begin(self, x, T):
+        """Stem and the cells' x halves for all T steps; x: observations with rows (t, n)."""
+        board, scalar = x['board'], x['scalar']
+        planes = scalar[..., None, None].expand(*scalar.shape, *BOARD)
+        h_e = self._bn_steps(self.bn1, self.conv1(torch.cat([planes, board], dim=-3)), T)
+        return {'T': T, 'N': board.shape[0] // T, 'h_e': h_e, 'zx': self.body.x_halves(h_e), 'scalar': scalar}
+
+    def sequence_step(self, seq, t, hidden):
+        """The cells at step t from the unroll's hidden state: (h_last, hidden)."""
+        n0, n1 = t * seq['N'], (t + 1) * seq['N']
+        hs, cs = list(hidden[0]), list(hidden[1])
+        return self.body.step_hip([z[n0:n1] for z in seq['zx']], hs, cs, self.num_repeats)
+
+    def sequence_end(self, seq, h_lasts):
+        """The heads over all T steps: {'policy', 'value', 'return'} with rows (t, n)."""
+        T, scalar = seq['T'], seq['scalar']
+        h = torch.cat([seq['h_e'], torch.cat(h_lasts)], dim=-3)
+        hp, hv, hr = self.head_p_move, self.head_v, self.head_r
+        p_move = hp.conv2(self._bn_steps(hp.bn, hp.conv1(h), T)).reshape(-1, hp.outputs)
+        policy = torch.cat([p_move, self.head_p_set(scalar[:, :1])], dim=-1)
+        v = hv.fc(self._bn_steps(hv.bn, hv.conv(h), T).reshape(-1, hv.hidden_units))
+        r = hr.fc(self._bn_steps(hr.bn, hr.conv(h), T).reshape(-1, hr.hidden_units))
+        return {'policy': policy, 'value': torch.tanh(v), 'return': r}
 
 
 class GeisterBatch:

@@ -201,27 +201,28 @@ def conv2d(x, w, b=None, padding=(0, 0), in_slice=None):
 
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu=False):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu=False, groups=1):
         N, C = x.shape[0], x.shape[1]
         HW = x[0, 0].numel()
         x = x.contiguous()
         lib = _native.load()
-        ws_bytes = lib.hrl_bn_workspace_bytes(N, C, HW)
+        ws_bytes = lib.hrl_bn_workspace_bytes_grouped(N, C, HW, groups)
         if ws_bytes < 0:
-            raise ValueError('hrl_bn: unsupported shape %s' % (tuple(x.shape),))
+            raise ValueError('hrl_bn: unsupported shape %s (groups %d)' % (tuple(x.shape), groups))
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
         y = torch.empty_like(x)
-        mean = torch.empty(C, dtype=torch.float32, device=x.device)
-        invstd = torch.empty(C, dtype=torch.float32, device=x.device)
-        code = lib.hrl_bn_forward_train(
-            _native.ptr(x), N, C, HW, _native.ptr(weight), _native.ptr(bias),
+        mean = torch.empty(groups, C, dtype=torch.float32, device=x.device)
+        invstd = torch.empty(groups, C, dtype=torch.float32, device=x.device)
+        code = lib.hrl_bn_forward_train_grouped(
+            _native.ptr(x), N, C, HW, groups, _native.ptr(weight), _native.ptr(bias),
             _native.ptr(running_mean), _native.ptr(running_var), float(momentum), float(eps), int(relu),
             _native.ptr(y), _native.ptr(mean), _native.ptr(invstd), _native.ptr(ws), ws_bytes,
             _native.stream_of(x.device))
-        _native.check(code, 'hrl_bn_forward_train')
+        _native.check(code, 'hrl_bn_forward_train_grouped')
         ctx.save_for_backward(x, weight, bias, mean, invstd)
         ctx.has_bias = bias is not None
         ctx.relu = bool(relu)
+        ctx.groups = groups
         ctx.defer = _DEFER if (weight is not None and weight.requires_grad) else None
         return y
 
@@ -232,25 +233,28 @@ class _BatchNormTrain(torch.autograd.Function):
         HW = x[0, 0].numel()
         dy = dy.contiguous()
         lib = _native.load()
-        ws_bytes = lib.hrl_bn_workspace_bytes(N, C, HW)
+        ws_bytes = lib.hrl_bn_workspace_bytes_grouped(N, C, HW, ctx.groups)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
         dx = torch.empty_like(x)
         dw = torch.empty(C, dtype=torch.float32, device=x.device) if weight is not None else None
         db = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_bias else None
-        code = lib.hrl_bn_backward(
-            _native.ptr(x), _native.ptr(dy), N, C, HW, _native.ptr(weight), _native.ptr(bias), _native.ptr(mean),
-            _native.ptr(invstd), int(ctx.relu), _native.ptr(dx), _native.ptr(dw), _native.ptr(db),
+        code = lib.hrl_bn_backward_grouped(
+            _native.ptr(x), _native.ptr(dy), N, C, HW, ctx.groups, _native.ptr(weight), _native.ptr(bias),
+            _native.ptr(mean), _native.ptr(invstd), int(ctx.relu), _native.ptr(dx), _native.ptr(dw), _native.ptr(db),
             _native.ptr(ws), ws_bytes, _native.stream_of(x.device))
-        _native.check(code, 'hrl_bn_backward')
+        _native.check(code, 'hrl_bn_backward_grouped')
         if ctx.defer is not None and (dw is not None or db is not None):
             ctx.defer.add_affine((weight, bias if ctx.has_bias else None), dw, db)
-            return dx, None, None, None, None, None, None, None
-        return dx, dw, db, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
-def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps, relu=False):
-    """F.batch_norm(..., training=True) [+ ReLU] on the HIP kernels (x: (N, C, *spatial) fp32 CUDA)."""
-    return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu)
+def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps, relu=False, groups=1):
+    """F.batch_norm(..., training=True) [+ ReLU] on the HIP kernels (x: (N, C, *spatial) fp32 CUDA).
+    ``groups`` > 1: rows [g*N/groups, (g+1)*N/groups) are normalised with statistics of their own, and the
+    running statistics advance once per group in order -- ``groups`` sequential calls in one launch each
+    way (a recurrent net's per-time-step BatchNorm over its whole unroll)."""
+    return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu, groups)
 
 
 def batch_norm_eval(x, weight, bias, running_mean, running_var, eps, relu=False):

@@ -163,6 +163,7 @@ def _rebuild(template, it):
 
 
 FLAT_HIDDEN = True   # recurrent state plumbing through csrc/hrl_hidden.hip on the GPU (False: torch ops)
+SEQUENCE_UNROLL = True   # nets with sequence_begin/step/end run their state-free parts once over all T
 
 
 def _flat_hidden_ok(hidden, tmask):
@@ -190,6 +191,25 @@ def _unroll_flat_hidden(model, hidden, batch, args):
     n = len(leaves)
     masks = batch['observation_mask'].reshape(B, T, P).transpose(0, 1).contiguous()   # (T, B, P)
     summed = args['turn_based_training'] and not args['observation']
+    seq_ok = getattr(model, 'sequence_ok', None)
+    if SEQUENCE_UNROLL and seq_ok is not None and seq_ok(map_r(observations, lambda o: o[:, 0])):
+        # the net runs its state-free parts once over all T steps (e.g. GeisterNet.sequence_begin/end):
+        # observations time-major, (T*N, ...) with N = B*P' in the per-step order
+        obs = map_r(observations, lambda o: o.transpose(0, 1).reshape(-1, *o.shape[3:]))
+        seq = model.sequence_begin(obs, T)
+        h_lasts = []
+        for t in range(T):
+            m = masks[t]
+            h_in = _rebuild(hidden, iter(_HiddenGather.apply(m, summed, B, P, *leaves)))
+            h_last, next_hidden = model.sequence_step(seq, t, h_in)
+            h_lasts.append(h_last)
+            nh = _leaves(next_hidden)
+            Pn = nh[0].shape[0] // B
+            leaves = list(_HiddenUpdate.apply(m, B, P, Pn, n, *leaves, *nh))
+        out = model.sequence_end(seq, h_lasts)
+        # (T*N, ...) -> (N, T, ...), the per-step loop's torch.stack(dim=1) layout
+        return {k: o.view(T, -1, *o.shape[1:]).transpose(0, 1).contiguous() for k, o in out.items()
+                if o is not None}
     per_t = {}
     for t in range(T):
         obs = map_r(observations, lambda o: o[:, t].reshape(-1, *o.shape[3:]))

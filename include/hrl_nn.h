@@ -73,6 +73,20 @@ int hrl_bn_forward_eval(const float *x, int64_t N, int64_t C, int64_t HW, const 
  * dbias and the apply coefficients kcoef, gmean (C floats each); then
  * dx = ((g - gmean) - (x - mean)*kcoef) * invstd * weight, g masked by the
  * recomputed ReLU when relu != 0 (hrl_bn_backward = reduce + these two). */
+/* Grouped BatchNorm: rows [g*N/G, (g+1)*N/G) are group g (N % G == 0), with statistics of its own --
+ * a recurrent net's per-time-step BatchNorm run over all T steps in one launch (rows time-major).
+ * save_mean / save_invstd are (G, C); the running statistics advance once per group, in group order,
+ * as G sequential hrl_bn_forward_train calls would; dweight / dbias are the groups' sums.
+ * workspace: hrl_bn_workspace_bytes_grouped(N, C, HW, G). */
+int64_t hrl_bn_workspace_bytes_grouped(int64_t N, int64_t C, int64_t HW, int64_t G);
+int hrl_bn_forward_train_grouped(const float *x, int64_t N, int64_t C, int64_t HW, int64_t G, const float *weight,
+                                 const float *bias, float *running_mean, float *running_var, double momentum,
+                                 double eps, int relu, float *y, float *save_mean, float *save_invstd,
+                                 void *workspace, int64_t workspace_bytes, void *stream);
+int hrl_bn_backward_grouped(const float *x, const float *dy, int64_t N, int64_t C, int64_t HW, int64_t G,
+                            const float *weight, const float *bias, const float *save_mean, const float *save_invstd,
+                            int relu, float *dx, float *dweight, float *dbias, void *workspace,
+                            int64_t workspace_bytes, void *stream);
 int hrl_bn_finalize_backward(const double *part, int64_t nparts, int64_t C, int64_t count, const float *weight,
                              const float *save_invstd, float *dweight, float *dbias, float *kcoef, float *gmean,
                              void *stream);

@@ -237,3 +237,46 @@ def test_gpu_recurrent_learner_matches_cpu_oracle(cuda, graph):
             assert torch.equal(got[n].detach().cpu(), init[n]), n
         else:
             torch.testing.assert_close(got[n].detach().cpu(), p.detach(), rtol=1e-4, atol=2e-6, msg=n)
+
+
+@pytest.mark.gpu
+def test_sequence_unroll_matches_per_step_unroll(cuda):
+    """GeisterNet's three-part unroll (stem, x halves and heads once over all T steps, per-step BatchNorm
+    statistics through nn.batch_norm_train(groups=T)) vs the per-step forward loop: outputs, every
+    gradient, and the BatchNorm running statistics and batch counters."""
+    from handyrl_amd import train as tr
+    from handyrl_amd.nn import accelerate
+    from handyrl_amd.synthetic import geister_batch, default_args
+    B, T = 16, 6
+    args = default_args(T, B)
+    batch = geister_batch(B, T, cuda, seed=5)
+    res = []
+    for seq in (False, True):
+        net = accelerate(seeded_net().to(cuda))
+        net.train()
+        hidden = tuple([h.to(cuda) for h in hs] for hs in net.init_hidden([B, 2]))
+        prev = tr.SEQUENCE_UNROLL
+        tr.SEQUENCE_UNROLL = seq
+        try:
+            out = tr.forward_prediction(net, hidden, batch, args)
+        finally:
+            tr.SEQUENCE_UNROLL = prev
+        if not res:
+            gen = torch.Generator(device=cuda).manual_seed(1)
+            wts = {k: torch.randn(o.shape, device=cuda, generator=gen) for k, o in out.items()}
+        # linear in the outputs: the masked policy holds -1e32 entries (action_mask), a square would overflow
+        loss = sum((out[k] * wts[k]).sum() for k in out)
+        loss.backward()
+        res.append((out, {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None},
+                    {n: b.clone() for n, b in net.named_buffers()}))
+    (o0, g0, b0), (o1, g1, b1) = res
+    for k in o0:
+        torch.testing.assert_close(o1[k], o0[k], rtol=1e-5, atol=1e-5, msg=k)
+    assert set(g0) == set(g1)
+    errs = {n: float((g1[n] - g).norm() / g.norm().clamp(min=1e-12)) for n, g in g0.items()}
+    assert max(errs.values()) < 1e-5, sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    for n, b in b0.items():
+        if n.endswith('num_batches_tracked'):
+            assert int(b1[n]) == int(b) == T, n
+        else:
+            torch.testing.assert_close(b1[n], b, rtol=1e-5, atol=1e-6, msg=n)
