@@ -159,7 +159,47 @@ __device__ __forceinline__ void policy_row(const float *zt, const float *zb, int
 }
 
 // action counts with a register-resident specialisation of the fused loss (TicTacToe 9, Hungry Geese 4);
-// any other A runs the loop form
+// any other A runs the wave form below
+
+// fixed xor butterflies over the 64 lanes: every lane ends with the same, order-fixed result
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// One policy row with the wave's lanes over its actions (A = 214 for Geister): coalesced loads and
+// fixed-order butterfly reductions instead of one lane walking the row.  The same quantities as
+// policy_row; the sums run in another (fixed) order.
+__device__ __forceinline__ void policy_row_wave(const float *zt, const float *zb, int A, int act, float em, int lane,
+                                                float &lt, float &crho, float &ent) {
+    float mt = -INFINITY, mb = -INFINITY;
+    for (int q = lane; q < A; q += 64) {
+        mt = fmaxf(mt, zt[q]);
+        mb = fmaxf(mb, zb[q]);
+    }
+    mt = wave_max(mt);
+    mb = wave_max(mb);
+    float st = 0.f, sb = 0.f;
+    for (int q = lane; q < A; q += 64) {
+        st += expf(zt[q] - mt);
+        sb += expf(zb[q] - mb);
+    }
+    st = wave_sum(st);
+    sb = wave_sum(sb);
+    lt = ((zt[act] - mt) - logf(st)) * em;                                  // train.py:224-225
+    const float lb = ((zb[act] - mb) - logf(sb)) * em;
+    const float lse = mt + logf(st);
+    float h = 0.f;
+    for (int q = lane; q < A; q += 64) h += (zt[q] - lse) * (expf(zt[q] - mt) / st);
+    ent = -wave_sum(h);
+    crho = fminf(fmaxf(expf(lt - lb), 0.f), 1.f);                            // train.py:228-231
+}
 
 // ---- fused forward: prep + both target scans + loss terms, one wave per G trajectories ------------
 //
@@ -256,7 +296,26 @@ __global__ __launch_bounds__(hrl_scan::kWave) void loss_fused_kernel(FusedArgs f
         const int tc = min(kLossTile, T - t0);
 
         // 1. prep: policy rows (g, t, pp)
-        {
+        if constexpr (AK == 0) {   // the wave on one row at a time, lanes over its actions
+            const int per = tc * Pp;
+            for (int e = 0; e < ntraj * per; ++e) {
+                const int gg = e / per;
+                const int rem = e - gg * per;
+                const int tt = rem / Pp;
+                const int pp = rem - tt * Pp;
+                const int64_t bt = (b0 + gg) * d.T + t0 + tt;
+                const int64_t row = bt * Pp + pp;
+                float lt, crho, ent;
+                policy_row_wave(a.tpol + row * A, a.bpol + row * A, A, (int)a.action[row], a.emask[bt], lane, lt,
+                                crho, ent);
+                if (lane == 0) {
+                    const int slot = gg * Lpr + tt * rhoC + pp;
+                    t_rho[slot] = crho;
+                    t_lt[slot] = lt;
+                    t_ent[slot] = ent;
+                }
+            }
+        } else {
             const int per = tc * Pp;
             const float inv_per = 1.0f / (float)per, inv_pp = 1.0f / (float)Pp;
             for (int e = lane; e < ntraj * per; e += kWave) {
@@ -551,6 +610,57 @@ __global__ __launch_bounds__(kThreads) void loss_backward_kernel(BwdArgs a, Loss
     }
 }
 
+// any A (Geister's 214): a wave per (b, t), lanes over the actions of each policy row, then over the
+// players for the value / return gradients; the same closed-form expressions as loss_backward_kernel
+__global__ __launch_bounds__(kThreads) void loss_backward_wave_kernel(BwdArgs a, LossDims d, Ws w) {
+    const int lane = threadIdx.x & 63;
+    const int64_t bt = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    if (bt >= d.BT) return;
+    const float dp = a.dl[0], dv = a.dl[1], dr = a.dl[2], de = a.dl[3], dt = a.dl[4];
+    const float *tm = a.tmask + bt * d.P;
+    const float *om = a.omask + bt * d.P;
+    const float em = a.emask[bt];
+    const float prog = 1.f - a.progress[bt] * (1.f - a.ent_decay);
+    const float cp = -(dp + dt) * w.turn[bt] * em;
+    for (int pp = 0; pp < d.Pp; ++pp) {
+        const int64_t row = bt * d.Pp + pp;
+        const float *z = a.tpol + row * d.A;
+        float *g = a.g_tpol + row * d.A;
+        float wsum = 0.f, wdec = 0.f;
+        for (int p = 0; p < d.P; ++p) {
+            if (d.Pp == 1 || p == pp) {
+                wsum += tm[p];
+                wdec += tm[p] * prog;
+            }
+        }
+        const float ce = de * wsum + dt * (-a.ent_coef) * wdec;
+        const float h = w.ent[row];
+        const int64_t act = a.action[row];
+        float m = -INFINITY;
+        for (int q = lane; q < d.A; q += 64) m = fmaxf(m, z[q]);
+        m = wave_max(m);
+        float s = 0.f;
+        for (int q = lane; q < d.A; q += 64) s += expf(z[q] - m);
+        s = wave_sum(s);
+        const float lse = m + logf(s);
+        for (int q = lane; q < d.A; q += 64) {
+            const float pq = expf(z[q] - m) / s;
+            const float la = z[q] - lse;
+            const float onehot = (q == act) ? 1.f : 0.f;
+            g[q] = cp * (onehot - pq) + ce * (-pq * (la + h));    // dH/dz = -p (log p + H)
+        }
+    }
+    for (int p = lane; p < d.P; p += 64) {
+        const int64_t i = bt * d.P + p;
+        if (a.g_value) a.g_value[i] = (dv + dt) * (a.value[i] - w.tv[i]) * om[p];
+        if (a.g_ret) {
+            const float x = a.ret_out[i] - w.tr[i];
+            const float sl = fminf(fmaxf(x, -1.f), 1.f);              // smooth_l1' (beta = 1)
+            a.g_ret[i] = (dr + dt) * sl * om[p];
+        }
+    }
+}
+
 bool dims_ok(int64_t B, int64_t T, int64_t P, int64_t Pp, int64_t A, LossDims &d) {
     if (B < 1 || T < 1 || P < 1 || P > 64 || A < 1 || !(Pp == 1 || Pp == P)) return false;
     d.B = B; d.T = T; d.BT = B * T; d.P = (int)P; d.Pp = (int)Pp; d.A = (int)A;
@@ -683,7 +793,9 @@ int hrl_loss_backward(const float *tpol, const int64_t *action, int64_t B, int64
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (A == 9) hipLaunchKernelGGL(loss_backward_kernel<9>, grid, block, 0, s, a, d, w);
     else if (A == 4) hipLaunchKernelGGL(loss_backward_kernel<4>, grid, block, 0, s, a, d, w);
-    else hipLaunchKernelGGL(loss_backward_kernel<0>, grid, block, 0, s, a, d, w);
+    else
+        hipLaunchKernelGGL(loss_backward_wave_kernel, dim3((unsigned)((d.BT + kThreads / 64 - 1) / (kThreads / 64))),
+                           block, 0, s, a, d, w);
     return status();
 }
 

@@ -230,13 +230,16 @@ class GeisterNet(nn.Module):
         board, scalar = x['board'], x['scalar']
         planes = scalar[..., None, None].expand(*scalar.shape, *BOARD)
         h_e = self._bn_steps(self.bn1, self.conv1(torch.cat([planes, board], dim=-3)), T)
-        return {'T': T, 'N': board.shape[0] // T, 'h_e': h_e, 'zx': self.body.x_halves(h_e), 'scalar': scalar}
+        N = board.shape[0] // T
+        # per-step views under ONE autograd node: the backward is a single concatenation, not T slice
+        # gradients accumulated
+        zx = [z.split(N) for z in self.body.x_halves(h_e)]
+        return {'T': T, 'N': N, 'h_e': h_e, 'zx': zx, 'scalar': scalar}
 
     def sequence_step(self, seq, t, hidden):
         """The cells at step t from the unroll's hidden state: (h_last, hidden)."""
-        n0, n1 = t * seq['N'], (t + 1) * seq['N']
         hs, cs = list(hidden[0]), list(hidden[1])
-        return self.body.step_hip([z[n0:n1] for z in seq['zx']], hs, cs, self.num_repeats)
+        return self.body.step_hip([z[t] for z in seq['zx']], hs, cs, self.num_repeats)
 
     def sequence_end(self, seq, h_lasts):
         """The heads over all T steps: {'policy', 'value', 'return'} with rows (t, n)."""
