@@ -195,6 +195,7 @@ struct ConvArgs {
     // SUMS: with v the stored output and m = [hmask > 0], per channel sum(v m) and sum(v m (yprev - mean))
     // (bn_bwd_reduce_kernel<MASK = 2> of the previous unit)
     const float *hmask, *yprev, *mean;
+    int co_total;   // output channels of y per sample; workgroup column blockIdx.y computes 32 of them
 };
 
 __device__ __forceinline__ float relu(float v) { return v < 0.f ? 0.f : v; }   // NaN stays NaN
@@ -280,7 +281,10 @@ __device__ __forceinline__ void store_sample_sums(float *tile, float *dst, int n
     s2 += (double)t2;
 }
 
-template <int KS, bool VEC, bool STATS, bool SPLIT, int PRO = 0, bool SUMS = false>
+// MT: 16-cell tiles (boards of at most 16*MT cells).  ZPAD: zero padding instead of the torus wrap (a 'same'
+// 3x3 nn.Conv2d, e.g. GeisterNet's 6x6 board): taps off the board read a slot that is never written.
+// blockIdx.y: the 32-channel output chunk (weights packed per chunk).
+template <int KS, bool VEC, bool STATS, bool SPLIT, int PRO = 0, bool SUMS = false, int MT = kMT, bool ZPAD = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void torus_conv_kernel(ConvArgs a) {
     static_assert(VEC || (PRO == 0 && !SUMS), "the prologue / sums forms need the float4 layout");
     const float *__restrict__ x = a.x;
@@ -294,7 +298,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
     const float *__restrict__ add = a.add;
     const float *__restrict__ add_mask = a.add_mask;
     constexpr int kNW = kTaps * KS * 2 * 64;
-    constexpr int kNLd = VEC ? (KS * 4 * kMaxCells / 4 + 63) / 64 : (KS * 4 * kMaxCells + 63) / 64;
+    constexpr int kCells = MT * 16;
+    constexpr int kNLd = VEC ? (KS * 4 * kCells / 4 + 63) / 64 : (KS * 4 * kCells + 63) / 64;
     __shared__ float w_lds[kNW];
     __shared__ float tiles[kWaves * kTile];
     __shared__ float coef_s[2 * kCo + 2];   // PRO: alpha[32], beta[32]; SUMS: mean[32]; +1 read past the last channel
@@ -305,7 +310,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int in_elem = Cin * HW;
     float *tile = tiles + wave * kTile;
 
-    for (int i = threadIdx.x; i < kNW; i += kThreads) w_lds[i] = wpk[i];
+    const int chunk = (int)blockIdx.y;
+    for (int i = threadIdx.x; i < kNW; i += kThreads) w_lds[i] = wpk[(int64_t)chunk * kNW + i];
     if constexpr (PRO != 0) {
         if (threadIdx.x < 2 * kCo) coef_s[threadIdx.x] = threadIdx.x < kCo ? a.alpha[threadIdx.x] : a.beta[threadIdx.x - kCo];
     }
@@ -318,25 +324,37 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
     // the lane's A-fragment cells: q = mt*16 + (lane & 15); cells past the board read cell q - HW.
     // nbr(q, tap) = row part (ky) + column part (kx), packed as row | column << 16: 15 registers instead
     // of 45 (the kernel sits at the 256-register limit of 2 waves per SIMD)
-    uint32_t nbp[kMT][3];
+    uint32_t nbp[MT][ZPAD ? 9 : 3];   // ZPAD: the offset per tap (taps off the board -> the zero slot kS-1)
 #pragma unroll
-    for (int mt = 0; mt < kMT; ++mt) {
+    for (int mt = 0; mt < MT; ++mt) {
         int q = mt * 16 + (lane & 15);
         while (q >= HW) q -= HW;
         const int r = q / W, c = q - r * W;
+        if constexpr (ZPAD) {
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            int rr = r + d - 1, cc = c + d - 1;
-            rr = rr < 0 ? rr + H : (rr >= H ? rr - H : rr);
-            cc = cc < 0 ? cc + W : (cc >= W ? cc - W : cc);
-            nbp[mt][d] = (uint32_t)(rr * W + (lane >> 4) * kS) | ((uint32_t)cc << 16);
+            for (int t = 0; t < 9; ++t) {
+                const int rr = r + t / 3 - 1, cc = c + t % 3 - 1;
+                const bool in = rr >= 0 && rr < H && cc >= 0 && cc < W;
+                nbp[mt][t] = (uint32_t)((in ? rr * W + cc : kS - 1) + (lane >> 4) * kS);
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                int rr = r + d - 1, cc = c + d - 1;
+                rr = rr < 0 ? rr + H : (rr >= H ? rr - H : rr);
+                cc = cc < 0 ? cc + W : (cc >= W ? cc - W : cc);
+                nbp[mt][d] = (uint32_t)(rr * W + (lane >> 4) * kS) | ((uint32_t)cc << 16);
+            }
         }
     }
-    auto nbr_ofs = [&](int mt, int t) -> int { return (int)(nbp[mt][t / 3] & 0xffffu) + (int)(nbp[mt][t % 3] >> 16); };
+    auto nbr_ofs = [&](int mt, int t) -> int {
+        if constexpr (ZPAD) return (int)nbp[mt][t];
+        else return (int)(nbp[mt][t / 3] & 0xffffu) + (int)(nbp[mt][t % 3] >> 16);
+    };
     float bias_v[2] = {0.f, 0.f};
     if (bias) {
-        bias_v[0] = bias[lane & 15];
-        bias_v[1] = bias[16 + (lane & 15)];
+        bias_v[0] = bias[chunk * kCo + (lane & 15)];
+        bias_v[1] = bias[chunk * kCo + 16 + (lane & 15)];
     }
     double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
 
@@ -359,9 +377,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
         const int64_t next = n + stride;
         if (next < N) st.load(x + next * in_elem, in_elem, lane);   // in flight during the MFMAs
 
-        f32x4 acc[kMT][2];
+        f32x4 acc[MT][2];
 #pragma unroll
-        for (int mt = 0; mt < kMT; ++mt) acc[mt][0] = acc[mt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int mt = 0; mt < MT; ++mt) acc[mt][0] = acc[mt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
         const float *wl = w_lds + lane;
         if constexpr (SPLIT) {
             // one k-step of 32 input channels per tap: lane l's A/B k are channels 8(l>>4) + e.
@@ -385,7 +403,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
                     split8(bv, Bh[ct], Bm[ct], Bl[ct]);
                 }
 #pragma unroll
-                for (int mt = 0; mt < kMT; ++mt) {
+                for (int mt = 0; mt < MT; ++mt) {
                     const float *ap = tile + nbr_ofs(mt, t) + cofs;
                     float av[8];
 #pragma unroll
@@ -405,7 +423,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
                 const float b0 = wl[((t * KS + s) * 2 + 0) * 64];
                 const float b1 = wl[((t * KS + s) * 2 + 1) * 64];
 #pragma unroll
-                for (int mt = 0; mt < kMT; ++mt) {
+                for (int mt = 0; mt < MT; ++mt) {
                     const float a = tile[nbr_ofs(mt, t) + s * 4 * kS];
                     acc[mt][0] = mfma(a, b0, acc[mt][0]);
                     acc[mt][1] = mfma(a, b1, acc[mt][1]);
@@ -421,7 +439,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
         // accumulators (cell = mt*16 + (lane>>4)*4 + r, co = ct*16 + (lane&15)) -> tile [co][cell]
         float t1[2] = {0.f, 0.f}, t2[2] = {0.f, 0.f};
 #pragma unroll
-        for (int mt = 0; mt < kMT; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
@@ -445,7 +463,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
             }
         }
         lds_fence();
-        const int64_t ob = n * (out_c * HW);
+        const int64_t ob = n * ((int64_t)a.co_total * HW) + (int64_t)chunk * kCo * HW;
         if constexpr (SUMS)
             store_sample_sums(tile, y + ob, out_c * HW, HW, inv_hw, lane, add + ob, add_mask + ob, a.hmask + ob,
                               a.yprev + ob, coef_s, s1[0], s2[0]);
@@ -507,6 +525,20 @@ __global__ void torus_pack_kernel(const float *__restrict__ w, int Cin, int KS, 
         if (oc < Cin) v = w[(ic * Cin + oc) * kTaps + (kTaps - 1 - tap)];
     }
     wpk[i] = v;
+}
+
+// Zero-padded board conv weights: W (Cout, cin_total, 3, 3) restricted to input channels [ci0, ci0 + 32) ->
+// per 32-channel output chunk the packed [tap][8][ct][64] layout of torus_pack_kernel.
+__global__ void board_pack_kernel(const float *__restrict__ w, int nchunks, int cin_total, int ci0,
+                                  float *__restrict__ wpk) {
+    constexpr int kNW = kTaps * 8 * 2 * 64;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nchunks * kNW) return;
+    const int chunk = i / kNW, j = i - chunk * kNW;
+    const int l = j & 63, ct = (j >> 6) & 1, s = (j >> 7) % 8, tap = j / (128 * 8);
+    const int oc = chunk * kCo + ct * 16 + (l & 15);
+    const int ic = s * 4 + (l >> 4);
+    wpk[i] = w[((int64_t)oc * cin_total + ci0 + ic) * kTaps + tap];
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -948,7 +980,7 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
                          (!add || (aligned16(add) && aligned16(add_mask)));
     ConvArgs a{};
     a.x = x; a.N = N; a.Cin = in_c; a.H = (int)H; a.W = (int)W; a.wpk = wpk; a.bias = bias; a.out_c = out_c;
-    a.vec_out = vec_out; a.y = y; a.part = part; a.add = add; a.add_mask = add_mask;
+    a.vec_out = vec_out; a.y = y; a.part = part; a.add = add; a.add_mask = add_mask; a.co_total = out_c;
     const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
 #define HRL_TORUS_LAUNCH(KS_, VEC_, ST_)                                                                           \
     do {                                                                                                         \
@@ -963,6 +995,44 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
         if (st) HRL_TORUS_LAUNCH(5, false, true); else HRL_TORUS_LAUNCH(5, false, false);
     }
 #undef HRL_TORUS_LAUNCH
+    return status();
+}
+
+int64_t hrl_board_conv_workspace_bytes(int64_t Cout) {
+    return (Cout < kCo || Cout % kCo) ? -1 : (Cout / kCo) * kTaps * 8 * 2 * 64 * 4;
+}
+
+int hrl_board_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t H, int64_t W, const float *weight,
+                           int64_t w_cin_total, int64_t w_ci0, int64_t Cout, const float *bias, float *y,
+                           void *workspace, int64_t workspace_bytes, void *stream) {
+    const int64_t HW = H * W;
+    if (N < 1 || Cin != kCo || H < 1 || W < 1 || HW < 4 || HW > kMaxCells || !x || !weight || !y || !workspace)
+        return HRL_EINVAL;
+    if (w_ci0 < 0 || w_ci0 + Cin > w_cin_total || hrl_board_conv_workspace_bytes(Cout) < 0 ||
+        workspace_bytes < hrl_board_conv_workspace_bytes(Cout) || N * Cout * HW >= ((int64_t)1 << 40))
+        return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int nchunks = (int)(Cout / kCo);
+    float *wpk = static_cast<float *>(workspace);
+    const int npk = nchunks * kTaps * 8 * 2 * 64;
+    hipLaunchKernelGGL(board_pack_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, weight, nchunks, (int)w_cin_total,
+                       (int)w_ci0, wpk);
+    int rc = status();
+    if (rc) return rc;
+    ConvArgs a{};
+    a.x = x; a.N = N; a.Cin = kCo; a.H = (int)H; a.W = (int)W; a.wpk = wpk; a.bias = bias; a.out_c = kCo;
+    a.vec_out = (kCo * HW) % 4 == 0 && aligned16(y); a.y = y; a.co_total = (int)Cout;
+    const bool vec = (kCo * HW) % 4 == 0 && aligned16(x);
+    const dim3 grid(grid_for(N, kGridConv), nchunks), block(kThreads);
+#define HRL_BOARD_LAUNCH(VEC_, MT_)                                                                                 \
+    do {                                                                                                          \
+        if (g_split) hipLaunchKernelGGL((torus_conv_kernel<8, VEC_, false, true, 0, false, MT_, true>), grid, block, 0, \
+                                        s, a);                                                                    \
+        else hipLaunchKernelGGL((torus_conv_kernel<8, VEC_, false, false, 0, false, MT_, true>), grid, block, 0, s, a); \
+    } while (0)
+    if (HW <= 48) { if (vec) HRL_BOARD_LAUNCH(true, 3); else HRL_BOARD_LAUNCH(false, 3); }
+    else { if (vec) HRL_BOARD_LAUNCH(true, 5); else HRL_BOARD_LAUNCH(false, 5); }
+#undef HRL_BOARD_LAUNCH
     return status();
 }
 
@@ -983,6 +1053,7 @@ int hrl_torus_unit_forward(const float *y_prev, const float *res, const float *a
     ConvArgs a{};
     a.x = y_prev; a.N = N; a.Cin = kCo; a.H = (int)H; a.W = (int)W; a.wpk = wpk; a.bias = bias; a.out_c = kCo;
     a.vec_out = true; a.y = y; a.part = part; a.res = res; a.alpha = alpha; a.beta = beta; a.hout = h;
+    a.co_total = kCo;
     const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
     if (res) {
         if (g_split) hipLaunchKernelGGL((torus_conv_kernel<8, true, true, true, 2>), grid, block, 0, s, a);
@@ -1015,6 +1086,7 @@ int hrl_torus_unit_input_grad(const float *dy, int64_t N, int64_t H, int64_t W, 
     ConvArgs a{};
     a.x = dy; a.N = N; a.Cin = kCo; a.H = (int)H; a.W = (int)W; a.wpk = wpk; a.out_c = kCo; a.vec_out = true;
     a.y = dh; a.part = part; a.add = g; a.add_mask = out; a.hmask = h_mask; a.yprev = y_prev; a.mean = mean_prev;
+    a.co_total = kCo;
     const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
     if (g_split) hipLaunchKernelGGL((torus_conv_kernel<8, true, false, true, 0, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((torus_conv_kernel<8, true, false, false, 0, true>), grid, block, 0, s, a);

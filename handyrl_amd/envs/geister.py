@@ -116,6 +116,8 @@ class DRC(nn.Module):
                 return (conv2d(x, ws[layers[0]], bias[layers[0]], pad, in_slice=(0, cin)),)
             w_x = torch.cat([ws[i][:, :cin] for i in layers])
             b_x = None if bias[0] is None else torch.cat([bias[i] for i in layers])
+            if not torch.is_grad_enabled() and hnn.board_conv_ok(x, w_x, 0, pad):   # inference: HIP MFMA conv
+                return hnn.board_conv_forward(x, w_x, b_x).chunk(len(layers), dim=-3)
             return F.conv2d(x, w_x, b_x, padding=pad).chunk(len(layers), dim=-3)
         if torch.is_grad_enabled() and n > 1:
             # Only the last layer reaches the output (every cell reads x and its own state), so the
@@ -133,11 +135,14 @@ class DRC(nn.Module):
         c_all = ws[0].shape[1]
         cin = c_all - self.blocks[0].hidden_dim
         deferred = hnn._DEFER is not None
-        w_h = None if deferred else [w[:, cin:].contiguous() for w in ws]
+        hip_h = not deferred and not torch.is_grad_enabled() and hnn.board_conv_ok(hs[0], ws[0], cin, pad)
+        w_h = None if (deferred or hip_h) else [w[:, cin:].contiguous() for w in ws]
         for _ in range(num_repeats):
             for i in range(len(self.blocks)):
                 if deferred:
                     zh = conv2d(hs[i], ws[i], None, pad, in_slice=(cin, c_all))
+                elif hip_h:   # inference (self-play): the h half read straight from the cell's weight
+                    zh = hnn.board_conv_forward(hs[i], ws[i], None, cin)
                 else:
                     zh = F.conv2d(hs[i], w_h[i], None, padding=pad)
                 hs[i], cs[i] = lstm_gates(zx[i], zh, cs[i])

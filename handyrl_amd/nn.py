@@ -160,6 +160,32 @@ def _ret(buf_direct):
     return None if direct else buf
 
 
+def board_conv_ok(x, w, ci0, pad):
+    """Shapes hrl_board_conv_forward covers: 'same' 3x3 zero padding, 32 input channels (a slice [ci0, ci0+32) of
+    w's), Cout a multiple of 32, boards of 4..80 cells, fp32 CUDA."""
+    return (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 4
+            and x.shape[0] > 0 and x.shape[1] == 32 and w.dim() == 4 and tuple(w.shape[2:]) == (3, 3)
+            and tuple(pad) == (1, 1) and w.shape[0] % 32 == 0 and 0 <= ci0 and ci0 + 32 <= w.shape[1]
+            and 4 <= x.shape[2] * x.shape[3] <= 80)
+
+
+def board_conv_forward(x, w, b, ci0=0):
+    """F.conv2d(x, w[:, ci0:ci0+32], b, padding=1) on csrc/hrl_torus.hip's MFMA path (zero padding); forward
+    only, no autograd (board_conv_ok must hold)."""
+    x, w = x.contiguous(), w.contiguous()
+    N, _, H, W = x.shape
+    Cout = w.shape[0]
+    lib = _native.load()
+    ws_bytes = lib.hrl_board_conv_workspace_bytes(Cout)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+    y = torch.empty(N, Cout, H, W, device=x.device, dtype=x.dtype)
+    _native.check(lib.hrl_board_conv_forward(_native.ptr(x), N, 32, H, W, _native.ptr(w), w.shape[1], ci0, Cout,
+                                             _native.ptr(b.contiguous()) if b is not None else None, _native.ptr(y),
+                                             _native.ptr(ws), ws_bytes, _native.stream_of(x.device)),
+                  'hrl_board_conv_forward')
+    return y
+
+
 class _DeferredConv(torch.autograd.Function):
     """conv2d (stride 1, 'same') whose weight/bias gradient is deferred to DeferredGrads.flush().
 
@@ -169,7 +195,11 @@ class _DeferredConv(torch.autograd.Function):
     def forward(ctx, x, w, b, sl, pad, rec):
         ctx.set_materialize_grads(False)
         wv = w if sl is None else w[:, sl[0]:sl[1]]
-        y = F.conv2d(x, wv, b, padding=pad)
+        ci0 = 0 if sl is None else sl[0]
+        if (sl is None or sl[1] - sl[0] == 32) and board_conv_ok(x, w, ci0, pad):
+            y = board_conv_forward(x, w.detach(), None if b is None else b.detach(), ci0)
+        else:
+            y = F.conv2d(x, wv, b, padding=pad)
         ctx.save_for_backward(x, w)
         ctx.meta = (sl, pad, rec, b)
         return y

@@ -281,6 +281,16 @@ int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin
 int hrl_torus_unit_forward(const float *y_prev, const float *res, const float *alpha, const float *beta, float *h,
                            int64_t N, int64_t H, int64_t W, const float *weight, const float *bias, float *y,
                            double *part, void *workspace, int64_t workspace_bytes, void *stream);
+/* A zero-padded 3x3 'same' nn.Conv2d, 32 input channels -> Cout (a multiple of 32) on a board of 4..80 cells,
+ * on the torus kernel's MFMA path (GeisterNet's ConvLSTM h / x halves, geister.py:48-59): x (N, 32, H, W),
+ * y (N, Cout, H, W); the weights are input channels [w_ci0, w_ci0 + 32) of a (Cout, w_cin_total, 3, 3)
+ * tensor (a cell's conv([x, h]) split into its halves); bias (Cout) or NULL.
+ * workspace: hrl_board_conv_workspace_bytes(Cout) bytes. */
+int64_t hrl_board_conv_workspace_bytes(int64_t Cout);
+int hrl_board_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t H, int64_t W, const float *weight,
+                           int64_t w_cin_total, int64_t w_ci0, int64_t Cout, const float *bias, float *y,
+                           void *workspace, int64_t workspace_bytes, void *stream);
+
 /* GeeseNet's head pooling (hungry_geese.py:52-53) on h (N, 32, H, W) and the net input x (its plane 0,
  * samples x_stride floats apart): head[n, c] = sum_q h[n, c, q] * x[n, 0, q], avg[n, c] = mean_q h[n, c, q]
  * (both (N, 32)); hrl_torus_head_unpool: the gradient w.r.t. h, g = dhead * x0 + davg / (H*W). */

@@ -225,3 +225,40 @@ def test_torus_wgrad_integer_data_is_exact(cuda, split, N, H, W):
         lib.hrl_torus_set_split(prev)
     assert torch.equal(dw.cpu().double(), w64.grad)
     assert torch.equal(db.cpu().double(), b64.grad)
+
+
+@pytest.mark.parametrize('split', [1, 0])
+@pytest.mark.parametrize('N,H,W,Cout,cin_total,ci0', [(37, 6, 6, 128, 64, 32), (300, 6, 6, 384, 32, 0),
+                                                      (5, 3, 5, 32, 32, 0), (9, 8, 10, 64, 96, 64),
+                                                      (2, 2, 2, 32, 32, 0)])
+def test_board_conv_integer_data_is_exact(cuda, split, N, H, W, Cout, cin_total, ci0):
+    """hrl_board_conv_forward (the torus kernel with zero padding, 3 or 5 cell tiles, 32-channel output chunks,
+    a channel slice of the weight): exact against fp64 on integer data, both arithmetics."""
+    from handyrl_amd.nn import board_conv_forward
+    lib = _native.load()
+    g = torch.Generator().manual_seed(N + Cout + ci0)
+    x = torch.randint(-4, 5, (N, 32, H, W), generator=g).float()
+    w = torch.randint(-4, 5, (Cout, cin_total, 3, 3), generator=g).float()
+    b = torch.randint(-4, 5, (Cout,), generator=g).float()
+    ref = torch.nn.functional.conv2d(x.double(), w[:, ci0:ci0 + 32].double(), b.double(), padding=1)
+    prev = lib.hrl_torus_set_split(split)
+    try:
+        y = board_conv_forward(x.to(cuda), w.to(cuda), b.to(cuda), ci0)
+        torch.cuda.synchronize(cuda)
+    finally:
+        lib.hrl_torus_set_split(prev)
+    assert torch.equal(y.cpu().double(), ref)
+
+
+def test_board_conv_error_within_fp32_error(cuda):
+    """Random data, 6x6 (GeisterNet's h half): within 2x torch-CPU fp32's error against fp64."""
+    from handyrl_amd.nn import board_conv_forward
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(257, 32, 6, 6, generator=g)
+    w = torch.randn(128, 64, 3, 3, generator=g) * 0.1
+    ref = torch.nn.functional.conv2d(x.double(), w[:, 32:].double(), None, padding=1)
+    t32 = torch.nn.functional.conv2d(x, w[:, 32:], None, padding=1).double()
+    scale = ref.abs().max()
+    bound = 2 * float((t32 - ref).abs().max() / scale) + 1e-7
+    y = board_conv_forward(x.to(cuda), w.to(cuda), None, 32).cpu().double()
+    assert float((y - ref).abs().max() / scale) <= bound
