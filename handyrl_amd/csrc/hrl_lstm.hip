@@ -122,10 +122,12 @@ __global__ void lstm_fwd_kernel(const float *__restrict__ zx, const float *__res
             put<VW>(cn, j, cc);
             put<VW>(hn, j, so * tanhf(cc));
         }
-        st<VW>(gates + zoff, gi);
-        st<VW>(gates + zoff + gstep, gf);
-        st<VW>(gates + zoff + 2 * gstep, go);
-        st<VW>(gates + zoff + 3 * gstep, gg);
+        if (gates) {   // NULL in inference: nothing to save for a backward
+            st<VW>(gates + zoff, gi);
+            st<VW>(gates + zoff + gstep, gf);
+            st<VW>(gates + zoff + 2 * gstep, go);
+            st<VW>(gates + zoff + 3 * gstep, gg);
+        }
         st<VW>(c_out + soff, cn);
         st<VW>(h_out + soff, hn);
     }
@@ -195,7 +197,7 @@ extern "C" {
 int hrl_lstm_gates_forward(const float *zx, int64_t zx_stride, const float *zh, const float *c, int64_t N, int64_t H,
                            int64_t HW, float *h_out, float *c_out, float *gates, void *stream) {
     if (N == 0) return HRL_OK;
-    if (!zh || !c || !h_out || !c_out || !gates || N < 0 || H < 1 || HW < 1) return HRL_EINVAL;
+    if (!zh || !c || !h_out || !c_out || N < 0 || H < 1 || HW < 1) return HRL_EINVAL;
     if (zx && zx_stride < 4 * H * HW) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool vec = HW % 4 == 0 && (!zx || zx_stride % 4 == 0) && aligned(zx) && aligned(zh) && aligned(c) &&

@@ -1002,28 +1002,34 @@ int64_t hrl_board_conv_workspace_bytes(int64_t Cout) {
     return (Cout < kCo || Cout % kCo) ? -1 : (Cout / kCo) * kTaps * 8 * 2 * 64 * 4;
 }
 
-int hrl_board_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t H, int64_t W, const float *weight,
-                           int64_t w_cin_total, int64_t w_ci0, int64_t Cout, const float *bias, float *y,
-                           void *workspace, int64_t workspace_bytes, void *stream) {
+int hrl_board_conv_pack(const float *weight, int64_t w_cin_total, int64_t w_ci0, int64_t Cout, void *packed,
+                        int64_t packed_bytes, void *stream) {
+    if (!weight || !packed || w_ci0 < 0 || w_ci0 + kCo > w_cin_total || hrl_board_conv_workspace_bytes(Cout) < 0 ||
+        packed_bytes < hrl_board_conv_workspace_bytes(Cout))
+        return HRL_EINVAL;
+    const int nchunks = (int)(Cout / kCo);
+    const int npk = nchunks * kTaps * 8 * 2 * 64;
+    hipLaunchKernelGGL(board_pack_kernel, dim3((npk + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       weight, nchunks, (int)w_cin_total, (int)w_ci0, static_cast<float *>(packed));
+    return status();
+}
+
+int hrl_board_conv_forward_packed(const float *x, int64_t N, int64_t Cin, int64_t H, int64_t W, const void *packed,
+                                  int64_t Cout, const float *bias, float *y, void *stream) {
     const int64_t HW = H * W;
-    if (N < 1 || Cin != kCo || H < 1 || W < 1 || HW < 4 || HW > kMaxCells || !x || !weight || !y || !workspace)
-        return HRL_EINVAL;
-    if (w_ci0 < 0 || w_ci0 + Cin > w_cin_total || hrl_board_conv_workspace_bytes(Cout) < 0 ||
-        workspace_bytes < hrl_board_conv_workspace_bytes(Cout) || N * Cout * HW >= ((int64_t)1 << 40))
-        return HRL_EINVAL;
+    if (N < 1 || Cin != kCo || H < 1 || W < 1 || HW < 4 || HW > kMaxCells || !x || !packed || !y) return HRL_EINVAL;
+    if (hrl_board_conv_workspace_bytes(Cout) < 0 || N * Cout * HW >= ((int64_t)1 << 40)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int nchunks = (int)(Cout / kCo);
-    float *wpk = static_cast<float *>(workspace);
-    const int npk = nchunks * kTaps * 8 * 2 * 64;
-    hipLaunchKernelGGL(board_pack_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, weight, nchunks, (int)w_cin_total,
-                       (int)w_ci0, wpk);
-    int rc = status();
-    if (rc) return rc;
+    const float *wpk = static_cast<const float *>(packed);
     ConvArgs a{};
     a.x = x; a.N = N; a.Cin = kCo; a.H = (int)H; a.W = (int)W; a.wpk = wpk; a.bias = bias; a.out_c = kCo;
     a.vec_out = (kCo * HW) % 4 == 0 && aligned16(y); a.y = y; a.co_total = (int)Cout;
     const bool vec = (kCo * HW) % 4 == 0 && aligned16(x);
-    const dim3 grid(grid_for(N, kGridConv), nchunks), block(kThreads);
+    // ~kGridConv workgroups in all: each loads its chunk's 37 KB of packed weights once, so at large N it
+    // must walk many samples (one sample per wave per chunk reloaded the weights every 4 samples)
+    const int cap = kGridConv / nchunks > 0 ? kGridConv / nchunks : 1;
+    const dim3 grid(grid_for(N, cap), nchunks), block(kThreads);
 #define HRL_BOARD_LAUNCH(VEC_, MT_)                                                                                 \
     do {                                                                                                          \
         if (g_split) hipLaunchKernelGGL((torus_conv_kernel<8, VEC_, false, true, 0, false, MT_, true>), grid, block, 0, \
@@ -1034,6 +1040,14 @@ int hrl_board_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t H, in
     else { if (vec) HRL_BOARD_LAUNCH(true, 5); else HRL_BOARD_LAUNCH(false, 5); }
 #undef HRL_BOARD_LAUNCH
     return status();
+}
+
+int hrl_board_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t H, int64_t W, const float *weight,
+                           int64_t w_cin_total, int64_t w_ci0, int64_t Cout, const float *bias, float *y,
+                           void *workspace, int64_t workspace_bytes, void *stream) {
+    const int rc = hrl_board_conv_pack(weight, w_cin_total, w_ci0, Cout, workspace, workspace_bytes, stream);
+    if (rc) return rc;
+    return hrl_board_conv_forward_packed(x, N, Cin, H, W, workspace, Cout, bias, y, stream);
 }
 
 int hrl_torus_unit_forward(const float *y_prev, const float *res, const float *alpha, const float *beta, float *h,

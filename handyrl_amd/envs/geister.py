@@ -116,8 +116,6 @@ class DRC(nn.Module):
                 return (conv2d(x, ws[layers[0]], bias[layers[0]], pad, in_slice=(0, cin)),)
             w_x = torch.cat([ws[i][:, :cin] for i in layers])
             b_x = None if bias[0] is None else torch.cat([bias[i] for i in layers])
-            if not torch.is_grad_enabled() and hnn.board_conv_ok(x, w_x, 0, pad):   # inference: HIP MFMA conv
-                return hnn.board_conv_forward(x, w_x, b_x).chunk(len(layers), dim=-3)
             return F.conv2d(x, w_x, b_x, padding=pad).chunk(len(layers), dim=-3)
         if torch.is_grad_enabled() and n > 1:
             # Only the last layer reaches the output (every cell reads x and its own state), so the
@@ -126,8 +124,9 @@ class DRC(nn.Module):
             return list(x_half(list(range(n - 1))) + x_half([n - 1]))
         return list(x_half(list(range(n))))
 
-    def step_hip(self, zx, hs, cs, num_repeats):
-        """One time step of the cells given their x halves zx (DRC.forward's repeats and layers)."""
+    def step_hip(self, zx, hs, cs, num_repeats, packed_h=None):
+        """One time step of the cells given their x halves zx (DRC.forward's repeats and layers); packed_h:
+        the cells' h-half weights packed for the board conv (GeisterNet.sequence_begin), or None."""
         from .. import nn as hnn
         from ..nn import lstm_gates, conv2d
         ws = [blk.conv.weight for blk in self.blocks]
@@ -135,14 +134,12 @@ class DRC(nn.Module):
         c_all = ws[0].shape[1]
         cin = c_all - self.blocks[0].hidden_dim
         deferred = hnn._DEFER is not None
-        hip_h = not deferred and not torch.is_grad_enabled() and hnn.board_conv_ok(hs[0], ws[0], cin, pad)
-        w_h = None if (deferred or hip_h) else [w[:, cin:].contiguous() for w in ws]
+        w_h = None if deferred else [w[:, cin:].contiguous() for w in ws]
         for _ in range(num_repeats):
             for i in range(len(self.blocks)):
                 if deferred:
-                    zh = conv2d(hs[i], ws[i], None, pad, in_slice=(cin, c_all))
-                elif hip_h:   # inference (self-play): the h half read straight from the cell's weight
-                    zh = hnn.board_conv_forward(hs[i], ws[i], None, cin)
+                    zh = conv2d(hs[i], ws[i], None, pad, in_slice=(cin, c_all),
+                                packed=None if packed_h is None else packed_h[i])
                 else:
                     zh = F.conv2d(hs[i], w_h[i], None, padding=pad)
                 hs[i], cs[i] = lstm_gates(zx[i], zh, cs[i])
@@ -239,12 +236,19 @@ class GeisterNet(nn.Module):
         # per-step views under ONE autograd node: the backward is a single concatenation, not T slice
         # gradients accumulated
         zx = [z.split(N) for z in self.body.x_halves(h_e)]
-        return {'T': T, 'N': N, 'h_e': h_e, 'zx': zx, 'scalar': scalar}
+        # the cells' h-half weights packed once for the whole unroll (T * repeats uses each)
+        from .. import nn as hnn
+        cells = [blk.conv for blk in self.body.blocks]
+        cin = cells[0].weight.shape[1] - self.body.blocks[0].hidden_dim
+        packed_h = None
+        if hnn._DEFER is not None and hnn.board_conv_ok(h_e[:1], cells[0].weight, cin, cells[0].padding):
+            packed_h = [hnn.board_conv_pack(c.weight.detach(), cin) for c in cells]
+        return {'T': T, 'N': N, 'h_e': h_e, 'zx': zx, 'scalar': scalar, 'packed_h': packed_h}
 
     def sequence_step(self, seq, t, hidden):
         """The cells at step t from the unroll's hidden state: (h_last, hidden)."""
         hs, cs = list(hidden[0]), list(hidden[1])
-        return self.body.step_hip([z[t] for z in seq['zx']], hs, cs, self.num_repeats)
+        return self.body.step_hip([z[t] for z in seq['zx']], hs, cs, self.num_repeats, seq['packed_h'])
 
     def sequence_end(self, seq, h_lasts):
         """The heads over all T steps: {'policy', 'value', 'return'} with rows (t, n)."""

@@ -169,20 +169,27 @@ def board_conv_ok(x, w, ci0, pad):
             and 4 <= x.shape[2] * x.shape[3] <= 80)
 
 
-def board_conv_forward(x, w, b, ci0=0):
+def board_conv_pack(w, ci0=0):
+    """w[:, ci0:ci0+32] packed for board_conv_forward (a recurrent unroll packs each weight once per forward)."""
+    lib = _native.load()
+    nbytes = lib.hrl_board_conv_workspace_bytes(w.shape[0])
+    wpk = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+    _native.check(lib.hrl_board_conv_pack(_native.ptr(w.contiguous()), w.shape[1], ci0, w.shape[0], _native.ptr(wpk),
+                                          nbytes, _native.stream_of(w.device)), 'hrl_board_conv_pack')
+    return wpk
+
+
+def board_conv_forward(x, w, b, ci0=0, packed=None):
     """F.conv2d(x, w[:, ci0:ci0+32], b, padding=1) on csrc/hrl_torus.hip's MFMA path (zero padding); forward
-    only, no autograd (board_conv_ok must hold)."""
-    x, w = x.contiguous(), w.contiguous()
+    only, no autograd (board_conv_ok must hold).  ``packed``: board_conv_pack(w, ci0) made for this forward."""
+    x = x.contiguous()
     N, _, H, W = x.shape
     Cout = w.shape[0]
-    lib = _native.load()
-    ws_bytes = lib.hrl_board_conv_workspace_bytes(Cout)
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+    wpk = board_conv_pack(w, ci0) if packed is None else packed
     y = torch.empty(N, Cout, H, W, device=x.device, dtype=x.dtype)
-    _native.check(lib.hrl_board_conv_forward(_native.ptr(x), N, 32, H, W, _native.ptr(w), w.shape[1], ci0, Cout,
-                                             _native.ptr(b.contiguous()) if b is not None else None, _native.ptr(y),
-                                             _native.ptr(ws), ws_bytes, _native.stream_of(x.device)),
-                  'hrl_board_conv_forward')
+    _native.check(_native.load().hrl_board_conv_forward_packed(
+        _native.ptr(x), N, 32, H, W, _native.ptr(wpk), Cout, _native.ptr(b.contiguous()) if b is not None else None,
+        _native.ptr(y), _native.stream_of(x.device)), 'hrl_board_conv_forward_packed')
     return y
 
 
@@ -192,12 +199,12 @@ class _DeferredConv(torch.autograd.Function):
     ``sl`` selects input channels [sl[0], sl[1]) of the weight (a ConvLSTM cell's h or x half)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, sl, pad, rec):
+    def forward(ctx, x, w, b, sl, pad, rec, packed=None):
         ctx.set_materialize_grads(False)
         wv = w if sl is None else w[:, sl[0]:sl[1]]
         ci0 = 0 if sl is None else sl[0]
         if (sl is None or sl[1] - sl[0] == 32) and board_conv_ok(x, w, ci0, pad):
-            y = board_conv_forward(x, w.detach(), None if b is None else b.detach(), ci0)
+            y = board_conv_forward(x, w.detach(), None if b is None else b.detach(), ci0, packed)
         else:
             y = F.conv2d(x, wv, b, padding=pad)
         ctx.save_for_backward(x, w)
@@ -207,7 +214,7 @@ class _DeferredConv(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         if dy is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         x, w = ctx.saved_tensors
         sl, pad, rec, b = ctx.meta
         dy = dy.contiguous()
@@ -217,14 +224,15 @@ class _DeferredConv(torch.autograd.Function):
             dx = torch.ops.aten.convolution_backward(dy, x, wv, None, [1, 1], list(pad), [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]
         rec.add_conv((w, b, sl, tuple(pad)), x, dy)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
-def conv2d(x, w, b=None, padding=(0, 0), in_slice=None):
+def conv2d(x, w, b=None, padding=(0, 0), in_slice=None, packed=None):
     """F.conv2d (stride 1) of the env nets; inside deferred_weight_grads() the weight gradient is
-    batched over the unroll (DeferredGrads)."""
+    batched over the unroll (DeferredGrads) and the forward of 3x3 32-channel board convs runs on
+    the MFMA board conv (``packed``: its weights packed once for the unroll, board_conv_pack)."""
     if _DEFER is not None and torch.is_grad_enabled() and w.requires_grad:
-        return _DeferredConv.apply(x, w, b, in_slice, tuple(padding), _DEFER)
+        return _DeferredConv.apply(x, w, b, in_slice, tuple(padding), _DEFER, packed)
     wv = w if in_slice is None else w[:, in_slice[0]:in_slice[1]]
     return F.conv2d(x, wv, b, padding=padding)
 
@@ -982,7 +990,7 @@ class _LSTMGates(torch.autograd.Function):
     """ConvLSTM cell gates (csrc/hrl_lstm.hip): z = zx + zh -> (h', c'), saved gate activations."""
 
     @staticmethod
-    def forward(ctx, zx, zh, c):
+    def forward(ctx, zx, zh, c, save=True):
         ctx.set_materialize_grads(False)   # a cell whose outputs reach no loss stays out of backward
         N, G, Hh, Ww = zh.shape
         H, HW = G // 4, Hh * Ww
@@ -992,7 +1000,8 @@ class _LSTMGates(torch.autograd.Function):
             zx = zx.contiguous()
         h_out = torch.empty_like(c)
         c_out = torch.empty_like(c)
-        gates = torch.empty_like(zh)
+        # inference (self-play) saves nothing for a backward: the kernel skips the 4 gate streams
+        gates = torch.empty_like(zh) if save else None
         lib = _native.load()
         _native.check(lib.hrl_lstm_gates_forward(_native.ptr(zx), 0 if zx is None else zx.stride(0), _native.ptr(zh),
                                                  _native.ptr(c), N, H, HW, _native.ptr(h_out), _native.ptr(c_out),
@@ -1005,7 +1014,7 @@ class _LSTMGates(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh, dc_out):
         if dh is None and dc_out is None:
-            return None, None, None
+            return None, None, None, None
         gates, c, c_out = ctx.saved_tensors
         N, G, Hh, Ww = gates.shape
         dz = torch.empty_like(gates)
@@ -1016,7 +1025,7 @@ class _LSTMGates(torch.autograd.Function):
             _native.ptr(gates), _native.ptr(c), _native.ptr(c_out), _native.ptr(dh), _native.ptr(dc_out),
             N, G // 4, Hh * Ww, _native.ptr(dz), _native.ptr(dc), _native.stream_of(gates.device)),
             'hrl_lstm_gates_backward')
-        return (dz if ctx.has_zx else None), dz, dc
+        return (dz if ctx.has_zx else None), dz, dc, None
 
 
 def lstm_gates(zx, zh, c):
@@ -1027,7 +1036,8 @@ def lstm_gates(zx, zh, c):
     """
     if not zh.is_cuda:
         raise RuntimeError('lstm_gates runs on the HIP device only (no CPU fallback)')
-    return _LSTMGates.apply(zx, zh, c)
+    save = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (zx, zh, c))
+    return _LSTMGates.apply(zx, zh, c, save)
 
 
 def _live(xs):

@@ -204,7 +204,7 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
  * its autograd backward).  Gate pre-activations z = zx + zh in channel order
  * i, f, o, g: zh (N, 4H, HW) contiguous; zx the same shape with per-sample
  * stride zx_stride floats (a channel slice of a wider tensor) or NULL.
- * Forward: gates (N, 4H, HW) = (sigmoid i, sigmoid f, sigmoid o, tanh g);
+ * Forward: gates (N, 4H, HW) = (sigmoid i, sigmoid f, sigmoid o, tanh g) (NULL: not saved, inference);
  *          c_out = f*c + i*g; h_out = o*tanh(c_out).
  * Backward: dz (N, 4H, HW) and dc (N, H, HW) from dh / dc_out (either may be NULL = zero).
  */
@@ -285,11 +285,16 @@ int hrl_torus_unit_forward(const float *y_prev, const float *res, const float *a
  * on the torus kernel's MFMA path (GeisterNet's ConvLSTM h / x halves, geister.py:48-59): x (N, 32, H, W),
  * y (N, Cout, H, W); the weights are input channels [w_ci0, w_ci0 + 32) of a (Cout, w_cin_total, 3, 3)
  * tensor (a cell's conv([x, h]) split into its halves); bias (Cout) or NULL.
- * workspace: hrl_board_conv_workspace_bytes(Cout) bytes. */
+ * workspace: hrl_board_conv_workspace_bytes(Cout) bytes.  hrl_board_conv_pack + hrl_board_conv_forward_packed
+ * split the weight packing out (a recurrent unroll packs each weight once per step). */
 int64_t hrl_board_conv_workspace_bytes(int64_t Cout);
 int hrl_board_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t H, int64_t W, const float *weight,
                            int64_t w_cin_total, int64_t w_ci0, int64_t Cout, const float *bias, float *y,
                            void *workspace, int64_t workspace_bytes, void *stream);
+int hrl_board_conv_pack(const float *weight, int64_t w_cin_total, int64_t w_ci0, int64_t Cout, void *packed,
+                        int64_t packed_bytes, void *stream);
+int hrl_board_conv_forward_packed(const float *x, int64_t N, int64_t Cin, int64_t H, int64_t W, const void *packed,
+                                  int64_t Cout, const float *bias, float *y, void *stream);
 
 /* GeeseNet's head pooling (hungry_geese.py:52-53) on h (N, 32, H, W) and the net input x (its plane 0,
  * samples x_stride floats apart): head[n, c] = sum_q h[n, c, q] * x[n, 0, q], avg[n, c] = mean_q h[n, c, q]
