@@ -316,12 +316,19 @@ class GeisterBatch:
         self.reset()
 
     def reset(self):
+        """State is allocated once, then reset and advanced in place (a captured ply keeps addressing it)."""
         E, dev = self.E, self.device
-        self.board = torch.full((E, 36), -1, dtype=torch.int8, device=dev)
-        self.color = torch.zeros(E, dtype=torch.long, device=dev)
-        self.turn_count = torch.full((E,), -2, dtype=torch.long, device=dev)
-        self.win = torch.full((E,), -1, dtype=torch.long, device=dev)
-        self.cnt = torch.zeros(E, 4, dtype=torch.long, device=dev)
+        if not hasattr(self, 'board'):
+            self.board = torch.full((E, 36), -1, dtype=torch.int8, device=dev)
+            self.color = torch.zeros(E, dtype=torch.long, device=dev)
+            self.turn_count = torch.full((E,), -2, dtype=torch.long, device=dev)
+            self.win = torch.full((E,), -1, dtype=torch.long, device=dev)
+            self.cnt = torch.zeros(E, 4, dtype=torch.long, device=dev)
+        self.board.fill_(-1)
+        self.color.zero_()
+        self.turn_count.fill_(-2)
+        self.win.fill_(-1)
+        self.cnt.zero_()
 
     def turn(self):
         return self.color
@@ -385,10 +392,10 @@ class GeisterBatch:
         self.board[rows, src] = src_val.to(torch.int8)
         dst_val = torch.where(on, piece, self.board[rows, dst_s].long())
         self.board[rows, dst_s] = dst_val.to(torch.int8)
-        self.color = torch.where(active, 1 - c, c)
-        self.turn_count = self.turn_count + active.long()
+        self.color.copy_(torch.where(active, 1 - c, c))
+        self.turn_count.add_(active.long())
         draw = moving & (self.turn_count >= self.MAX_MOVES) & (win < 0)
-        self.win = torch.where(draw, torch.full_like(win, 2), win)
+        self.win.copy_(torch.where(draw, torch.full_like(win, 2), win))
 
     COMPLETE_INFO = False   # CIGeister (ci_geister.py:520-568) shows the opponent's colours in every view
 

@@ -49,11 +49,18 @@ class TicTacToeBatch:
         self.reset()
 
     def reset(self):
+        """State tensors are allocated once and then reset and advanced in place, so a HIP graph captured
+        over a ply (DeviceGenerator) keeps addressing them."""
         E, dev = self.E, self.device
-        self.board = torch.zeros(E, 9, dtype=torch.int8, device=dev)     # +1 black, -1 white
-        self.color = torch.ones(E, dtype=torch.int8, device=dev)          # side to move
-        self.nmoves = torch.zeros(E, dtype=torch.int32, device=dev)
-        self.winner = torch.zeros(E, dtype=torch.int8, device=dev)
+        if not hasattr(self, 'board'):
+            self.board = torch.zeros(E, 9, dtype=torch.int8, device=dev)     # +1 black, -1 white
+            self.color = torch.ones(E, dtype=torch.int8, device=dev)          # side to move
+            self.nmoves = torch.zeros(E, dtype=torch.int32, device=dev)
+            self.winner = torch.zeros(E, dtype=torch.int8, device=dev)
+        self.board.zero_()
+        self.color.fill_(1)
+        self.nmoves.zero_()
+        self.winner.zero_()
 
     def turn(self):
         """Index of the player to move: 0 (black) on even plies."""
@@ -84,9 +91,9 @@ class TicTacToeBatch:
         self.board[rows, act] = new
         sums = self.board.long()[:, self.lines].sum(-1)                   # (E, 8)
         won = active & (sums == 3 * self.color.long().view(-1, 1)).any(-1)
-        self.winner = torch.where(won, self.color, self.winner)
-        self.color = torch.where(active, -self.color, self.color)
-        self.nmoves = self.nmoves + active.int()
+        self.winner.copy_(torch.where(won, self.color, self.winner))
+        self.color.copy_(torch.where(active, -self.color, self.color))
+        self.nmoves.add_(active.int())
 
     def outcome(self):
         """(E, 2) float: +1/-1 for the winner/loser, 0/0 for a draw (tictactoe.py:140-147)."""
@@ -110,82 +117,180 @@ class DeviceGenerator:
     (``env.reward()``, e.g. Geister's -0.01 per ply) are recorded for both
     players every ply and turned into discounted returns in fp64 exactly as
     the reference's Python-float loop (generation.py:73-77).
+
+    Every buffer of a call (episode tensors, hidden state, the ply's uniforms,
+    the ply index as a device scalar) is allocated once and reset in place, and
+    the ply body addresses the current ply through that device scalar.  So on
+    a GPU the ply is captured ONCE per mover parity as a HIP graph (``graph``;
+    default: on for CUDA envs whose mover is ply % P) and each ply is one
+    graph replay instead of ≈100 small launches; the discounted-return loop is
+    a third graph.  Eager and graph mode run the same ply function on the same
+    uniforms (one (Tm, E, A) draw per call), so they give the same episodes.
     """
 
-    def __init__(self, env_batch, net, gamma=0.8, check_every=16):
+    def __init__(self, env_batch, net, gamma=0.8, check_every=16, graph=None):
         self.env = env_batch
         self.net = net
         self.gamma = gamma
         self.check_every = check_every
+        self.graph = graph
+        self._st = None
+
+    def _use_graph(self):
+        dev = torch.device(self.env.device)
+        if self.graph is None:
+            return dev.type == 'cuda' and getattr(self.env, 'ALTERNATING', False)
+        return bool(self.graph) and dev.type == 'cuda'
+
+    def _state(self):
+        """The call's buffers, allocated once per (generator, net)."""
+        if self._st is not None and self._st['net'] is self.net:
+            return self._st
+        env, E, dev = self.env, self.env.E, self.env.device
+        Tm, A, P = env.MAX_PLIES, env.A, env.P
+        st = {'net': self.net, 'graphs': None,
+              'obs': _alloc(env.OBS_SHAPE, (E, Tm), dev),
+              'policy': torch.zeros(E, Tm, A, device=dev),
+              'amask': torch.full((E, Tm, A), 1e32, device=dev),
+              'action': torch.zeros(E, Tm, dtype=torch.long, device=dev),
+              'value': torch.zeros(E, Tm, device=dev),
+              'turn': torch.zeros(E, Tm, dtype=torch.long, device=dev),
+              'reward': torch.zeros(E, Tm, P, device=dev, dtype=torch.float64),  # Python floats in the reference
+              'ret': torch.zeros(E, Tm, P, device=dev),
+              'U': torch.empty(Tm, E, A, device=dev),
+              't': torch.zeros(1, dtype=torch.long, device=dev),
+              'rows': torch.arange(E, device=dev),
+              'hidden': None}
+        if hasattr(self.net, 'init_hidden'):
+            st['hidden'] = map_r(self.net.init_hidden([E, P]), lambda h: h.to(dev).contiguous())
+        self._st = st
+        return st
+
+    def _reset(self, st, generator, draw=True):
+        self.env.reset()
+        map_r(st['obs'], lambda b: b.zero_())
+        for k in ('policy', 'action', 'value', 'turn', 'reward', 'ret'):
+            st[k].zero_()
+        st['amask'].fill_(1e32)
+        if st['hidden'] is not None:
+            map_r(st['hidden'], lambda h: h.zero_())
+        if draw:
+            torch.rand(st['U'].shape, out=st['U'], generator=generator, device=st['U'].device)
+            st['U'].clamp_(1e-20, 1.0)
+        st['t'].zero_()
+
+    def _ply(self, st, mover):
+        """One ply for every game at ply index st['t'] (a device scalar, advanced here); ``mover``: the
+        player index every live game moves with (ALTERNATING envs), or None."""
+        env, E = self.env, self.env.E
+        t = st['t']
+        hidden = st['hidden']
+        active = ~env.terminal()
+        player = env.turn()
+        o = env.observation(player)
+        # envs whose mover is ply % P in every live game (TicTacToe, Geister): the mover's state is a view
+        if hidden is None:
+            h_in = None
+        elif mover is not None:
+            h_in = map_r(hidden, lambda h: h[:, mover])
+        else:
+            h_in = map_r(hidden, lambda h: h[st['rows'], player])
+        out = self.net(o, h_in)
+        m = torch.where(env.legal(), 0.0, 1e32)                        # generation.py:50-51
+        p = out['policy'] - m
+        u = st['U'].index_select(0, t).view(E, -1)
+        a = torch.argmax(p - torch.log(-torch.log(u)), dim=-1)          # Gumbel-max = softmax over legal
+        act = active.view(-1, 1)
+
+        # slot t of every record is written once per call, so a finished game keeps the reset value
+        def record(buf, x, fill=0):
+            live = active.view(-1, *([1] * (x.dim() - 1)))
+            buf.index_copy_(1, t, torch.where(live, x, fill).to(buf.dtype).unsqueeze(1))
+        bimap_r(st['obs'], o, record)
+        record(st['policy'], p)
+        record(st['amask'], m, 1e32)
+        record(st['action'], a)
+        record(st['value'], out['value'].view(-1))
+        record(st['turn'], player)
+        if hasattr(env, 'reward'):
+            record(st['reward'], env.reward())
+        if hidden is not None:
+            def advance(h, nh):
+                live = active.view(-1, *([1] * (nh.dim() - 1)))
+                if mover is not None:
+                    h[:, mover].copy_(torch.where(live, nh, h[:, mover]))
+                else:
+                    h[st['rows'], player] = torch.where(live, nh, h[st['rows'], player])
+            bimap_r(hidden, out['hidden'], advance)
+        env.step(a, active)
+        t.add_(1)
+
+    def _returns(self, st):
+        """Discounted returns per player, fp64 like the reference's Python floats (generation.py:73-77)."""
+        reward, ret = st['reward'], st['ret']
+        acc = torch.zeros_like(reward[:, 0])
+        for t in range(reward.shape[1] - 1, -1, -1):
+            acc = reward[:, t] + self.gamma * acc
+            ret[:, t].copy_(acc)
+
+    def _capture(self, st, keys):
+        """Graphs of the ply (one per mover key) and of the return loop; warm-up plies run first on a side
+        stream (library workspaces), then the state is reset."""
+        dev = torch.device(self.env.device)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for k in keys:
+                self._ply(st, k)
+            self._returns(st)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graphs, pool = {}, None
+        for k in list(keys) + ['returns']:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                if k == 'returns':
+                    self._returns(st)
+                else:
+                    self._ply(st, k)
+            pool = g.pool()
+            graphs[k] = g
+        st['graphs'] = graphs
+        self._reset(st, None, draw=False)   # the call's uniforms stay as drawn
 
     @torch.no_grad()
     def generate(self, generator=None):
-        env, E, dev = self.env, self.env.E, self.env.device
-        Tm, A, P = env.MAX_PLIES, env.A, env.P
-        env.reset()
-        rows = torch.arange(E, device=dev)
-        obs = _alloc(env.OBS_SHAPE, (E, Tm), dev)
-        policy = torch.zeros(E, Tm, A, device=dev)
-        amask = torch.full((E, Tm, A), 1e32, device=dev)
-        action = torch.zeros(E, Tm, dtype=torch.long, device=dev)
-        value = torch.zeros(E, Tm, device=dev)
-        turn = torch.zeros(E, Tm, dtype=torch.long, device=dev)
-        reward = torch.zeros(E, Tm, P, device=dev, dtype=torch.float64)   # Python floats in the reference
-        has_reward = hasattr(env, 'reward')
-        hidden = None
-        if hasattr(self.net, 'init_hidden'):
-            hidden = map_r(self.net.init_hidden([E, P]), lambda h: h.to(dev))
+        env = self.env
+        Tm, P = env.MAX_PLIES, env.P
+        alternating = getattr(env, 'ALTERNATING', False)
+        st = self._state()
         was_training = self.net.training
         self.net.eval()
+        self._reset(st, generator)
+        graphs = None
+        if self._use_graph():
+            if st['graphs'] is None:
+                self._capture(st, list(range(P)) if alternating else [None])
+            graphs = st['graphs']
         for t in range(Tm):
             if t and self.check_every and t % self.check_every == 0 and bool(env.terminal().all()):
                 break
-            active = ~env.terminal()
-            player = env.turn()
-            o = env.observation(player)
-            # envs whose mover is ply % P in every live game (TicTacToe, Geister): the mover's state is a view
-            mover = t % P if getattr(env, 'ALTERNATING', False) else None
-            if hidden is None:
-                h_in = None
-            elif mover is not None:
-                h_in = map_r(hidden, lambda h: h[:, mover])
+            mover = t % P if alternating else None
+            if graphs is not None:
+                graphs[mover].replay()
             else:
-                h_in = map_r(hidden, lambda h: h[rows, player])
-            out = self.net(o, h_in)
-            m = torch.where(env.legal(), 0.0, 1e32)                        # generation.py:50-51
-            p = out['policy'] - m
-            u = torch.rand(E, A, device=dev, generator=generator).clamp_(1e-20, 1.0)
-            a = torch.argmax(p - torch.log(-torch.log(u)), dim=-1)          # Gumbel-max = softmax over legal
-            act = active.view(-1, 1)
-            bimap_r(obs, o, lambda buf, x: buf[:, t].copy_(
-                torch.where(active.view(-1, *([1] * (x.dim() - 1))), x, buf[:, t])))
-            policy[:, t] = torch.where(act, p, policy[:, t])
-            amask[:, t] = torch.where(act, m, amask[:, t])
-            action[:, t] = torch.where(active, a, action[:, t])
-            value[:, t] = torch.where(active, out['value'].view(-1), value[:, t])
-            turn[:, t] = torch.where(active, player, turn[:, t])
-            if has_reward:
-                reward[:, t] = torch.where(act, env.reward(), reward[:, t])
-            if hidden is not None:
-                def advance(h, nh):
-                    m = active.view(-1, *([1] * (nh.dim() - 1)))
-                    if mover is not None:
-                        h[:, mover].copy_(torch.where(m, nh, h[:, mover]))
-                    else:
-                        h[rows, player] = torch.where(m, nh, h[rows, player])
-                bimap_r(hidden, out['hidden'], advance)
-            env.step(a, active)
+                self._ply(st, mover)
         self.net.train(was_training)
-        length = env.plies().long()
-        # discounted returns per player, fp64 like the reference's Python floats (generation.py:73-77)
-        ret = torch.zeros(E, Tm, P, device=dev)
-        acc = torch.zeros(E, P, dtype=torch.float64, device=dev)
-        if has_reward:
-            for t in range(Tm - 1, -1, -1):
-                acc = reward[:, t] + self.gamma * acc
-                ret[:, t] = acc.float()
-        return {'observation': obs, 'policy': policy, 'action_mask': amask, 'action': action, 'value': value,
-                'turn': turn, 'length': length, 'outcome': env.outcome(), 'reward': reward.float(), 'return': ret}
+        if hasattr(env, 'reward'):
+            if graphs is not None:
+                graphs['returns'].replay()
+            else:
+                self._returns(st)
+        out = {'observation': map_r(st['obs'], lambda b: b.clone())}
+        for key, k in (('policy', 'policy'), ('action_mask', 'amask'), ('action', 'action'), ('value', 'value'),
+                       ('turn', 'turn'), ('return', 'ret')):
+            out[key] = st[k].clone()
+        out.update(length=env.plies().long(), outcome=env.outcome(), reward=st['reward'].float())
+        return out
 
 
 class DeviceReplay:

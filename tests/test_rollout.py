@@ -185,3 +185,35 @@ def test_selfplay_training_learns_tictactoe(cuda):
     after = evaluate_vs_random(net, cuda)
     assert after['win'] >= 0.8 and after['loss'] <= 0.05, (before, after)
     assert after['win'] > before['win'] + 0.2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('env_name', ['tictactoe', 'geister'])
+def test_graph_generate_equals_eager(cuda, env_name):
+    """DeviceGenerator's HIP-graph ply (one capture per mover parity, replayed every ply) plays exactly the
+    games of the eager ply loop on the same uniforms: every episode tensor bit-identical, over two calls (the
+    second replays the graphs captured by the first)."""
+    from handyrl_amd.rollout import TicTacToeBatch, DeviceGenerator
+    from handyrl_amd.nn import accelerate
+    if env_name == 'tictactoe':
+        from handyrl_amd.envs.tictactoe import SimpleConv2dModel as Net
+        env_cls, E = TicTacToeBatch, 512
+    else:
+        from handyrl_amd.envs.geister import GeisterNet as Net, GeisterBatch as env_cls
+        E = 64
+    torch.manual_seed(1)
+    net = accelerate(Net().to(cuda))
+    eager = DeviceGenerator(env_cls(E, cuda), net, graph=False)
+    graph = DeviceGenerator(env_cls(E, cuda), net, graph=True)
+    for call in range(2):
+        a = eager.generate(generator=torch.Generator(device=cuda).manual_seed(call))
+        b = graph.generate(generator=torch.Generator(device=cuda).manual_seed(call))
+        assert graph._st['graphs'] is not None and eager._st['graphs'] is None
+        assert set(a) == set(b)
+        for k in a:
+            if isinstance(a[k], dict):
+                for kk in a[k]:
+                    assert torch.equal(a[k][kk], b[k][kk]), (call, k, kk)
+            else:
+                assert torch.equal(a[k], b[k]), (call, k)
+        assert int(a['length'].min()) > 0

@@ -21,6 +21,7 @@ def main():
     ap.add_argument('--env', default='geister')
     ap.add_argument('--games', type=int, default=2048)
     ap.add_argument('--reps', type=int, default=2)
+    ap.add_argument('--graph', type=int, default=1, help='1: one HIP graph per ply (default), 0: eager plies')
     opts = ap.parse_args()
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
@@ -30,7 +31,7 @@ def main():
     else:
         from handyrl_amd.envs.tictactoe import SimpleConv2dModel
         net, env = accelerate(SimpleConv2dModel().to(dev)), TicTacToeBatch(opts.games, dev)
-    gen = DeviceGenerator(env, net)
+    gen = DeviceGenerator(env, net, graph=bool(opts.graph))
     g = torch.Generator(device=dev).manual_seed(0)
     gen.generate(generator=g)
     torch.cuda.synchronize(dev)
@@ -42,7 +43,7 @@ def main():
         loops += int(ep['length'].max())
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    print(json.dumps({'env': opts.env, 'games': opts.games, 'env_steps_per_s': round(plies / dt, 1),
+    print(json.dumps({'env': opts.env, 'games': opts.games, 'graph': opts.graph, 'env_steps_per_s': round(plies / dt, 1),
                       'ms_per_ply_loop': round(dt / loops * 1e3, 3), 'ply_loops': loops}), flush=True)
 
 
