@@ -150,9 +150,20 @@ SIGNATURES = {
                                              ctypes.c_void_p]),
     'hrl_bn_backward_apply_masked': (ctypes.c_int, [_f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p,
                                                     _f32p, _f32p, _f32p, ctypes.c_void_p]),
+    'hrl_geister_legal': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _i64, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+    'hrl_geister_observation': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               _i64, ctypes.c_int, _f32p, _f32p, ctypes.c_void_p]),
+    'hrl_geister_step': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_selfplay_sample_record': (ctypes.c_int, [_f32p, _i64, ctypes.c_void_p, _f32p, ctypes.c_void_p, _f32p,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _i64, _i64,
+                                                  _i64, _i64, ctypes.c_void_p, _f32p, _f32p, ctypes.c_void_p, _f32p,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _lib = None
 

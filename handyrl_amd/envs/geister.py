@@ -339,8 +339,19 @@ class GeisterBatch:
     def terminal(self):
         return self.win >= 0
 
+    def _hip(self):
+        """On a GPU the rules run as csrc/hrl_geister.hip (one launch per call instead of ~30-95 torch ops);
+        the torch formulation below is the CPU path and the GPU rules test's twin."""
+        return self.board.is_cuda
+
     def legal(self):
         """(E, 214) bool legal-action mask of the side to move (geister.py:460-487)."""
+        if self._hip():
+            from .._native import load, check, ptr, stream_of
+            out = torch.empty(self.E, self.A, dtype=torch.bool, device=self.device)
+            check(load().hrl_geister_legal(ptr(self.board), ptr(self.color), ptr(self.turn_count), self.E, ptr(out),
+                                           stream_of(self.board.device)), 'hrl_geister_legal')
+            return out
         b = self.board.long()
         own = (b >= 0) & (b // 2 == self.color.view(-1, 1))                     # (E, 36)
         own_blue = own & (b % 2 == 0)
@@ -357,6 +368,15 @@ class GeisterBatch:
     def step(self, action, active):
         """Play `action` (E,) for the side to move in every `active` game (geister.py:359-394)."""
         E, dev = self.E, self.device
+        if self._hip():
+            from .._native import load, check, ptr, stream_of
+            assert action.shape == (E,) and active.shape == (E,)
+            action = action.to(torch.long).contiguous()
+            active = active.to(torch.bool).contiguous()
+            check(load().hrl_geister_step(ptr(self.board), ptr(self.color), ptr(self.turn_count), ptr(self.win),
+                                          ptr(self.cnt), ptr(action), ptr(active), ptr(self.layout_type),
+                                          ptr(self.opos), E, stream_of(self.board.device)), 'hrl_geister_step')
+            return
         rows = torch.arange(E, device=dev)
         c = self.color
         setting = active & (self.turn_count < 0)
@@ -402,6 +422,16 @@ class GeisterBatch:
     def observation(self, player, full=False):
         """{'board': (E,7,6,6), 'scalar': (E,18)} seen by `player` (E,) (geister.py:495-535, player given);
         ``full``: the reference's ``observation(None)`` view, which also shows the opponent's colours."""
+        if self._hip():
+            from .._native import load, check, ptr, stream_of
+            player = player.to(torch.long).contiguous()
+            assert player.shape == (self.E,)
+            planes = torch.empty(self.E, BOARD_PLANES, *BOARD, device=self.device)
+            scalar = torch.empty(self.E, SCALARS, device=self.device)
+            check(load().hrl_geister_observation(ptr(self.board), ptr(self.color), ptr(self.cnt), ptr(player), self.E,
+                                                 int(bool(full or self.COMPLETE_INFO)), ptr(planes), ptr(scalar),
+                                                 stream_of(self.board.device)), 'hrl_geister_observation')
+            return {'board': planes, 'scalar': scalar}
         turn_view = player == self.color
         me = torch.where(turn_view, self.color, 1 - self.color)
         opp = 1 - me

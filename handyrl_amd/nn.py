@@ -1083,6 +1083,24 @@ class _HiddenGather(torch.autograd.Function):
         return (None, None, None, None, *dH)
 
 
+def hidden_advance_(H, nh, mask):
+    """Self-play's recurrent state advance in place, one launch for every state tensor:
+    H[l] = H[l] * (1 - mask) + nh[l] * mask  (hrl_hidden_update with the output aliasing H; each element is
+    read and written by the same thread).  H[l]: (E, P, *shape) contiguous state per game and player,
+    nh[l]: (E, *shape) the mover's new state, mask: (E, P) fp32 {0, 1}.  For finite states this is
+    torch.where(mask, nh, H) exactly (generation.py:38-41: only the mover's state advances)."""
+    E, P = mask.shape
+    assert mask.dtype == torch.float32 and mask.is_contiguous() and len(H) == len(nh)
+    nh = [x.contiguous() for x in nh]
+    for h, x in zip(H, nh):
+        assert h.is_contiguous() and h.dtype == torch.float32 and h.shape[:2] == (E, P) and x.shape[0] == E
+        assert h[0, 0].numel() == x[0].numel()
+    F = [h[0, 0].numel() for h in H]
+    _native.check(_native.load().hrl_hidden_update(
+        _native.ptr_array(H), _native.ptr_array(nh), 1, _native.ptr(mask), E, P, len(H), _native.i64_array(F),
+        _native.ptr_array(H), _native.stream_of(mask.device)), 'hrl_hidden_update')
+
+
 class _HiddenUpdate(torch.autograd.Function):
     """New state H[l] * (1 - m) + nh[l] * m (csrc/hrl_hidden.hip, train.py:167-174), one launch for all.
 

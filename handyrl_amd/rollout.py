@@ -101,11 +101,70 @@ class TicTacToeBatch:
         return torch.stack([w, -w], dim=1)
 
 
+def _leaves(x):
+    """The tensors of a nested list / tuple / dict, in order."""
+    out = []
+    map_r(x, out.append)
+    return out
+
+
 def _alloc(spec, lead, device, dtype=torch.float32):
     """Zero tensors (*lead, *shape) for an observation spec: a shape tuple or {name: shape}."""
     if isinstance(spec, dict):
         return {k: torch.zeros(*lead, *v, device=device, dtype=dtype) for k, v in spec.items()}
     return torch.zeros(*lead, *spec, device=device, dtype=dtype)
+
+
+def sample_record_torch(st, logits, legal, value, active, player, reward):
+    """The ply's sampling and recording tail as torch ops (generation.py:43-62): illegal logits masked by
+    -1e32, Gumbel-max over the ply's uniforms st['U'][t] (the distribution of random.choices over the softmax
+    of the legal logits), and slot t of the policy / action mask / action / value / turn / reward records
+    (reset values for finished games).  Returns the sampled action per game."""
+    E, t = logits.shape[0], st['t']
+    m = torch.where(legal, 0.0, 1e32)                                  # generation.py:50-51
+    p = logits - m
+    u = st['U'].index_select(0, t).view(E, -1)
+    a = torch.argmax(p - torch.log(-torch.log(u)), dim=-1)              # Gumbel-max = softmax over legal
+
+    def record(buf, x, fill=0):
+        live = active.view(-1, *([1] * (x.dim() - 1)))
+        buf.index_copy_(1, t, torch.where(live, x, fill).to(buf.dtype).unsqueeze(1))
+    record(st['policy'], p)
+    record(st['amask'], m, 1e32)
+    record(st['action'], a)
+    record(st['value'], value.reshape(-1))
+    record(st['turn'], player)
+    if reward is not None:
+        record(st['reward'], reward)
+    return a
+
+
+def sample_record_hip(st, logits, legal, value, active, player, reward):
+    """sample_record_torch as ONE launch (csrc/hrl_selfplay.hip, one wave per game): the same fp32 operations,
+    torch.argmax's tie order, the same records."""
+    from . import _native
+    E, A = logits.shape
+    Tm = st['action'].shape[1]
+    P = st['reward'].shape[2]
+    logits = logits.float()
+    if logits.stride(1) != 1:
+        logits = logits.contiguous()
+    value = value.reshape(E).float().contiguous()
+    legal, active = legal.contiguous(), active.contiguous()
+    player = player.to(torch.long).contiguous()
+    assert legal.shape == (E, A) and legal.dtype == torch.bool and active.shape == (E,) and player.shape == (E,)
+    assert st['policy'].shape == (E, Tm, A) and st['U'].shape == (Tm, E, A)
+    if reward is not None:
+        reward = reward.to(torch.float64).contiguous()
+        assert reward.shape == (E, P)
+    a = torch.empty(E, dtype=torch.long, device=logits.device)
+    _native.check(_native.load().hrl_selfplay_sample_record(
+        _native.ptr(logits), logits.stride(0), _native.ptr(legal), _native.ptr(st['U']), _native.ptr(st['t']),
+        _native.ptr(value), _native.ptr(active), _native.ptr(player), _native.ptr(reward), E, A, Tm, P,
+        _native.ptr(a), _native.ptr(st['policy']), _native.ptr(st['amask']), _native.ptr(st['action']),
+        _native.ptr(st['value']), _native.ptr(st['turn']), None if reward is None else _native.ptr(st['reward']),
+        _native.stream_of(logits.device)), 'hrl_selfplay_sample_record')
+    return a
 
 
 class DeviceGenerator:
@@ -160,9 +219,12 @@ class DeviceGenerator:
               'U': torch.empty(Tm, E, A, device=dev),
               't': torch.zeros(1, dtype=torch.long, device=dev),
               'rows': torch.arange(E, device=dev),
-              'hidden': None}
+              'hidden': None, 'obs_dev': torch.device(dev).type}
+        st['hmask'] = None
         if hasattr(self.net, 'init_hidden'):
             st['hidden'] = map_r(self.net.init_hidden([E, P]), lambda h: h.to(dev).contiguous())
+            if torch.device(dev).type == 'cuda' and all(h.dtype == torch.float32 for h in _leaves(st['hidden'])):
+                st['hmask'] = torch.zeros(E, P, device=dev)
         self._st = st
         return st
 
@@ -196,25 +258,21 @@ class DeviceGenerator:
         else:
             h_in = map_r(hidden, lambda h: h[st['rows'], player])
         out = self.net(o, h_in)
-        m = torch.where(env.legal(), 0.0, 1e32)                        # generation.py:50-51
-        p = out['policy'] - m
-        u = st['U'].index_select(0, t).view(E, -1)
-        a = torch.argmax(p - torch.log(-torch.log(u)), dim=-1)          # Gumbel-max = softmax over legal
-        act = active.view(-1, 1)
-
+        reward = env.reward() if hasattr(env, 'reward') else None
         # slot t of every record is written once per call, so a finished game keeps the reset value
         def record(buf, x, fill=0):
             live = active.view(-1, *([1] * (x.dim() - 1)))
             buf.index_copy_(1, t, torch.where(live, x, fill).to(buf.dtype).unsqueeze(1))
         bimap_r(st['obs'], o, record)
-        record(st['policy'], p)
-        record(st['amask'], m, 1e32)
-        record(st['action'], a)
-        record(st['value'], out['value'].view(-1))
-        record(st['turn'], player)
-        if hasattr(env, 'reward'):
-            record(st['reward'], env.reward())
-        if hidden is not None:
+        sample = sample_record_hip if st['obs_dev'] == 'cuda' else sample_record_torch
+        a = sample(st, out['policy'], env.legal(), out['value'], active, player, reward)
+        if hidden is not None and mover is not None and st['hmask'] is not None:
+            # one HIP launch for every state tensor (nn.hidden_advance_) instead of a where + copy per tensor
+            from .nn import hidden_advance_
+            st['hmask'].zero_()
+            st['hmask'][:, mover].copy_(active)
+            hidden_advance_(_leaves(hidden), _leaves(out['hidden']), st['hmask'])
+        elif hidden is not None:
             def advance(h, nh):
                 live = active.view(-1, *([1] * (nh.dim() - 1)))
                 if mover is not None:

@@ -155,3 +155,37 @@ def test_geister_replay_gather_equals_make_batch(generated, T):
             got = batch[k]
             assert got.shape == v.shape and got.dtype == v.dtype, (k, got.shape, v.shape)
             np.testing.assert_array_equal(got.numpy(), v.numpy(), err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('full', [False, True])
+def test_hip_rules_match_torch_rules_random_games(cuda, full):
+    """csrc/hrl_geister.hip (GeisterBatch on a GPU) vs the torch rules (GeisterBatch on the CPU, pinned to the
+    reference games above): 512 random games side by side, every ply's legal mask, both players' views (and
+    the complete-information view), the state tensors and the outcomes identical.  Exercises escapes,
+    captures of both colours, the 200-move draw and frozen finished games far more often than 24 games."""
+    E = 512
+    gpu, cpu = GeisterBatch(E, cuda), GeisterBatch(E, torch.device('cpu'))
+    g = torch.Generator().manual_seed(11 + full)
+    for t in range(GeisterBatch.MAX_PLIES):
+        for name in ('board', 'color', 'turn_count', 'win', 'cnt'):
+            assert torch.equal(getattr(gpu, name).cpu(), getattr(cpu, name)), (t, name)
+        legal = cpu.legal()
+        assert torch.equal(gpu.legal().cpu(), legal), t
+        for q in (0, 1):
+            pl = torch.full((E,), q, dtype=torch.long)
+            a, b = gpu.observation(pl.to(cuda), full=full), cpu.observation(pl, full=full)
+            for k in ('board', 'scalar'):
+                assert torch.equal(a[k].cpu(), b[k]), (t, q, k)
+        active = ~cpu.terminal()
+        if not bool(active.any()):
+            break
+        # a random legal action per game (uniform over the legal labels); finished games pass action 0
+        w = legal.float() + 1e-12
+        act = torch.multinomial(w, 1, generator=g).view(-1)
+        gpu.step(act.to(cuda), active.to(cuda))
+        cpu.step(act, active)
+    assert bool(cpu.terminal().all())
+    wins = set(cpu.win.tolist())
+    assert {0, 1, 2} <= wins, wins
+    assert torch.equal(gpu.outcome().cpu(), cpu.outcome())

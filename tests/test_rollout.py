@@ -217,3 +217,39 @@ def test_graph_generate_equals_eager(cuda, env_name):
             else:
                 assert torch.equal(a[k], b[k]), (call, k)
         assert int(a['length'].min()) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('A', [9, 214])
+def test_sample_record_hip_matches_torch(cuda, A):
+    """csrc/hrl_selfplay.hip (one launch) vs the torch formulation of the ply tail on the same device tensors:
+    sampled actions and every record slot bit-identical, including rows with no legal action (all logits
+    -1e32: torch.argmax's tie order picks the lowest label), finished games (reset values) and untouched
+    slots of other plies."""
+    from handyrl_amd.rollout import sample_record_torch, sample_record_hip
+    E, Tm, P = 300, 5, 2
+    g = torch.Generator(device=cuda).manual_seed(A)
+
+    def state():
+        return {'policy': torch.full((E, Tm, A), 7.0, device=cuda), 'amask': torch.full((E, Tm, A), 3.0, device=cuda),
+                'action': torch.full((E, Tm), 5, dtype=torch.long, device=cuda),
+                'value': torch.full((E, Tm), 2.0, device=cuda),
+                'turn': torch.full((E, Tm), 4, dtype=torch.long, device=cuda),
+                'reward': torch.full((E, Tm, P), 9.0, dtype=torch.float64, device=cuda),
+                'U': torch.rand(Tm, E, A, device=cuda, generator=g).clamp_(1e-20, 1.0),
+                't': torch.tensor([3], device=cuda)}
+    a_st = state()
+    b_st = {k: v.clone() for k, v in a_st.items()}
+    logits = torch.randn(E, A + 3, device=cuda, generator=g)[:, :A]          # strided rows
+    legal = torch.rand(E, A, device=cuda, generator=g) < 0.4
+    legal[:7] = False
+    value = torch.randn(E, 1, device=cuda, generator=g)
+    active = torch.rand(E, device=cuda, generator=g) < 0.8
+    player = (torch.rand(E, device=cuda, generator=g) < 0.5).long()
+    reward = torch.randn(E, P, device=cuda, generator=g, dtype=torch.float64)
+    a = sample_record_torch(a_st, logits, legal, value, active, player, reward)
+    b = sample_record_hip(b_st, logits, legal, value, active, player, reward)
+    assert torch.equal(a, b)
+    assert bool((a[:7] == 0).all())
+    for k in ('policy', 'amask', 'action', 'value', 'turn', 'reward'):
+        assert torch.equal(a_st[k], b_st[k]), k
