@@ -161,6 +161,9 @@ SIGNATURES = {
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _i64, _i64,
                                                   _i64, _i64, ctypes.c_void_p, _f32p, _f32p, ctypes.c_void_p, _f32p,
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    'hrl_masked_rows_copy': (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _i64,
+                                            ctypes.c_void_p]),
 }
 
 ABI_VERSION = 14

@@ -81,9 +81,48 @@ __global__ __launch_bounds__(kWave *kGamesPerBlock) void sample_record_kernel(
     }
 }
 
+// ---- the movers' recurrent state advance (generation.py:38-41): dst[l] row e <- src[l] row e where mask[e] ----
+constexpr int kMaxRowLeaves = 16;
+struct RowLeaves {
+    float *dst[kMaxRowLeaves];
+    const float *src[kMaxRowLeaves];
+    int64_t dst_stride[kMaxRowLeaves], src_stride[kMaxRowLeaves], F[kMaxRowLeaves];
+};
+
+__global__ __launch_bounds__(256) void masked_rows_kernel(const uint8_t *__restrict__ mask, RowLeaves L) {
+    const int64_t e = blockIdx.x;
+    const int l = blockIdx.y;
+    if (!mask[e]) return;
+    const float *s = L.src[l] + e * L.src_stride[l];
+    float *d = L.dst[l] + e * L.dst_stride[l];
+    for (int64_t f = threadIdx.x; f < L.F[l]; f += blockDim.x) d[f] = s[f];
+}
+
 }  // namespace
 
 extern "C" {
+
+int hrl_masked_rows_copy(int nleaves, float *const *dst, const int64_t *dst_stride, const float *const *src,
+                         const int64_t *src_stride, const int64_t *F, const uint8_t *mask, int64_t E, void *stream) {
+    if (nleaves < 1 || nleaves > kMaxRowLeaves || !dst || !dst_stride || !src || !src_stride || !F || !mask || E < 0 ||
+        E > 0x7fffffff)
+        return HRL_EINVAL;
+    RowLeaves L{};
+    for (int l = 0; l < nleaves; ++l) {
+        if (!dst[l] || !src[l] || F[l] < 1 || dst_stride[l] < F[l] || src_stride[l] < F[l]) return HRL_EINVAL;
+        L.dst[l] = dst[l];
+        L.src[l] = src[l];
+        L.dst_stride[l] = dst_stride[l];
+        L.src_stride[l] = src_stride[l];
+        L.F[l] = F[l];
+    }
+    if (E == 0) return HRL_OK;
+    hipLaunchKernelGGL(masked_rows_kernel, dim3((unsigned)E, nleaves), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       mask, L);
+    const hipError_t err = hipGetLastError();
+    return err == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)err;
+}
+
 
 int hrl_selfplay_sample_record(const float *logits, int64_t logit_stride, const uint8_t *legal, const float *U,
                                const int64_t *t, const float *value, const uint8_t *active, const int64_t *player,

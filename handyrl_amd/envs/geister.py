@@ -82,6 +82,8 @@ class DRC(nn.Module):
             hidden = tuple([t.to(x.device) for t in ts] for ts in self.init_hidden(x.shape[-2:], x.shape[:-3]))
         hs, cs = list(hidden[0]), list(hidden[1])
         if self.use_hip and x.is_cuda:
+            if not torch.is_grad_enabled():
+                return self._inference_stacked(x, hs, cs, num_repeats)
             return self._forward_hip(x, hs, cs, num_repeats)
         for _ in range(num_repeats):
             for i, blk in enumerate(self.blocks):
@@ -98,6 +100,35 @@ class DRC(nn.Module):
         concatenation, one gate launch per cell and direction.
         """
         return self.step_hip(self.x_halves(x), hs, cs, num_repeats)
+
+    def _inference_stacked(self, x, hs, cs, num_repeats):
+        """Inference (self-play, no autograd) with the layers stacked along channels.
+
+        Within a repeat the cells are independent (each reads x and its own state), so the n layers' h
+        halves run as ONE grouped convolution (n*H -> n*4H, groups = n) and their gates as one HIP
+        launch over n*E cells; the x halves are one n*4H-channel convolution as in _forward_hip.  Per
+        step n*repeats convolutions and gate passes become repeats of each (9 -> 3 for GeisterNet).
+        The grouped convolution computes each group's products as the per-layer one does
+        (tests/test_geister.py::test_stacked_inference_matches_cells).  The state comes back as channel
+        slices of the stacked tensors."""
+        from ..nn import lstm_gates
+        n = len(self.blocks)
+        ws = [blk.conv.weight for blk in self.blocks]
+        pad = self.blocks[0].conv.padding
+        hd = self.blocks[0].hidden_dim
+        cin = ws[0].shape[1] - hd
+        E, HW = x.shape[0], x.shape[-2:]
+        bias = None if self.blocks[0].conv.bias is None else torch.cat([blk.conv.bias for blk in self.blocks])
+        z = F.conv2d(x, torch.cat([w[:, :cin] for w in ws]), bias, padding=pad)       # (E, n*4H, *HW)
+        w_h = torch.cat([w[:, cin:] for w in ws])                                        # (n*4H, H, 3, 3)
+        h, c = torch.cat(hs, 1), torch.cat(cs, 1)                                        # (E, n*H, *HW)
+        zx = z.view(E * n, 4 * hd, *HW)
+        for _ in range(num_repeats):
+            zh = F.conv2d(h, w_h, None, padding=pad, groups=n)
+            h, c = lstm_gates(zx, zh.view(E * n, 4 * hd, *HW), c.view(E * n, hd, *HW))
+            h, c = h.view(E, n * hd, *HW), c.view(E, n * hd, *HW)
+        hs, cs = list(h.split(hd, 1)), list(c.split(hd, 1))
+        return hs[-1], (hs, cs)
 
     def x_halves(self, x):
         """conv_x(x) + bias of every cell (the part of conv([x, h]) that does not depend on the state); x may

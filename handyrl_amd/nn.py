@@ -1083,22 +1083,22 @@ class _HiddenGather(torch.autograd.Function):
         return (None, None, None, None, *dH)
 
 
-def hidden_advance_(H, nh, mask):
-    """Self-play's recurrent state advance in place, one launch for every state tensor:
-    H[l] = H[l] * (1 - mask) + nh[l] * mask  (hrl_hidden_update with the output aliasing H; each element is
-    read and written by the same thread).  H[l]: (E, P, *shape) contiguous state per game and player,
-    nh[l]: (E, *shape) the mover's new state, mask: (E, P) fp32 {0, 1}.  For finite states this is
-    torch.where(mask, nh, H) exactly (generation.py:38-41: only the mover's state advances)."""
-    E, P = mask.shape
-    assert mask.dtype == torch.float32 and mask.is_contiguous() and len(H) == len(nh)
-    nh = [x.contiguous() for x in nh]
-    for h, x in zip(H, nh):
-        assert h.is_contiguous() and h.dtype == torch.float32 and h.shape[:2] == (E, P) and x.shape[0] == E
-        assert h[0, 0].numel() == x[0].numel()
-    F = [h[0, 0].numel() for h in H]
-    _native.check(_native.load().hrl_hidden_update(
-        _native.ptr_array(H), _native.ptr_array(nh), 1, _native.ptr(mask), E, P, len(H), _native.i64_array(F),
-        _native.ptr_array(H), _native.stream_of(mask.device)), 'hrl_hidden_update')
+def masked_rows_copy_(dst, src, mask):
+    """dst[l][e] = src[l][e] where mask[e], for every tensor pair, in ONE launch (csrc/hrl_selfplay.hip):
+    self-play's recurrent state advance (generation.py:38-41, only the mover's state moves).  dst[l], src[l]:
+    (E, *shape) fp32 with contiguous rows (any row stride, e.g. the mover's slice h[:, p] of an (E, P, ...)
+    state or a channel slice of a stacked one); mask: (E,) bool.  Exactly torch.where(mask, src, dst)."""
+    E = mask.shape[0]
+    assert mask.dtype == torch.bool and mask.is_contiguous() and len(dst) == len(src)
+    F = []
+    for d, x in zip(dst, src):
+        assert d.is_cuda and d.dtype == torch.float32 and x.dtype == torch.float32
+        assert d.shape == x.shape and d.shape[0] == E and d[0].is_contiguous() and x[0].is_contiguous()
+        F.append(d[0].numel())
+    _native.check(_native.load().hrl_masked_rows_copy(
+        len(dst), _native.ptr_array(dst), _native.i64_array([d.stride(0) for d in dst]), _native.ptr_array(src),
+        _native.i64_array([x.stride(0) for x in src]), _native.i64_array(F), _native.ptr(mask), E,
+        _native.stream_of(mask.device)), 'hrl_masked_rows_copy')
 
 
 class _HiddenUpdate(torch.autograd.Function):

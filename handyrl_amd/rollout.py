@@ -220,11 +220,8 @@ class DeviceGenerator:
               't': torch.zeros(1, dtype=torch.long, device=dev),
               'rows': torch.arange(E, device=dev),
               'hidden': None, 'obs_dev': torch.device(dev).type}
-        st['hmask'] = None
         if hasattr(self.net, 'init_hidden'):
             st['hidden'] = map_r(self.net.init_hidden([E, P]), lambda h: h.to(dev).contiguous())
-            if torch.device(dev).type == 'cuda' and all(h.dtype == torch.float32 for h in _leaves(st['hidden'])):
-                st['hmask'] = torch.zeros(E, P, device=dev)
         self._st = st
         return st
 
@@ -266,12 +263,10 @@ class DeviceGenerator:
         bimap_r(st['obs'], o, record)
         sample = sample_record_hip if st['obs_dev'] == 'cuda' else sample_record_torch
         a = sample(st, out['policy'], env.legal(), out['value'], active, player, reward)
-        if hidden is not None and mover is not None and st['hmask'] is not None:
-            # one HIP launch for every state tensor (nn.hidden_advance_) instead of a where + copy per tensor
-            from .nn import hidden_advance_
-            st['hmask'].zero_()
-            st['hmask'][:, mover].copy_(active)
-            hidden_advance_(_leaves(hidden), _leaves(out['hidden']), st['hmask'])
+        if hidden is not None and mover is not None and st['obs_dev'] == 'cuda':
+            # one HIP launch for every state tensor (nn.masked_rows_copy_) instead of a where + copy per tensor
+            from .nn import masked_rows_copy_
+            masked_rows_copy_([h[:, mover] for h in _leaves(hidden)], _leaves(out['hidden']), active.contiguous())
         elif hidden is not None:
             def advance(h, nh):
                 live = active.view(-1, *([1] * (nh.dim() - 1)))

@@ -52,6 +52,13 @@ int hrl_selfplay_sample_record(const float *logits, int64_t logit_stride, const 
                                float *policy_buf, float *amask_buf, int64_t *action_buf, float *value_buf,
                                int64_t *turn_buf, double *reward_buf, void *stream);
 
+/* Masked row copy for the movers' recurrent state (generation.py:38-41: only the mover's hidden state
+ * advances): for each of nleaves (<= 16) fp32 tensors, row e of dst[l] (E rows of F[l] contiguous floats,
+ * row stride dst_stride[l] elements) becomes row e of src[l] where mask[e] != 0; other rows are untouched.
+ * One launch for every state tensor, exactly torch.where(mask, src, dst). */
+int hrl_masked_rows_copy(int nleaves, float *const *dst, const int64_t *dst_stride, const float *const *src,
+                         const int64_t *src_stride, const int64_t *F, const uint8_t *mask, int64_t E, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -200,6 +200,31 @@ def test_drc_hip_path_matches_reference_cells(golden, cuda):
 
 
 @pytest.mark.gpu
+def test_stacked_inference_matches_cells(golden, cuda):
+    """Inference (no autograd) stacks the DRC layers: one grouped h convolution and one gate launch per
+    repeat instead of one per layer.  Same outputs and states as the per-layer HIP path, and the reference
+    golden forward still holds."""
+    from handyrl_amd.nn import accelerate
+    _, arrays = golden
+    net = accelerate(seeded_net().to(cuda)).eval()
+    obs, hidden = fwd_inputs(arrays)
+    obs = {k: v.to(cuda) for k, v in obs.items()}
+    torch.manual_seed(3)
+    x = torch.randn(96, 32, 6, 6, device=cuda)
+    hs = [torch.randn(96, 32, 6, 6, device=cuda) for _ in range(3)]
+    cs = [torch.randn(96, 32, 6, 6, device=cuda) for _ in range(3)]
+    with torch.no_grad():
+        h_a, (hs_a, cs_a) = net.body._inference_stacked(x, list(hs), list(cs), 3)
+        h_b, (hs_b, cs_b) = net.body._forward_hip(x, list(hs), list(cs), 3)
+        for a, b in zip([h_a] + hs_a + cs_a, [h_b] + hs_b + cs_b):
+            torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6)
+        h = ([t.to(cuda) for t in hidden[0]], [t.to(cuda) for t in hidden[1]])
+        net.train()
+        out = net(obs, h)       # training-mode BatchNorm as in the golden, stacked DRC (no autograd)
+    check_forward(out, arrays, atol=2e-5)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('graph', [False, True])
 def test_gpu_recurrent_learner_matches_cpu_oracle(cuda, graph):
     """Three recurrent learner steps (LearnerStep on the GPU, HIP graph or eager) vs the oracle's
