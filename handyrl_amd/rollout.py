@@ -203,11 +203,13 @@ class DeviceGenerator:
 
     def _state(self):
         """The call's buffers, allocated once per (generator, net)."""
-        if self._st is not None and self._st['net'] is self.net:
+        # a captured ply reads the net's parameters and buffers where they live: recapture if any moved
+        key = tuple(t.data_ptr() for t in list(self.net.parameters()) + list(self.net.buffers()))
+        if self._st is not None and self._st['net'] is self.net and self._st['key'] == key:
             return self._st
         env, E, dev = self.env, self.env.E, self.env.device
         Tm, A, P = env.MAX_PLIES, env.A, env.P
-        st = {'net': self.net, 'graphs': None,
+        st = {'net': self.net, 'key': key, 'graphs': None,
               'obs': _alloc(env.OBS_SHAPE, (E, Tm), dev),
               'policy': torch.zeros(E, Tm, A, device=dev),
               'amask': torch.full((E, Tm, A), 1e32, device=dev),
