@@ -24,6 +24,8 @@ Observation format
 {'board': (7, 6, 6), 'scalar': (18,)}, 214 actions.
 """
 
+import contextlib
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -101,6 +103,34 @@ class DRC(nn.Module):
         """
         return self.step_hip(self.x_halves(x), hs, cs, num_repeats)
 
+    _session = None   # the stacked weights of an inference session (DRC.inference_session)
+
+    def _stacked_weights(self, out=None):
+        """The layers' x-half weights and biases and h-half weights, concatenated along the output channels
+        (into ``out``'s tensors when given)."""
+        ws = [blk.conv.weight for blk in self.blocks]
+        cin = ws[0].shape[1] - self.blocks[0].hidden_dim
+        out = out or {}
+        w_x = torch.cat([w[:, :cin] for w in ws], out=out.get('w_x'))
+        w_h = torch.cat([w[:, cin:] for w in ws], out=out.get('w_h'))
+        b_x = None
+        if self.blocks[0].conv.bias is not None:
+            b_x = torch.cat([blk.conv.bias for blk in self.blocks], out=out.get('b_x'))
+        return {'w_x': w_x, 'w_h': w_h, 'b_x': b_x}
+
+    @contextlib.contextmanager
+    def inference_session(self):
+        """Within the session the stacked inference weights are built once (refreshed in place from the
+        current parameters on entry, so HIP graphs captured in an earlier session stay valid) instead of
+        once per forward: DeviceGenerator.generate runs its plies in one."""
+        with torch.no_grad():
+            self._session_buf = self._stacked_weights(getattr(self, '_session_buf', None))
+        self._session = self._session_buf
+        try:
+            yield
+        finally:
+            self._session = None
+
     def _inference_stacked(self, x, hs, cs, num_repeats):
         """Inference (self-play, no autograd) with the layers stacked along channels.
 
@@ -118,9 +148,11 @@ class DRC(nn.Module):
         hd = self.blocks[0].hidden_dim
         cin = ws[0].shape[1] - hd
         E, HW = x.shape[0], x.shape[-2:]
-        bias = None if self.blocks[0].conv.bias is None else torch.cat([blk.conv.bias for blk in self.blocks])
-        z = F.conv2d(x, torch.cat([w[:, :cin] for w in ws]), bias, padding=pad)       # (E, n*4H, *HW)
-        w_h = torch.cat([w[:, cin:] for w in ws])                                        # (n*4H, H, 3, 3)
+        cache = self._session
+        if cache is None:
+            cache = self._stacked_weights()
+        z = F.conv2d(x, cache['w_x'], cache['b_x'], padding=pad)                          # (E, n*4H, *HW)
+        w_h = cache['w_h']                                                               # (n*4H, H, 3, 3)
         h, c = torch.cat(hs, 1), torch.cat(cs, 1)                                        # (E, n*H, *HW)
         zx = z.view(E * n, 4 * hd, *HW)
         for _ in range(num_repeats):
@@ -224,6 +256,9 @@ class GeisterNet(nn.Module):
         return self.body.init_hidden(BOARD, batch_size)
 
     def forward(self, x, hidden):
+        if (not self.training and self.body.use_hip and not torch.is_grad_enabled() and x['board'].is_cuda
+                and all(b.running_mean is not None for b in self._sequence_bns())):
+            return self._forward_inference(x, hidden)
         board, scalar = x['board'], x['scalar']
         planes = scalar[..., None, None].expand(*scalar.shape, *BOARD)
         h_e = F.relu(self.bn1(self.conv1(torch.cat([planes, board], dim=-3))))
@@ -232,6 +267,29 @@ class GeisterNet(nn.Module):
         policy = torch.cat([self.head_p_move(h), self.head_p_set(scalar[:, :1])], dim=-1)
         return {'policy': policy, 'value': torch.tanh(self.head_v(h)), 'return': self.head_r(h),
                 'hidden': hidden}
+
+    def inference_session(self):
+        return self.body.inference_session()
+
+    def _forward_inference(self, x, hidden):
+        """forward in eval mode without autograd on the HIP path (self-play): the same operations, with each
+        BatchNorm's ReLU folded into its HIP inference kernel (4 launches fewer per ply) and the DRC stacked
+        (DRC._inference_stacked)."""
+        from ..nn import batch_norm_eval
+
+        def bn_relu(bn, y):
+            return batch_norm_eval(y, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, relu=True)
+        board, scalar = x['board'], x['scalar']
+        planes = scalar[..., None, None].expand(*scalar.shape, *BOARD)
+        h_e = bn_relu(self.bn1, self.conv1(torch.cat([planes, board], dim=-3)))
+        h_last, hidden = self.body(h_e, hidden, self.num_repeats)
+        h = torch.cat([h_e, h_last], dim=-3)
+        hp, hv, hr = self.head_p_move, self.head_v, self.head_r
+        p_move = hp.conv2(bn_relu(hp.bn, hp.conv1(h))).reshape(-1, hp.outputs)
+        policy = torch.cat([p_move, self.head_p_set(scalar[:, :1])], dim=-1)
+        v = hv.fc(bn_relu(hv.bn, hv.conv(h)).reshape(-1, hv.hidden_units))
+        r = hr.fc(bn_relu(hr.bn, hr.conv(h)).reshape(-1, hr.hidden_units))
+        return {'policy': policy, 'value': torch.tanh(v), 'return': r, 'hidden': hidden}
 
     # ---- the learner's unroll in three parts (train._unroll_sequence) ----
     # forward_prediction runs the net once per time step (train.py:155-174).  Only the cells depend on

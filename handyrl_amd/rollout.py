@@ -25,6 +25,8 @@ Scope: turn-based two-player training without opponent observation
 (turn_based_training=True, observation=False), the TicTacToe configuration.
 """
 
+import contextlib
+
 import numpy as np
 import torch
 
@@ -314,12 +316,19 @@ class DeviceGenerator:
 
     @torch.no_grad()
     def generate(self, generator=None):
-        env = self.env
-        Tm, P = env.MAX_PLIES, env.P
-        alternating = getattr(env, 'ALTERNATING', False)
+        alternating = getattr(self.env, 'ALTERNATING', False)
         st = self._state()
         was_training = self.net.training
         self.net.eval()
+        session = getattr(self.net, 'inference_session', None)   # per-call weight preparation (GeisterNet)
+        with session() if session is not None else contextlib.nullcontext():
+            out = self._generate(st, generator, alternating)
+        self.net.train(was_training)
+        return out
+
+    def _generate(self, st, generator, alternating):
+        env = self.env
+        Tm, P = env.MAX_PLIES, env.P
         self._reset(st, generator)
         graphs = None
         if self._use_graph():
@@ -334,7 +343,6 @@ class DeviceGenerator:
                 graphs[mover].replay()
             else:
                 self._ply(st, mover)
-        self.net.train(was_training)
         if hasattr(env, 'reward'):
             if graphs is not None:
                 graphs['returns'].replay()

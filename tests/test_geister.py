@@ -225,6 +225,34 @@ def test_stacked_inference_matches_cells(golden, cuda):
 
 
 @pytest.mark.gpu
+def test_inference_forward_matches_module_path(golden, cuda):
+    """Self-play's eval forward on the HIP path (GeisterNet._forward_inference: BatchNorm + ReLU in one HIP
+    launch, stacked DRC, and inside an inference session the stacked weights built once) vs the plain
+    module forward of the same net on the CPU: policy, value, return and every state tensor."""
+    from handyrl_amd.nn import accelerate
+    _, arrays = golden
+    cpu = seeded_net().eval()
+    with torch.no_grad():   # non-trivial running statistics
+        for b in cpu._sequence_bns():
+            b.running_mean.uniform_(-0.5, 0.5)
+            b.running_var.uniform_(0.5, 2.0)
+    gpu = accelerate(seeded_net().to(cuda)).eval()
+    gpu.load_state_dict(cpu.state_dict())
+    obs, hidden = fwd_inputs(arrays)
+    with torch.no_grad():
+        ref = cpu(obs, hidden)
+        h = ([t.to(cuda) for t in hidden[0]], [t.to(cuda) for t in hidden[1]])
+        outs = [gpu({k: v.to(cuda) for k, v in obs.items()}, h)]
+        with gpu.inference_session():
+            outs.append(gpu({k: v.to(cuda) for k, v in obs.items()}, h))
+    for out in outs:
+        for k in ('policy', 'value', 'return'):
+            torch.testing.assert_close(out[k].cpu(), ref[k], rtol=1e-5, atol=2e-5, msg=k)
+        for a, b in zip(out['hidden'][0] + out['hidden'][1], ref['hidden'][0] + ref['hidden'][1]):
+            torch.testing.assert_close(a.cpu(), b, rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('graph', [False, True])
 def test_gpu_recurrent_learner_matches_cpu_oracle(cuda, graph):
     """Three recurrent learner steps (LearnerStep on the GPU, HIP graph or eager) vs the oracle's
