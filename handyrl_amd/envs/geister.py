@@ -64,6 +64,22 @@ class ConvLSTMCell(nn.Module):
         return torch.sigmoid(go) * torch.tanh(c), c
 
 
+def _stacked(ts):
+    """The layers' states as one (E, n*H, *HW) tensor: a view when they are adjacent channel slices of one
+    contiguous tensor (GeisterNet.inference_hidden), a concatenation otherwise."""
+    t0 = ts[0]
+    E, hd = t0.shape[0], t0.shape[1]
+    inner = t0[0].numel()
+    n = len(ts)
+    if (t0[0].is_contiguous() and t0.stride(0) == n * inner
+            and all(t.shape == t0.shape and t.stride() == t0.stride()
+                    and t.storage_offset() == t0.storage_offset() + i * inner
+                    and t.untyped_storage().data_ptr() == t0.untyped_storage().data_ptr()
+                    for i, t in enumerate(ts))):
+        return t0.as_strided((E, n * hd, *t0.shape[2:]), (n * inner, *t0.stride()[1:]))
+    return torch.cat(ts, 1)
+
+
 class DRC(nn.Module):
     """Stack of ConvLSTM cells, each fed the same encoder output, repeated per step."""
 
@@ -153,7 +169,7 @@ class DRC(nn.Module):
             cache = self._stacked_weights()
         z = F.conv2d(x, cache['w_x'], cache['b_x'], padding=pad)                          # (E, n*4H, *HW)
         w_h = cache['w_h']                                                               # (n*4H, H, 3, 3)
-        h, c = torch.cat(hs, 1), torch.cat(cs, 1)                                        # (E, n*H, *HW)
+        h, c = _stacked(hs), _stacked(cs)                                                # (E, n*H, *HW)
         zx = z.view(E * n, 4 * hd, *HW)
         for _ in range(num_repeats):
             zh = F.conv2d(h, w_h, None, padding=pad, groups=n)
@@ -254,6 +270,17 @@ class GeisterNet(nn.Module):
 
     def init_hidden(self, batch_size=None):
         return self.body.init_hidden(BOARD, batch_size)
+
+    def inference_hidden(self, E, P, device):
+        """Self-play state for E games and P players, player-major: leaf l is (P, E, H, 6, 6) and the
+        layers' leaves are adjacent channel slices of one (P, E, layers*H, 6, 6) tensor per kind, so the
+        mover's state h[p] is already the stacked input of DRC._inference_stacked (no concatenation)."""
+        n, hd = len(self.body.blocks), self.body.blocks[0].hidden_dim
+        out = []
+        for _ in range(2):   # h, c
+            buf = torch.zeros(P, E, n * hd, *BOARD, device=device)
+            out.append([buf[:, :, i * hd:(i + 1) * hd] for i in range(n)])
+        return tuple(out)
 
     def forward(self, x, hidden):
         if (not self.training and self.body.use_hip and not torch.is_grad_enabled() and x['board'].is_cuda

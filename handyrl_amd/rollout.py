@@ -224,7 +224,11 @@ class DeviceGenerator:
               't': torch.zeros(1, dtype=torch.long, device=dev),
               'rows': torch.arange(E, device=dev),
               'hidden': None, 'obs_dev': torch.device(dev).type}
-        if hasattr(self.net, 'init_hidden'):
+        st['pmajor'] = False   # state leaves (E, P, ...) as init_hidden gives them
+        if hasattr(self.net, 'inference_hidden') and torch.device(dev).type == 'cuda':
+            st['hidden'] = self.net.inference_hidden(E, P, dev)   # leaves (P, E, ...), the net's own layout
+            st['pmajor'] = True
+        elif hasattr(self.net, 'init_hidden'):
             st['hidden'] = map_r(self.net.init_hidden([E, P]), lambda h: h.to(dev).contiguous())
         self._st = st
         return st
@@ -255,7 +259,9 @@ class DeviceGenerator:
         if hidden is None:
             h_in = None
         elif mover is not None:
-            h_in = map_r(hidden, lambda h: h[:, mover])
+            h_in = map_r(hidden, (lambda h: h[mover]) if st['pmajor'] else (lambda h: h[:, mover]))
+        elif st['pmajor']:
+            h_in = map_r(hidden, lambda h: h[player, st['rows']])
         else:
             h_in = map_r(hidden, lambda h: h[st['rows'], player])
         out = self.net(o, h_in)
@@ -270,11 +276,14 @@ class DeviceGenerator:
         if hidden is not None and mover is not None and st['obs_dev'] == 'cuda':
             # one HIP launch for every state tensor (nn.masked_rows_copy_) instead of a where + copy per tensor
             from .nn import masked_rows_copy_
-            masked_rows_copy_([h[:, mover] for h in _leaves(hidden)], _leaves(out['hidden']), active.contiguous())
+            masked_rows_copy_([h[mover] if st['pmajor'] else h[:, mover] for h in _leaves(hidden)],
+                              _leaves(out['hidden']), active.contiguous())
         elif hidden is not None:
             def advance(h, nh):
                 live = active.view(-1, *([1] * (nh.dim() - 1)))
-                if mover is not None:
+                if st['pmajor']:
+                    h[player, st['rows']] = torch.where(live, nh, h[player, st['rows']])
+                elif mover is not None:
                     h[:, mover].copy_(torch.where(live, nh, h[:, mover]))
                 else:
                     h[st['rows'], player] = torch.where(live, nh, h[st['rows'], player])

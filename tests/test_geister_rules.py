@@ -110,9 +110,33 @@ def test_generated_geister_games(generated):
 def test_recurrent_inference_matches_per_game_loop(generated):
     """generation.py:23-41: one hidden state per player, advanced only on the player's own plies."""
     net, ep = generated
+    _check_per_game(net, ep)
+
+
+@pytest.mark.gpu
+def test_gpu_selfplay_matches_per_game_loop(cuda):
+    """The GPU self-play path (HIP graph per ply, HIP rules and ply tail, stacked player-major DRC state,
+    fused BatchNorm + ReLU inference) against the reference's per-game loop run with the same weights on
+    the CPU: every recorded value and legal policy logit of three games."""
+    from handyrl_amd.nn import accelerate
+    from handyrl_amd.rollout import DeviceGenerator
+    from handyrl_amd.envs.geister import GeisterNet
+    torch.manual_seed(6)
+    cpu = GeisterNet()
+    net = accelerate(GeisterNet().to(cuda))
+    net.load_state_dict(cpu.state_dict())
+    gen = DeviceGenerator(GeisterBatch(16, cuda), net, gamma=0.8)
+    gen.generate(generator=torch.Generator(device=cuda).manual_seed(1))     # capture
+    ep = gen.generate(generator=torch.Generator(device=cuda).manual_seed(2))
+    assert gen._st['graphs'] is not None and gen._st['pmajor']
+    ep = {k: ({kk: vv.cpu() for kk, vv in v.items()} if isinstance(v, dict) else v.cpu()) for k, v in ep.items()}
+    _check_per_game(cpu, ep, games=(0, 7, 15))
+
+
+def _check_per_game(net, ep, games=(0, 5)):
     net.eval()
     with torch.no_grad():
-        for e in (0, 5):
+        for e in games:
             hidden = {p: net.init_hidden() for p in (0, 1)}
             for t in range(int(ep['length'][e])):
                 p = int(ep['turn'][e, t])
