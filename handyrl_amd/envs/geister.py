@@ -295,8 +295,38 @@ class GeisterNet(nn.Module):
         return {'policy': policy, 'value': torch.tanh(self.head_v(h)), 'return': self.head_r(h),
                 'hidden': hidden}
 
+    _bn_coef = None   # BatchNorm (alpha, beta) of an inference session, per module
+
+    @contextlib.contextmanager
     def inference_session(self):
-        return self.body.inference_session()
+        """Per-call preparation for self-play (DeviceGenerator.generate): the DRC's stacked weights and the
+        four BatchNorms' inference coefficients alpha = invstd * weight, beta = bias - mean * alpha
+        (hrl_bn_forward_eval's own coefficient kernel) are refreshed in place once, so a ply is only the
+        apply passes.  Outside a session every forward derives them itself."""
+        from .. import _native
+        bufs = getattr(self, '_bn_coef_buf', None) or {}
+        with torch.no_grad():
+            for name, bn in (('bn1', self.bn1), ('p', self.head_p_move.bn), ('v', self.head_v.bn),
+                             ('r', self.head_r.bn)):
+                C = bn.num_features
+                if name not in bufs:
+                    bufs[name] = (torch.empty(2 * C, device=bn.running_mean.device),
+                                  torch.zeros(1, C, 1, 1, device=bn.running_mean.device))
+                coef, dummy = bufs[name]
+                if coef.is_cuda:
+                    _native.check(_native.load().hrl_bn_forward_eval(
+                        _native.ptr(dummy), 1, C, 1, _native.ptr(bn.weight), _native.ptr(bn.bias),
+                        _native.ptr(bn.running_mean), _native.ptr(bn.running_var), float(bn.eps), 1,
+                        _native.ptr(torch.empty_like(dummy)), _native.ptr(coef), _native.stream_of(coef.device)),
+                        'hrl_bn_forward_eval')
+        self._bn_coef_buf = bufs
+        self._bn_coef = {id(m): bufs[k][0] for k, m in (('bn1', self.bn1), ('p', self.head_p_move.bn),
+                                                         ('v', self.head_v.bn), ('r', self.head_r.bn))}
+        try:
+            with self.body.inference_session():
+                yield
+        finally:
+            self._bn_coef = None
 
     def _forward_inference(self, x, hidden):
         """forward in eval mode without autograd on the HIP path (self-play): the same operations, with each
@@ -304,8 +334,20 @@ class GeisterNet(nn.Module):
         (DRC._inference_stacked)."""
         from ..nn import batch_norm_eval
 
+        coefs = self._bn_coef
+
         def bn_relu(bn, y):
-            return batch_norm_eval(y, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, relu=True)
+            if coefs is None or id(bn) not in coefs:
+                return batch_norm_eval(y, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, relu=True)
+            from .. import _native
+            y = y.contiguous()
+            out = torch.empty_like(y)
+            C = y.shape[1]
+            coef = coefs[id(bn)]
+            _native.check(_native.load().hrl_bn_apply(
+                _native.ptr(y), y.shape[0], C, y[0, 0].numel(), _native.ptr(coef), _native.ptr(coef[C:]), 1,
+                _native.ptr(out), _native.stream_of(y.device)), 'hrl_bn_apply')
+            return out
         board, scalar = x['board'], x['scalar']
         planes = scalar[..., None, None].expand(*scalar.shape, *BOARD)
         h_e = bn_relu(self.bn1, self.conv1(torch.cat([planes, board], dim=-3)))
