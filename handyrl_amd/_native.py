@@ -108,8 +108,8 @@ SIGNATURES = {
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     'hrl_hidden_update_backward': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, _i64, ctypes.c_int,
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
-    'hrl_lstm_gates_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p,
-                                              ctypes.c_void_p]),
+    'hrl_lstm_gates_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _i64, _i64, _i64, _f32p, _i64, _f32p,
+                                              _f32p, _f32p, ctypes.c_void_p]),
     'hrl_lstm_gates_backward': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p,
                                                ctypes.c_void_p]),
     'hrl_torus_workspace_bytes': (ctypes.c_int64, [_i64]),
@@ -166,7 +166,7 @@ SIGNATURES = {
                                             ctypes.c_void_p]),
 }
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _lib = None
 

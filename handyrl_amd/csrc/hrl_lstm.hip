@@ -72,6 +72,8 @@ struct Geo {
     int64_t N;
     int H, HW, nq;          // nq = HW / VW vectors per channel plane
     int64_t zx_stride;      // floats between samples of zx
+    const float *bias;      // (bias_rows, 4H) added to zx before zh, or NULL
+    int bias_rows;          // sample n uses bias row n % bias_rows (stacked layers)
 };
 
 template <int VW>
@@ -100,12 +102,25 @@ __global__ void lstm_fwd_kernel(const float *__restrict__ zx, const float *__res
             xo = ld<VW>(zx + xoff + 2 * gstep);
             xg = ld<VW>(zx + xoff + 3 * gstep);
         }
+        float bi = 0.f, bf = 0.f, bo = 0.f, bg = 0.f;
+        if (g.bias) {   // the x half's conv bias, added as the biased convolution would: (zx + b) + zh
+            const float *b = g.bias + (n % g.bias_rows) * 4 * g.H + ch;
+            bi = b[0];
+            bf = b[g.H];
+            bo = b[2 * g.H];
+            bg = b[3 * g.H];
+        }
         const V cv = ld<VW>(c + soff);
         V gi, gf, go, gg, cn, hn;
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
             float a_i = get<VW>(zi, j), a_f = get<VW>(zf, j), a_o = get<VW>(zo, j), a_g = get<VW>(zg, j);
-            if (zx) {
+            if (zx && g.bias) {
+                a_i = (get<VW>(xi, j) + bi) + a_i;
+                a_f = (get<VW>(xf, j) + bf) + a_f;
+                a_o = (get<VW>(xo, j) + bo) + a_o;
+                a_g = (get<VW>(xg, j) + bg) + a_g;
+            } else if (zx) {
                 a_i = get<VW>(xi, j) + a_i;
                 a_f = get<VW>(xf, j) + a_f;
                 a_o = get<VW>(xo, j) + a_o;
@@ -195,14 +210,16 @@ unsigned grid_for(int64_t total) {
 extern "C" {
 
 int hrl_lstm_gates_forward(const float *zx, int64_t zx_stride, const float *zh, const float *c, int64_t N, int64_t H,
-                           int64_t HW, float *h_out, float *c_out, float *gates, void *stream) {
+                           int64_t HW, const float *bias, int64_t bias_rows, float *h_out, float *c_out, float *gates,
+                           void *stream) {
     if (N == 0) return HRL_OK;
     if (!zh || !c || !h_out || !c_out || N < 0 || H < 1 || HW < 1) return HRL_EINVAL;
+    if (bias && (!zx || bias_rows < 1)) return HRL_EINVAL;
     if (zx && zx_stride < 4 * H * HW) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool vec = HW % 4 == 0 && (!zx || zx_stride % 4 == 0) && aligned(zx) && aligned(zh) && aligned(c) &&
                      aligned(h_out) && aligned(c_out) && aligned(gates);
-    Geo g{N, (int)H, (int)HW, (int)(vec ? HW / 4 : HW), zx_stride};
+    Geo g{N, (int)H, (int)HW, (int)(vec ? HW / 4 : HW), zx_stride, bias, (int)(bias ? bias_rows : 1)};
     const int64_t total = N * H * g.nq;
     if (vec)
         hipLaunchKernelGGL(lstm_fwd_kernel<4>, dim3(grid_for(total)), dim3(256), 0, s, zx, zh, c, g, h_out, c_out,

@@ -167,13 +167,14 @@ class DRC(nn.Module):
         cache = self._session
         if cache is None:
             cache = self._stacked_weights()
-        z = F.conv2d(x, cache['w_x'], cache['b_x'], padding=pad)                          # (E, n*4H, *HW)
+        z = F.conv2d(x, cache['w_x'], None, padding=pad)                                 # (E, n*4H, *HW)
         w_h = cache['w_h']                                                               # (n*4H, H, 3, 3)
         h, c = _stacked(hs), _stacked(cs)                                                # (E, n*H, *HW)
         zx = z.view(E * n, 4 * hd, *HW)
         for _ in range(num_repeats):
             zh = F.conv2d(h, w_h, None, padding=pad, groups=n)
-            h, c = lstm_gates(zx, zh.view(E * n, 4 * hd, *HW), c.view(E * n, hd, *HW))
+            # the x half's bias rides in the gate kernel: (zx + b) + zh, the biased convolution's order
+            h, c = lstm_gates(zx, zh.view(E * n, 4 * hd, *HW), c.view(E * n, hd, *HW), cache['b_x'], n)
             h, c = h.view(E, n * hd, *HW), c.view(E, n * hd, *HW)
         hs, cs = list(h.split(hd, 1)), list(c.split(hd, 1))
         return hs[-1], (hs, cs)

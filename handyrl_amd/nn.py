@@ -990,7 +990,7 @@ class _LSTMGates(torch.autograd.Function):
     """ConvLSTM cell gates (csrc/hrl_lstm.hip): z = zx + zh -> (h', c'), saved gate activations."""
 
     @staticmethod
-    def forward(ctx, zx, zh, c, save=True):
+    def forward(ctx, zx, zh, c, save=True, bias=None, bias_rows=1):
         ctx.set_materialize_grads(False)   # a cell whose outputs reach no loss stays out of backward
         N, G, Hh, Ww = zh.shape
         H, HW = G // 4, Hh * Ww
@@ -1003,9 +1003,12 @@ class _LSTMGates(torch.autograd.Function):
         # inference (self-play) saves nothing for a backward: the kernel skips the 4 gate streams
         gates = torch.empty_like(zh) if save else None
         lib = _native.load()
+        if bias is not None:
+            assert zx is not None and not save and bias.is_contiguous() and bias.numel() == bias_rows * G
         _native.check(lib.hrl_lstm_gates_forward(_native.ptr(zx), 0 if zx is None else zx.stride(0), _native.ptr(zh),
-                                                 _native.ptr(c), N, H, HW, _native.ptr(h_out), _native.ptr(c_out),
-                                                 _native.ptr(gates), _native.stream_of(zh.device)),
+                                                 _native.ptr(c), N, H, HW, _native.ptr(bias), bias_rows,
+                                                 _native.ptr(h_out), _native.ptr(c_out), _native.ptr(gates),
+                                                 _native.stream_of(zh.device)),
                       'hrl_lstm_gates_forward')
         ctx.save_for_backward(gates, c, c_out)
         ctx.has_zx = zx is not None
@@ -1014,7 +1017,7 @@ class _LSTMGates(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh, dc_out):
         if dh is None and dc_out is None:
-            return None, None, None, None
+            return None, None, None, None, None, None
         gates, c, c_out = ctx.saved_tensors
         N, G, Hh, Ww = gates.shape
         dz = torch.empty_like(gates)
@@ -1025,19 +1028,23 @@ class _LSTMGates(torch.autograd.Function):
             _native.ptr(gates), _native.ptr(c), _native.ptr(c_out), _native.ptr(dh), _native.ptr(dc_out),
             N, G // 4, Hh * Ww, _native.ptr(dz), _native.ptr(dc), _native.stream_of(gates.device)),
             'hrl_lstm_gates_backward')
-        return (dz if ctx.has_zx else None), dz, dc, None
+        return (dz if ctx.has_zx else None), dz, dc, None, None, None
 
 
-def lstm_gates(zx, zh, c):
+def lstm_gates(zx, zh, c, bias=None, bias_rows=1):
     """(h', c') of a ConvLSTM cell from its gate pre-activations zx + zh (i, f, o, g order).
 
     ``zx`` (may be None) can be a channel slice of a wider tensor; the HIP
-    kernels run forward and backward in one launch each.
+    kernels run forward and backward in one launch each.  ``bias`` (inference
+    only): the x half's convolution bias, (bias_rows, 4H) for rows n % bias_rows,
+    added as (zx + bias) + zh.
     """
     if not zh.is_cuda:
         raise RuntimeError('lstm_gates runs on the HIP device only (no CPU fallback)')
     save = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (zx, zh, c))
-    return _LSTMGates.apply(zx, zh, c, save)
+    if bias is not None and save:
+        raise ValueError('lstm_gates: the folded bias is an inference-only form')
+    return _LSTMGates.apply(zx, zh, c, save, bias, bias_rows)
 
 
 def _live(xs):

@@ -204,12 +204,15 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
  * its autograd backward).  Gate pre-activations z = zx + zh in channel order
  * i, f, o, g: zh (N, 4H, HW) contiguous; zx the same shape with per-sample
  * stride zx_stride floats (a channel slice of a wider tensor) or NULL.
+ * bias (bias_rows, 4H) or NULL: the x half's convolution bias, added as z = (zx + bias[n % bias_rows]) + zh
+ * (the biased convolution's own order; bias_rows > 1 for layers stacked along N, sample n = e*rows + layer).
  * Forward: gates (N, 4H, HW) = (sigmoid i, sigmoid f, sigmoid o, tanh g) (NULL: not saved, inference);
  *          c_out = f*c + i*g; h_out = o*tanh(c_out).
  * Backward: dz (N, 4H, HW) and dc (N, H, HW) from dh / dc_out (either may be NULL = zero).
  */
 int hrl_lstm_gates_forward(const float *zx, int64_t zx_stride, const float *zh, const float *c, int64_t N, int64_t H,
-                           int64_t HW, float *h_out, float *c_out, float *gates, void *stream);
+                           int64_t HW, const float *bias, int64_t bias_rows, float *h_out, float *c_out, float *gates,
+                           void *stream);
 int hrl_lstm_gates_backward(const float *gates, const float *c, const float *c_out, const float *dh,
                             const float *dc_out, int64_t N, int64_t H, int64_t HW, float *dz, float *dc,
                             void *stream);
