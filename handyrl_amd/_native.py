@@ -164,9 +164,13 @@ SIGNATURES = {
     'hrl_masked_rows_copy': (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _i64,
                                             ctypes.c_void_p]),
+    'hrl_geister_observation_record': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_void_p, _i64, ctypes.c_int, _f32p, _f32p,
+                                                      ctypes.c_void_p, ctypes.c_void_p, _i64, _f32p, _f32p,
+                                                      ctypes.c_void_p]),
 }
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 _lib = None
 

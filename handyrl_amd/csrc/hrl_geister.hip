@@ -69,9 +69,19 @@ __global__ void legal_kernel(const int8_t *__restrict__ board, const int64_t *__
     legal[i] = ok ? 1 : 0;
 }
 
+// Rec: optional episode record of the observation (DeviceGenerator): slot t (read from device memory) of
+// planes (E, Tm, 7, 36) / scalar (E, Tm, 18) gets the view when the game is active, zeros otherwise.
+struct Rec {
+    const uint8_t *active;
+    const int64_t *t;
+    int64_t Tm;
+    float *planes, *scalar;
+};
+
 __global__ void observation_kernel(const int8_t *__restrict__ board, const int64_t *__restrict__ color,
                                    const int64_t *__restrict__ cnt, const int64_t *__restrict__ player,
-                                   int64_t E, int full, float *__restrict__ planes, float *__restrict__ scalar) {
+                                   int64_t E, int full, float *__restrict__ planes, float *__restrict__ scalar,
+                                   Rec rec) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= E * kCells) return;
     const int64_t e = i / kCells;
@@ -85,14 +95,18 @@ __global__ void observation_kernel(const int8_t *__restrict__ board, const int64
     const bool own = blue_c || red_c;
     const bool opp_all = p >= 0 && !own;
     const bool blue_o = full && p == opp * 2, red_o = full && p == opp * 2 + 1;
+    const float pv[7] = {1.0f, own ? 1.0f : 0.0f, opp_all ? 1.0f : 0.0f, blue_c ? 1.0f : 0.0f,
+                         red_c ? 1.0f : 0.0f, blue_o ? 1.0f : 0.0f, red_o ? 1.0f : 0.0f};
     float *o = planes + e * 7 * kCells + cell;
-    o[0 * kCells] = 1.0f;
-    o[1 * kCells] = own ? 1.0f : 0.0f;
-    o[2 * kCells] = opp_all ? 1.0f : 0.0f;
-    o[3 * kCells] = blue_c ? 1.0f : 0.0f;
-    o[4 * kCells] = red_c ? 1.0f : 0.0f;
-    o[5 * kCells] = blue_o ? 1.0f : 0.0f;
-    o[6 * kCells] = red_o ? 1.0f : 0.0f;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) o[k * kCells] = pv[k];
+    const bool live = rec.planes && rec.active[e];
+    const int64_t slot = rec.planes ? e * rec.Tm + *rec.t : 0;
+    if (rec.planes) {
+        float *r = rec.planes + slot * 7 * kCells + cell;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) r[k * kCells] = live ? pv[k] : 0.0f;
+    }
     if (cell < 18) {   // [me is black, turn view, one-hot counts 1..4 of (my blue, my red, opp blue, opp red)]
         float v;
         if (cell == 0) {
@@ -105,6 +119,7 @@ __global__ void observation_kernel(const int8_t *__restrict__ board, const int64
             v = cnt[e * 4 + side * 2 + (which & 1)] == n ? 1.0f : 0.0f;
         }
         scalar[e * 18 + cell] = v;
+        if (rec.planes) rec.scalar[slot * 18 + cell] = live ? v : 0.0f;
     }
 }
 
@@ -168,10 +183,20 @@ int hrl_geister_legal(const int8_t *board, const int64_t *color, const int64_t *
 
 int hrl_geister_observation(const int8_t *board, const int64_t *color, const int64_t *cnt, const int64_t *player,
                             int64_t E, int full, float *planes, float *scalar, void *stream) {
+    return hrl_geister_observation_record(board, color, cnt, player, E, full, planes, scalar, nullptr, nullptr, 0,
+                                          nullptr, nullptr, stream);
+}
+
+int hrl_geister_observation_record(const int8_t *board, const int64_t *color, const int64_t *cnt,
+                                   const int64_t *player, int64_t E, int full, float *planes, float *scalar,
+                                   const uint8_t *active, const int64_t *t, int64_t Tm, float *rec_planes,
+                                   float *rec_scalar, void *stream) {
     if (E == 0) return HRL_OK;
     if (!board || !color || !cnt || !player || !planes || !scalar || E < 0) return HRL_EINVAL;
+    if (rec_planes && (!rec_scalar || !active || !t || Tm < 1)) return HRL_EINVAL;
+    const Rec rec{active, t, Tm, rec_planes, rec_planes ? rec_scalar : nullptr};
     hipLaunchKernelGGL(observation_kernel, dim3(grid_for(E * kCells)), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), board, color, cnt, player, E, full, planes, scalar);
+                       static_cast<hipStream_t>(stream), board, color, cnt, player, E, full, planes, scalar, rec);
     { const hipError_t err = hipGetLastError(); return err == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)err; }
 }
 

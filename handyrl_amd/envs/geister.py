@@ -578,6 +578,25 @@ class GeisterBatch:
 
     COMPLETE_INFO = False   # CIGeister (ci_geister.py:520-568) shows the opponent's colours in every view
 
+    def observation_record(self, player, rec, t, active):
+        """observation(player) on the GPU that also writes slot t (device scalar) of the episode record
+        rec = {'board': (E, Tm, 7, 6, 6), 'scalar': (E, Tm, 18)}: the view where `active`, zeros elsewhere --
+        DeviceGenerator's obs record in the same launch."""
+        from .._native import load, check, ptr, stream_of
+        player = player.to(torch.long).contiguous()
+        active = active.contiguous()
+        assert player.shape == (self.E,) and active.shape == (self.E,) and active.dtype == torch.bool
+        Tm = rec['board'].shape[1]
+        assert rec['board'].shape == (self.E, Tm, BOARD_PLANES, *BOARD) and rec['board'].is_contiguous()
+        assert rec['scalar'].shape == (self.E, Tm, SCALARS) and rec['scalar'].is_contiguous()
+        planes = torch.empty(self.E, BOARD_PLANES, *BOARD, device=self.device)
+        scalar = torch.empty(self.E, SCALARS, device=self.device)
+        check(load().hrl_geister_observation_record(
+            ptr(self.board), ptr(self.color), ptr(self.cnt), ptr(player), self.E, int(bool(self.COMPLETE_INFO)),
+            ptr(planes), ptr(scalar), ptr(active), ptr(t), Tm, ptr(rec['board']), ptr(rec['scalar']),
+            stream_of(self.board.device)), 'hrl_geister_observation_record')
+        return {'board': planes, 'scalar': scalar}
+
     def observation(self, player, full=False):
         """{'board': (E,7,6,6), 'scalar': (E,18)} seen by `player` (E,) (geister.py:495-535, player given);
         ``full``: the reference's ``observation(None)`` view, which also shows the opponent's colours."""

@@ -254,7 +254,9 @@ class DeviceGenerator:
         hidden = st['hidden']
         active = ~env.terminal()
         player = env.turn()
-        o = env.observation(player)
+        # envs with a GPU observation kernel record the view into slot t in the same launch
+        obs_recorded = st['obs_dev'] == 'cuda' and hasattr(env, 'observation_record')
+        o = env.observation_record(player, st['obs'], t, active) if obs_recorded else env.observation(player)
         # envs whose mover is ply % P in every live game (TicTacToe, Geister): the mover's state is a view
         if hidden is None:
             h_in = None
@@ -270,7 +272,8 @@ class DeviceGenerator:
         def record(buf, x, fill=0):
             live = active.view(-1, *([1] * (x.dim() - 1)))
             buf.index_copy_(1, t, torch.where(live, x, fill).to(buf.dtype).unsqueeze(1))
-        bimap_r(st['obs'], o, record)
+        if not obs_recorded:
+            bimap_r(st['obs'], o, record)
         sample = sample_record_hip if st['obs_dev'] == 'cuda' else sample_record_torch
         a = sample(st, out['policy'], env.legal(), out['value'], active, player, reward)
         if hidden is not None and mover is not None and st['obs_dev'] == 'cuda':

@@ -33,6 +33,15 @@ int hrl_geister_legal(const int8_t *board, const int64_t *color, const int64_t *
 int hrl_geister_observation(const int8_t *board, const int64_t *color, const int64_t *cnt, const int64_t *player,
                             int64_t E, int full, float *planes, float *scalar, void *stream);
 
+/* hrl_geister_observation that also records the view for DeviceGenerator's episode: slot t (read from
+ * device memory) of rec_planes (E,Tm,7,6,6) / rec_scalar (E,Tm,18) gets the view where active[e], zeros
+ * elsewhere (the record of generation.py:55-62 with its reset value for finished games); rec_planes NULL:
+ * no record. */
+int hrl_geister_observation_record(const int8_t *board, const int64_t *color, const int64_t *cnt,
+                                   const int64_t *player, int64_t E, int full, float *planes, float *scalar,
+                                   const uint8_t *active, const int64_t *t, int64_t Tm, float *rec_planes,
+                                   float *rec_scalar, void *stream);
+
 /* Play action (E,) in every game whose active byte is set (geister.py:359-394): layouts, moves,
  * captures, escapes, piece counts, winner, the 200-move draw; the side to move flips.
  * layout_type (70,8) int8 piece type per initial slot, opos (2,8) int64 initial cells per colour. */

@@ -213,3 +213,29 @@ def test_hip_rules_match_torch_rules_random_games(cuda, full):
     wins = set(cpu.win.tolist())
     assert {0, 1, 2} <= wins, wins
     assert torch.equal(gpu.outcome().cpu(), cpu.outcome())
+
+
+@pytest.mark.gpu
+def test_observation_record_kernel(cuda):
+    """GeisterBatch.observation_record: the same view as observation(), and slot t of the episode record holds
+    it for active games and zeros for finished ones; the other slots are untouched."""
+    from handyrl_amd.envs.geister import BOARD_PLANES, SCALARS
+    E, Tm = 300, 6
+    env = GeisterBatch(E, cuda)
+    g = torch.Generator().manual_seed(5)
+    for _ in range(9):   # a few random plies: layouts, then moves
+        legal = env.legal().cpu()
+        env.step(torch.multinomial(legal.float() + 1e-12, 1, generator=g).view(-1).to(cuda),
+                 torch.ones(E, dtype=torch.bool, device=cuda))
+    rec = {'board': torch.full((E, Tm, BOARD_PLANES, 6, 6), 7.0, device=cuda),
+           'scalar': torch.full((E, Tm, SCALARS), 7.0, device=cuda)}
+    t = torch.tensor([4], device=cuda)
+    active = torch.rand(E, generator=g) < 0.7
+    player = env.turn()
+    o = env.observation_record(player, rec, t, active.to(cuda))
+    ref = env.observation(player)
+    for k in ('board', 'scalar'):
+        assert torch.equal(o[k], ref[k]), k
+        live = active.to(cuda).view(-1, *([1] * (ref[k].dim() - 1)))
+        assert torch.equal(rec[k][:, 4], torch.where(live, ref[k], torch.zeros_like(ref[k]))), k
+        assert bool((rec[k][:, :4] == 7.0).all()) and bool((rec[k][:, 5:] == 7.0).all()), k
