@@ -156,7 +156,7 @@ SIGNATURES = {
                                                _i64, ctypes.c_int, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_geister_step': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                        ctypes.c_void_p, _i64, ctypes.c_void_p]),
+                                        ctypes.c_void_p, _i64, ctypes.c_void_p, ctypes.c_void_p]),
     'hrl_selfplay_sample_record': (ctypes.c_int, [_f32p, _i64, ctypes.c_void_p, _f32p, ctypes.c_void_p, _f32p,
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _i64, _i64,
                                                   _i64, _i64, ctypes.c_void_p, _f32p, _f32p, ctypes.c_void_p, _f32p,
@@ -170,7 +170,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 _lib = None
 

@@ -125,8 +125,8 @@ __global__ void observation_kernel(const int8_t *__restrict__ board, const int64
 
 __global__ void step_kernel(int8_t *__restrict__ board, int64_t *__restrict__ color, int64_t *__restrict__ turn_count,
                             int64_t *__restrict__ win, int64_t *__restrict__ cnt, const int64_t *__restrict__ action,
-                            const uint8_t *__restrict__ active, const int8_t *__restrict__ layout_type,
-                            const int64_t *__restrict__ opos, int64_t E) {
+                            const uint8_t *active, const int8_t *__restrict__ layout_type,
+                            const int64_t *__restrict__ opos, int64_t E, uint8_t *__restrict__ live) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E || !active[e]) return;
     int8_t *b = board + e * kCells;
@@ -164,6 +164,7 @@ __global__ void step_kernel(int8_t *__restrict__ board, int64_t *__restrict__ co
     win[e] = w;
     color[e] = 1 - c;
     turn_count[e] = tc;
+    if (live) live[e] = w < 0 ? 1 : 0;   // may alias `active`: this thread read active[e] above
 }
 
 inline int grid_for(int64_t n) { return (int)((n + 255) / 256); }
@@ -202,12 +203,12 @@ int hrl_geister_observation_record(const int8_t *board, const int64_t *color, co
 
 int hrl_geister_step(int8_t *board, int64_t *color, int64_t *turn_count, int64_t *win, int64_t *cnt,
                      const int64_t *action, const uint8_t *active, const int8_t *layout_type, const int64_t *opos,
-                     int64_t E, void *stream) {
+                     int64_t E, uint8_t *live, void *stream) {
     if (E == 0) return HRL_OK;
     if (!board || !color || !turn_count || !win || !cnt || !action || !active || !layout_type || !opos || E < 0)
         return HRL_EINVAL;
     hipLaunchKernelGGL(step_kernel, dim3(grid_for(E)), dim3(256), 0, static_cast<hipStream_t>(stream), board, color,
-                       turn_count, win, cnt, action, active, layout_type, opos, E);
+                       turn_count, win, cnt, action, active, layout_type, opos, E, live);
     { const hipError_t err = hipGetLastError(); return err == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)err; }
 }
 

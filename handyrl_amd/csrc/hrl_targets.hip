@@ -431,7 +431,7 @@ int hrl_debug_set_stamps_targets(void *buf) {
 }
 #endif
 
-int hrl_abi_version(void) { return 16; }
+int hrl_abi_version(void) { return 17; }
 
 const char *hrl_strerror(int code) {
     if (code == HRL_OK) return "success";

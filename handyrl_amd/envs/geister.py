@@ -483,6 +483,9 @@ class GeisterBatch:
             self.turn_count = torch.full((E,), -2, dtype=torch.long, device=dev)
             self.win = torch.full((E,), -1, dtype=torch.long, device=dev)
             self.cnt = torch.zeros(E, 4, dtype=torch.long, device=dev)
+            self.live = torch.ones(E, dtype=torch.bool, device=dev)   # ~terminal(), kept by the HIP step
+            self._reward = torch.full((E, 2), -0.01, dtype=torch.float64, device=dev)
+        self.live.fill_(True)
         self.board.fill_(-1)
         self.color.zero_()
         self.turn_count.fill_(-2)
@@ -534,7 +537,8 @@ class GeisterBatch:
             active = active.to(torch.bool).contiguous()
             check(load().hrl_geister_step(ptr(self.board), ptr(self.color), ptr(self.turn_count), ptr(self.win),
                                           ptr(self.cnt), ptr(action), ptr(active), ptr(self.layout_type),
-                                          ptr(self.opos), E, stream_of(self.board.device)), 'hrl_geister_step')
+                                          ptr(self.opos), E, ptr(self.live), stream_of(self.board.device)),
+                  'hrl_geister_step')
             return
         rows = torch.arange(E, device=dev)
         c = self.color
@@ -632,8 +636,14 @@ class GeisterBatch:
         return {'board': planes.view(-1, BOARD_PLANES, *BOARD), 'scalar': scalar}
 
     def reward(self):
-        """(E, 2) fp64: -0.01 per ply for both players (geister.py:427-429; a Python float there)."""
-        return torch.full((self.E, 2), -0.01, dtype=torch.float64, device=self.device)
+        """(E, 2) fp64: -0.01 per ply for both players (geister.py:427-429; a Python float there).  One constant
+        tensor (read-only for callers)."""
+        return self._reward
+
+    def active(self):
+        """(E,) bool games still running: ~terminal(); on the GPU the step kernel keeps it, so the self-play
+        ply reads it without a launch (read-only for callers)."""
+        return self.live if self._hip() else ~self.terminal()
 
     def outcome(self):
         """(E, 2): +1/-1 for the winning colour, 0/0 for a draw (geister.py:431-438)."""

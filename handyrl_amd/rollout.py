@@ -252,7 +252,7 @@ class DeviceGenerator:
         env, E = self.env, self.env.E
         t = st['t']
         hidden = st['hidden']
-        active = ~env.terminal()
+        active = env.active() if hasattr(env, 'active') else ~env.terminal()
         player = env.turn()
         # envs with a GPU observation kernel record the view into slot t in the same launch
         obs_recorded = st['obs_dev'] == 'cuda' and hasattr(env, 'observation_record')

@@ -44,10 +44,12 @@ int hrl_geister_observation_record(const int8_t *board, const int64_t *color, co
 
 /* Play action (E,) in every game whose active byte is set (geister.py:359-394): layouts, moves,
  * captures, escapes, piece counts, winner, the 200-move draw; the side to move flips.
- * layout_type (70,8) int8 piece type per initial slot, opos (2,8) int64 initial cells per colour. */
+ * layout_type (70,8) int8 piece type per initial slot, opos (2,8) int64 initial cells per colour.
+ * live (E,) bytes or NULL: set to (win < 0) for every played game (the next ply's active mask; may be
+ * the same array as `active`). */
 int hrl_geister_step(int8_t *board, int64_t *color, int64_t *turn_count, int64_t *win, int64_t *cnt,
                      const int64_t *action, const uint8_t *active, const int8_t *layout_type, const int64_t *opos,
-                     int64_t E, void *stream);
+                     int64_t E, uint8_t *live, void *stream);
 
 /* The sampling and recording tail of a self-play ply (generation.py:43-62), one wave per game:
  * m = legal ? 0 : 1e32, p = logits - m, action = argmax(p - log(-log(U[t]))) (torch.argmax's tie order);

@@ -194,6 +194,7 @@ def test_hip_rules_match_torch_rules_random_games(cuda, full):
     for t in range(GeisterBatch.MAX_PLIES):
         for name in ('board', 'color', 'turn_count', 'win', 'cnt'):
             assert torch.equal(getattr(gpu, name).cpu(), getattr(cpu, name)), (t, name)
+        assert torch.equal(gpu.active().cpu(), ~cpu.terminal()), t    # the live mask the HIP step keeps
         legal = cpu.legal()
         assert torch.equal(gpu.legal().cpu(), legal), t
         for q in (0, 1):
