@@ -120,6 +120,7 @@ class DRC(nn.Module):
         return self.step_hip(self.x_halves(x), hs, cs, num_repeats)
 
     _session = None   # the stacked weights of an inference session (DRC.inference_session)
+    _inplace = False  # the session advances a stacked state in place (DeviceGenerator)
 
     def _stacked_weights(self, out=None):
         """The layers' x-half weights and biases and h-half weights, concatenated along the output channels
@@ -135,17 +136,21 @@ class DRC(nn.Module):
         return {'w_x': w_x, 'w_h': w_h, 'b_x': b_x}
 
     @contextlib.contextmanager
-    def inference_session(self):
+    def inference_session(self, inplace_state=False):
         """Within the session the stacked inference weights are built once (refreshed in place from the
         current parameters on entry, so HIP graphs captured in an earlier session stay valid) instead of
-        once per forward: DeviceGenerator.generate runs its plies in one."""
+        once per forward: DeviceGenerator.generate runs its plies in one.  ``inplace_state``: a state given
+        in the stacked layout (GeisterNet.inference_hidden) is advanced in place and returned as views of
+        itself -- the caller's state buffers ARE the new state (the generator's own buffers only)."""
         with torch.no_grad():
             self._session_buf = self._stacked_weights(getattr(self, '_session_buf', None))
         self._session = self._session_buf
+        self._inplace = inplace_state
         try:
             yield
         finally:
             self._session = None
+            self._inplace = False
 
     def _inference_stacked(self, x, hs, cs, num_repeats):
         """Inference (self-play, no autograd) with the layers stacked along channels.
@@ -170,12 +175,17 @@ class DRC(nn.Module):
         z = F.conv2d(x, cache['w_x'], None, padding=pad)                                 # (E, n*4H, *HW)
         w_h = cache['w_h']                                                               # (n*4H, H, 3, 3)
         h, c = _stacked(hs), _stacked(cs)                                                # (E, n*H, *HW)
+        # in an in-place session (DeviceGenerator's own stacked state) the gates write the new state over
+        # the old one: h is consumed by the convolution before, c read and written at the same index
+        inplace = (self._inplace and h.is_contiguous() and c.is_contiguous()
+                   and h.data_ptr() == hs[0].data_ptr() and c.data_ptr() == cs[0].data_ptr())
         zx = z.view(E * n, 4 * hd, *HW)
         for _ in range(num_repeats):
             zh = F.conv2d(h, w_h, None, padding=pad, groups=n)
+            out = (h.view(E * n, hd, *HW), c.view(E * n, hd, *HW)) if inplace else None
             # the x half's bias rides in the gate kernel: (zx + b) + zh, the biased convolution's order
-            h, c = lstm_gates(zx, zh.view(E * n, 4 * hd, *HW), c.view(E * n, hd, *HW), cache['b_x'], n)
-            h, c = h.view(E, n * hd, *HW), c.view(E, n * hd, *HW)
+            hn, cn = lstm_gates(zx, zh.view(E * n, 4 * hd, *HW), c.view(E * n, hd, *HW), cache['b_x'], n, out=out)
+            h, c = hn.view(E, n * hd, *HW), cn.view(E, n * hd, *HW)
         hs, cs = list(h.split(hd, 1)), list(c.split(hd, 1))
         return hs[-1], (hs, cs)
 
@@ -299,7 +309,7 @@ class GeisterNet(nn.Module):
     _bn_coef = None   # BatchNorm (alpha, beta) of an inference session, per module
 
     @contextlib.contextmanager
-    def inference_session(self):
+    def inference_session(self, inplace_state=False):
         """Per-call preparation for self-play (DeviceGenerator.generate): the DRC's stacked weights and the
         four BatchNorms' inference coefficients alpha = invstd * weight, beta = bias - mean * alpha
         (hrl_bn_forward_eval's own coefficient kernel) are refreshed in place once, so a ply is only the
@@ -324,7 +334,7 @@ class GeisterNet(nn.Module):
         self._bn_coef = {id(m): bufs[k][0] for k, m in (('bn1', self.bn1), ('p', self.head_p_move.bn),
                                                          ('v', self.head_v.bn), ('r', self.head_r.bn))}
         try:
-            with self.body.inference_session():
+            with self.body.inference_session(inplace_state):
                 yield
         finally:
             self._bn_coef = None

@@ -990,7 +990,7 @@ class _LSTMGates(torch.autograd.Function):
     """ConvLSTM cell gates (csrc/hrl_lstm.hip): z = zx + zh -> (h', c'), saved gate activations."""
 
     @staticmethod
-    def forward(ctx, zx, zh, c, save=True, bias=None, bias_rows=1):
+    def forward(ctx, zx, zh, c, save=True, bias=None, bias_rows=1, out=None):
         ctx.set_materialize_grads(False)   # a cell whose outputs reach no loss stays out of backward
         N, G, Hh, Ww = zh.shape
         H, HW = G // 4, Hh * Ww
@@ -998,8 +998,13 @@ class _LSTMGates(torch.autograd.Function):
         c = c.contiguous()
         if zx is not None and (zx.shape != zh.shape or zx.stride()[1:] != zh.stride()[1:]):
             zx = zx.contiguous()
-        h_out = torch.empty_like(c)
-        c_out = torch.empty_like(c)
+        if out is not None:   # inference: given (h', c') buffers, possibly c itself (same-index read then write)
+            h_out, c_out = out
+            assert not save and h_out.shape == c.shape and c_out.shape == c.shape
+            assert h_out.is_contiguous() and c_out.is_contiguous()
+        else:
+            h_out = torch.empty_like(c)
+            c_out = torch.empty_like(c)
         # inference (self-play) saves nothing for a backward: the kernel skips the 4 gate streams
         gates = torch.empty_like(zh) if save else None
         lib = _native.load()
@@ -1017,7 +1022,7 @@ class _LSTMGates(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh, dc_out):
         if dh is None and dc_out is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         gates, c, c_out = ctx.saved_tensors
         N, G, Hh, Ww = gates.shape
         dz = torch.empty_like(gates)
@@ -1028,10 +1033,10 @@ class _LSTMGates(torch.autograd.Function):
             _native.ptr(gates), _native.ptr(c), _native.ptr(c_out), _native.ptr(dh), _native.ptr(dc_out),
             N, G // 4, Hh * Ww, _native.ptr(dz), _native.ptr(dc), _native.stream_of(gates.device)),
             'hrl_lstm_gates_backward')
-        return (dz if ctx.has_zx else None), dz, dc, None, None, None
+        return (dz if ctx.has_zx else None), dz, dc, None, None, None, None
 
 
-def lstm_gates(zx, zh, c, bias=None, bias_rows=1):
+def lstm_gates(zx, zh, c, bias=None, bias_rows=1, out=None):
     """(h', c') of a ConvLSTM cell from its gate pre-activations zx + zh (i, f, o, g order).
 
     ``zx`` (may be None) can be a channel slice of a wider tensor; the HIP
@@ -1042,9 +1047,9 @@ def lstm_gates(zx, zh, c, bias=None, bias_rows=1):
     if not zh.is_cuda:
         raise RuntimeError('lstm_gates runs on the HIP device only (no CPU fallback)')
     save = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (zx, zh, c))
-    if bias is not None and save:
-        raise ValueError('lstm_gates: the folded bias is an inference-only form')
-    return _LSTMGates.apply(zx, zh, c, save, bias, bias_rows)
+    if (bias is not None or out is not None) and save:
+        raise ValueError('lstm_gates: the folded bias and output buffers are inference-only forms')
+    return _LSTMGates.apply(zx, zh, c, save, bias, bias_rows, out)
 
 
 def _live(xs):

@@ -277,10 +277,14 @@ class DeviceGenerator:
         sample = sample_record_hip if st['obs_dev'] == 'cuda' else sample_record_torch
         a = sample(st, out['policy'], env.legal(), out['value'], active, player, reward)
         if hidden is not None and mover is not None and st['obs_dev'] == 'cuda':
-            # one HIP launch for every state tensor (nn.masked_rows_copy_) instead of a where + copy per tensor
-            from .nn import masked_rows_copy_
-            masked_rows_copy_([h[mover] if st['pmajor'] else h[:, mover] for h in _leaves(hidden)],
-                              _leaves(out['hidden']), active.contiguous())
+            dst = [h[mover] if st['pmajor'] else h[:, mover] for h in _leaves(hidden)]
+            src = _leaves(out['hidden'])
+            # a net that advanced its stacked state in place (GeisterNet in an in-place session) left nothing to
+            # copy: finished games' states moved too, but nothing reads them again (their records are reset
+            # values); otherwise one HIP launch for every state tensor instead of a where + copy per tensor
+            if not all(d.data_ptr() == x.data_ptr() and d.stride() == x.stride() for d, x in zip(dst, src)):
+                from .nn import masked_rows_copy_
+                masked_rows_copy_(dst, src, active.contiguous())
         elif hidden is not None:
             def advance(h, nh):
                 live = active.view(-1, *([1] * (nh.dim() - 1)))
@@ -332,8 +336,9 @@ class DeviceGenerator:
         st = self._state()
         was_training = self.net.training
         self.net.eval()
-        session = getattr(self.net, 'inference_session', None)   # per-call weight preparation (GeisterNet)
-        with session() if session is not None else contextlib.nullcontext():
+        # per-call weight preparation (GeisterNet); its own stacked state is advanced in place by the net
+        session = getattr(self.net, 'inference_session', None)
+        with session(inplace_state=st['pmajor']) if session is not None else contextlib.nullcontext():
             out = self._generate(st, generator, alternating)
         self.net.train(was_training)
         return out
