@@ -307,6 +307,7 @@ class GeisterNet(nn.Module):
                 'hidden': hidden}
 
     _bn_coef = None   # BatchNorm (alpha, beta) of an inference session, per module
+    _vr_session = None   # the value / return heads stacked for an inference session
 
     @contextlib.contextmanager
     def inference_session(self, inplace_state=False):
@@ -333,11 +334,22 @@ class GeisterNet(nn.Module):
         self._bn_coef_buf = bufs
         self._bn_coef = {id(m): bufs[k][0] for k, m in (('bn1', self.bn1), ('p', self.head_p_move.bn),
                                                          ('v', self.head_v.bn), ('r', self.head_r.bn))}
+        hv, hr = self.head_v, self.head_r
+        if (bufs['v'][0].is_cuda and hv.conv.weight.shape[0] == 1 and hr.conv.weight.shape[0] == 1
+                and hv.bn.num_features == 1 and hr.bn.num_features == 1):
+            with torch.no_grad():   # [alpha_v, alpha_r, beta_v, beta_r] and the two 1x1 conv weights
+                vr = getattr(self, '_vr_buf', None) or {}
+                vr['w'] = torch.cat([hv.conv.weight, hr.conv.weight], out=vr.get('w'))
+                cv, cr = bufs['v'][0], bufs['r'][0]
+                vr['coef'] = torch.cat([cv[:1], cr[:1], cv[1:], cr[1:]], out=vr.get('coef'))
+            self._vr_buf = vr
+            self._vr_session = vr
         try:
             with self.body.inference_session(inplace_state):
                 yield
         finally:
             self._bn_coef = None
+            self._vr_session = None
 
     def _forward_inference(self, x, hidden):
         """forward in eval mode without autograd on the HIP path (self-play): the same operations, with each
@@ -367,8 +379,21 @@ class GeisterNet(nn.Module):
         hp, hv, hr = self.head_p_move, self.head_v, self.head_r
         p_move = hp.conv2(bn_relu(hp.bn, hp.conv1(h))).reshape(-1, hp.outputs)
         policy = torch.cat([p_move, self.head_p_set(scalar[:, :1])], dim=-1)
-        v = hv.fc(bn_relu(hv.bn, hv.conv(h)).reshape(-1, hv.hidden_units))
-        r = hr.fc(bn_relu(hr.bn, hr.conv(h)).reshape(-1, hr.hidden_units))
+        vr = self._vr_session
+        if vr is not None and hv.hidden_units == hr.hidden_units:
+            # in a session the value and return heads' 1x1 convs run as one 2-channel conv and their
+            # BatchNorm + ReLU as one apply (per-channel: the same values as the two heads apart)
+            from .. import _native
+            y = F.conv2d(h, vr['w'])
+            a = torch.empty_like(y)
+            _native.check(_native.load().hrl_bn_apply(
+                _native.ptr(y), y.shape[0], 2, y[0, 0].numel(), _native.ptr(vr['coef']), _native.ptr(vr['coef'][2:]),
+                1, _native.ptr(a), _native.stream_of(y.device)), 'hrl_bn_apply')
+            v = hv.fc(a[:, 0].reshape(-1, hv.hidden_units))
+            r = hr.fc(a[:, 1].reshape(-1, hr.hidden_units))
+        else:
+            v = hv.fc(bn_relu(hv.bn, hv.conv(h)).reshape(-1, hv.hidden_units))
+            r = hr.fc(bn_relu(hr.bn, hr.conv(h)).reshape(-1, hr.hidden_units))
         return {'policy': policy, 'value': torch.tanh(v), 'return': r, 'hidden': hidden}
 
     # ---- the learner's unroll in three parts (train._unroll_sequence) ----
