@@ -473,6 +473,7 @@ class GeisterBatch:
     P = 2
     MAX_PLIES = 202
     ALTERNATING = True   # the mover is ply % 2 in every live game (colours alternate, geister.py:389)
+    REWARD_STATELESS = True   # reward() does not depend on the state: the generator may read it before step()
     OBS_SHAPE = {'board': (BOARD_PLANES, *BOARD), 'scalar': (SCALARS,)}
     MOVES = 144
     # initial squares of the 8 pieces of each colour (geister.py:179-182); 'B2' = x 1, y 1
@@ -708,6 +709,11 @@ class Environment(BaseEnvironment):
     def reset(self, args=None):
         self.game.reset()
         self.record = []
+        # piece identities (geister.py:202-227: board_index / piece_position): the reference lists legal
+        # moves piece by piece in this order, and seeded samplers draw over that list (generation.py:53)
+        self._where = [-1] * 16         # piece index (colour * 8 + initial slot) -> cell x*6+y, -1 off board
+        self._who = [-1] * 36           # cell -> piece index
+        self._layouts_set = 0
 
     def __str__(self):
         b = self.game.board[0].view(6, 6).tolist()
@@ -717,8 +723,34 @@ class Environment(BaseEnvironment):
             self.action2str(a, i % 2) for i, a in enumerate(self.record))
 
     def play(self, action, _=None):
-        self.game.step(torch.tensor([int(action)]), torch.tensor([True]))
-        self.record.append(int(action))
+        action = int(action)
+        self._track(action, self.turn())
+        self.game.step(torch.tensor([action]), torch.tensor([True]))
+        if action < GeisterBatch.MOVES:
+            self.record.append(action)
+
+    def _track(self, action, c):
+        """Follow the pieces' identities through a move (geister.py:208-236, 359-393)."""
+        if action >= GeisterBatch.MOVES:                       # a layout: pieces c*8 .. c*8+7 placed
+            for idx, cell in enumerate(GeisterBatch.OPOS[c]):
+                self._where[c * 8 + idx] = cell
+                self._who[cell] = c * 8 + idx
+            return
+        d, x, y = action // 36, (action % 36) // 6, action % 6
+        if c == 1:
+            d, x, y = 3 - d, 5 - x, 5 - y
+        dx, dy = GeisterBatch.DIRS[d]
+        src, nx, ny = x * 6 + y, x + dx, y + dy
+        piece = self._who[src]
+        self._who[src] = -1
+        if not (0 <= nx < 6 and 0 <= ny < 6):                 # off the board through a goal
+            self._where[piece] = -1
+            return
+        dst = nx * 6 + ny
+        if self._who[dst] >= 0:                                # capture
+            self._where[self._who[dst]] = -1
+        self._who[dst] = piece
+        self._where[piece] = dst
 
     def turn(self):
         return int(self.game.color[0])
@@ -734,7 +766,24 @@ class Environment(BaseEnvironment):
         return {0: o[0], 1: o[1]}
 
     def legal_actions(self, _=None):
-        return torch.nonzero(self.game.legal()[0]).view(-1).tolist()
+        """In the reference's order (geister.py:472-486): layouts 144..213 before the game, then the mover's
+        pieces by index, each piece's directions 0..3."""
+        legal = self.game.legal()[0].tolist()
+        if legal[GeisterBatch.MOVES]:
+            return [a for a in range(GeisterBatch.MOVES, ACTIONS) if legal[a]]
+        c = self.turn()
+        out = []
+        for cell in self._where[c * 8:(c + 1) * 8]:
+            if cell < 0:
+                continue
+            x, y = divmod(cell, 6)
+            if c == 1:
+                x, y = 5 - x, 5 - y
+            for d in range(4):
+                a = (3 - d if c == 1 else d) * 36 + x * 6 + y
+                if legal[a]:
+                    out.append(a)
+        return out
 
     def action_length(self):
         return ACTIONS

@@ -14,9 +14,10 @@ initial weights as the reference module would):
   tanh(Linear(64, 1)), both bias-free.  116,928 parameters.
 
 The rules live in kaggle_environments, which is not installed here, so this
-module has no batched rules; ``Environment`` is the reference plugin's
-environment (with this net) where kaggle_environments and a HandyRL checkout
-are importable, and raises the reference module's ImportError otherwise.  The learner trains GeeseNet
+module has no rules of its own; ``Environment`` raises an ImportError that
+points to the reference plugin by module path (``make_env`` imports any
+module path, so ``env: handyrl.envs.kaggle.hungry_geese`` in config.yaml
+drops the reference env in unchanged).  The learner trains GeeseNet
 on make_batch-layout batches (solo training, turn_based_training=False:
 P = Pp = 1, train.py:57-58), see synthetic.geese_batch.
 
@@ -93,26 +94,18 @@ class GeeseNet(nn.Module):
 
 
 class Environment:
-    """Hungry Geese rules.  The reference's rules wrap kaggle_environments (hungry_geese.py:18, :60-230);
-    they are not restated here.  With kaggle_environments and a HandyRL checkout on ``sys.path``,
-    ``Environment(args)`` is the reference plugin's environment with ``net()`` returning this module's
-    GeeseNet (same modules and state_dict keys, HIP torus convs after ``nn.accelerate``); without them it
-    raises the ImportError the reference module would."""
+    """Hungry Geese rules.  The reference's rules wrap kaggle_environments (hungry_geese.py:18, :60-230) and are
+    not restated here, and this package never imports the reference.  ``Environment(args)`` raises an
+    ImportError naming the way in: with kaggle_environments and a HandyRL checkout importable, name the
+    reference plugin by module path in ``config.yaml`` (``env: handyrl.envs.kaggle.hungry_geese``), which
+    ``make_env`` imports as given; its ``net()`` has this module's GeeseNet keys, so ``nn.accelerate`` runs it on
+    the HIP torus convs."""
 
-    def __new__(cls, args=None):
-        try:
-            import kaggle_environments  # noqa: F401
-        except ImportError as e:
-            raise ImportError('Hungry Geese rules need kaggle_environments, which is not installed; '
-                              'GeeseNet trains on make_batch-layout batches without it') from e
-        try:
-            from handyrl.envs.kaggle import hungry_geese as reference
-        except ImportError as e:
-            raise ImportError('Hungry Geese rules: the reference plugin handyrl.envs.kaggle.hungry_geese '
-                              '(a HandyRL checkout on sys.path) provides them') from e
-        env = reference.Environment(args or {})
-        env.net = cls.net.__get__(env)
-        return env
+    def __init__(self, args=None):
+        raise ImportError("Hungry Geese rules live in the reference plugin (they need kaggle_environments): set "
+                          "'env: handyrl.envs.kaggle.hungry_geese' in config.yaml with kaggle_environments and a "
+                          "HandyRL checkout importable; GeeseNet itself trains on make_batch-layout batches "
+                          "without them")
 
     def net(self):
         return GeeseNet

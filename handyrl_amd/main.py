@@ -12,14 +12,24 @@ written) with the actors and the learner on the GPU:
 
 * ``prepare_env`` / ``make_env`` resolve the env by name or module path
   (environment.py:18-39) and ``env.net()`` gives the model class;
-* generation is the env module's batched form (``BATCHED``) played by
-  ``rollout.DeviceGenerator``, ``update_episodes`` games per epoch with the
-  current weights (the reference's workers hold the latest published model);
-* episodes go to ``rollout.DeviceReplay`` (``maximum_episodes``, recency
-  weighting); training starts once ``minimum_episodes`` are stored;
+* generation: an env module with a batched (device) twin (``BATCHED``:
+  TicTacToe, Geister, CIGeister) in the stock layout (turn_based_training,
+  no opponent observation) is played by ``rollout.DeviceGenerator`` into
+  ``rollout.DeviceReplay``; ANY other env -- a user's module, ParallelTicTacToe,
+  the reference's own plugins named by module path, ``observation: True``,
+  solo training -- is played through the plugin API by
+  ``hostgen.HostBatchGenerator`` (host envs, one batched GPU forward per
+  ply, generation.py's semantics) into ``hostgen.MomentReplay``;
+  ``generator: host`` in train_args forces that path for every env;
+* ``update_episodes`` games per epoch with the current weights (the
+  reference's workers hold the latest published model), recency-weighted
+  replay of ``maximum_episodes``; training starts once ``minimum_episodes``
+  are stored.  The three counts are global, as in the reference: under
+  torchrun each rank generates and keeps 1/world of them;
 * ``trainer.Trainer`` runs the epoch (its lr / data-count EMA schedule is the
   reference's, train.py:394-401) for ``steps_per_epoch`` steps (default: the
-  epoch's new env-steps over B*T, at least 1);
+  epoch's new env-steps of ALL ranks over the global batch world*B*T, at
+  least 1 -- every rank runs the same count, so their collectives pair up);
 * data parallel under torchrun: every rank generates and trains its own
   shard, the gradients are SUMmed over RCCL (distributed.py), rank 0 saves.
 
@@ -37,6 +47,7 @@ import yaml
 
 from . import distributed as hdist
 from .environment import make_env, prepare_env
+from .hostgen import HostBatchGenerator, MomentReplay
 from .rollout import DeviceGenerator, DeviceReplay, TicTacToeBatch
 from .trainer import Trainer
 
@@ -74,11 +85,13 @@ class ReplayBatcher:
         return self.replay.sample(self.args['batch_size'], self.args['forward_steps'], generator=self.g)
 
 
+def _per_rank(n, world):
+    return max(1, -(-int(n) // world))
+
+
 def train_main(args, device=None, loss_fn=None, model_dir='models', log=print):
     """The learner cycle of train.py:425-560 on the device; returns the trained model (CPU copy)."""
     env_args, targs = args['env_args'], {**TRAIN_DEFAULTS, **args['train_args']}
-    if not (targs['turn_based_training'] and not targs['observation']):
-        raise ValueError('device self-play covers turn_based_training=True, observation=False')
     rank, world, local = hdist.init_process_group('cuda' if device is None else device.type)
     if device is None:
         if not torch.cuda.is_available():
@@ -89,8 +102,13 @@ def train_main(args, device=None, loss_fn=None, model_dir='models', log=print):
     env = make_env(env_args)
     module = type(env).__module__
     batched = _batched_envs().get(module)
-    if batched is None:
-        raise ValueError('no batched (device) form of env %r for self-play' % module)
+    mode = targs.get('generator', 'auto')
+    if mode not in ('auto', 'device', 'host'):
+        raise ValueError("train_args['generator'] must be auto, device or host, not %r" % (mode,))
+    stock = targs['turn_based_training'] and not targs['observation']
+    if mode == 'device' and (batched is None or not stock):
+        raise ValueError('no batched (device) form of env %r for this training mode' % module)
+    use_device = batched is not None and stock and mode != 'host'
     seed = int(targs['seed']) + rank
     torch.manual_seed(targs['seed'])            # the same initial weights on every rank
     net = env.net()()
@@ -99,12 +117,30 @@ def train_main(args, device=None, loss_fn=None, model_dir='models', log=print):
         net.load_state_dict(torch.load(os.path.join(model_dir, '%d.pth' % restart), map_location='cpu',
                                        weights_only=True))
     net = net.to(device)
-    games = int(targs['update_episodes'])
-    gen = DeviceGenerator(batched(games, device), net, gamma=targs['gamma'])
-    # binary observation planes live in HBM as uint8 (widened by the gather)
-    replay = DeviceReplay(int(targs['maximum_episodes']), batched.MAX_PLIES, batched.OBS_SHAPE, batched.A,
-                          batched.P, device, maximum_episodes=int(targs['maximum_episodes']), obs_dtype=torch.uint8)
+    # the episode counts are global (train.py:480-503, 549-552): each rank plays and keeps 1/world of them
+    games = _per_rank(targs['update_episodes'], world)
+    minimum = _per_rank(targs['minimum_episodes'], world)
+    maximum = _per_rank(targs['maximum_episodes'], world)
     rng = torch.Generator(device=device).manual_seed(seed)
+    if use_device:
+        gen = DeviceGenerator(batched(games, device), net, gamma=targs['gamma'])
+        # binary observation planes live in HBM as uint8 (widened by the gather)
+        replay = DeviceReplay(maximum, batched.MAX_PLIES, batched.OBS_SHAPE, batched.A, batched.P, device,
+                              maximum_episodes=maximum, obs_dtype=torch.uint8)
+
+        def play():
+            ep = gen.generate(generator=rng)
+            replay.add(ep)
+            return float(ep['length'].float().sum())
+    else:
+        slots = min(games, int(targs.get('host_envs', 256)))
+        gen = HostBatchGenerator(lambda: make_env(env_args), net, targs, E=slots, seed=seed)
+        replay = MomentReplay({**targs, 'maximum_episodes': maximum}, device, maximum_episodes=maximum)
+
+        def play():
+            eps = gen.generate(games)
+            replay.add(eps)
+            return float(sum(ep['steps'] for ep in eps))
     trainer = Trainer(targs, net, ReplayBatcher(replay, targs, rng), device=device, world_size=world,
                       loss_fn=loss_fn)
     episodes = 0
@@ -112,18 +148,25 @@ def train_main(args, device=None, loss_fn=None, model_dir='models', log=print):
 
     def generate():
         nonlocal episodes
-        ep = gen.generate(generator=rng)
-        replay.add(ep)
         episodes += games
-        return float(ep['length'].float().sum())
+        return play()
+
+    def global_steps(n):
+        """Every rank's new env-steps summed: all ranks derive the same step count from it."""
+        if world == 1:
+            return n
+        t = torch.tensor([n], dtype=torch.float64, device=device if device.type == 'cuda' else 'cpu')
+        return float(hdist.all_reduce_sum_([t])[0].item())
+
     new_steps = 0.0
-    while episodes < int(targs['minimum_episodes']):
+    while episodes < minimum:
         new_steps += generate()
     epoch = restart
     model = None
     while targs['epochs'] < 0 or epoch < restart + targs['epochs']:
         new_steps += generate()
-        steps = targs.get('steps_per_epoch') or max(1, math.ceil(new_steps / (targs['batch_size'] * targs['forward_steps'])))
+        steps = targs.get('steps_per_epoch') or max(1, math.ceil(
+            global_steps(new_steps) / (world * targs['batch_size'] * targs['forward_steps'])))
         new_steps = 0.0
         model = trainer.train(max_steps=int(steps))
         epoch += 1

@@ -267,7 +267,12 @@ class DeviceGenerator:
         else:
             h_in = map_r(hidden, lambda h: h[st['rows'], player])
         out = self.net(o, h_in)
-        reward = env.reward() if hasattr(env, 'reward') else None
+        # the reference reads the reward after env.step (generation.py:59-65); an env whose reward does not
+        # depend on the state (REWARD_STATELESS, e.g. Geister's -0.01 per ply) has it recorded by the
+        # sampling launch, any other env's after its step below
+        has_reward = hasattr(env, 'reward')
+        early = has_reward and getattr(env, 'REWARD_STATELESS', False)
+        reward = env.reward() if early else None
         # slot t of every record is written once per call, so a finished game keeps the reset value
         def record(buf, x, fill=0):
             live = active.view(-1, *([1] * (x.dim() - 1)))
@@ -296,6 +301,9 @@ class DeviceGenerator:
                     h[st['rows'], player] = torch.where(live, nh, h[st['rows'], player])
             bimap_r(hidden, out['hidden'], advance)
         env.step(a, active)
+        if has_reward and not early:
+            r = env.reward().to(st['reward'].dtype)
+            st['reward'].index_copy_(1, t, torch.where(active.view(-1, 1), r, 0).unsqueeze(1))
         t.add_(1)
 
     def _returns(self, st):

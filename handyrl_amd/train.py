@@ -365,11 +365,15 @@ def backward_total(losses, inputs=None, retain_graph=None):
     if vec is None:
         torch.autograd.backward(total, inputs=inputs, retain_graph=retain_graph)
         return
-    seed = _SEEDS.get(vec.device)
-    if seed is None:   # made once, in the eager warm-up before any graph capture
+    key = (vec.device, vec.dtype)
+    seed = _SEEDS.get(key)
+    if seed is None:
         seed = torch.zeros(6, dtype=vec.dtype, device=vec.device)
         seed[4] = 1.0
-        _SEEDS[vec.device] = seed
+        # cached only when made outside a graph capture (the eager warm-up): a seed made inside one lives in
+        # the capture's pool and is the capture's own
+        if not (vec.is_cuda and torch.cuda.is_current_stream_capturing()):
+            _SEEDS[key] = seed
     torch.autograd.backward(vec, grad_tensors=seed, inputs=inputs, retain_graph=retain_graph)
 
 

@@ -42,6 +42,16 @@ Fixtures written
     list that raises ``update_flag`` at the epoch's last batch): the lr and
     ``data_cnt_ema`` after each epoch (the epoch-end schedule, :396-398) and
     the final weights.
+``generation.npz`` + ``generation.json``
+    ``handyrl.generation.Generator.generate`` (generation.py:20-88) on seeded
+    games with a seeded env network (batch-1 ``ModelWrapper.inference``,
+    model.py:43-53): TicTacToe with and without ``observation``,
+    ParallelTicTacToe (simultaneous ``turns()``; its step draws from
+    ``random``) with and without ``observation``, Geister (recurrent
+    GeisterNet) with ``observation``.  Game k of a case runs after
+    ``random.seed(seed + k)``.  Every moment is stored as arrays: turn players,
+    observations / values (observation flags), masked policies, action masks,
+    actions, rewards (None flags), returns, and the outcome.
 ``learner.npz`` + ``learner.json``
     Three learner steps of the TicTacToe ``SimpleConv2dModel`` exactly as
     ``Trainer.train`` runs them (train.py:375-385): loss, backward,
@@ -50,7 +60,9 @@ Fixtures written
 Usage:  python tests/golden/make_golden.py
 """
 
+import bz2
 import json
+import pickle
 import os
 import random
 import sys
@@ -609,8 +621,109 @@ def trainer_case():
     return arrays, {'args': args, 'epochs': epochs, 'seed': 2025}
 
 
+# ---------------------------------------------------------------------------
+# generation.py episodes (host-env batched generator parity)
+# ---------------------------------------------------------------------------
+
+GEN_CASES = (   # (name, env, observation, games, game seed, net seed)
+    ('ttt_obs', 'TicTacToe', True, 6, 4000, 11),
+    ('ttt', 'TicTacToe', False, 4, 4100, 11),
+    ('pttt', 'ParallelTicTacToe', False, 6, 4200, 11),
+    ('pttt_obs', 'ParallelTicTacToe', True, 6, 4300, 11),
+    ('geister_obs', 'Geister', True, 1, 4400, 12),
+)
+
+
+def generation_cases():
+    arrays, manifest = {}, []
+    nets = {}
+    for ci, (name, env_name, obs_flag, games, seed, net_seed) in enumerate(GEN_CASES):
+        env = make_env({'env': env_name})
+        torch.manual_seed(net_seed)
+        net = env.net()()
+        key = (env_name if env_name != 'ParallelTicTacToe' else 'TicTacToe', net_seed)
+        if key not in nets:
+            nets[key] = net
+            if key[0] == 'TicTacToe':      # 29k parameters: stored; GeisterNet is rebuilt from its seed
+                for k, v in net.state_dict().items():
+                    arrays['net:%s:%d:%s' % (key[0], net_seed, k)] = _np(v)
+        sums = {k: float(v.double().sum()) for k, v in net.state_dict().items()}
+        model = ModelWrapper(net)
+        gen = Generator(env, {'observation': obs_flag, 'gamma': 0.8, 'compress_steps': 4})
+        players = env.players()
+        P = len(players)
+        case = {'id': ci, 'name': name, 'env': env_name, 'observation': obs_flag, 'net_seed': net_seed,
+                'net_key': key[0], 'seeds': [], 'steps': [], 'obs_keys': None, 'players': players,
+                'param_sums': sums}
+        for k in range(games):
+            random.seed(seed + k)
+            ep = gen.generate({p: model for p in players}, {'player': players})
+            assert ep is not None
+            moments = sum([pickle.loads(bz2.decompress(b)) for b in ep['moment']], [])
+            L = len(moments)
+            m0 = moments[0]
+            o0 = m0['observation'][m0['turn'][0]]
+            A = len(m0['policy'][m0['turn'][0]])
+            pre = '%d:%d:' % (ci, k)
+            turn = np.zeros((L, P), dtype=bool)
+            omask = np.zeros((L, P), dtype=bool)
+            tmask = np.zeros((L, P), dtype=bool)
+            pol = np.zeros((L, P, A), dtype=np.float32)
+            amask = np.zeros((L, P, A), dtype=np.float32)
+            act = np.full((L, P), -1, dtype=np.int64)
+            val = np.zeros((L, P), dtype=np.float32)
+            rew = np.full((L, P), np.nan, dtype=np.float64)
+            ret = np.zeros((L, P), dtype=np.float64)
+            if isinstance(o0, dict):
+                case['obs_keys'] = list(o0.keys())
+                obs = {kk: np.zeros((L, P) + np.shape(vv), dtype=np.float32) for kk, vv in o0.items()}
+            else:
+                obs = np.zeros((L, P) + np.shape(o0), dtype=np.float32)
+            for t, m in enumerate(moments):
+                for j, p in enumerate(players):
+                    turn[t, j] = p in m['turn']
+                    if m['observation'][p] is not None:
+                        omask[t, j] = True
+                        if isinstance(obs, dict):
+                            for kk in obs:
+                                obs[kk][t, j] = m['observation'][p][kk]
+                        else:
+                            obs[t, j] = m['observation'][p]
+                    if m['value'][p] is not None:
+                        val[t, j] = np.asarray(m['value'][p]).reshape(-1)[0]
+                    if m['policy'][p] is not None:
+                        tmask[t, j] = True
+                        pol[t, j] = m['policy'][p]
+                        amask[t, j] = m['action_mask'][p]
+                        act[t, j] = m['action'][p]
+                    if m['reward'][p] is not None:
+                        rew[t, j] = m['reward'][p]
+                    ret[t, j] = m['return'][p]
+            for nm, a in (('turn', turn), ('omask', omask), ('tmask', tmask), ('policy', pol),
+                          ('amask', amask), ('action', act), ('value', val), ('reward', rew), ('return', ret)):
+                arrays[pre + nm] = a
+            if isinstance(obs, dict):
+                for kk, a in obs.items():
+                    arrays[pre + 'obs.' + kk] = a
+            else:
+                arrays[pre + 'obs'] = obs
+            arrays[pre + 'outcome'] = np.array([ep['outcome'][p] for p in players], dtype=np.float64)
+            case['seeds'].append(seed + k)
+            case['steps'].append(L)
+        manifest.append(case)
+    return arrays, manifest
+
+
 def main():
     only = sys.argv[1:]
+    if only == ['generation'] or not only:
+        arr, man = generation_cases()
+        np.savez_compressed(os.path.join(OUT, 'generation.npz'), **arr)
+        with open(os.path.join(OUT, 'generation.json'), 'w') as f:
+            json.dump(man, f, indent=1)
+        print('generation: %d cases, %s plies' % (len(man), [c['steps'] for c in man]))
+        if only:
+            return
     if only == ['trainer']:
         arr, meta = trainer_case()
         np.savez_compressed(os.path.join(OUT, 'trainer.npz'), **arr)

@@ -49,47 +49,31 @@ def test_make_env_by_module_path():
     assert env.action_length() == 9
 
 
-def test_hungry_geese_rules_need_kaggle():
-    """As the reference module (hungry_geese.py:18) the rules need kaggle_environments; the net does not."""
-    try:
-        import kaggle_environments  # noqa: F401
-        pytest.skip('kaggle_environments installed')
-    except ImportError:
-        pass
-    with pytest.raises(ImportError):
+def test_hungry_geese_points_to_the_reference_plugin():
+    """The rules need kaggle_environments (hungry_geese.py:18); this package never imports the reference, it
+    raises an ImportError naming the module path that drops the reference env in; the net is available."""
+    with pytest.raises(ImportError, match='handyrl.envs.kaggle.hungry_geese'):
         make_env({'env': 'HungryGeese'})
     from handyrl_amd.envs.hungry_geese import Environment
     assert Environment.net(None).__name__ == 'GeeseNet'
 
 
-def test_hungry_geese_delegates_to_reference_plugin(monkeypatch):
-    """With kaggle_environments and the reference plugin importable (stand-ins here), make_env returns the
-    plugin's environment, its net() this package's GeeseNet."""
+def test_make_env_imports_a_plugin_module_path(monkeypatch):
+    """A plugin named by module path in config.yaml (e.g. the reference's handyrl.envs.kaggle.hungry_geese)
+    is imported as given and instantiated with the env args (environment.py:29-37)."""
     import sys
     import types
     calls = []
 
-    class PluginEnv:
+    class PluginEnv(BaseEnvironment):
         def __init__(self, args):
             calls.append(args)
 
-        def net(self):
-            return None
-
-    plugin = types.ModuleType('handyrl.envs.kaggle.hungry_geese')
+    plugin = types.ModuleType('my_plugin_envs_geese')
     plugin.Environment = PluginEnv
-    pkgs = {name: types.ModuleType(name) for name in ('handyrl', 'handyrl.envs', 'handyrl.envs.kaggle')}
-    pkgs['handyrl'].envs = pkgs['handyrl.envs']
-    pkgs['handyrl.envs'].kaggle = pkgs['handyrl.envs.kaggle']
-    pkgs['handyrl.envs.kaggle'].hungry_geese = plugin
-    monkeypatch.setitem(sys.modules, 'kaggle_environments', types.ModuleType('kaggle_environments'))
-    for name, m in pkgs.items():
-        monkeypatch.setitem(sys.modules, name, m)
-    monkeypatch.setitem(sys.modules, 'handyrl.envs.kaggle.hungry_geese', plugin)
-    env = make_env({'env': 'HungryGeese', 'x': 1})
-    assert isinstance(env, PluginEnv) and calls == [{'env': 'HungryGeese', 'x': 1}]
-    from handyrl_amd.envs.hungry_geese import GeeseNet
-    assert env.net() is GeeseNet
+    monkeypatch.setitem(sys.modules, 'my_plugin_envs_geese', plugin)
+    env = make_env({'env': 'my_plugin_envs_geese', 'x': 1})
+    assert isinstance(env, PluginEnv) and calls == [{'env': 'my_plugin_envs_geese', 'x': 1}]
 
 
 def test_geister_plugin_replays_reference_games(games):   # noqa: F811
