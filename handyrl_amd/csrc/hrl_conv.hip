@@ -681,6 +681,8 @@ struct BlockBwdArgs {
 };
 
 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // buffer descriptor over `bytes` bytes at `base`; the inputs are made provably wave-uniform so the compiler
 // keeps the descriptor in SGPRs (no waterfall loops around the buffer ops)
@@ -954,6 +956,522 @@ __global__ __launch_bounds__(kThreads) void conv3x3_block_bwd_kernel(BlockBwdArg
     HRL_STAMP_WALL(15);
 }
 
+// ------------------------------------------------------------------ one chain block's backward, tile-shared
+// conv3x3_block_bwd_kernel gives every wave a 16-row tile of its own and runs load + BN apply, the weight
+// gradient and the input gradient back to back with one wave per SIMD: HBM is busy in the load phase only and
+// idles through both MFMA phases (no registers left for a prefetch; profiles/r02_stamps_block_bwd.txt).  This
+// form shares each tile among a workgroup of 8 waves (2 per SIMD) and pipelines the tiles:
+//  * every wave stages 1/8 of tile k+1 -- BN_i's backward apply gives dY, the prologue gives x' = relu(x*a + b),
+//    both split exactly into bf16 h/m/l parts -- into a second LDS buffer while the tile-k MFMAs run, and its
+//    loads of tile k+2 are in flight behind that (30 registers per lane);
+//  * LDS per buffer: dY and x' as part images [part][cell][channel][row] (27 KB each), so no MFMA operand is
+//    split twice and none needs VALU: the weight gradient reads x'_p and dY_q (channel per lane, 8 rows) with
+//    ds_read_b128, the input gradient reads dY_p (row per lane, 8 channels) with ds_read_b64_tr_b16 (T10);
+//    the 16-byte chunks are XOR-swizzled so these reads are conflict-free, and a wave stages a diagonal of
+//    (channel, row pair)s so the stage's 4-byte writes are too;
+//  * waves 4-7 own the weight gradient (taps {0,1}, {2,5}, {3,4}, {6,7,8}), waves 0-3 the input gradient
+//    (column tile ct = wave & 1, output cells {4..8} or {0..3}) with the h and m parts of their weights in
+//    registers (the l parts in LDS); the MFMA cycles of each SIMD's two waves (w, w+4) are balanced to 2 %;
+//  * the two waves of a SIMD order their phases oppositely (the heavier one computes first), so one wave's
+//    staging VALU and LDS writes run beside its partner's MFMAs;
+//  * the epilogue re-reads the raw x it needs (its loads are issued before the tile's MFMAs) and the gin tile
+//    leaves through an 18 KB staging buffer with coalesced 16-byte stores.
+// The input gradient runs split_tile_mfma's arithmetic in its order (bit-identical gin); the weight gradient sums
+// each tap over the workgroup's tiles in one accumulator: the same pairs in the same per-tile order, a different
+// association across tiles than the per-wave kernel.
+namespace bb2 {
+
+// diagnostic variants (tools/bb2_variants.sh builds them; the product is 0): bit 1 = no stage VALU (raw bits
+// packed into the images), bit 2 = no MFMA phase, bit 4 = no epilogue / gin store, bit 8 = every wave computes
+// first, bit 16 = no gin store (epilogue kept)
+#ifndef BB2_VARIANT
+#define BB2_VARIANT 0
+#endif
+constexpr int kVariant = BB2_VARIANT;
+
+constexpr int kWaves = 8;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kPartBytes = kCells * kC * kTile * 2;        // one bf16 part image (9 KB)
+constexpr int kImgBytes = 3 * kPartBytes;                  // h, m, l (27 KB)
+constexpr int kOutBytes = kTile * kRow * 4;                // gin staging tile [16][288] fp32 (18 KB)
+constexpr int kWlBytes = kTaps * 2 * 64 * 16;              // the weights' l parts [tap][ct][lane] (18 KB)
+constexpr int kDy0 = 0;                                    // dY images, buffers 0/1
+constexpr int kX0 = 2 * kImgBytes;                         // x' images, buffers 0/1
+constexpr int kOut0 = 4 * kImgBytes;
+constexpr int kWl0 = kOut0 + kOutBytes;
+constexpr int kLdsBytes = kWl0 + kWlBytes;                 // 147,456 B
+static_assert(kLdsBytes <= 160 * 1024, "LDS");
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// byte offset of the 16-byte chunk holding rows 8*half .. 8*half+7 of (cell c, channel ch) in a part image:
+// chunk (2*(ch&7) + half) ^ 9*((ch>>3)&1) of the cell's 256-byte row ch>>3
+__device__ __forceinline__ int img_off(int c, int ch, int half) {
+    const int R = ch >> 3, j = ch & 7;
+    return c * 1024 + R * 256 + 16 * ((2 * j + half) ^ (9 * (R & 1)));
+}
+
+__device__ __forceinline__ void bar_lds() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// wave roles: input-gradient waves 0-3 (column tile kCt, output cells kQ[0..kNq)), weight-gradient waves 4-7
+// (taps kTap[0..kNt)); kCFirst: compute before staging
+template <int W> struct Role;
+template <> struct Role<0> { static constexpr bool kIg = true, kCFirst = true; static constexpr int kCt = 0, kNq = 5, kNt = 0;
+                             static constexpr int kQ[5] = {4, 5, 6, 7, 8}; static constexpr int kTap[1] = {0}; };
+template <> struct Role<1> { static constexpr bool kIg = true, kCFirst = true; static constexpr int kCt = 1, kNq = 5, kNt = 0;
+                             static constexpr int kQ[5] = {4, 5, 6, 7, 8}; static constexpr int kTap[1] = {0}; };
+template <> struct Role<2> { static constexpr bool kIg = true, kCFirst = false; static constexpr int kCt = 0, kNq = 4, kNt = 0;
+                             static constexpr int kQ[4] = {0, 1, 2, 3}; static constexpr int kTap[1] = {0}; };
+template <> struct Role<3> { static constexpr bool kIg = true, kCFirst = false; static constexpr int kCt = 1, kNq = 4, kNt = 0;
+                             static constexpr int kQ[4] = {0, 1, 2, 3}; static constexpr int kTap[1] = {0}; };
+template <> struct Role<4> { static constexpr bool kIg = false, kCFirst = false; static constexpr int kCt = 0, kNq = 0, kNt = 2;
+                             static constexpr int kQ[1] = {0}; static constexpr int kTap[2] = {0, 1}; };
+template <> struct Role<5> { static constexpr bool kIg = false, kCFirst = false; static constexpr int kCt = 0, kNq = 0, kNt = 2;
+                             static constexpr int kQ[1] = {0}; static constexpr int kTap[2] = {2, 5}; };
+template <> struct Role<6> { static constexpr bool kIg = false, kCFirst = true; static constexpr int kCt = 0, kNq = 0, kNt = 2;
+                             static constexpr int kQ[1] = {0}; static constexpr int kTap[2] = {3, 4}; };
+template <> struct Role<7> { static constexpr bool kIg = false, kCFirst = true; static constexpr int kCt = 0, kNq = 0, kNt = 3;
+                             static constexpr int kQ[1] = {0}; static constexpr int kTap[3] = {6, 7, 8}; };
+
+// does the wave's work involve input cell p (weight gradient: x'_p; input gradient: dY_p)?
+template <int W> __device__ constexpr bool uses_p(int p) {
+    using R = Role<W>;
+    if constexpr (R::kIg) {
+        for (int s = 0; s < R::kNq; ++s)
+            if (tap_of(p, R::kQ[s]) >= 0) return true;
+    } else {
+        for (int s = 0; s < R::kNt; ++s) {
+            const int dy = R::kTap[s] / 3, dx = R::kTap[s] % 3;
+            const int qy = p / 3 - dy + 1, qx = p % 3 - dx + 1;
+            if (qy >= 0 && qy < 3 && qx >= 0 && qx < 3) return true;
+        }
+    }
+    return false;
+}
+// does the input-gradient wave use tap t?
+template <int W> __device__ constexpr bool uses_tap(int t) {
+    using R = Role<W>;
+    for (int s = 0; s < R::kNq; ++s)
+        for (int p = 0; p < kCells; ++p)
+            if (tap_of(p, R::kQ[s]) == t) return true;
+    return false;
+}
+
+// diagnostic build (-DHRL_STAMPS, tools/bb2_stamps.py): lane 0 of every wave writes the shader clock at the
+// phase boundaries of iterations 2 and 3, WITHOUT draining (the wave's issue timeline; the compiler's own waits
+// for loaded registers stay where they are): slot = ((block * 8 + wave) * 2 + iteration - 2) * 8 + point
+#ifdef HRL_STAMPS
+#define BB2_STAMP(it, k)                                                                                        \
+    do {                                                                                                       \
+        if ((it) == 2 || (it) == 3) {                                                                          \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                        \
+            if (lane == 0 && g_hrl_stamps)                                                                     \
+                g_hrl_stamps[(((size_t)blockIdx.x * 8 + W) * 2 + (it) - 2) * 8 + (k)] = t_;                    \
+        }                                                                                                      \
+    } while (0)
+#else
+#define BB2_STAMP(it, k) do { } while (0)
+#endif
+
+template <bool PRO, int EPI, int W>
+__device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, int lane) {
+    using R = Role<W>;
+    constexpr bool kIg = R::kIg;
+    constexpr int kNq = R::kNq > 0 ? R::kNq : 1;
+    constexpr int kNt = R::kNt > 0 ? R::kNt : 1;
+    constexpr int kCt = R::kCt;
+    const int ch = lane & 31, hh = lane >> 5;
+    // BN_i's backward apply for channel ch (bn_bwd_apply_kernel's per-channel values), the prologue's BN_{i-1}
+    const float mu = a.bn_mean[ch], kk = a.bn_k[ch], gmn = a.bn_gm[ch], is = a.bn_invstd[ch];
+    const float ww = a.bn_w ? a.bn_w[ch] : 1.0f;
+    const float al = is * ww;
+    const float be = (a.bn_b ? a.bn_b[ch] : 0.0f) - mu * al;
+    float pa = 1.f, pb = 0.f;
+    if constexpr (PRO) {
+        pa = a.in_alpha[ch];
+        pb = a.in_beta[ch];
+    }
+    // the input gradient's weights: h and m parts of its taps in registers ([tap][ct][part][lane] layout of
+    // conv3x3_block_bwd_kernel's LDS fragments: lane l holds W'[tap][ci = 8(l>>4) + e][co = 16ct + (l&15)])
+    uint4 wh[kTaps], wm[kTaps];
+    if constexpr (kIg) {
+        const int ci0 = 8 * (lane >> 4), j = lane & 15;
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) {
+            if (!uses_tap<W>(t)) continue;
+            uint32_t hv[4], mv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int tc = t * 2 + kCt;
+                const float w0 = a.wpk[(tc * kC + ci0 + 2 * d) * 16 + j];
+                const float w1 = a.wpk[(tc * kC + ci0 + 2 * d + 1) * 16 + j];
+                uint32_t h0, m0, l0, h1, m1, l1;
+                hrl_split::split3(w0, h0, m0, l0);
+                hrl_split::split3(w1, h1, m1, l1);
+                hv[d] = h0 | (h1 << 16);
+                mv[d] = m0 | (m1 << 16);
+            }
+            wh[t] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+            wm[t] = make_uint4(mv[0], mv[1], mv[2], mv[3]);
+        }
+    }
+    float em = 0.f, ea = 1.f, eb = 0.f;     // epilogue 2: BN_{i-1} of this lane's output channel
+    if constexpr (EPI == 2 && kIg) {
+        em = a.ep_mean[kCt * 16 + (lane & 15)];
+        ea = a.ep_alpha[kCt * 16 + (lane & 15)];
+        eb = a.ep_beta[kCt * 16 + (lane & 15)];
+    }
+    double s1 = 0.0, s2 = 0.0;
+    f32x16 wacc[kNt];
+#pragma unroll
+    for (int t = 0; t < kNt; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wacc[t][i] = 0.f;
+
+    const int64_t ntiles = (a.M + kTile - 1) / kTile;
+    const int64_t t0 = blockIdx.x;
+    const int64_t step = gridDim.x;
+    const int n_iter = t0 < ntiles ? (int)((ntiles - 1 - t0) / step + 1) : 0;
+    // this lane stages rows rho0, rho0 + 1 (a diagonal over the waves: conflict-free image writes) and cells
+    // c0 .. c0+4 of channel ch (lanes hh = 1 take cells 4..8)
+    const int rho0 = 2 * ((W + (ch >> 2)) & 7);
+    const int c0 = hh ? 4 : 0;
+    const int ldoff = (rho0 * kRow + ch * kCells + c0) * 4;
+    float G[2][5], Y[2][5], X[2][5];
+    auto rsrc_of = [&](const float *base, int it, int &rows) __attribute__((always_inline)) {
+        const int64_t t = t0 + (int64_t)it * step;
+        const bool ok = it < n_iter;
+        rows = ok ? (int)min<int64_t>(kTile, a.M - t * kTile) : 0;
+        return wave_rsrc(base + (ok ? t * kTile * kRow : 0), (uint32_t)rows * kRow * 4);
+    };
+    auto issue = [&](int it) __attribute__((always_inline)) {   // loads of iteration it's tile (zeros past the end)
+        int rows;
+        const __amdgpu_buffer_rsrc_t rg = rsrc_of(a.g, it, rows), ry = rsrc_of(a.y, it, rows),
+                                     rx = rsrc_of(a.x, it, rows);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int off = ldoff + r * kRow * 4;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const __amdgpu_buffer_rsrc_t rs = k == 0 ? rg : (k == 1 ? ry : rx);
+                float(&d)[5] = k == 0 ? G[r] : (k == 1 ? Y[r] : X[r]);
+                const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+                const u32x2 u = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 12, 0, 0);
+                d[0] = __uint_as_float(v.x);
+                d[1] = __uint_as_float(v.y);
+                d[2] = __uint_as_float(v.z);
+                d[3] = __uint_as_float(u.x);
+                d[4] = __uint_as_float(u.y);
+            }
+        }
+    };
+    auto stage = [&](int it) __attribute__((always_inline)) {   // registers -> the images of buffer it & 1
+        const int64_t t = t0 + (int64_t)it * step;
+        const int rows = (int)max<int64_t>(0, min<int64_t>(kTile, a.M - t * kTile));
+        unsigned char *dyi = smem + kDy0 + (it & 1) * kImgBytes;
+        unsigned char *xi = smem + kX0 + (it & 1) * kImgBytes;
+        uint32_t dp[3][5], xp[3][5];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const bool valid = rho0 + r < rows;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                // dY = BN_i backward apply (bn_bwd_apply_kernel's float operations); rows past the batch are 0
+                const float yv = Y[r][i];
+                float gv = G[r][i];
+                if (!(yv * al + be > 0.f)) gv = 0.f;
+                const float tt = (yv - mu) * kk;
+                float d = (((gv - gmn) - tt) * is) * ww;
+                d = valid ? d : 0.f;
+                float xv = X[r][i];
+                if constexpr (PRO) {   // bn_apply_kernel's float operations
+                    const float u = xv * pa + pb;
+                    xv = u < 0.f ? 0.f : u;
+                }
+                uint32_t h, m, l, xh, xm, xl;
+                if constexpr (kVariant & 1) {
+                    h = __float_as_uint(G[r][i]) >> 16; m = h; l = h;
+                    xh = __float_as_uint(X[r][i]) >> 16; xm = xh; xl = __float_as_uint(Y[r][i]) >> 16;
+                } else {
+                    hrl_split::split3(d, h, m, l);
+                    hrl_split::split3(xv, xh, xm, xl);
+                }
+                const int sh = 16 * r;
+                if (r == 0) {
+                    dp[0][i] = h; dp[1][i] = m; dp[2][i] = l;
+                    xp[0][i] = xh; xp[1][i] = xm; xp[2][i] = xl;
+                } else {
+                    dp[0][i] |= h << sh; dp[1][i] |= m << sh; dp[2][i] |= l << sh;
+                    xp[0][i] |= xh << sh; xp[1][i] |= xm << sh; xp[2][i] |= xl << sh;
+                }
+            }
+        }
+        const int half = rho0 >> 3, sub = 2 * (rho0 & 7);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const int o = img_off(c0 + i, ch, half) + sub;
+#pragma unroll
+            for (int part = 0; part < 3; ++part) {
+                *reinterpret_cast<uint32_t *>(dyi + part * kPartBytes + o) = dp[part][i];
+                *reinterpret_cast<uint32_t *>(xi + part * kPartBytes + o) = xp[part][i];
+            }
+        }
+    };
+    f32x4 acc[kNq];
+    float rv[kNq < 4 ? 4 : kNq][4];   // the epilogue's raw x, loaded before the tile's MFMAs
+    auto load_ref = [&](int it) __attribute__((always_inline)) {
+        // the wave's output cells are consecutive (kQ[s] = kQ[0] + s): per row one run of kNq floats
+        if constexpr (kIg && (EPI == 2 || EPI == 3)) {
+            static_assert(R::kQ[R::kNq - 1] == R::kQ[0] + R::kNq - 1, "consecutive output cells");
+            int rows;
+            const __amdgpu_buffer_rsrc_t rx = rsrc_of(a.x, it, rows);
+            const int co = kCt * 16 + (lane & 15);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = (lane >> 4) * 4 + rr;
+                const int off = (row * kRow + co * kCells + R::kQ[0]) * 4;
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+                rv[0][rr] = __uint_as_float(v.x);
+                rv[1][rr] = __uint_as_float(v.y);
+                rv[2][rr] = __uint_as_float(v.z);
+                rv[3][rr] = __uint_as_float(v.w);
+                if constexpr (R::kNq > 4)
+                    rv[4 % kNq][rr] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, off + 16, 0, 0));
+            }
+        }
+    };
+    auto compute = [&](int it) __attribute__((always_inline)) {
+        const unsigned char *dyi = smem + kDy0 + (it & 1) * kImgBytes;
+        if constexpr (kVariant & 2) {
+            if constexpr (kIg) {
+#pragma unroll
+                for (int s = 0; s < kNq; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            }
+        } else if constexpr (!kIg) {
+            // weight gradient: dW[tap] += x'_p^T (32 ci x 16 rows) . dY_q (16 rows x 32 co), p ascending
+            const unsigned char *xi = smem + kX0 + (it & 1) * kImgBytes;
+            const int kg = lane >> 5;
+#pragma unroll
+            for (int p = 0; p < kCells; ++p) {
+                if (!uses_p<W>(p)) continue;
+                const int o = img_off(p, ch, kg);
+                const uint4 Ah = *reinterpret_cast<const uint4 *>(xi + o);
+                const uint4 Am = *reinterpret_cast<const uint4 *>(xi + kPartBytes + o);
+                const uint4 Al = *reinterpret_cast<const uint4 *>(xi + 2 * kPartBytes + o);
+#pragma unroll
+                for (int s = 0; s < R::kNt; ++s) {
+                    const int dy = R::kTap[s] / 3, dx = R::kTap[s] % 3;
+                    const int qy = p / 3 - dy + 1, qx = p % 3 - dx + 1;
+                    if (qy < 0 || qy > 2 || qx < 0 || qx > 2) continue;
+                    const int ob = img_off(qy * 3 + qx, ch, kg);
+                    const uint4 Bh = *reinterpret_cast<const uint4 *>(dyi + ob);
+                    const uint4 Bm = *reinterpret_cast<const uint4 *>(dyi + kPartBytes + ob);
+                    const uint4 Bl = *reinterpret_cast<const uint4 *>(dyi + 2 * kPartBytes + ob);
+                    f32x16 c = wacc[s];
+                    c = mfma32(Al, Bh, c);   // smallest terms first
+                    c = mfma32(Am, Bm, c);
+                    c = mfma32(Ah, Bl, c);
+                    c = mfma32(Am, Bh, c);
+                    c = mfma32(Ah, Bm, c);
+                    c = mfma32(Ah, Bh, c);
+                    wacc[s] = c;
+                }
+            }
+        } else {
+            // input gradient blocks (q, kCt): acc += sum_p dY_p (16 rows x 32 co) . W'[tap(p, q)][kCt], p ascending
+#pragma unroll
+            for (int s = 0; s < kNq; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            const uint4 *wl = reinterpret_cast<const uint4 *>(smem + kWl0) + lane;
+            const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+            const int tr_sub = 8 * (pp & 1);
+#pragma unroll
+            for (int p = 0; p < kCells; ++p) {
+                if (!uses_p<W>(p)) continue;
+                uint32_t A[3][4];
+#pragma unroll
+                for (int part = 0; part < 3; ++part) {
+#pragma unroll
+                    for (int hlf = 0; hlf < 2; ++hlf) {
+                        const int o = part * kPartBytes + img_off(p, 8 * g + 4 * hlf + qq, pp >> 1) + tr_sub;
+                        const v4s r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_v4s *)((__attribute__((address_space(3))) unsigned char *)(dyi + o)));
+                        const uint2 u = __builtin_bit_cast(uint2, r);
+                        A[part][2 * hlf] = u.x;
+                        A[part][2 * hlf + 1] = u.y;
+                    }
+                }
+                const uint4 Ah = make_uint4(A[0][0], A[0][1], A[0][2], A[0][3]);
+                const uint4 Am = make_uint4(A[1][0], A[1][1], A[1][2], A[1][3]);
+                const uint4 Al = make_uint4(A[2][0], A[2][1], A[2][2], A[2][3]);
+#pragma unroll
+                for (int s = 0; s < R::kNq; ++s) {
+                    const int tap = tap_of(p, R::kQ[s]);
+                    if (tap < 0) continue;
+                    const uint4 Bl = wl[(tap * 2 + kCt) * 64];
+                    f32x4 c = acc[s];
+                    c = mfma_bf16(Al, wh[tap], c);   // smallest terms first
+                    c = mfma_bf16(Am, wm[tap], c);
+                    c = mfma_bf16(Ah, Bl, c);
+                    c = mfma_bf16(Am, wh[tap], c);
+                    c = mfma_bf16(Ah, wm[tap], c);
+                    c = mfma_bf16(Ah, wh[tap], c);
+                    acc[s] = c;
+                }
+            }
+        }
+    };
+    auto epilogue = [&](int it) __attribute__((always_inline)) {   // accumulators -> the gin staging tile
+        if constexpr (kIg) {
+            const int64_t t = t0 + (int64_t)it * step;
+            const int rows = (int)min<int64_t>(kTile, a.M - t * kTile);
+            float *out = reinterpret_cast<float *>(smem + kOut0);
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int s = 0; s < R::kNq; ++s) {
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int row = (lane >> 4) * 4 + rr;         // C/D: row = (lane>>4)*4 + reg, col = lane & 15
+                    const int co = kCt * 16 + (lane & 15);
+                    float v = acc[s][rr];
+                    if constexpr (EPI == 3) {
+                        if (!(rv[s][rr] > 0.f)) v = 0.f;
+                    } else if constexpr (EPI == 2) {   // bn_bwd_reduce_kernel's mask and sums
+                        const float x0 = rv[s][rr];
+                        const float gm = (x0 * ea + eb > 0.f && row < rows) ? v : 0.f;
+                        t1 += gm;
+                        t2 += gm * (x0 - em);
+                    }
+                    out[row * kRow + co * kCells + R::kQ[s]] = v;
+                }
+            }
+            if constexpr (EPI == 2) {
+                s1 += (double)t1;
+                s2 += (double)t2;
+            }
+        }
+    };
+    auto store = [&](int it) __attribute__((always_inline)) {   // the gin tile, coalesced: 1152 float4
+        int rows;
+        const __amdgpu_buffer_rsrc_t ro = rsrc_of(a.gin, it, rows);
+        const float *out = reinterpret_cast<const float *>(smem + kOut0);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            const int f = W * 64 + lane + kThreads * m;
+            if (f < kTile * kRow / 4) {
+                const float4 v = *reinterpret_cast<const float4 *>(out + 4 * f);
+                u32x4 w;
+                w.x = __float_as_uint(v.x);
+                w.y = __float_as_uint(v.y);
+                w.z = __float_as_uint(v.z);
+                w.w = __float_as_uint(v.w);
+                __builtin_amdgcn_raw_buffer_store_b128(w, ro, 16 * f, 0, 0);   // rows past the batch: dropped
+            }
+        }
+    };
+
+    if (n_iter > 0) {
+        issue(0);
+        stage(0);
+        issue(1);
+    }
+    bar_lds();                                      // weights' l parts and tile 0 in LDS
+    for (int it = 0; it < n_iter; ++it) {
+        BB2_STAMP(it, 0);
+        load_ref(it);
+        // stage / issue run unconditionally (past the last tile they stage and load zeros that nothing reads):
+        // a branch around them makes the compiler's wait for the loaded registers vmcnt(0) at the loop head,
+        // which then also waits for the previous iteration's gin stores
+        if constexpr (R::kCFirst || (kVariant & 8)) {
+            compute(it);
+            BB2_STAMP(it, 1);
+            stage(it + 1);
+            issue(it + 2);
+            BB2_STAMP(it, 2);
+        } else {
+            stage(it + 1);
+            issue(it + 2);
+            BB2_STAMP(it, 1);
+            compute(it);
+            BB2_STAMP(it, 2);
+        }
+        bar_lds();                                  // tile it+1 staged; the previous gin tile stored
+        BB2_STAMP(it, 3);
+        if constexpr (!(kVariant & 4)) {
+            epilogue(it);
+            BB2_STAMP(it, 4);
+            bar_lds();                              // the gin tile complete in LDS
+            BB2_STAMP(it, 5);
+            if constexpr (!(kVariant & 16)) store(it);
+        }
+        BB2_STAMP(it, 6);
+    }
+    // weight-gradient partials partial[block][tap][ci][co] (C/D layout of 32x32x16: col = co = lane & 31,
+    // row = ci = (i&3) + 8(i>>2) + 4h); each tap has one owner wave: no fold inside the workgroup
+    if constexpr (!kIg) {
+        constexpr int kW = kTaps * kC * kC;
+        float *outp = a.wpart + (int64_t)blockIdx.x * kW;
+        const int h = lane >> 5;
+#pragma unroll
+        for (int s = 0; s < R::kNt; ++s)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int ci = (i & 3) + 8 * (i >> 2) + 4 * h;
+                outp[(R::kTap[s] * kC + ci) * kC + ch] = wacc[s][i];
+            }
+    }
+    if constexpr (EPI == 2) {   // BN_{i-1}'s sums: waves 0-3 [wave][lane] -> channel (wave&1)*16 + (lane&15)
+        __syncthreads();
+        double *dred = reinterpret_cast<double *>(smem);
+        if (kIg) {
+            dred[(W * 64 + lane) * 2 + 0] = s1;
+            dred[(W * 64 + lane) * 2 + 1] = s2;
+        }
+        __syncthreads();
+        if (W == 0) {
+            const int c = lane >> 1, k = lane & 1, ct = c >> 4, l16 = c & 15;
+            double tot = 0.0;
+            for (int w = ct; w < 4; w += 2)
+                for (int lg = 0; lg < 4; ++lg) tot += dred[(w * 64 + lg * 16 + l16) * 2 + k];
+            a.part[((int64_t)blockIdx.x * kC + c) * 2 + k] = tot;
+        }
+    }
+}
+
+}  // namespace bb2
+
+template <bool PRO, int EPI>
+__global__ __launch_bounds__(bb2::kThreads) void conv3x3_block_bwd2_kernel(BlockBwdArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[bb2::kLdsBytes];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    {   // the weights' l parts: [tap][ct][lane] x 16 bytes (lane l: W'[tap][ci = 8(l>>4) + e][co = 16ct + (l&15)])
+        uint32_t *wl = reinterpret_cast<uint32_t *>(smem + bb2::kWl0);
+        constexpr int kWords = bb2::kWlBytes / 4;
+        for (int i = threadIdx.x; i < kWords; i += bb2::kThreads) {
+            const int d = i & 3, l = (i >> 2) & 63, tc = i >> 8;      // tc = tap*2 + ct
+            const int ci = 8 * (l >> 4) + 2 * d, j = l & 15;
+            const float w0 = a.wpk[(tc * kC + ci) * 16 + j];
+            const float w1 = a.wpk[(tc * kC + ci + 1) * 16 + j];
+            wl[i] = split_part(w0, 2) | (split_part(w1, 2) << 16);
+        }
+    }
+    switch (wave) {
+    case 0: bb2::run<PRO, EPI, 0>(a, smem, lane); break;
+    case 1: bb2::run<PRO, EPI, 1>(a, smem, lane); break;
+    case 2: bb2::run<PRO, EPI, 2>(a, smem, lane); break;
+    case 3: bb2::run<PRO, EPI, 3>(a, smem, lane); break;
+    case 4: bb2::run<PRO, EPI, 4>(a, smem, lane); break;
+    case 5: bb2::run<PRO, EPI, 5>(a, smem, lane); break;
+    case 6: bb2::run<PRO, EPI, 6>(a, smem, lane); break;
+    default: bb2::run<PRO, EPI, 7>(a, smem, lane); break;
+    }
+}
+
 // fold per-workgroup partials into dW[co][ci][3][3]: a workgroup owns 64 consecutive
 // outputs; its 4 waves take every 4th partial (4 independent sums in flight per
 // thread) and combine in a fixed order -> deterministic.
@@ -1012,6 +1530,9 @@ __global__ void conv3x3_pack_n_kernel(WeightList wl, int n, float *__restrict__ 
 
 // Forward / input-gradient arithmetic: exact-split bf16 MFMA (1, default) or fp32 MFMA (0).
 int g_split = 1;
+// Chain block backward with an input gradient: 1 = tile-shared conv3x3_block_bwd2_kernel (default),
+// 0 = the per-wave conv3x3_block_bwd_kernel.
+int g_block_form = 1;
 
 // One 4-wave workgroup per CU (LDS: 109 KB forward, 145 KB weight gradient);
 // the waves walk row tiles grid-stride so the next tile's loads overlap MFMAs.
@@ -1044,6 +1565,12 @@ int64_t hrl_conv3x3_workspace_bytes(int64_t M) {
 }
 
 int64_t hrl_conv3x3_stats_blocks(int64_t M) { return M < 1 ? -1 : grid_for(M); }
+
+int hrl_conv3x3_set_block_form(int form) {
+    const int prev = g_block_form;
+    g_block_form = form ? 1 : 0;
+    return prev;
+}
 
 int hrl_conv3x3_set_split(int on) {
     const int prev = g_split;
@@ -1162,16 +1689,27 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
     const bool pro = in_alpha != nullptr;
 #define HRL_BLOCK_LAUNCH(PRO, EPI, DG) \
     hipLaunchKernelGGL((conv3x3_block_bwd_kernel<PRO, EPI, DG>), dim3(grid), dim3(kThreads), 0, s, a)
+#define HRL_BLOCK2_LAUNCH(PRO, EPI) \
+    hipLaunchKernelGGL((conv3x3_block_bwd2_kernel<PRO, EPI>), dim3(grid), dim3(bb2::kThreads), 0, s, a)
     if (!gin) {
         if (pro) HRL_BLOCK_LAUNCH(true, 0, false); else HRL_BLOCK_LAUNCH(false, 0, false);
+    } else if (g_block_form == 0) {   // the per-wave form (kept for comparison)
+        if (epilogue == 2) {
+            if (pro) HRL_BLOCK_LAUNCH(true, 2, true); else HRL_BLOCK_LAUNCH(false, 2, true);
+        } else if (epilogue == 3) {
+            if (pro) HRL_BLOCK_LAUNCH(true, 3, true); else HRL_BLOCK_LAUNCH(false, 3, true);
+        } else {
+            if (pro) HRL_BLOCK_LAUNCH(true, 0, true); else HRL_BLOCK_LAUNCH(false, 0, true);
+        }
     } else if (epilogue == 2) {
-        if (pro) HRL_BLOCK_LAUNCH(true, 2, true); else HRL_BLOCK_LAUNCH(false, 2, true);
+        if (pro) HRL_BLOCK2_LAUNCH(true, 2); else HRL_BLOCK2_LAUNCH(false, 2);
     } else if (epilogue == 3) {
-        if (pro) HRL_BLOCK_LAUNCH(true, 3, true); else HRL_BLOCK_LAUNCH(false, 3, true);
+        if (pro) HRL_BLOCK2_LAUNCH(true, 3); else HRL_BLOCK2_LAUNCH(false, 3);
     } else {
-        if (pro) HRL_BLOCK_LAUNCH(true, 0, true); else HRL_BLOCK_LAUNCH(false, 0, true);
+        if (pro) HRL_BLOCK2_LAUNCH(true, 0); else HRL_BLOCK2_LAUNCH(false, 0);
     }
 #undef HRL_BLOCK_LAUNCH
+#undef HRL_BLOCK2_LAUNCH
     int rc = status();
     if (rc) return rc;
     hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, wpart, grid,

@@ -167,6 +167,12 @@ int64_t hrl_conv3x3_stats_blocks(int64_t M);
  * both fp32 operands on v_mfma_f32_16x16x32_bf16 (six partial products, fp32 accumulation; error below one fp32
  * rounding per product), 0 the fp32 v_mfma_f32_16x16x4_f32.  Process-wide; returns the previous setting. */
 int hrl_conv3x3_set_split(int on);
+/* Kernel form of hrl_conv3x3_block_backward with an input gradient: form != 0 (the default) the tile-shared,
+ * pipelined kernel (8 waves share each 16-row tile: weight gradient and input gradient blocks split over the
+ * waves, the next tile staged in a second LDS buffer while the MFMAs run), 0 the per-wave kernel.  The input
+ * gradient and the epilogue are the same in both; the weight gradient sums the tiles in a different
+ * association.  Process-wide; returns the previous setting. */
+int hrl_conv3x3_set_block_form(int form);
 /* Both packed layouts of n <= 8 weights (32, 32, 3, 3) in one launch: packed[(l*2 + f) * 9216], f = 0 forward,
  * 1 input gradient (host array of device pointers).  hrl_conv3x3_forward_ex with flip | 2 takes `weight`
  * as such a packed layout and skips its own packing launch. */

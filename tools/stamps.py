@@ -15,17 +15,17 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, 'tools', 'micro', 'libhrl_stamps.so')
-SRCS = ['hrl_targets.hip', 'hrl_loss.hip', 'hrl_conv.hip']
+SRCS = sorted(f for f in os.listdir(os.path.join(ROOT, 'handyrl_amd', 'csrc')) if f.endswith('.hip'))   # all: _native binds every symbol
 
 
 def build():
     flags = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-DHRL_STAMPS',
              '-I', os.path.join(ROOT, 'include')]
-    objs = []
-    for s in SRCS:
-        o = '/tmp/stamps_' + s + '.o'
-        subprocess.check_call(['hipcc'] + flags + ['-c', os.path.join(ROOT, 'handyrl_amd', 'csrc', s), '-o', o])
-        objs.append(o)
+    objs = ['/tmp/stamps_' + s + '.o' for s in SRCS]
+    procs = [subprocess.Popen(['hipcc'] + flags + ['-c', os.path.join(ROOT, 'handyrl_amd', 'csrc', s), '-o', o])
+             for s, o in zip(SRCS, objs)]
+    if any(p.wait() for p in procs):
+        raise RuntimeError('stamps build failed')
     subprocess.check_call(['hipcc', '--offload-arch=gfx950', '-shared', '-fPIC', '-o', LIB] + objs)
     print('built', LIB)
 
