@@ -17,6 +17,10 @@ Rank 0 prints ONE JSON line with, besides the metric:
                 bytes per launch / mean launch time from HIP events on the
                 launch stream, at the step's own size and at a cold,
                 larger-than-Infinity-Cache size;
+  loss_roofline the step's fused loss forward (csrc/hrl_loss.hip, the scans inside it), algorithmic bytes
+                / HIP-event time;
+  block_roofline the step's dominant kernel, one chain block's backward (3 launches per step): HBM and
+                split-MFMA fractions;
   cpu_baseline  the CPU learner oracle (oracle/learner.py, restating
                 train.py:218-258 + 382-385) timed on this host, 1 thread as the
                 reference ships (model.py:8), on a bounded sample (N=1 only).
@@ -151,6 +155,115 @@ def time_conv(device, M, iters=20):
             'launches_per_step': '3 forward + 3 input-gradient (same kernel) + 3 weight-gradient',
             'note': 'achieved = algorithmic fp32 FLOPs / time; peak = bf16 dense MFMA peak / 6 partial products of the '
                     'exact bf16 split (fp32-accurate); SURVEY D3: reported beside, not instead of, the scan roofline'}
+
+
+def loss_bytes_per_launch(B, T, P=2, Pp=1, A=9):
+    """Algorithmic bytes of the fused loss forward (csrc/hrl_loss.hip, value head only).
+
+    Per env-step (b, t): reads target and behaviour logits 8*Pp*A, action 8*Pp, episode mask 4, progress 4,
+    turn / observation masks and the value head 12*P; writes the backward's entropy 4*Pp, value target 4*P and
+    turn advantage 4; per trajectory the outcome 4*P.
+    """
+    per_step = 8 * Pp * A + 8 * Pp + 8 + 12 * P + 4 * Pp + 4 * P + 4
+    return B * T * per_step + B * 4 * P
+
+
+def time_loss(device, B, T, iters=50):
+    """The step's loss forward as it runs in the step (loss_fused_kernel + its fixed-order fold), timed with
+    HIP events on the launch stream over `iters` launches captured in one HIP graph."""
+    from handyrl_amd.train import _FusedLoss
+    from handyrl_amd import _native
+    batch = tictactoe_batch(B, T, device, seed=5)
+    g = torch.Generator(device=device).manual_seed(4)
+    tpol = (torch.randn(B, T, 1, 9, device=device, generator=g) - batch['action_mask']).contiguous()
+    value = torch.tanh(torch.randn(B, T, 2, 1, device=device, generator=g))
+    args = default_args(T, B)
+    alg = _native.ALG
+    cfg = {'value_target': alg[args['value_target']], 'policy_target': alg[args['policy_target']], 'symmetrize': 1,
+           'lambda': float(args['lambda']), 'gamma': float(args['gamma']),
+           'ent_coef': float(args['entropy_regularization']), 'ent_decay': float(args['entropy_regularization_decay'])}
+
+    def launch():
+        with torch.no_grad():
+            _FusedLoss.apply(tpol, value, None, batch['policy'], batch['action'], batch['episode_mask'],
+                             batch['turn_mask'], batch['observation_mask'], batch['progress'], batch['outcome'],
+                             None, None, cfg)
+    for _ in range(3):
+        launch()
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(side):
+        launch()
+    torch.cuda.current_stream(device).wait_stream(side)
+    with torch.cuda.graph(graph):
+        for _ in range(iters):
+            launch()
+    stream = torch.cuda.current_stream(device)
+    graph.replay()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    start.record(stream)
+    graph.replay()
+    end.record(stream)
+    end.synchronize()
+    us = start.elapsed_time(end) * 1e3 / iters
+    nbytes = loss_bytes_per_launch(B, T)
+    gbs = nbytes / (us * 1e-6) / 1e9
+    return {'kernel': 'loss_fused_kernel<VTRACE,UPGO,value,no return,A=9> + loss_reduce_kernel (the step\'s fused '
+                      'loss forward, its scans included)',
+            'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None, 'bytes_per_launch': nbytes,
+            'us_per_launch': round(us, 3), 'B': B, 'T': T,
+            'note': 'algorithmic bytes (DESIGN.md §4.4) / HIP-event time of the two launches; latency-bound at '
+                    'the step size (the wave\'s prep -> scan chain -> terms critical path)'}
+
+
+def time_block_backward(device, M, iters=20):
+    """The step's dominant kernel: one chain block's backward (conv3x3_block_bwd2_kernel, BN backward apply +
+    weight gradient + input gradient, csrc/hrl_conv.hip) at M = B*T rows, HIP events over back-to-back launches
+    (its weight-gradient fold launch included)."""
+    from handyrl_amd import _native
+    lib = _native.load()
+    P = _native.ptr
+    stream = _native.stream_of(device)
+    g0 = torch.Generator(device=device).manual_seed(1)
+    rnd = lambda *sh: torch.randn(*sh, device=device, generator=g0)   # noqa: E731
+    g, y, x = rnd(M, 288), rnd(M, 288), rnd(M, 288)
+    w = rnd(32, 32, 3, 3) * 0.1
+    c = [rnd(32).abs() + 0.5 for _ in range(11)]
+    packed = torch.empty(1, 2, 9216, device=device)
+    _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array([w]), 1, P(packed), stream), 'pack')
+    ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
+    part = torch.empty(lib.hrl_conv3x3_stats_blocks(M) * 64, dtype=torch.float64, device=device)
+    dw, gin = torch.empty(32, 32, 3, 3, device=device), torch.empty_like(g)
+
+    def launch():
+        _native.check(lib.hrl_conv3x3_block_backward(
+            P(g), P(y), M, *[P(t) for t in c[:6]], P(x), P(c[6]), P(c[7]), P(packed[0, 1]), P(dw), P(gin), 2,
+            P(c[8]), P(c[9]), P(c[10]), P(part), P(ws), ws_bytes, stream), 'block')
+    for _ in range(3):
+        launch()
+    s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    s0.record(torch.cuda.current_stream(device))
+    for _ in range(iters):
+        launch()
+    e0.record(torch.cuda.current_stream(device))
+    e0.synchronize()
+    us = s0.elapsed_time(e0) * 1e3 / iters
+    nbytes = 4 * M * 288 * 4                       # reads g, y, x; writes gin
+    flops = 2 * (2.0 * M * 49 * 32 * 32)           # weight gradient + input gradient
+    gbs, tf = nbytes / (us * 1e-6) / 1e9, flops / (us * 1e-6) / 1e12
+    mfma_peak = MFMA_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
+    return {'kernel': 'conv3x3_block_bwd2_kernel<PRO, EPI=2> + wgrad fold (one chain block backward)',
+            'bound': 'hbm+mfma', 'achieved_GBps': round(gbs, 1), 'frac_hbm': round(gbs / HBM_PEAK_GBS, 4),
+            'achieved_TFLOPs': round(tf, 1), 'frac_mfma_split': round(tf / mfma_peak, 4),
+            'bytes_per_launch': nbytes, 'flops_per_launch': flops, 'us_per_launch': round(us, 2), 'M': M,
+            'launches_per_step': 3,
+            'note': 'bytes = g, y, x read + gin written (dY and x\' stay on chip); flops = weight + input gradient '
+                    'on the 49 on-board tap blocks; split ceiling = bf16 dense peak / 6'}
 
 
 def pmc_traffic(B, T):
@@ -420,6 +533,8 @@ def main():
                              'traffic': pmc_traffic(cold['B'], T)},
         }
         net_roof = time_conv(device, B * T)
+        loss_roof = time_loss(device, B, T)
+        block_roof = time_block_backward(device, B * T)
         cpu = cpu_baseline() if (opts.cpu_baseline and world == 1) else None
         t9 = secondary_t9(device) if (opts.secondary and world == 1) else None
         ro = secondary_rollout(device) if (opts.secondary and world == 1) else None
@@ -445,6 +560,8 @@ def main():
                        'parallelism': 'dp%d' % world, 'hip_graph': use_graph},
             'roofline': roof,
             'net_roofline': net_roof,
+            'loss_roofline': loss_roof,
+            'block_roofline': block_roof,
             'cpu_baseline': cpu,
             'loss_per_dcnt': {k: v / max(stats.get('dcnt', 1.0), 1e-9) for k, v in stats.items()
                               if k in ('p', 'v', 'ent', 'total')},

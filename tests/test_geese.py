@@ -139,6 +139,32 @@ def test_geese_learner_matches_cpu_oracle(cuda, graph):
 
 
 @pytest.mark.gpu
+def test_geese_learner_full_T_vs_oracle(cuda):
+    """configs[3]'s T=64 at B=512 (32,768 trajectory cells; the CPU oracle's fp32 and fp64 steps take
+    ~30 s of 8 threads together): one LearnerStep with the HIP torus tower vs the CPU oracle learner from the
+    same seeded GeeseNet and batch: losses and gradient norm at rel 1e-5 against the fp32 oracle, every
+    parameter's clipped gradient against the fp64 step (no worse than twice the fp32 oracle's own error)."""
+    from handyrl_amd.synthetic import geese_batch, geese_args
+    from handyrl_amd.trainer import LearnerStep
+    from tests.test_learner_gpu import oracle_step_grads, check_grads_vs_fp64
+    B, T = 512, 64
+    args = geese_args(T, B)
+    batch = geese_batch(B, T, cuda, seed=9)
+    torch.manual_seed(2)
+    state = GeeseNet().state_dict()
+    r32, r64 = oracle_step_grads(GeeseNet, state, batch, args)
+    net = GeeseNet()
+    net.load_state_dict(state)
+    step = LearnerStep(net, args, cuda, graph=False)
+    out = step.step(batch)
+    torch.cuda.synchronize()
+    for k in ('p', 'v', 'ent', 'total', 'grad_norm'):
+        assert abs(float(out[k]) - r32[k]) <= 1e-5 * max(1.0, abs(r32[k])), (k, float(out[k]), r32[k])
+    got = {n: p.grad.detach().cpu().double() for n, p in step.net.named_parameters()}
+    check_grads_vs_fp64(got, r32, r64)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('residual,cin,N', [(True, 32, 41), (False, 17, 23), (True, 32, 1500)])
 def test_fused_torus_block_matches_torch(cuda, residual, cin, N):
     """nn.torus_block (conv with BN statistics in its epilogue, residual apply, masked BN backward,

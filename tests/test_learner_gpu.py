@@ -6,7 +6,9 @@
 * three learner steps of the TicTacToe net from the reference's initial
   weights: per-step losses and final weights vs the reference's;
 * the HIP-graph-captured step equals the eager step;
-* the BASELINE-size synthetic batch (B=4096, T=32) against the CPU oracle.
+* the BASELINE-size synthetic batch (B=4096, T=32) against the CPU oracle: the fused loss on fixed outputs,
+  and one full learner step of the real SimpleConv2dModel (HIP net, BN, chain block backward, clip, Adam)
+  at B=4096 with T=32 and T=9 (configs[1]).
 """
 
 import numpy as np
@@ -115,6 +117,75 @@ def test_baseline_batch_losses_vs_oracle(cuda, B, T):
     ref['total'].backward()
     np.testing.assert_allclose(net_gpu.p.grad.cpu().numpy(), net_cpu.p.grad.numpy(), rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(net_gpu.v.grad.cpu().numpy(), net_cpu.v.grad.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def oracle_step_grads(net_cls, state, batch, args, seed_threads=8):
+    """One CPU oracle learner step in fp32 (the reference's arithmetic: losses, grad norm, clipped gradients)
+    and in fp64 (the gradients' exact value to ~1e-15) from the same weights and batch."""
+    out = {}
+    threads = torch.get_num_threads()
+    torch.set_num_threads(seed_threads)
+    try:
+        for dt in (torch.float32, torch.float64):
+            net = net_cls()
+            net.load_state_dict(state)
+            net = net.to(dt)
+            b = {k: (v.cpu().to(dt) if v.is_floating_point() else v.cpu()) for k, v in batch.items()}
+            r = ol.CpuLearner(net, args).step(b)
+            r['grads'] = {n: p.grad.double().clone() for n, p in net.named_parameters()}
+            r['buffers'] = {n: t.clone() for n, t in net.named_buffers()}
+            out[dt] = r
+    finally:
+        torch.set_num_threads(threads)
+    return out[torch.float32], out[torch.float64]
+
+
+def check_grads_vs_fp64(got, r32, r64, floor=1e-5):
+    """Every parameter's clipped gradient: its norm-relative error against the fp64 oracle may not exceed
+    twice the fp32 CPU oracle's own (fp32 sums over B*T*cells terms with cancellation), nor `floor` when the
+    CPU's is smaller.  Returns the worst (name, gpu error, cpu error)."""
+    worst = None
+    for n, g64 in r64['grads'].items():
+        den = float(g64.norm())
+        if den == 0.0:
+            continue
+        e_gpu = float((got[n] - g64).norm()) / den
+        e_cpu = float((r32['grads'][n] - g64).norm()) / den
+        assert e_gpu <= max(2 * e_cpu, floor), (n, e_gpu, e_cpu)
+        if worst is None or e_gpu > worst[1]:
+            worst = (n, e_gpu, e_cpu)
+    return worst
+
+
+@pytest.mark.parametrize('T', [32, 9])
+def test_full_size_learner_step_vs_oracle(cuda, T):
+    """One LearnerStep of the real TicTacToe net at the metric's B=4096 (T=32, and configs[1]'s T=9) vs
+    oracle.learner.CpuLearner on the same batch from the same seeded weights: losses and the clipped
+    gradient norm at rel 1e-5 against the fp32 oracle, dcnt exact, every parameter's clipped gradient against
+    the same step in fp64 (no worse than twice the fp32 oracle's own error, check_grads_vs_fp64), and the
+    BatchNorm running statistics after the step."""
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.synthetic import tictactoe_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    B = 4096
+    args = default_args(T, B)
+    batch = tictactoe_batch(B, T, cuda, seed=11 + T)
+    torch.manual_seed(1)
+    state = SimpleConv2dModel().state_dict()
+    r32, r64 = oracle_step_grads(SimpleConv2dModel, state, batch, args)
+    net = SimpleConv2dModel()
+    net.load_state_dict(state)
+    step = LearnerStep(net, args, cuda, graph=False)
+    out = step.step(batch)
+    torch.cuda.synchronize()
+    assert out['dcnt'].item() == r32['dcnt']
+    for k in ('p', 'v', 'ent', 'total', 'grad_norm'):
+        _close(float(out[k]), r32[k], what=k)
+    got = {n: p.grad.detach().cpu().double() for n, p in step.net.named_parameters()}
+    check_grads_vs_fp64(got, r32, r64)
+    for n, b in step.net.named_buffers():
+        if n in r32['buffers'] and b.dtype.is_floating_point:
+            torch.testing.assert_close(b.cpu(), r32['buffers'][n], rtol=1e-5, atol=1e-6, msg=n)
 
 
 ALGS = ('MC', 'TD', 'UPGO', 'VTRACE')
