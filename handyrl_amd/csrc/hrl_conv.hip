@@ -974,8 +974,9 @@ __global__ __launch_bounds__(kThreads) void conv3x3_block_bwd_kernel(BlockBwdArg
 //    registers (the l parts in LDS); the MFMA cycles of each SIMD's two waves (w, w+4) are balanced to 2 %;
 //  * the two waves of a SIMD order their phases oppositely (the heavier one computes first), so one wave's
 //    staging VALU and LDS writes run beside its partner's MFMAs;
-//  * the epilogue re-reads the raw x it needs (its loads are issued before the tile's MFMAs) and the gin tile
-//    leaves through an 18 KB staging buffer with coalesced 16-byte stores.
+//  * the epilogue re-reads the raw x it needs (its loads are issued before the tile's MFMAs) and each input-
+//    gradient wave stores its gin block straight from the accumulators right after its MFMAs (per row one run of
+//    4-5 floats), so one barrier per tile remains and no wave waits for a staged gin tile.
 // The input gradient runs split_tile_mfma's arithmetic in its order (bit-identical gin); the weight gradient sums
 // each tap over the workgroup's tiles in one accumulator: the same pairs in the same per-tile order, a different
 // association across tiles than the per-wave kernel.
@@ -993,13 +994,11 @@ constexpr int kWaves = 8;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kPartBytes = kCells * kC * kTile * 2;        // one bf16 part image (9 KB)
 constexpr int kImgBytes = 3 * kPartBytes;                  // h, m, l (27 KB)
-constexpr int kOutBytes = kTile * kRow * 4;                // gin staging tile [16][288] fp32 (18 KB)
 constexpr int kWlBytes = kTaps * 2 * 64 * 16;              // the weights' l parts [tap][ct][lane] (18 KB)
 constexpr int kDy0 = 0;                                    // dY images, buffers 0/1
 constexpr int kX0 = 2 * kImgBytes;                         // x' images, buffers 0/1
-constexpr int kOut0 = 4 * kImgBytes;
-constexpr int kWl0 = kOut0 + kOutBytes;
-constexpr int kLdsBytes = kWl0 + kWlBytes;                 // 147,456 B
+constexpr int kWl0 = 4 * kImgBytes;
+constexpr int kLdsBytes = kWl0 + kWlBytes;                 // 129,024 B
 static_assert(kLdsBytes <= 160 * 1024, "LDS");
 
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -1325,51 +1324,49 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
             }
         }
     };
-    auto epilogue = [&](int it) __attribute__((always_inline)) {   // accumulators -> the gin staging tile
-        if constexpr (kIg) {
-            const int64_t t = t0 + (int64_t)it * step;
-            const int rows = (int)min<int64_t>(kTile, a.M - t * kTile);
-            float *out = reinterpret_cast<float *>(smem + kOut0);
-            float t1 = 0.f, t2 = 0.f;
+    auto epilogue = [&](int it) __attribute__((always_inline)) {   // accumulators -> gin, straight from registers
+        if constexpr (kIg && !(kVariant & 4)) {
+            int rows;
+            const __amdgpu_buffer_rsrc_t ro = rsrc_of(a.gin, it, rows);
+            const int co = kCt * 16 + (lane & 15);
+            if constexpr (EPI == 2) {   // bn_bwd_reduce_kernel's mask and sums
+                float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-            for (int s = 0; s < R::kNq; ++s) {
+                for (int s = 0; s < R::kNq; ++s) {
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    const int row = (lane >> 4) * 4 + rr;         // C/D: row = (lane>>4)*4 + reg, col = lane & 15
-                    const int co = kCt * 16 + (lane & 15);
-                    float v = acc[s][rr];
-                    if constexpr (EPI == 3) {
-                        if (!(rv[s][rr] > 0.f)) v = 0.f;
-                    } else if constexpr (EPI == 2) {   // bn_bwd_reduce_kernel's mask and sums
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = (lane >> 4) * 4 + rr;     // C/D: row = (lane>>4)*4 + reg, col = lane & 15
                         const float x0 = rv[s][rr];
-                        const float gm = (x0 * ea + eb > 0.f && row < rows) ? v : 0.f;
+                        const float gm = (x0 * ea + eb > 0.f && row < rows) ? acc[s][rr] : 0.f;
                         t1 += gm;
                         t2 += gm * (x0 - em);
                     }
-                    out[row * kRow + co * kCells + R::kQ[s]] = v;
                 }
-            }
-            if constexpr (EPI == 2) {
                 s1 += (double)t1;
                 s2 += (double)t2;
             }
-        }
-    };
-    auto store = [&](int it) __attribute__((always_inline)) {   // the gin tile, coalesced: 1152 float4
-        int rows;
-        const __amdgpu_buffer_rsrc_t ro = rsrc_of(a.gin, it, rows);
-        const float *out = reinterpret_cast<const float *>(smem + kOut0);
+            // per row the wave's output cells are one run of kNq floats (rows past the batch: dropped)
+            if constexpr (!(kVariant & 16)) {
 #pragma unroll
-        for (int m = 0; m < 3; ++m) {
-            const int f = W * 64 + lane + kThreads * m;
-            if (f < kTile * kRow / 4) {
-                const float4 v = *reinterpret_cast<const float4 *>(out + 4 * f);
-                u32x4 w;
-                w.x = __float_as_uint(v.x);
-                w.y = __float_as_uint(v.y);
-                w.z = __float_as_uint(v.z);
-                w.w = __float_as_uint(v.w);
-                __builtin_amdgcn_raw_buffer_store_b128(w, ro, 16 * f, 0, 0);   // rows past the batch: dropped
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int row = (lane >> 4) * 4 + rr;
+                    const int off = (row * kRow + co * kCells + R::kQ[0]) * 4;
+                    float v[kNq];
+#pragma unroll
+                    for (int s = 0; s < R::kNq; ++s) {
+                        v[s] = acc[s][rr];
+                        if constexpr (EPI == 3)
+                            if (!(rv[s][rr] > 0.f)) v[s] = 0.f;
+                    }
+                    u32x4 w;
+                    w.x = __float_as_uint(v[0]);
+                    w.y = __float_as_uint(v[1]);
+                    w.z = __float_as_uint(v[2]);
+                    w.w = __float_as_uint(v[3]);
+                    __builtin_amdgcn_raw_buffer_store_b128(w, ro, off, 0, 0);
+                    if constexpr (R::kNq > 4)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[4 % kNq]), ro, off + 16, 0, 0);
+                }
             }
         }
     };
@@ -1388,6 +1385,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         // which then also waits for the previous iteration's gin stores
         if constexpr (R::kCFirst || (kVariant & 8)) {
             compute(it);
+            epilogue(it);
             BB2_STAMP(it, 1);
             stage(it + 1);
             issue(it + 2);
@@ -1397,18 +1395,11 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
             issue(it + 2);
             BB2_STAMP(it, 1);
             compute(it);
+            epilogue(it);
             BB2_STAMP(it, 2);
         }
-        bar_lds();                                  // tile it+1 staged; the previous gin tile stored
+        bar_lds();                                  // tile it+1 staged, tile it's images free
         BB2_STAMP(it, 3);
-        if constexpr (!(kVariant & 4)) {
-            epilogue(it);
-            BB2_STAMP(it, 4);
-            bar_lds();                              // the gin tile complete in LDS
-            BB2_STAMP(it, 5);
-            if constexpr (!(kVariant & 16)) store(it);
-        }
-        BB2_STAMP(it, 6);
     }
     // weight-gradient partials partial[block][tap][ci][co] (C/D layout of 32x32x16: col = co = lane & 31,
     // row = ci = (i&3) + 8(i>>2) + 4h); each tap has one owner wave: no fold inside the workgroup

@@ -92,7 +92,15 @@ class FlatGrads:
 
 
 class GradAllReduce:
-    """Bucketed, backward-overlapped SUM all-reduce of a FlatGrads buffer."""
+    """Bucketed, backward-overlapped SUM all-reduce of a FlatGrads buffer.
+
+    A bucket's all-reduce is launched as soon as every gradient in it is final.  When that is, the first
+    step learns: a parameter's gradient can arrive in several events -- its autograd accumulate hook (which
+    also fires when a HIP Function wrote the gradient in place and returned None, nn.direct_grads), and
+    mark_ready() after nn.DeferredGrads.flush has added the batched weight gradients of a recurrent unroll,
+    i.e. after that parameter's hook already fired.  The first step counts each parameter's events and
+    launches every bucket at finish(); later steps count a parameter for its bucket at its last event.  A
+    parameter that gets no gradient (expected 0 events) never holds its bucket back."""
 
     def __init__(self, flat_grads, group=None, bucket_bytes=256 * 1024):
         self.fg = flat_grads
@@ -114,9 +122,10 @@ class GradAllReduce:
                 for j in cur:
                     self.param_bucket[j] = bid
                 cur, cur_lo, cur_hi = [], None, None
+        self._index = {id(p): i for i, p in enumerate(params)}
+        self.expected = None        # per parameter: gradient events per step (learned in the first step)
+        self._seen = [0] * len(params)
         self.bucket_size = [0] * len(self.buckets)
-        for j, b in self.param_bucket.items():
-            self.bucket_size[b] += 1
         self._pending = list(self.bucket_size)
         self._works = [None] * len(self.buckets)
         self._next = 0
@@ -124,29 +133,31 @@ class GradAllReduce:
 
     def _make_hook(self, i):
         def hook(_param):
-            if not self.enabled:
-                return      # a probe or capture pass: nothing is counted (and nothing launched)
-            b = self.param_bucket[i]
-            self._pending[b] -= 1
-            self._launch_ready()
+            self._event(i)
         return hook
 
     enabled = True
 
+    def _event(self, i):
+        if not self.enabled:
+            return      # a probe or capture pass: nothing is counted (and nothing launched)
+        self._seen[i] += 1
+        if self.expected is None:
+            return      # the learning step: every bucket launches at finish()
+        if self._seen[i] > self.expected[i]:
+            raise RuntimeError('parameter %d got %d gradient events this step, %d in the first: its bucket was '
+                               'already all-reduced' % (i, self._seen[i], self.expected[i]))
+        if self._seen[i] == self.expected[i]:
+            self._pending[self.param_bucket[i]] -= 1
+            self._launch_ready()
+
     def mark_ready(self, params):
-        """Params whose gradient was written outside autograd (nn.DeferredGrads.flush): count them
-        as accumulated, as their post-accumulate hook would.  Each parameter counts once, however
-        often it appears in ``params``."""
+        """Params whose gradient was written outside autograd (nn.DeferredGrads.flush): one more gradient
+        event each, however often a parameter appears in ``params``."""
         if not self.enabled:
             return
-        index = {id(p): i for i, p in enumerate(self.fg.params)}
-        seen = set()
-        for p in params:
-            i = index.get(id(p))
-            if i is not None and i not in seen:
-                seen.add(i)
-                self._pending[self.param_bucket[i]] -= 1
-        self._launch_ready()
+        for i in sorted({self._index[id(p)] for p in params if id(p) in self._index}):
+            self._event(i)
 
     def _launch_ready(self):
         if not self.enabled:
@@ -158,32 +169,28 @@ class GradAllReduce:
                                                       group=self.group, async_op=True)
             self._next += 1
 
-    def set_live(self, live):
-        """Only params with live[i] fire their accumulate hook (the others get no gradient, as under the
-        reference's autograd); a bucket is complete when its live params are."""
-        self.bucket_size = [0] * len(self.buckets)
-        for j, b in self.param_bucket.items():
-            if live[j]:
-                self.bucket_size[b] += 1
-        self._pending = list(self.bucket_size)
-
     def finish(self):
-        """Launch any bucket whose params got no gradient, then wait for all of them."""
+        """Launch the buckets not launched yet (all of them in the learning step), then wait for all."""
+        if self.expected is None and any(self._seen):
+            self.expected = list(self._seen)
+            self.bucket_size = [0] * len(self.buckets)
+            for j, b in self.param_bucket.items():
+                if self.expected[j] > 0:
+                    self.bucket_size[b] += 1
         for b in range(self._next, len(self.buckets)):
             self._pending[b] = 0
         self._launch_ready()
         for w in self._works:
             if w is not None:
                 w.wait()
-        self._pending = list(self.bucket_size)
-        self._works = [None] * len(self.buckets)
-        self._next = 0
+        self.reset()
 
     def reset(self):
-        """Forget partially counted buckets (after a capture, whose hooks counted but launched nothing)."""
+        """Forget a partially counted step (after a probe or a capture, whose hooks counted nothing)."""
         self._pending = list(self.bucket_size)
         self._works = [None] * len(self.buckets)
         self._next = 0
+        self._seen = [0] * len(self._seen)
 
     def all_reduce_flat(self):
         """SUM all-reduce of the whole flat buffer as one message, ordered on the current stream

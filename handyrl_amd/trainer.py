@@ -120,8 +120,6 @@ class LearnerStep:
             kw = dict(self._opt_kwargs)
             kw['lr'] = self.optimizer.param_groups[0]['lr']   # keep a set_lr() made before the first step
             self.optimizer = torch.optim.Adam([p for p, l in zip(self.params, live) if l], **kw)
-            if self.reducer is not None:
-                self.reducer.set_live(live)
 
     def _grads(self, batch, hidden):
         """zero -> forward_prediction -> losses -> backward; returns (losses, dcnt)."""

@@ -152,6 +152,87 @@ def test_bucket_layout_covers_flat_buffer():
     assert fg.flat.numel() == sum(p.numel() for p in net.parameters())
 
 
+class _Deferred(torch.autograd.Function):
+    """y = x @ w.T whose weight gradient is held back (returned as None, so w's accumulate hook fires with
+    nothing added) and written later by a flush -- nn.DeferredGrads' pattern for a recurrent unroll."""
+
+    @staticmethod
+    def forward(ctx, x, w, store):
+        ctx.save_for_backward(x, w)
+        ctx.store = store
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        ctx.store.append(g.t() @ x)
+        return g @ w, None, None
+
+
+def _deferred_rank_main(rank, world, port, out_path, steps, slow):
+    """Each rank: two unrolled uses of a deferred weight and a plain head; after the backward the flush
+    adds the held-back weight gradients and marks them ready.  ``slow`` delays the flush, so a bucket
+    launched at the weight's hook (before its gradient is complete) would all-reduce a partial sum."""
+    import time
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from handyrl_amd.distributed import FlatGrads, GradAllReduce
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.manual_seed(0)
+    w = nn.Parameter(torch.randn(6, 6))
+    head = nn.Linear(6, 1)
+    fg = FlatGrads([w, head.weight, head.bias])
+    red = GradAllReduce(fg, bucket_bytes=64)         # a bucket per parameter
+    g = torch.Generator().manual_seed(10 + rank)
+    out = []
+    for _ in range(steps):
+        fg.zero()
+        x = torch.randn(5, 6, generator=g)
+        store = []
+        h = torch.tanh(_Deferred.apply(torch.tanh(_Deferred.apply(x, w, store)), w, store))
+        head(h).square().sum().backward()
+        if slow:
+            time.sleep(0.2)
+        w.grad.add_(sum(store))
+        red.mark_ready([w, w])
+        red.finish()
+        out.append(fg.flat.clone())
+    gathered = [torch.zeros_like(torch.stack(out)) for _ in range(world)]
+    dist.all_gather(gathered, torch.stack(out))
+    if rank == 0:
+        torch.save({'flat': gathered, 'expected': red.expected}, out_path)
+    dist.destroy_process_group()
+
+
+def test_deferred_gradient_bucket_waits_for_the_flush():
+    """A parameter whose gradient arrives in two events (its accumulate hook, then mark_ready after a flush)
+    counts for its bucket only at the second from the second step on: both ranks end every step with the
+    same summed gradient, equal to the sum of the ranks' own full gradients."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, 'r0.pt')
+        mp.spawn(_deferred_rank_main, args=(2, _free_port(), out, 3, True), nprocs=2, join=True)
+        res = torch.load(out, weights_only=True)
+    assert res['expected'] == [2, 1, 1]
+    a, b = res['flat']
+    assert torch.equal(a, b)
+    # each rank's own (un-reduced) gradient, recomputed in-process
+    torch.manual_seed(0)
+    w = nn.Parameter(torch.randn(6, 6))
+    head = nn.Linear(6, 1)
+    tot = None
+    for r in range(2):
+        g = torch.Generator().manual_seed(10 + r)
+        rows = []
+        for _ in range(3):
+            w.grad = None
+            head.zero_grad(set_to_none=True)
+            x = torch.randn(5, 6, generator=g)
+            h = torch.tanh(torch.tanh(x @ w.t()) @ w.t())
+            head(h).square().sum().backward()
+            rows.append(torch.cat([w.grad.reshape(-1), head.weight.grad.reshape(-1), head.bias.grad]))
+        tot = torch.stack(rows) if tot is None else tot + torch.stack(rows)
+    torch.testing.assert_close(a, tot, rtol=1e-5, atol=1e-6)
+
+
 def _gpu_rank_main(rank, world, port, out_path, steps, graph=False):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK='0')
@@ -330,3 +411,128 @@ def test_segmented_graph_step_matches_one_segment_step(cuda):
     assert not diff, diff
     for k in ('p', 'v', 'ent', 'total', 'dcnt'):
         assert r['sums'][k] == ref['sums'][k], k
+
+
+def _net_case(name, dev):
+    """(net class, batch, args, hidden maker) of a BatchNorm net the learner trains: the TicTacToe net,
+    GeeseNet (configs[3], torus tower) or GeisterNet (recurrent: DeferredGrads -> mark_ready)."""
+    from handyrl_amd.synthetic import tictactoe_batch, default_args, geese_batch, geese_args, geister_batch
+    if name == 'TicTacToe':
+        from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+        return SimpleConv2dModel, tictactoe_batch(64, 9, dev, seed=4), default_args(9, 64), None
+    if name == 'Geese':
+        from handyrl_amd.envs.hungry_geese import GeeseNet
+        return GeeseNet, geese_batch(16, 8, dev, seed=4), geese_args(8, 16), None
+    from handyrl_amd.envs.geister import GeisterNet
+    return GeisterNet, geister_batch(16, 6, dev, seed=4), default_args(6, 16), True
+
+
+def _hidden(net, B, P, dev):
+    return tuple([h.to(dev) for h in hs] for hs in net.init_hidden([B, P]))
+
+
+def _dp_rank_main(rank, world, port, out_path, name, graph):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK='0')
+    from handyrl_amd.trainer import LearnerStep
+    import handyrl_amd.distributed as hd
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    cls, batch, args, rec = _net_case(name, dev)
+    B = batch['value'].size(0)
+    shard = {k: (v[rank * B // world:(rank + 1) * B // world].contiguous() if isinstance(v, torch.Tensor) else
+                 {kk: vv[rank * B // world:(rank + 1) * B // world].contiguous() for kk, vv in v.items()})
+             for k, v in batch.items()}
+    args = dict(args, batch_size=B // world)
+    torch.manual_seed(0)
+    net = cls()
+    step = LearnerStep(net, args, dev, world_size=world, bucket_bytes=16 * 1024, graph=graph)
+    launched = []
+    real_finish = hd.GradAllReduce.finish
+
+    def finish(self):
+        launched.append(self._next)           # buckets launched during the backward, before finish()
+        return real_finish(self)
+    hd.GradAllReduce.finish = finish
+    hidden = _hidden(net, B // world, batch['value'].size(2), dev) if rec else None
+    for _ in range(2):
+        step.step(shard, hidden)
+    torch.cuda.synchronize()
+    sums, _ = step.pop_stats()
+    flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).cpu()
+    bufs = torch.cat([b.detach().double().reshape(-1) for b in net.buffers()]).cpu()
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    gb = [torch.zeros_like(bufs) for _ in range(world)]
+    dist.all_gather(gb, bufs)
+    if rank == 0:
+        torch.save({'params': gathered, 'buffers': gb, 'sums': sums, 'launched': launched,
+                    'nbuckets': len(step.reducer.buckets),
+                    'expected': step.reducer.expected}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _simulated_dp(name, dev, steps=2, world=2):
+    """The data-parallel update without any collective: one replica per shard (its own BatchNorm statistics,
+    as under the reference's nn.DataParallel), each computing its shard's gradients with LearnerStep's own
+    backward; the SUM of the replicas' gradients is clipped and applied by Adam with the global batch's lr
+    (3e-8 * world * B_shard * T, train.py:318) on every replica."""
+    from handyrl_amd.trainer import LearnerStep
+    cls, batch, args, rec = _net_case(name, dev)
+    B = batch['value'].size(0)
+    args = dict(args, batch_size=B // world)
+    lr = 3e-8 * B * args['forward_steps']
+    shards = [{k: (v[r * B // world:(r + 1) * B // world].contiguous() if isinstance(v, torch.Tensor) else
+                   {kk: vv[r * B // world:(r + 1) * B // world].contiguous() for kk, vv in v.items()})
+               for k, v in batch.items()} for r in range(world)]
+    reps = []
+    for r in range(world):
+        torch.manual_seed(0)
+        net = cls()
+        reps.append((net, LearnerStep(net, args, dev, lr=lr)))
+    for _ in range(steps):
+        grads = []
+        for (net, st), sh in zip(reps, shards):
+            hidden = _hidden(net, B // world, batch['value'].size(2), dev) if rec else None
+            st._grads(sh, hidden)
+            grads.append(st.grads.flat.clone())
+        total = sum(grads[1:], grads[0].clone())
+        for net, st in reps:
+            st.grads.flat.copy_(total)
+            st.grads.clip_(4.0)
+            st.optimizer.step()
+    torch.cuda.synchronize()
+    params = torch.cat([p.detach().reshape(-1) for p in reps[0][0].parameters()]).cpu()
+    bufs = [torch.cat([b.detach().double().reshape(-1) for b in net.buffers()]).cpu() for net, _ in reps]
+    return params, bufs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['TicTacToe', 'Geese', 'Geister'])
+@pytest.mark.parametrize('graph', [False, True])
+def test_two_rank_bn_nets_match_simulated_replicas(cuda, name, graph):
+    """Two ranks (gloo over device tensors, one GPU) train the TicTacToe net, GeeseNet (torus tower) and
+    GeisterNet (recurrent unroll, batched weight gradients marked ready at their flush) for two steps,
+    eager (hook-launched buckets) and HIP-graph (flat all-reduce between the backward and
+    update graphs): parameters equal on both ranks and equal to the collective-free simulation of the same
+    update (per-replica BatchNorm, summed gradients, clip, Adam at the global lr); each rank's BatchNorm
+    statistics are its replica's.  Eager: from the second step on buckets launch during the backward, each
+    when its parameters' last gradient event (accumulate hook, or mark_ready after DeferredGrads.flush) has
+    come, as the first step counted them."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, 'r0.pt')
+        mp.spawn(_dp_rank_main, args=(2, _free_port(), out, name, graph), nprocs=2, join=True)
+        res = torch.load(out, weights_only=True)
+    ref, ref_bufs = _simulated_dp(name, cuda)
+    p0, p1 = res['params']
+    assert torch.equal(p0, p1)
+    torch.testing.assert_close(p0, ref, rtol=1e-5, atol=2e-6)
+    for r in range(2):
+        torch.testing.assert_close(res['buffers'][r], ref_bufs[r], rtol=1e-5, atol=1e-6)
+    if not graph:
+        assert res['launched'][0] == 0                     # the learning step launches at finish()
+        assert res['launched'][-1] > 0, res['launched']   # second step: buckets launched before finish()
+        if name == 'Geister':   # deferred weights: the accumulate hook, then mark_ready after the flush
+            assert 2 in res['expected'], res['expected']
