@@ -31,6 +31,7 @@ _dbl = ctypes.c_double
 # symbol -> (restype, argtypes); mirrors include/*.h exactly
 SIGNATURES = {
     'hrl_abi_version': (ctypes.c_int, []),
+    'hrl_targets_set_short_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_strerror': (ctypes.c_char_p, [ctypes.c_int]),
     'hrl_compute_target': (ctypes.c_int, [
         ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _f32p,

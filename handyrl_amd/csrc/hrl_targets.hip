@@ -206,7 +206,13 @@ struct Args {
 // TGT: algorithm whose target is written (kNone: no target output).
 // ADV: algorithm whose advantages are written.
 // REW: rewards present.  RETT: MC reads returns at every t (ret_T == T).
-template <int TGT, int ADV, bool REW, bool RETT, bool VEC>
+// LDS row stride for a tile of Cx columns per step read column-wise by lanes (g, c): an odd multiple of Cx, so
+// g*Lp + c are distinct modulo 32 over each 32-lane half when Cx divides 32 (conflict-free ds_read_b32) with no
+// more padding than one step's columns (padded_row pads a T = 9, Cx = 1 row of 9 floats to 33).
+__host__ __device__ __forceinline__ int odd_row(int tmax, int Cx) { return Cx * (tmax | 1); }
+
+// ONE: T <= kTChunk, the whole trajectory is one chunk (no prefetch path: ~70 registers instead of 216).
+template <int TGT, int ADV, bool REW, bool RETT, bool VEC, bool ONE>
 __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
     constexpr bool kRho = (TGT == HRL_ALG_VTRACE) || (ADV == HRL_ALG_VTRACE);
     constexpr bool kRet = RETT && (ADV == HRL_ALG_MC);
@@ -218,19 +224,20 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
     const int J = G * C;                      // value columns per wave
     const int T = a.T;
     const int tmax = T < kTChunk ? T : kTChunk;
-    const int Lpv = padded_row(tmax * C, C);         // value-shaped rows
-    const int Lpr = padded_row(tmax * a.rhoC, 1);    // rho rows (lanes of one g share a slot)
+    const int Lpv = odd_row(tmax, C);                // value-shaped rows
+    const int Lpr = odd_row(tmax, a.rhoC);           // rho rows (lanes of one g share a slot)
 
     const int64_t b0 = (int64_t)blockIdx.x * G;
     const int ntraj = (int)min<int64_t>(G, a.B - b0);
 
-    // LDS carve-up (sizes fixed by tmax, see launch)
+    // LDS carve-up (sizes fixed by tmax, see launch).  The targets overwrite the values in place: recur_chunk
+    // reads a column's inputs before it writes that column's outputs, and no lane touches another's column.
     const int vt = G * Lpv, rt = G * Lpr;
     float *t_v = lds;
     float *t_r = t_v + vt;
     float *t_ret = t_r + (REW ? vt : 0);
-    float *t_tgt = t_ret + (kRet ? vt : 0);
-    float *t_adv = t_tgt + (TGT != kNone ? vt : 0);
+    float *t_tgt = t_v;
+    float *t_adv = t_ret + (kRet ? vt : 0);
     float *t_rho = t_adv + vt;
     float *t_cs = t_rho + (kRho ? rt : 0);
 
@@ -316,10 +323,68 @@ __global__ __launch_bounds__(kWave) void targets_kernel(Args a) {
         store_chunk<VEC>(out, t_adv, a.advantages + off);
         HRL_STAMP(4 + 3 * (nchunks - 1 - ch));
     };
-    for (int ch = nchunks - 1; ch > 0; --ch) process(ch, std::true_type{});
+    if constexpr (!ONE)
+        for (int ch = nchunks - 1; ch > 0; --ch) process(ch, std::true_type{});
     process(0, std::false_type{});
     HRL_STAMP_WALL(15);
 }
+
+// Short trajectories (T <= kTChunk): targets_kernel spends a group's life in serial phases -- load, LDS
+// transpose, barrier, chain, barrier, transpose, store -- and its LDS tiles and 216 registers hold the chip to
+// ~8 waves per CU, so at T = 9 it streams at a third of HBM.  Here a lane owns one (trajectory, column) and
+// nothing else: its T inputs come straight from global memory into registers (4-byte loads; a wave's loads of
+// one step touch the same lines as its other steps', which L1/L2 serve once), the chain runs, and each step's
+// outputs are stored as they are produced.  No LDS, no barrier, ~70 registers: enough waves in flight to hide
+// the HBM latency.  The per-column arithmetic is fused_step's, in recur_chunk's order: bit-identical results.
+template <int TGT, int ADV, bool REW, bool RETT>
+__global__ __launch_bounds__(256) void targets_lane_kernel(Args a) {
+    constexpr bool kRho = (TGT == HRL_ALG_VTRACE) || (ADV == HRL_ALG_VTRACE);
+    constexpr bool kRet = RETT && (ADV == HRL_ALG_MC);
+    const int C = a.C, T = a.T, G = a.G;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / C;
+    const int c = lane - g * C;
+    const int64_t b = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + g;
+    if (g >= G || b >= a.B) return;            // no barrier below
+    const int64_t row = b * (int64_t)T;
+    const float *pv = a.values + row * C + c;
+    const float *pr = REW ? a.rewards + row * C + c : nullptr;
+    const float *pret = kRet ? a.returns + row * C + c : nullptr;
+    const int rc = c / a.rhoDiv;
+    const float *prho = kRho ? a.rhos + row * a.rhoC + rc : nullptr;
+    const float *pcs = kRho ? a.cs + row * a.rhoC + rc : nullptr;
+    float xv[kTChunk], xr[kTChunk], xrho[kTChunk], xc[kTChunk], xret[kTChunk];
+    const float boot = a.returns[b * (int64_t)a.retT * C + (int64_t)(a.retT - 1) * C + c];
+#pragma unroll
+    for (int tt = 0; tt < kTChunk; ++tt) {
+        if (tt < T) {
+            xv[tt] = pv[tt * C];
+            xr[tt] = REW ? pr[tt * C] : 0.f;
+            xret[tt] = kRet ? pret[tt * C] : boot;
+            xrho[tt] = kRho ? prho[tt * a.rhoC] : 0.f;
+            xc[tt] = kRho ? pcs[tt * a.rhoC] : 0.f;
+        }
+    }
+    float *ptg = TGT != kNone ? a.targets + row * C + c : nullptr;
+    float *pad = a.advantages + row * C + c;
+    Carry s{0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tt = kTChunk - 1; tt >= 0; --tt) {
+        if (tt < T) {
+            float tg, ad;
+            fused_step<TGT, ADV, false>(s, tt == T - 1, xv[tt], xr[tt], xrho[tt], xc[tt], xret[tt], boot, a.k, tg,
+                                        ad);
+            if constexpr (TGT != kNone) ptg[tt * C] = tg;
+            pad[tt * C] = ad;
+        }
+    }
+}
+
+// hrl_targets_set_short_form, for T <= kTChunk: 1 (default) targets_lane_kernel for small batches (B*C <= 32768,
+// where it is 10% faster: fewer serial phases per wave) and targets_kernel otherwise (coalesced loads: 48.6% of HBM
+// at B = 2^20, T = 9 cold against the lane kernel's 29.5%, whose 4-byte column loads touch ~18 lines each);
+// 2 the lane kernel always, 0 targets_kernel always
+int g_short_form = 1;
 
 template <int TGT, int ADV, bool REW, bool RETT, bool VEC>
 int launch_one(const Args &a, hipStream_t stream) {
@@ -327,14 +392,28 @@ int launch_one(const Args &a, hipStream_t stream) {
     constexpr bool kRet = RETT && (ADV == HRL_ALG_MC);
     const int G = a.G;
     const int tmax = a.T < kTChunk ? a.T : kTChunk;
-    const int vtiles = 1 + (REW ? 1 : 0) + (kRet ? 1 : 0) + (TGT != kNone ? 1 : 0) + 1;
-    const size_t vt = (size_t)G * padded_row(tmax * a.C, a.C);
-    const size_t rt = (size_t)G * padded_row(tmax * a.rhoC, 1);
+    const int vtiles = 1 + (REW ? 1 : 0) + (kRet ? 1 : 0) + 1;    // values (then targets), rewards, returns, adv
+    const size_t vt = (size_t)G * odd_row(tmax, a.C);
+    const size_t rt = (size_t)G * odd_row(tmax, a.rhoC);
     const size_t lds = sizeof(float) * (vtiles * vt + (kRho ? 2 : 0) * rt);
     const int64_t blocks = (a.B + G - 1) / G;
     if (blocks > 0x7fffffff) return HRL_EINVAL;
-    hipLaunchKernelGGL((targets_kernel<TGT, ADV, REW, RETT, VEC>), dim3((unsigned)blocks), dim3(kWave), lds,
-                       stream, a);
+    if (a.T <= kTChunk && (g_short_form == 2 || (g_short_form == 1 && a.B * a.C <= 32768))) {
+        Args b = a;
+        b.G = kWave / a.C;
+        const int64_t waves = (a.B + b.G - 1) / b.G;
+        const int64_t wgs = (waves + 3) / 4;
+        if (wgs > 0x7fffffff) return HRL_EINVAL;
+        hipLaunchKernelGGL((targets_lane_kernel<TGT, ADV, REW, RETT>), dim3((unsigned)wgs), dim3(4 * kWave), 0,
+                           stream, b);
+    } else {
+        if (a.T <= kTChunk)
+            hipLaunchKernelGGL((targets_kernel<TGT, ADV, REW, RETT, VEC, true>), dim3((unsigned)blocks), dim3(kWave),
+                               lds, stream, a);
+        else
+            hipLaunchKernelGGL((targets_kernel<TGT, ADV, REW, RETT, VEC, false>), dim3((unsigned)blocks), dim3(kWave),
+                               lds, stream, a);
+    }
     const hipError_t err = hipGetLastError();
     return err == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)err;
 }
@@ -432,6 +511,12 @@ int hrl_debug_set_stamps_targets(void *buf) {
 #endif
 
 int hrl_abi_version(void) { return 17; }
+
+int hrl_targets_set_short_form(int form) {
+    const int prev = g_short_form;
+    g_short_form = form < 0 ? 0 : (form > 2 ? 2 : form);
+    return prev;
+}
 
 const char *hrl_strerror(int code) {
     if (code == HRL_OK) return "success";

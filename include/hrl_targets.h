@@ -57,6 +57,12 @@ int hrl_abi_version(void);
 /* Human-readable text for a return code (static storage). */
 const char *hrl_strerror(int code);
 
+/* Kernel form of the scans for T <= 16: 2 one lane per (trajectory, column) straight from global memory (no
+ * LDS), 0 the chunked LDS-transpose kernel every T uses, 1 (the default) the first for small batches
+ * (B*C <= 32768) and the second otherwise.  Results are bit-identical.  Process-wide; returns the previous
+ * setting. */
+int hrl_targets_set_short_form(int form);
+
 /*
  * One algorithm, one head: the drop-in for a single compute_target call
  * (losses.py:61).  targets may be NULL; for MC it must be NULL.

@@ -82,11 +82,30 @@ def _check_fused(dev, B, T, P, K, Pr, head, seed, tgt_alg, adv_alg, exact=True):
         np.testing.assert_array_equal(adv, ra)
 
 
+class _short_form:
+    """hrl_targets_set_short_form(form) for the block (T <= 16: 2 = lane-per-column kernel, 0 = chunked, 1 = the
+    default choice by batch size)."""
+
+    def __init__(self, form):
+        self.form = form
+
+    def __enter__(self):
+        from handyrl_amd import _native
+        self.prev = _native.load().hrl_targets_set_short_form(self.form)
+
+    def __exit__(self, *exc):
+        from handyrl_amd import _native
+        _native.load().hrl_targets_set_short_form(self.prev)
+        return False
+
+
+@pytest.mark.parametrize('form', [2, 0])
 @pytest.mark.parametrize('tgt_alg', ALGS)
 @pytest.mark.parametrize('adv_alg', ALGS)
 @pytest.mark.parametrize('head', ['value', 'return'])
-def test_fused_pairs(cuda, tgt_alg, adv_alg, head):
-    _check_fused(cuda, 37, 9, 2, 1, 1, head, 11, tgt_alg, adv_alg)
+def test_fused_pairs(cuda, tgt_alg, adv_alg, head, form):
+    with _short_form(form):
+        _check_fused(cuda, 37, 9, 2, 1, 1, head, 11, tgt_alg, adv_alg)
 
 
 @pytest.mark.parametrize('B,T,P,K,Pr', [
@@ -102,8 +121,32 @@ def test_fused_pairs(cuda, tgt_alg, adv_alg, head):
 ])
 @pytest.mark.parametrize('head', ['value', 'return'])
 def test_edge_shapes(cuda, B, T, P, K, Pr, head):
-    for tgt_alg, adv_alg in (('VTRACE', 'UPGO'), ('TD', 'VTRACE'), ('UPGO', 'MC'), ('MC', 'TD')):
-        _check_fused(cuda, B, T, P, K, Pr, head, B * 1000 + T, tgt_alg, adv_alg)
+    for form in ((2, 0) if T <= 16 else (1,)):
+        with _short_form(form):
+            for tgt_alg, adv_alg in (('VTRACE', 'UPGO'), ('TD', 'VTRACE'), ('UPGO', 'MC'), ('MC', 'TD')):
+                _check_fused(cuda, B, T, P, K, Pr, head, B * 1000 + T, tgt_alg, adv_alg)
+
+
+@pytest.mark.parametrize('T', [9, 16])
+def test_short_forms_identical_at_two_to_the_twenty(cuda, T):
+    """configs[1]'s T=9 (and the longest short T) at B = 2^20: the lane-per-column kernel and the chunked
+    kernel give bit-identical targets and advantages for the value head (V-trace + UPGO) and the return head
+    (TD + V-trace with rewards), both checked against the oracle at B = 4096 in test_baseline_sizes."""
+    from handyrl_amd.losses import compute_targets_fused
+    B = 1 << 20
+    g = torch.Generator(device=cuda).manual_seed(T)
+    v = torch.tanh(torch.randn(B, T, 2, 1, device=cuda, generator=g))
+    ret = torch.randint(-1, 2, (B, 1, 2, 1), device=cuda, generator=g).float()
+    rew = 0.01 * torch.randn(B, T, 2, 1, device=cuda, generator=g)
+    rho = torch.rand(B, T, 1, 1, device=cuda, generator=g)
+    cs = torch.rand(B, T, 1, 1, device=cuda, generator=g)
+    for args in (('VTRACE', 'UPGO', v, ret, None, 0.7, 1, rho, cs), ('TD', 'VTRACE', v, ret, rew, 0.7, 0.8, rho, cs)):
+        out = {}
+        for form in (2, 0):
+            with _short_form(form):
+                out[form] = compute_targets_fused(*args)
+        for a, b in zip(out[2], out[0]):
+            assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))
 
 
 def test_empty_batch(cuda):
