@@ -133,7 +133,19 @@ class DRC(nn.Module):
         b_x = None
         if self.blocks[0].conv.bias is not None:
             b_x = torch.cat([blk.conv.bias for blk in self.blocks], out=out.get('b_x'))
-        return {'w_x': w_x, 'w_h': w_h, 'b_x': b_x}
+        res = {'w_x': w_x, 'w_h': w_h, 'b_x': b_x}
+        if self._gboard_ok(w_x, w_h):   # the same weights as hrl_gboard's split fragments, packed once
+            from .. import nn as hnn
+            res['pk_x'] = hnn.gboard_pack(w_x, out=out.get('pk_x'))
+            res['pk_h'] = hnn.gboard_pack(w_h, out=out.get('pk_h'))
+        return res
+
+    def _gboard_ok(self, w_x, w_h):
+        n = len(self.blocks)
+        conv = self.blocks[0].conv
+        return (w_x.is_cuda and tuple(conv.kernel_size) == (3, 3) and tuple(conv.padding) == (1, 1)
+                and tuple(conv.stride) == (1, 1) and tuple(conv.dilation) == (1, 1) and conv.groups == 1
+                and w_x.shape[1] <= 64 and w_h.shape[1] <= 64 and (w_h.shape[0] // n) % 16 == 0)
 
     @contextlib.contextmanager
     def inference_session(self, inplace_state=False):
@@ -162,6 +174,7 @@ class DRC(nn.Module):
         The grouped convolution computes each group's products as the per-layer one does
         (tests/test_geister.py::test_stacked_inference_matches_cells).  The state comes back as channel
         slices of the stacked tensors."""
+        from .. import nn as hnn
         from ..nn import lstm_gates
         n = len(self.blocks)
         ws = [blk.conv.weight for blk in self.blocks]
@@ -172,16 +185,24 @@ class DRC(nn.Module):
         cache = self._session
         if cache is None:
             cache = self._stacked_weights()
-        z = F.conv2d(x, cache['w_x'], None, padding=pad)                                 # (E, n*4H, *HW)
         w_h = cache['w_h']                                                               # (n*4H, H, 3, 3)
         h, c = _stacked(hs), _stacked(cs)                                                # (E, n*H, *HW)
+        # the 6x6 board's convolutions on hrl_gboard (games as MFMA rows, fp32-accurate split)
+        gb = 'pk_x' in cache and hnn.gboard_ok(x) and hnn.gboard_ok(h)
+        if gb:
+            z = hnn.gboard_conv(x, cache['pk_x'], n * 4 * hd, cin)                       # (E, n*4H, *HW)
+        else:
+            z = F.conv2d(x, cache['w_x'], None, padding=pad)
         # in an in-place session (DeviceGenerator's own stacked state) the gates write the new state over
         # the old one: h is consumed by the convolution before, c read and written at the same index
         inplace = (self._inplace and h.is_contiguous() and c.is_contiguous()
                    and h.data_ptr() == hs[0].data_ptr() and c.data_ptr() == cs[0].data_ptr())
         zx = z.view(E * n, 4 * hd, *HW)
         for _ in range(num_repeats):
-            zh = F.conv2d(h, w_h, None, padding=pad, groups=n)
+            if gb and hnn.gboard_ok(h):
+                zh = hnn.gboard_conv(h, cache['pk_h'], n * 4 * hd, hd, groups=n)
+            else:
+                zh = F.conv2d(h, w_h, None, padding=pad, groups=n)
             out = (h.view(E * n, hd, *HW), c.view(E * n, hd, *HW)) if inplace else None
             # the x half's bias rides in the gate kernel: (zx + b) + zh, the biased convolution's order
             hn, cn = lstm_gates(zx, zh.view(E * n, 4 * hd, *HW), c.view(E * n, hd, *HW), cache['b_x'], n, out=out)
@@ -308,6 +329,7 @@ class GeisterNet(nn.Module):
 
     _bn_coef = None   # BatchNorm (alpha, beta) of an inference session, per module
     _vr_session = None   # the value / return heads stacked for an inference session
+    _gb_session = None   # hrl_gboard's packed stem / move-head weights of an inference session
 
     @contextlib.contextmanager
     def inference_session(self, inplace_state=False):
@@ -316,6 +338,7 @@ class GeisterNet(nn.Module):
         (hrl_bn_forward_eval's own coefficient kernel) are refreshed in place once, so a ply is only the
         apply passes.  Outside a session every forward derives them itself."""
         from .. import _native
+        from .. import nn as hnn
         bufs = getattr(self, '_bn_coef_buf', None) or {}
         with torch.no_grad():
             for name, bn in (('bn1', self.bn1), ('p', self.head_p_move.bn), ('v', self.head_v.bn),
@@ -334,6 +357,18 @@ class GeisterNet(nn.Module):
         self._bn_coef_buf = bufs
         self._bn_coef = {id(m): bufs[k][0] for k, m in (('bn1', self.bn1), ('p', self.head_p_move.bn),
                                                          ('v', self.head_v.bn), ('r', self.head_r.bn))}
+        gb = getattr(self, '_gb_buf', None) or {}
+        self._gb_session = None
+        c1, hc = self.conv1, self.head_p_move.conv1
+        if (bufs['bn1'][0].is_cuda and BOARD == (6, 6)
+                and all(tuple(c.kernel_size) == (3, 3) and tuple(c.padding) == (1, 1) and tuple(c.stride) == (1, 1)
+                        and c.groups == 1 and c.bias is None for c in (c1, hc))
+                and c1.weight.shape[1] <= 32 and hc.weight.shape[1] == 2 * c1.weight.shape[0] == 64):
+            with torch.no_grad():   # hrl_gboard's split fragments of the stem and move-head convolutions
+                gb['conv1'] = hnn.gboard_pack(c1.weight, out=gb.get('conv1'))
+                gb['head'] = hnn.gboard_pack(hc.weight, out=gb.get('head'))
+            self._gb_buf = gb
+            self._gb_session = gb
         hv, hr = self.head_v, self.head_r
         if (bufs['v'][0].is_cuda and hv.conv.weight.shape[0] == 1 and hr.conv.weight.shape[0] == 1
                 and hv.bn.num_features == 1 and hr.bn.num_features == 1):
@@ -350,6 +385,7 @@ class GeisterNet(nn.Module):
         finally:
             self._bn_coef = None
             self._vr_session = None
+            self._gb_session = None
 
     def _forward_inference(self, x, hidden):
         """forward in eval mode without autograd on the HIP path (self-play): the same operations, with each
@@ -371,13 +407,28 @@ class GeisterNet(nn.Module):
                 _native.ptr(y), y.shape[0], C, y[0, 0].numel(), _native.ptr(coef), _native.ptr(coef[C:]), 1,
                 _native.ptr(out), _native.stream_of(y.device)), 'hrl_bn_apply')
             return out
+        from .. import nn as hnn
         board, scalar = x['board'], x['scalar']
         planes = scalar[..., None, None].expand(*scalar.shape, *BOARD)
-        h_e = bn_relu(self.bn1, self.conv1(torch.cat([planes, board], dim=-3)))
+        x_in = torch.cat([planes, board], dim=-3)
+        gb = self._gb_session
+        if gb is not None and hnn.gboard_ok(x_in):   # the conv with the BatchNorm + ReLU in its epilogue
+            C = self.bn1.num_features
+            c1 = coefs[id(self.bn1)]
+            h_e = hnn.gboard_conv(x_in, gb['conv1'], C, x_in.shape[1], alpha=c1[:C], beta=c1[C:], relu=True)
+        else:
+            h_e = bn_relu(self.bn1, self.conv1(x_in))
         h_last, hidden = self.body(h_e, hidden, self.num_repeats)
         h = torch.cat([h_e, h_last], dim=-3)
         hp, hv, hr = self.head_p_move, self.head_v, self.head_r
-        p_move = hp.conv2(bn_relu(hp.bn, hp.conv1(h))).reshape(-1, hp.outputs)
+        if gb is not None and hnn.gboard_ok(h_e, x2=h_last):   # [h_e, h_last] read in place
+            C = hp.bn.num_features
+            cp = coefs[id(hp.bn)]
+            a = hnn.gboard_conv(h_e, gb['head'], C, 2 * h_e.shape[1], x2=h_last, alpha=cp[:C], beta=cp[C:],
+                                relu=True)
+        else:
+            a = bn_relu(hp.bn, hp.conv1(h))
+        p_move = hp.conv2(a).reshape(-1, hp.outputs)
         policy = torch.cat([p_move, self.head_p_set(scalar[:, :1])], dim=-1)
         vr = self._vr_session
         if vr is not None and hv.hidden_units == hr.hidden_units:

@@ -193,6 +193,44 @@ def board_conv_forward(x, w, b, ci0=0, packed=None):
     return y
 
 
+def gboard_ok(x, groups=1, x2=None):
+    """Inputs hrl_gboard_forward covers: fp32 CUDA games on the 6x6 board, float4-aligned storage."""
+    ts = [x] if x2 is None else [x, x2]
+    return all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 4 and tuple(t.shape[2:]) == (6, 6)
+               and t.stride(1) == 36 and t.stride(2) == 6 and t.stride(3) == 1 and t.stride(0) % 4 == 0
+               and t.data_ptr() % 16 == 0 for t in ts) and x.shape[0] > 0
+
+
+def gboard_pack(w, cin_g=None, ci0=0, out=None):
+    """Input channels [ci0, ci0 + cin_g) of the 3x3 weight w (Cout, Cin_total, 3, 3) as hrl_gboard's split
+    fragments (written into ``out`` when given: a graph captured over the packed buffer sees the refresh)."""
+    lib = _native.load()
+    Cout, cin_total = w.shape[0], w.shape[1]
+    cin_g = cin_total - ci0 if cin_g is None else cin_g
+    nbytes = lib.hrl_gboard_pack_bytes(Cout, cin_g)
+    if nbytes < 0:
+        raise ValueError('hrl_gboard_pack: unsupported weight %s' % (tuple(w.shape),))
+    wpk = torch.empty(nbytes, dtype=torch.uint8, device=w.device) if out is None else out
+    _native.check(lib.hrl_gboard_pack(_native.ptr(w.contiguous()), Cout, cin_g, cin_total, ci0, _native.ptr(wpk),
+                                      wpk.numel(), _native.stream_of(w.device)), 'hrl_gboard_pack')
+    return wpk
+
+
+def gboard_conv(x, packed, Cout, cin_g, groups=1, x2=None, bias=None, alpha=None, beta=None, relu=False, out=None):
+    """F.conv2d(x, W, bias, padding=1, groups=groups) on the 6x6 board (csrc/hrl_gboard.hip, forward only, no
+    autograd), W packed by gboard_pack; optional BatchNorm-apply (y*alpha + beta) and ReLU epilogue.  x may be
+    a channel slice of a wider tensor; x2: channels 32.. of a two-source input (x then holds channels 0..31)."""
+    N = x.shape[0]
+    y = torch.empty(N, Cout, 6, 6, device=x.device, dtype=torch.float32) if out is None else out
+    P = _native.ptr
+    _native.check(_native.load().hrl_gboard_forward(
+        P(x), x.stride(0), None if x2 is None else P(x2), 0 if x2 is None else x2.stride(0), N, cin_g, groups,
+        P(packed), Cout, None if bias is None else P(bias), None if alpha is None else P(alpha),
+        None if beta is None else P(beta), int(relu), P(y), y.stride(0), _native.stream_of(x.device)),
+        'hrl_gboard_forward')
+    return y
+
+
 class _DeferredConv(torch.autograd.Function):
     """conv2d (stride 1, 'same') whose weight/bias gradient is deferred to DeferredGrads.flush().
 

@@ -305,6 +305,24 @@ int hrl_board_conv_pack(const float *weight, int64_t w_cin_total, int64_t w_ci0,
 int hrl_board_conv_forward_packed(const float *x, int64_t N, int64_t Cin, int64_t H, int64_t W, const void *packed,
                                   int64_t Cout, const float *bias, float *y, void *stream);
 
+/* GeisterNet's 3x3 'same' convolutions at self-play sizes (geister.py:17-63 ConvLSTMCell, :99-167 GeisterNet)
+ * on the 6x6 board with games as the MFMA rows (csrc/hrl_gboard.hip): the stem, the cells' x halves, their
+ * grouped h halves and the move head's first conv replace the vendor convolutions of the inference forward.
+ * hrl_gboard_pack: input channels [w_ci0, w_ci0 + Cin_g) of weight (Cout, w_cin_total, 3, 3) -> split fragments
+ *   (packed: hrl_gboard_pack_bytes(Cout, Cin_g) bytes; pack once, convolve many times).
+ * hrl_gboard_forward: y[n, co] = conv(x[n, group(co) * Cin_g ..], W[co]) for N games, groups | Cout
+ *   (groups > 1: Cout / groups a multiple of 16), Cin_g <= 64.  Game n of x starts at x + n * x_stride floats
+ *   (channel c at + c * 36); x2 (or NULL; groups 1, Cin_g > 32 only): channels 32.. read from x2 instead
+ *   (the head's [h_e, h_last] without the concatenation).  y: game n at y + n * y_stride.  Epilogue, in order:
+ *   + bias[co] (or NULL), * alpha[co] + beta[co] (a BatchNorm's inference coefficients, or both NULL),
+ *   relu.  x, x2, y 16-byte aligned, strides multiples of 4. */
+int64_t hrl_gboard_pack_bytes(int64_t Cout, int64_t Cin_g);
+int hrl_gboard_pack(const float *weight, int64_t Cout, int64_t Cin_g, int64_t w_cin_total, int64_t w_ci0,
+                    void *packed, int64_t packed_bytes, void *stream);
+int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_t x2_stride, int64_t N, int64_t Cin_g,
+                       int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
+                       const float *beta, int relu, float *y, int64_t y_stride, void *stream);
+
 /* GeeseNet's head pooling (hungry_geese.py:52-53) on h (N, 32, H, W) and the net input x (its plane 0,
  * samples x_stride floats apart): head[n, c] = sum_q h[n, c, q] * x[n, 0, q], avg[n, c] = mean_q h[n, c, q]
  * (both (N, 32)); hrl_torus_head_unpool: the gradient w.r.t. h, g = dhead * x0 + davg / (H*W). */

@@ -51,16 +51,15 @@ def main():
             P(c[8]), P(c[9]), P(c[10]), P(part), P(ws), ws_bytes, stream), 'block')
     torch.cuda.synchronize(dev)
     st = buf.view(nblk, 8, 2, 8).cpu().numpy().astype(np.int64)
-    labels = ['P1 first part', 'P1 second part', 'barrier 1', 'epilogue', 'barrier 2', 'store']
-    print('points: 0 start, 1 after first part, 2 after second part, 3 after barrier 1, 4 after epilogue, '
-          '5 after barrier 2, 6 after store; first part = compute for waves 0-3, stage+issue for waves 4-7')
+    labels = ['first part', 'second part', 'barrier']
+    print('points: 0 loop head, 1 after the first part, 2 after the second part, 3 after the barrier; the first '
+          'part is compute + gin store for compute-first waves (kCFirst: 0, 1, 6, 7), stage + issue for the others')
     for wv in range(8):
-        d = st[:, wv, :, 1:7] - st[:, wv, :, 0:6]
+        d = st[:, wv, :, 1:4] - st[:, wv, :, 0:3]
         it_total = np.median(st[:, wv, 1, 0] - st[:, wv, 0, 0])
-        med = np.median(d.reshape(-1, 6), axis=0)
+        med = np.median(d.reshape(-1, 3), axis=0)
         print('wave %d: ' % wv + '  '.join('%s %6.0f' % (l, m) for l, m in zip(labels, med))
               + '  | iteration %6.0f cyc' % it_total)
-
 
 if __name__ == '__main__':
     main()
