@@ -37,7 +37,7 @@ constexpr int kQuads = kHW / 4;   // float4 groups of cells per channel row
 constexpr int kTaps = 9;
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
-constexpr int kSlots = 1024;      // waves the chip holds at one wave per SIMD
+constexpr int kCUs = 256;         // one 4-wave workgroup per CU (one wave per SIMD)
 
 struct GbArgs {
     const float *x, *x2;   // x2 (optional): input channels 32.. (the move head's [h_e, h_last] without a copy)
@@ -45,7 +45,6 @@ struct GbArgs {
     int cin_g, cout_g;     // input / output channels per group
     const uint4 *wpk;      // split weight fragments [ct][kc][tap][part][64]
     int nct, cout;         // 16-channel column tiles; output channels stored
-    int tpw;               // waves per column tile (the game tiles are dealt round robin among them)
     const float *bias, *alpha, *beta;
     int relu;
     float *y;
@@ -70,103 +69,149 @@ __device__ __forceinline__ void static_for(F &&f) {
 
 __device__ __forceinline__ float relu_f(float v) { return v < 0.f ? 0.f : v; }   // NaN stays NaN
 
-template <int KC, bool PADC>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void gboard_conv_kernel(GbArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int nwg = gridDim.x, b = blockIdx.x;
-    // consecutive logical workgroups (which share game tiles) on one XCD (hardware deals b round robin)
-    const int L = (nwg % 8 == 0) ? (b & 7) * (nwg >> 3) + (b >> 3) : b;
-    const int w = L * kWaves + wave;
-    if (w >= a.nct * a.tpw) return;
-    const int ct = w % a.nct;
-    const int64_t ntiles = (a.N + 15) >> 4;
-    const int r = lane & 15, g = lane >> 4;
-    const int grp = (ct * 16) / a.cout_g;
-    const float *xb = a.x + (int64_t)(grp * a.cin_g + 8 * g) * kHW;
+__device__ __forceinline__ void bar_lds() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 
-    // A rows: game n0 + r (clamped: rows past the batch compute values that are never stored)
-    auto src = [&](int64_t tile, int kc) -> const float * {
-        const int64_t n = min(tile * 16 + r, a.N - 1);
-        if (KC > 1 && kc >= 1 && a.x2) return a.x2 + n * a.xs2 + (int64_t)((kc - 1) * 32 + 8 * g) * kHW;
-        return xb + n * a.xs + (int64_t)(32 * kc) * kHW;
+// output-cell bands: NB waves share a column tile, wave band b owns the cells of quads [band_q0, band_q1)
+__host__ __device__ constexpr int band_q0(int NB, int b) { return NB == 1 ? 0 : (NB == 2 ? 5 * b : 2 * b); }
+__host__ __device__ constexpr int band_q1(int NB, int b) {
+    return NB == 1 ? kQuads : (NB == 2 ? (b == 0 ? 5 : kQuads) : (b == 3 ? kQuads : 2 * b + 2));
+}
+// does output band b of NB use input cell p?
+__host__ __device__ constexpr bool band_uses(int NB, int b, int p) {
+    for (int q = 4 * band_q0(NB, b); q < 4 * band_q1(NB, b); ++q)
+        if (tap_pq(p, q) >= 0) return true;
+    return false;
+}
+
+constexpr int kPartBytes = 4 * 16 * 32 * 2;   // one split part of one quad's image: [cell][game][channel] bf16
+constexpr int kSlotBytes = 3 * kPartBytes;     // 12 KB per quad
+constexpr int kLdsBytes = 3 * kSlotBytes;      // ring of three quads
+
+// One wave of gboard_conv_kernel: column tile (task's tile group * NCTW + ctl), output band BAND of NB = 4 / NCTW.
+template <int KC, bool PADC, int NCTW, int BAND>
+__device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem, int lane, int wave, int L) {
+    constexpr int NB = 4 / NCTW;
+    constexpr int Q0 = band_q0(NB, BAND), Q1 = band_q1(NB, BAND);
+    constexpr int NCELL = 4 * (Q1 - Q0);
+    const int ctl = wave % NCTW;
+    const int n_ctg = a.nct / NCTW;
+    const int64_t ntiles = (a.N + 15) >> 4;
+    const int64_t ntasks = ntiles * n_ctg;
+    const int r = lane & 15, g = lane >> 4;
+    // staging role: game 4*wave + (lane >> 4) of the tile, channels 2cp, 2cp + 1 of the k-step
+    const int sg = 4 * wave + (lane >> 4), cp = lane & 15;
+
+    int64_t task = L;
+    if (task >= ntasks) return;   // uniform over the workgroup: no barrier is left waiting
+    auto tile_of = [&](int64_t t) { return t / n_ctg; };
+    auto ct_of = [&](int64_t t) { return (int)(t % n_ctg) * NCTW + ctl; };
+    // the staging lane's source row for (task, kc): channels 32kc + 2cp (+1) of game sg of the task's tile
+    // (PADC: rows at or past cin_g read row cin_g - 1 and are zeroed)
+    auto src = [&](int64_t t, int kc, int &c0, int &c1) -> const float * {
+        const int64_t n = min(tile_of(t) * 16 + sg, a.N - 1);
+        const int grp = (ct_of(t) - ctl) * 16 / a.cout_g;   // the group of the task's first column tile
+        c0 = 32 * kc + 2 * cp;
+        c1 = c0 + 1;
+        if constexpr (PADC) {
+            c0 = min(c0, a.cin_g - 1);
+            c1 = min(c1, a.cin_g - 1);
+        }
+        if (KC > 1 && kc >= 1 && a.x2) return a.x2 + n * a.xs2 + (int64_t)(-32) * kHW;
+        return a.x + n * a.xs + (int64_t)(grp * a.cin_g) * kHW;
     };
-    // PADC: channel rows at or past cin_g (only the last k-step is ragged) read row cin_g - 1 and are zeroed;
-    // emax may be negative (the lane's whole octet is past cin_g: its offsets reach back into valid rows)
-    int emax = 7;
-    if constexpr (PADC) emax = min(7, a.cin_g - 1 - 8 * g - 32 * (KC - 1));
-    // every register array below is indexed by compile-time constants only (static_for): a runtime index,
-    // even one that unrolling later folds, keeps the array in scratch
-    float4 raw[3][8];
-    auto issue = [&](const float *s, int quad, auto slot_c, bool last_kc) __attribute__((always_inline)) {
+    float4 raw[3][2];
+    auto issue = [&](int64_t t, int kc, int quad, auto slot_c) __attribute__((always_inline)) {
         constexpr int slot = decltype(slot_c)::value;
-        static_for<0, 8>([&](auto e_c) __attribute__((always_inline)) {
-            constexpr int e = decltype(e_c)::value;
-            int ee = e;
-            if constexpr (PADC) ee = last_kc ? min(e, emax) : e;
-            raw[slot][e] = *reinterpret_cast<const float4 *>(s + ee * kHW + 4 * quad);
+        int c0, c1;
+        const float *s = src(t, kc, c0, c1);
+        raw[slot][0] = *reinterpret_cast<const float4 *>(s + c0 * kHW + 4 * quad);
+        raw[slot][1] = *reinterpret_cast<const float4 *>(s + c1 * kHW + 4 * quad);
+    };
+    auto stage = [&](int kc, auto slot_c) __attribute__((always_inline)) {   // raw[slot] -> LDS slot
+        constexpr int slot = decltype(slot_c)::value;
+        const int c0 = 32 * kc + 2 * cp;
+        unsigned char *dst = smem + slot * kSlotBytes + sg * 64 + cp * 4;
+        static_for<0, 4>([&](auto u_c) __attribute__((always_inline)) {
+            constexpr int u = decltype(u_c)::value;
+            const float4 &f0 = raw[slot][0], &f1 = raw[slot][1];
+            float v0 = u == 0 ? f0.x : (u == 1 ? f0.y : (u == 2 ? f0.z : f0.w));
+            float v1 = u == 0 ? f1.x : (u == 1 ? f1.y : (u == 2 ? f1.z : f1.w));
+            if constexpr (PADC) {
+                if (c0 >= a.cin_g) v0 = 0.f;
+                if (c0 + 1 >= a.cin_g) v1 = 0.f;
+            }
+            uint32_t h0, m0, l0, h1, m1, l1;
+            hrl_split::split3(v0, h0, m0, l0);
+            hrl_split::split3(v1, h1, m1, l1);
+            *reinterpret_cast<uint32_t *>(dst + (0 * 4 + u) * 1024) = h0 | (h1 << 16);
+            *reinterpret_cast<uint32_t *>(dst + (1 * 4 + u) * 1024) = m0 | (m1 << 16);
+            *reinterpret_cast<uint32_t *>(dst + (2 * 4 + u) * 1024) = l0 | (l1 << 16);
         });
     };
     uint4 Bw[kTaps][3];
-    auto load_b = [&](int kc) __attribute__((always_inline)) {
+    auto load_b = [&](int ct, int kc) __attribute__((always_inline)) {
         const uint4 *wp = a.wpk + (((int64_t)ct * KC + kc) * kTaps * 3) * 64 + lane;
         static_for<0, kTaps * 3>([&](auto i_c) __attribute__((always_inline)) {
             constexpr int i = decltype(i_c)::value;
             Bw[i / 3][i % 3] = wp[i * 64];
         });
     };
-    f32x4 acc[kHW];
-    static_for<0, kHW>([&](auto q_c) __attribute__((always_inline)) {
+    f32x4 acc[NCELL];
+    static_for<0, NCELL>([&](auto q_c) __attribute__((always_inline)) {
         acc[decltype(q_c)::value] = (f32x4){0.f, 0.f, 0.f, 0.f};
     });
 
-    int64_t tile = w / a.nct;
-    if (tile >= ntiles) return;
-    if constexpr (KC == 1) load_b(0);
-    // prologue: quads 0 and 1 of the first (tile, k-step)
-    {
-        const float *s0 = src(tile, 0);
-        issue(s0, 0, IC<0>{}, KC == 1);
-        issue(s0, 1, IC<1>{}, KC == 1);
-    }
-    for (; tile < ntiles; tile += a.tpw) {
-        const int64_t next = tile + a.tpw < ntiles ? tile + a.tpw : tile;   // loads past the end: re-read
+    const int64_t step = gridDim.x;
+    // prologue: quad 0 staged, quad 1 in flight
+    issue(task, 0, 0, IC<0>{});
+    issue(task, 0, 1, IC<1>{});
+    stage(0, IC<0>{});
+    int ct_b = -1;
+    bar_lds();
+    for (; task < ntasks; task += step) {
+        const int64_t nxt = task + step < ntasks ? task + step : task;   // loads past the end: re-read
+        const int ct = ct_of(task);
+        if (KC == 1 && ct != ct_b) load_b(ct, 0);
+        ct_b = ct;
         static_for<0, KC>([&](auto kc_c) __attribute__((always_inline)) {
             constexpr int kc = decltype(kc_c)::value;
-            if constexpr (KC > 1) load_b(kc);
-            const float *s_cur = src(tile, kc);
-            const float *s_nxt = kc + 1 < KC ? src(tile, kc + 1) : src(next, 0);
-            constexpr bool cur_last = kc == KC - 1;
-            constexpr bool nxt_last = kc + 1 < KC ? kc + 1 == KC - 1 : KC == 1;
+            if constexpr (KC > 1) load_b(ct, kc);
             static_for<0, kQuads>([&](auto j_c) __attribute__((always_inline)) {
                 constexpr int j = decltype(j_c)::value;
-                // two quads ahead (slot (j + 2) % 3: kQuads is a multiple of 3, so slots line up across k-steps)
-                if constexpr (j + 2 < kQuads) issue(s_cur, j + 2, IC<(j + 2) % 3>{}, cur_last);
-                else issue(s_nxt, j + 2 - kQuads, IC<(j + 2) % 3>{}, nxt_last);
-                constexpr int slot = j % 3;
+                constexpr int s = kc * kQuads + j;   // step within the task; slots are s % 3 (kQuads % 3 == 0)
+                // loads two quads ahead into the slot staged last step, then stage the next quad
+                constexpr int s2 = s + 2, s1 = s + 1;
+                if constexpr (s2 < KC * kQuads) issue(task, s2 / kQuads, s2 % kQuads, IC<s2 % 3>{});
+                else issue(nxt, (s2 - KC * kQuads) / kQuads, (s2 - KC * kQuads) % kQuads, IC<s2 % 3>{});
+                // compute quad j from slot s % 3
+                const unsigned char *img = smem + (s % 3) * kSlotBytes + r * 64 + g * 16;
                 static_for<0, 4>([&](auto u_c) __attribute__((always_inline)) {
                     constexpr int u = decltype(u_c)::value;
                     constexpr int p = 4 * j + u;
-                    float v[8];
-                    static_for<0, 8>([&](auto e_c) __attribute__((always_inline)) {
-                        constexpr int e = decltype(e_c)::value;
-                        const float4 &f = raw[slot][e];
-                        v[e] = u == 0 ? f.x : (u == 1 ? f.y : (u == 2 ? f.z : f.w));
-                        if constexpr (PADC && cur_last)
-                            if (e > emax) v[e] = 0.f;
-                    });
-                    uint4 Ah, Am, Al;
-                    split8(v, Ah, Am, Al);
-                    static_for<0, kHW>([&](auto q_c) __attribute__((always_inline)) {
-                        constexpr int q = decltype(q_c)::value;
-                        constexpr int t = tap_pq(p, q);
-                        if constexpr (t >= 0) acc[q] = mfma_split(Ah, Am, Al, Bw[t][0], Bw[t][1], Bw[t][2], acc[q]);
-                    });
+                    if constexpr (band_uses(NB, BAND, p)) {
+                        const uint4 Ah = *reinterpret_cast<const uint4 *>(img + (0 * 4 + u) * 1024);
+                        const uint4 Am = *reinterpret_cast<const uint4 *>(img + (1 * 4 + u) * 1024);
+                        const uint4 Al = *reinterpret_cast<const uint4 *>(img + (2 * 4 + u) * 1024);
+                        static_for<4 * Q0, 4 * Q1>([&](auto q_c) __attribute__((always_inline)) {
+                            constexpr int q = decltype(q_c)::value;
+                            constexpr int t = tap_pq(p, q);
+                            if constexpr (t >= 0)
+                                acc[q - 4 * Q0] = mfma_split(Ah, Am, Al, Bw[t][0], Bw[t][1], Bw[t][2], acc[q - 4 * Q0]);
+                        });
+                    }
                 });
+                if constexpr (s1 < KC * kQuads) stage(s1 / kQuads, IC<s1 % 3>{});
+                else stage(0, IC<s1 % 3>{});   // the next task's quad 0
+                bar_lds();
             });
         });
         // epilogue: C/D row (game) = 4g + i, column (channel) = r
         const int co = ct * 16 + r;
+        const int64_t tile = tile_of(task);
         if (co < a.cout) {
             const float bv = a.bias ? a.bias[co] : 0.f;
             const float al = a.alpha ? a.alpha[co] : 1.f;
@@ -176,12 +221,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
                 const int64_t n = tile * 16 + 4 * g + i;
                 if (n < a.N) {
                     float *yo = a.y + n * a.ys + (int64_t)co * kHW;
-                    static_for<0, kQuads>([&](auto j_c) __attribute__((always_inline)) {
+                    static_for<Q0, Q1>([&](auto j_c) __attribute__((always_inline)) {
                         constexpr int j = decltype(j_c)::value;
                         float o[4];
                         static_for<0, 4>([&](auto u_c) __attribute__((always_inline)) {
                             constexpr int u = decltype(u_c)::value;
-                            float v = acc[4 * j + u][i];
+                            float v = acc[4 * (j - Q0) + u][i];
                             if (a.bias) v = v + bv;
                             if (a.alpha) v = v * al + be;
                             if (a.relu) v = relu_f(v);
@@ -192,9 +237,36 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
                 }
             });
         }
-        static_for<0, kHW>([&](auto q_c) __attribute__((always_inline)) {
+        static_for<0, NCELL>([&](auto q_c) __attribute__((always_inline)) {
             acc[decltype(q_c)::value] = (f32x4){0.f, 0.f, 0.f, 0.f};
         });
+    }
+}
+
+// A workgroup's 4 waves share one 16-game tile per task: each stages a quarter of every quad (16 games x 32
+// channels x 4 cells, split once into the LDS ring) and computes NCTW column tiles x (4 / NCTW) output bands.
+template <int KC, bool PADC, int NCTW>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void gboard_conv_kernel(GbArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[kLdsBytes];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nwg = gridDim.x, b = blockIdx.x;
+    // consecutive logical workgroups (which share game tiles) on one XCD (hardware deals b round robin)
+    const int L = (nwg % 8 == 0) ? (b & 7) * (nwg >> 3) + (b >> 3) : b;
+    constexpr int NB = 4 / NCTW;
+    const int band = wave / NCTW;
+    if constexpr (NB == 1) {
+        gboard_run<KC, PADC, NCTW, 0>(a, smem, lane, wave, L);
+    } else if constexpr (NB == 2) {
+        if (band == 0) gboard_run<KC, PADC, NCTW, 0>(a, smem, lane, wave, L);
+        else gboard_run<KC, PADC, NCTW, 1>(a, smem, lane, wave, L);
+    } else {
+        switch (band) {
+        case 0: gboard_run<KC, PADC, NCTW, 0>(a, smem, lane, wave, L); break;
+        case 1: gboard_run<KC, PADC, NCTW, 1>(a, smem, lane, wave, L); break;
+        case 2: gboard_run<KC, PADC, NCTW, 2>(a, smem, lane, wave, L); break;
+        default: gboard_run<KC, PADC, NCTW, 3>(a, smem, lane, wave, L); break;
+        }
     }
 }
 
@@ -268,24 +340,35 @@ int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_
     a.nct = (int)((Cout + 15) / 16); a.cout = (int)Cout;
     a.bias = bias; a.alpha = alpha; a.beta = beta; a.relu = relu; a.y = y; a.ys = y_stride;
     const int64_t ntiles = (N + 15) / 16;
-    // waves per column tile: fill the chip's wave slots, a multiple of 4 when that keeps the workgroups a
-    // multiple of 8 (the XCD mapping), never more than there are game tiles
-    int tpw = (int)(kSlots / a.nct > 0 ? kSlots / a.nct : 1);
-    if (tpw >= 8) tpw &= ~3;
-    if (tpw > ntiles) tpw = (int)ntiles;
-    a.tpw = tpw;
-    const int waves = a.nct * tpw;
-    const dim3 grid((waves + kWaves - 1) / kWaves), block(kThreads);
+    // column tiles per workgroup (NCTW = 4, 2, 1; the other waves split the output cells into 4 / NCTW bands):
+    // the fewest task rounds per band over the chip's 256 CUs (one 4-wave workgroup each), ties to the wider
+    // NCTW (fewer workgroups stage each tile)
+    int nctw = 1;
+    double best = 1e30;
+    for (int c = 4; c >= 1; c >>= 1) {
+        if (a.nct % c || (groups > 1 && (cout_g / 16) % c)) continue;   // a workgroup's tiles share one group
+        const int64_t tasks = ntiles * (a.nct / c);
+        const double rounds = (double)((tasks + kCUs - 1) / kCUs) * c / 4.0;
+        if (rounds < best - 1e-9) { best = rounds; nctw = c; }
+    }
+    const int64_t tasks = ntiles * (a.nct / nctw);
+    int grid = (int)(tasks < kCUs ? tasks : kCUs);
+    const dim3 block(kThreads);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int KC = (int)((Cin_g + 31) / 32);
     const bool padc = Cin_g % 32 != 0;
+#define HRL_GB_LAUNCH(KC_, PADC_)                                                                                  \
+    do {                                                                                                         \
+        if (nctw == 4) hipLaunchKernelGGL((gboard_conv_kernel<KC_, PADC_, 4>), dim3(grid), block, 0, s, a);      \
+        else if (nctw == 2) hipLaunchKernelGGL((gboard_conv_kernel<KC_, PADC_, 2>), dim3(grid), block, 0, s, a); \
+        else hipLaunchKernelGGL((gboard_conv_kernel<KC_, PADC_, 1>), dim3(grid), block, 0, s, a);                \
+    } while (0)
     if (KC == 1) {
-        if (padc) hipLaunchKernelGGL((gboard_conv_kernel<1, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((gboard_conv_kernel<1, false>), grid, block, 0, s, a);
+        if (padc) HRL_GB_LAUNCH(1, true); else HRL_GB_LAUNCH(1, false);
     } else {
-        if (padc) hipLaunchKernelGGL((gboard_conv_kernel<2, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((gboard_conv_kernel<2, false>), grid, block, 0, s, a);
+        if (padc) HRL_GB_LAUNCH(2, true); else HRL_GB_LAUNCH(2, false);
     }
+#undef HRL_GB_LAUNCH
     return status();
 }
 
