@@ -291,6 +291,52 @@ __global__ void gboard_pack_kernel(const float *__restrict__ w, int cout, int ci
     out[i] = hrl_split::split_part(wv(ci), part) | (hrl_split::split_part(wv(ci + 1), part) << 16);
 }
 
+// 1x1 convolution over the 6x6 board's channels (GeisterNet's move head conv2 8 -> 4 and the value / return heads'
+// conv 64 -> 1 each, geister.py:238-264): y[n, o, q] = sum_c w[o, c] x[n, c, q] over x1's C1 channels then x2's
+// C2 (the heads' [h_e, h_last] read in place), then the optional BatchNorm apply (y*alpha + beta) and ReLU.
+// HBM-bound: a thread per (game, cell) walks the channels (consecutive threads read consecutive cells) with
+// its O sums in registers, channels in order.
+template <int O>
+__global__ __launch_bounds__(256) void pointwise_kernel(const float *__restrict__ x1, int64_t s1, int C1,
+                                                        const float *__restrict__ x2, int64_t s2, int C2,
+                                                        const float *__restrict__ w, const float *__restrict__ alpha,
+                                                        const float *__restrict__ beta, int relu,
+                                                        float *__restrict__ y, int64_t ys, int64_t N) {
+    __shared__ float ws[O * 128];
+    const int C = C1 + C2;
+    for (int i = threadIdx.x; i < O * C; i += blockDim.x) ws[i] = w[i];
+    __syncthreads();
+    const int64_t total = N * kHW;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t n = e / kHW;
+        const int q = (int)(e - n * kHW);
+        float acc[O];
+#pragma unroll
+        for (int o = 0; o < O; ++o) acc[o] = 0.f;
+        const float *xp = x1 + n * s1 + q;
+        for (int c = 0; c < C1; ++c) {
+            const float v = xp[c * kHW];
+#pragma unroll
+            for (int o = 0; o < O; ++o) acc[o] = acc[o] + ws[o * C + c] * v;
+        }
+        if (x2) {
+            const float *xq = x2 + n * s2 + q;
+            for (int c = 0; c < C2; ++c) {
+                const float v = xq[c * kHW];
+#pragma unroll
+                for (int o = 0; o < O; ++o) acc[o] = acc[o] + ws[o * C + C1 + c] * v;
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < O; ++o) {
+            float v = acc[o];
+            if (alpha) v = v * alpha[o] + beta[o];
+            if (relu) v = relu_f(v);
+            y[n * ys + o * kHW + q] = v;
+        }
+    }
+}
+
 int status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
@@ -369,6 +415,24 @@ int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_
         if (padc) HRL_GB_LAUNCH(2, true); else HRL_GB_LAUNCH(2, false);
     }
 #undef HRL_GB_LAUNCH
+    return status();
+}
+
+int hrl_gboard_pointwise(const float *x1, int64_t x1_stride, int64_t C1, const float *x2, int64_t x2_stride,
+                          int64_t C2, int64_t N, const float *weight, int64_t O, const float *alpha, const float *beta,
+                          int relu, float *y, int64_t y_stride, void *stream) {
+    if (!x1 || !weight || !y || N < 1 || C1 < 1 || C2 < 0 || (C2 > 0) != (x2 != nullptr) || C1 + C2 > 128 ||
+        (O != 1 && O != 2 && O != 4 && O != 8) || (alpha == nullptr) != (beta == nullptr))
+        return HRL_EINVAL;
+    if (x1_stride < C1 * kHW || (x2 && x2_stride < C2 * kHW) || y_stride < O * kHW) return HRL_EINVAL;
+    const int64_t total = N * kHW;
+    const int grid = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+#define HRL_PW(O_)                                                                                                \
+    hipLaunchKernelGGL(pointwise_kernel<O_>, dim3(grid), dim3(256), 0, s, x1, x1_stride, (int)C1, x2, x2_stride,  \
+                       (int)C2, weight, alpha, beta, relu, y, y_stride, N)
+    if (O == 1) HRL_PW(1); else if (O == 2) HRL_PW(2); else if (O == 4) HRL_PW(4); else HRL_PW(8);
+#undef HRL_PW
     return status();
 }
 

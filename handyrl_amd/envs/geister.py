@@ -363,10 +363,14 @@ class GeisterNet(nn.Module):
         if (bufs['bn1'][0].is_cuda and BOARD == (6, 6)
                 and all(tuple(c.kernel_size) == (3, 3) and tuple(c.padding) == (1, 1) and tuple(c.stride) == (1, 1)
                         and c.groups == 1 and c.bias is None for c in (c1, hc))
-                and c1.weight.shape[1] <= 32 and hc.weight.shape[1] == 2 * c1.weight.shape[0] == 64):
+                and c1.weight.shape[1] <= 32 and hc.weight.shape[1] == 2 * c1.weight.shape[0] == 64
+                and self.head_p_move.conv2.bias is None and self.head_p_move.conv2.weight.shape[0] in (1, 2, 4, 8)
+                and tuple(self.head_p_move.conv2.weight.shape[2:]) == (1, 1)):
             with torch.no_grad():   # hrl_gboard's split fragments of the stem and move-head convolutions
                 gb['conv1'] = hnn.gboard_pack(c1.weight, out=gb.get('conv1'))
                 gb['head'] = hnn.gboard_pack(hc.weight, out=gb.get('head'))
+                w2 = self.head_p_move.conv2.weight
+                gb['head2'] = w2.detach().clone() if gb.get('head2') is None else gb['head2'].copy_(w2)
             self._gb_buf = gb
             self._gb_session = gb
         hv, hr = self.head_v, self.head_r
@@ -419,30 +423,40 @@ class GeisterNet(nn.Module):
         else:
             h_e = bn_relu(self.bn1, self.conv1(x_in))
         h_last, hidden = self.body(h_e, hidden, self.num_repeats)
-        h = torch.cat([h_e, h_last], dim=-3)
         hp, hv, hr = self.head_p_move, self.head_v, self.head_r
-        if gb is not None and hnn.gboard_ok(h_e, x2=h_last):   # [h_e, h_last] read in place
+        # in a session on the 6x6 board every head convolution is a HIP kernel reading [h_e, h_last] in place
+        # (no concatenation): the move head's 3x3 conv with its BatchNorm + ReLU epilogue and its 1x1 conv,
+        # and the value / return heads' 1x1 convs as one 2-channel pointwise pass with both BatchNorms + ReLUs
+        two = gb is not None and hnn.gboard_ok(h_e, x2=h_last)
+        h = None if two else torch.cat([h_e, h_last], dim=-3)
+        if two:
             C = hp.bn.num_features
             cp = coefs[id(hp.bn)]
             a = hnn.gboard_conv(h_e, gb['head'], C, 2 * h_e.shape[1], x2=h_last, alpha=cp[:C], beta=cp[C:],
                                 relu=True)
+            p_move = hnn.gboard_pointwise(a, gb['head2']).reshape(-1, hp.outputs)
         else:
-            a = bn_relu(hp.bn, hp.conv1(h))
-        p_move = hp.conv2(a).reshape(-1, hp.outputs)
+            p_move = hp.conv2(bn_relu(hp.bn, hp.conv1(h))).reshape(-1, hp.outputs)
         policy = torch.cat([p_move, self.head_p_set(scalar[:, :1])], dim=-1)
         vr = self._vr_session
         if vr is not None and hv.hidden_units == hr.hidden_units:
             # in a session the value and return heads' 1x1 convs run as one 2-channel conv and their
             # BatchNorm + ReLU as one apply (per-channel: the same values as the two heads apart)
             from .. import _native
-            y = F.conv2d(h, vr['w'])
-            a = torch.empty_like(y)
-            _native.check(_native.load().hrl_bn_apply(
-                _native.ptr(y), y.shape[0], 2, y[0, 0].numel(), _native.ptr(vr['coef']), _native.ptr(vr['coef'][2:]),
-                1, _native.ptr(a), _native.stream_of(y.device)), 'hrl_bn_apply')
+            if two:
+                a = hnn.gboard_pointwise(h_e, vr['w'], x2=h_last, alpha=vr['coef'][:2], beta=vr['coef'][2:],
+                                         relu=True)
+            else:
+                y = F.conv2d(h, vr['w'])
+                a = torch.empty_like(y)
+                _native.check(_native.load().hrl_bn_apply(
+                    _native.ptr(y), y.shape[0], 2, y[0, 0].numel(), _native.ptr(vr['coef']),
+                    _native.ptr(vr['coef'][2:]), 1, _native.ptr(a), _native.stream_of(y.device)), 'hrl_bn_apply')
             v = hv.fc(a[:, 0].reshape(-1, hv.hidden_units))
             r = hr.fc(a[:, 1].reshape(-1, hr.hidden_units))
         else:
+            if h is None:
+                h = torch.cat([h_e, h_last], dim=-3)
             v = hv.fc(bn_relu(hv.bn, hv.conv(h)).reshape(-1, hv.hidden_units))
             r = hr.fc(bn_relu(hr.bn, hr.conv(h)).reshape(-1, hr.hidden_units))
         return {'policy': policy, 'value': torch.tanh(v), 'return': r, 'hidden': hidden}

@@ -231,6 +231,21 @@ def gboard_conv(x, packed, Cout, cin_g, groups=1, x2=None, bias=None, alpha=None
     return y
 
 
+def gboard_pointwise(x, w, x2=None, alpha=None, beta=None, relu=False):
+    """1x1 conv (no bias) of x (and then x2's channels) on the 6x6 board with weight w (O, C, 1, 1), optional
+    BatchNorm apply + ReLU (csrc/hrl_gboard.hip, forward only): F.conv2d(cat([x, x2]), w) without the cat."""
+    N, C1 = x.shape[0], x.shape[1]
+    C2 = 0 if x2 is None else x2.shape[1]
+    O = w.shape[0]
+    y = torch.empty(N, O, 6, 6, device=x.device, dtype=torch.float32)
+    P = _native.ptr
+    _native.check(_native.load().hrl_gboard_pointwise(
+        P(x), x.stride(0), C1, None if x2 is None else P(x2), 0 if x2 is None else x2.stride(0), C2, N,
+        P(w.contiguous()), O, None if alpha is None else P(alpha), None if beta is None else P(beta), int(relu),
+        P(y), y.stride(0), _native.stream_of(x.device)), 'hrl_gboard_pointwise')
+    return y
+
+
 class _DeferredConv(torch.autograd.Function):
     """conv2d (stride 1, 'same') whose weight/bias gradient is deferred to DeferredGrads.flush().
 

@@ -323,6 +323,14 @@ int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_
                        int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
                        const float *beta, int relu, float *y, int64_t y_stride, void *stream);
 
+/* A 1x1 convolution on the 6x6 board (no bias; GeisterNet's move-head conv2 and value / return head convs,
+ * geister.py:238-264): y[n, o, q] = sum_c W[o, c] x[n, c, q] over x1's C1 channels, then x2's C2 (x2 NULL when
+ * C2 = 0), then y*alpha[o] + beta[o] (both or neither) and relu.  weight (O, C1 + C2) row-major, O in
+ * {1, 2, 4, 8}, C1 + C2 <= 128; games x1_stride / x2_stride / y_stride floats apart. */
+int hrl_gboard_pointwise(const float *x1, int64_t x1_stride, int64_t C1, const float *x2, int64_t x2_stride,
+                          int64_t C2, int64_t N, const float *weight, int64_t O, const float *alpha, const float *beta,
+                          int relu, float *y, int64_t y_stride, void *stream);
+
 /* GeeseNet's head pooling (hungry_geese.py:52-53) on h (N, 32, H, W) and the net input x (its plane 0,
  * samples x_stride floats apart): head[n, c] = sum_q h[n, c, q] * x[n, 0, q], avg[n, c] = mean_q h[n, c, q]
  * (both (N, 32)); hrl_torus_head_unpool: the gradient w.r.t. h, g = dhead * x0 + davg / (H*W). */

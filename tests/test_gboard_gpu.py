@@ -127,3 +127,23 @@ def test_gboard_rejects_bad_shapes(cuda):
     pk = hnn.gboard_pack(torch.zeros(40, 32, 3, 3, device=cuda))
     with pytest.raises(ValueError):   # 40 / 2 groups = 20 channels per group: not a multiple of 16
         hnn.gboard_conv(x[:, :64], pk, 40, 32, groups=2)
+
+
+@pytest.mark.parametrize('O,C1,C2', [(4, 8, 0), (2, 32, 32), (1, 25, 0), (8, 64, 64)])
+def test_gboard_pointwise_matches_conv1x1(cuda, O, C1, C2):
+    """hrl_gboard_pointwise == F.conv2d(cat([x1, x2]), w) (1x1, fp32 on the CPU) with the optional BatchNorm apply
+    and ReLU; x2 a channel slice of a wider tensor, as the heads read h_last from the stacked state."""
+    g = torch.Generator().manual_seed(O * 100 + C1 + C2)
+    N = 37
+    x1 = torch.randn(N, C1, 6, 6, generator=g)
+    wide = torch.randn(N, C2 + 16, 6, 6, generator=g)
+    x2 = wide[:, 8:8 + C2]
+    w = torch.randn(O, C1 + C2, 1, 1, generator=g)
+    al, be = torch.rand(O, generator=g) + 0.5, torch.randn(O, generator=g)
+    ref = F.conv2d(torch.cat([x1, x2], 1) if C2 else x1, w).double()
+    y = hnn.gboard_pointwise(x1.to(cuda), w.to(cuda), x2=wide.to(cuda)[:, 8:8 + C2] if C2 else None).cpu().double()
+    assert _close(y, ref)
+    y = hnn.gboard_pointwise(x1.to(cuda), w.to(cuda), x2=wide.to(cuda)[:, 8:8 + C2] if C2 else None,
+                             alpha=al.to(cuda), beta=be.to(cuda), relu=True).cpu().double()
+    ref = (ref * al.double()[None, :, None, None] + be.double()[None, :, None, None]).clamp_min(0)
+    assert _close(y, ref)
