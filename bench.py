@@ -13,14 +13,15 @@ clip 4.0 and Adam.  Every rank trains its own B=4096 x T=32 batch (weak
 scaling); value = N*B*T*K / max-over-ranks time of the K timed steps.
 
 Rank 0 prints ONE JSON line with, besides the metric:
-  roofline      the V-trace scan kernel (the metric's second half): algorithmic
-                bytes per launch / mean launch time from HIP events on the
-                launch stream, at the step's own size and at a cold,
-                larger-than-Infinity-Cache size;
+  roofline      the step's dominant kernel, one chain block's backward (conv3x3_block_bwd2_kernel + its
+                weight-gradient fold, 3 launches, ~40% of the step): algorithmic bytes per launch / mean
+                duration from HIP events on the launch stream around the step's own launches (eager steps
+                after the timed region); its split-MFMA fraction beside it;
+  scan_roofline the B1 operator, the V-trace scan kernel: algorithmic bytes per launch / mean launch time
+                from HIP events, at the step's own size and at a cold, larger-than-Infinity-Cache size;
   loss_roofline the step's fused loss forward (csrc/hrl_loss.hip, the scans inside it), algorithmic bytes
                 / HIP-event time;
-  block_roofline the step's dominant kernel, one chain block's backward (3 launches per step): HBM and
-                split-MFMA fractions;
+  block_roofline the same block backward launched alone on random data (back-to-back launches);
   cpu_baseline  the CPU learner oracle (oracle/learner.py, restating
                 train.py:218-258 + 382-385) timed on this host, 1 thread as the
                 reference ships (model.py:8), on a bounded sample (N=1 only).
@@ -264,6 +265,31 @@ def time_block_backward(device, M, iters=20):
             'launches_per_step': 3,
             'note': 'bytes = g, y, x read + gin written (dY and x\' stay on chip); flops = weight + input gradient '
                     'on the 49 on-board tap blocks; split ceiling = bf16 dense peak / 6'}
+
+
+def time_block_in_step(learner, batch, device, steps=4):
+    """The dominant kernel as the step runs it: HIP events on the launch stream around every chain block backward
+    launch (conv3x3_block_bwd2_kernel + its weight-gradient fold) of a few EAGER learner steps (the same
+    kernels the graph replays, on the step's own data), after the timed region."""
+    from handyrl_amd import nn as hnn
+    hnn.BLOCK_TIMING = []
+    try:
+        for _ in range(steps):
+            learner._body(batch, None)
+        torch.cuda.synchronize(device)
+        ts = [s.elapsed_time(e) * 1e3 for s, e in hnn.BLOCK_TIMING[3:]]   # the first eager step warms up
+    finally:
+        hnn.BLOCK_TIMING = None
+    return sum(ts) / max(len(ts), 1), len(ts)
+
+
+def block_traffic():
+    """HBM bytes per chain block backward launch from the committed rocprofv3 PMC passes (profiles/), or None."""
+    path = os.path.join(ROOT, 'profiles', 'r03_block_pmc.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get('bytes_per_launch')
 
 
 def pmc_traffic(B, T):
@@ -516,7 +542,7 @@ def main():
         value = steps_total / elapsed
         hot = time_scan(device, B, T, opts.scan_iters)
         cold = time_scan(device, 1 << 18, T, 60, cold=True)
-        roof = {
+        scan_roof = {
             'kernel': 'targets_kernel<VTRACE,UPGO> value head (hrl_compute_targets_fused)',
             'bound': 'hbm',
             'achieved': round(hot['GBps'], 1),
@@ -535,6 +561,30 @@ def main():
         net_roof = time_conv(device, B * T)
         loss_roof = time_loss(device, B, T)
         block_roof = time_block_backward(device, B * T)
+        # the roofline line is the step's dominant kernel: the chain block backward (3 launches, ~40% of the step)
+        us_blk, n_blk = time_block_in_step(learner, batch, device)
+        blk_bytes = block_roof['bytes_per_launch']
+        blk_gbs = blk_bytes / (us_blk * 1e-6) / 1e9
+        blk_tf = block_roof['flops_per_launch'] / (us_blk * 1e-6) / 1e12
+        roof = {
+            'kernel': 'conv3x3_block_bwd2_kernel (+ its weight-gradient fold): one chain block backward of the step '
+                      '(BN backward apply + weight gradient + input gradient, csrc/hrl_conv.hip)',
+            'bound': 'hbm',
+            'achieved': round(blk_gbs, 1),
+            'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s',
+            'frac': round(blk_gbs / HBM_PEAK_GBS, 4),
+            'traffic': block_traffic(),
+            'traffic_source': 'profiles/r03_block_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes over '
+                              'tools/block_bench.py, gfx950-corrected)',
+            'bytes_per_launch': blk_bytes,
+            'us_per_launch': round(us_blk, 2),
+            'launches_timed': n_blk,
+            'timing': 'HIP events on the launch stream around each of the step\'s block backward launches in eager '
+                      'steps after the timed region (the graph replays the same launches)',
+            'mfma_achieved_TFLOPs': round(blk_tf, 1),
+            'mfma_frac_split': round(blk_tf / (MFMA_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS), 4),
+        }
         cpu = cpu_baseline() if (opts.cpu_baseline and world == 1) else None
         t9 = secondary_t9(device) if (opts.secondary and world == 1) else None
         ro = secondary_rollout(device) if (opts.secondary and world == 1) else None
@@ -559,6 +609,7 @@ def main():
                        'global_batch': world * B, 'per_gpu_batch': B, 'seq_len': T, 'players': 2,
                        'parallelism': 'dp%d' % world, 'hip_graph': use_graph},
             'roofline': roof,
+            'scan_roofline': scan_roof,
             'net_roofline': net_roof,
             'loss_roofline': loss_roof,
             'block_roofline': block_roof,

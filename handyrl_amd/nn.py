@@ -193,6 +193,26 @@ def board_conv_forward(x, w, b, ci0=0, packed=None):
     return y
 
 
+# bench.py's in-step timing of the dominant kernel: a list that collects (start, end) HIP events recorded on the
+# launch stream around every chain block backward launch of an eager step (None: off; never inside a capture)
+BLOCK_TIMING = None
+
+
+def _block_timing_start():
+    if BLOCK_TIMING is None or torch.cuda.is_current_stream_capturing():
+        return None
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()
+    return ev
+
+
+def _block_timing_end(ev):
+    if ev is not None:
+        end = torch.cuda.Event(enable_timing=True)
+        end.record()
+        BLOCK_TIMING.append((ev, end))
+
+
 def gboard_ok(x, groups=1, x2=None):
     """Inputs hrl_gboard_forward covers: fp32 CUDA games on the 6x6 board, float4-aligned storage."""
     ts = [x] if x2 is None else [x, x2]
@@ -1410,10 +1430,12 @@ def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, pa
                 gin, epi, ep = torch.empty_like(h0), 2, (coefs[i - 1][0], coefs[i - 1][2], coefs[i - 1][3])
             elif need_input_grad:
                 gin, epi = torch.empty_like(h0), (3 if relu_in else 0)
+            ev = _block_timing_start()
             _native.check(lib.hrl_conv3x3_block_backward(
                 P(g), P(ys[i]), M, P(gamma), P(beta), P(mean), P(invstd), P(kg[0]), P(kg[1]), P(x), P(a), P(b),
                 P(packed[i, 1]), P(dw), P(gin), epi, P(ep[0]), P(ep[1]), P(ep[2]), P(part) if i > 0 else None,
                 P(ws), ws_bytes, stream), 'hrl_conv3x3_block_backward')
+            _block_timing_end(ev)
             grads[3 * i:3 * i + 3] = [_ret(bw), _ret(bgam), _ret(bbet)]
             g = gin
             if i > 0:
