@@ -994,11 +994,14 @@ constexpr int kWaves = 8;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kPartBytes = kCells * kC * kTile * 2;        // one bf16 part image (9 KB)
 constexpr int kImgBytes = 3 * kPartBytes;                  // h, m, l (27 KB)
-constexpr int kWlBytes = kTaps * 2 * 64 * 16;              // the weights' l parts [tap][ct][lane] (18 KB)
 constexpr int kDy0 = 0;                                    // dY images, buffers 0/1
 constexpr int kX0 = 2 * kImgBytes;                         // x' images, buffers 0/1
-constexpr int kWl0 = 4 * kImgBytes;
-constexpr int kLdsBytes = kWl0 + kWlBytes;                 // 129,024 B
+// the epilogue's raw x (fp32, [row][channel][cell], rows kXrStride floats apart), buffers 0/1: staged with the
+// images instead of re-read from HBM (the re-read cost more than the MFMAs: tools/bb2_variants.sh)
+constexpr int kXrStride = kRow + 4;                        // 292: the 4 row groups of a read 16 banks apart
+constexpr int kXrBytes = kTile * kXrStride * 4;            // 18,688 B
+constexpr int kXr0 = 4 * kImgBytes;
+constexpr int kLdsBytes = kXr0 + 2 * kXrBytes;             // 147,968 B
 static_assert(kLdsBytes <= 160 * 1024, "LDS");
 
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -1095,15 +1098,15 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         pa = a.in_alpha[ch];
         pb = a.in_beta[ch];
     }
-    // the input gradient's weights: h and m parts of its taps in registers ([tap][ct][part][lane] layout of
+    // the input gradient's weights: all three parts of its taps in registers ([tap][ct][part][lane] layout of
     // conv3x3_block_bwd_kernel's LDS fragments: lane l holds W'[tap][ci = 8(l>>4) + e][co = 16ct + (l&15)])
-    uint4 wh[kTaps], wm[kTaps];
+    uint4 wh[kTaps], wm[kTaps], wl[kTaps];
     if constexpr (kIg) {
         const int ci0 = 8 * (lane >> 4), j = lane & 15;
 #pragma unroll
         for (int t = 0; t < kTaps; ++t) {
             if (!uses_tap<W>(t)) continue;
-            uint32_t hv[4], mv[4];
+            uint32_t hv[4], mv[4], lv[4];
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
                 const int tc = t * 2 + kCt;
@@ -1114,9 +1117,11 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                 hrl_split::split3(w1, h1, m1, l1);
                 hv[d] = h0 | (h1 << 16);
                 mv[d] = m0 | (m1 << 16);
+                lv[d] = l0 | (l1 << 16);
             }
             wh[t] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
             wm[t] = make_uint4(mv[0], mv[1], mv[2], mv[3]);
+            wl[t] = make_uint4(lv[0], lv[1], lv[2], lv[3]);
         }
     }
     float em = 0.f, ea = 1.f, eb = 0.f;     // epilogue 2: BN_{i-1} of this lane's output channel
@@ -1220,30 +1225,15 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                 *reinterpret_cast<uint32_t *>(xi + part * kPartBytes + o) = xp[part][i];
             }
         }
-    };
-    f32x4 acc[kNq];
-    float rv[kNq < 4 ? 4 : kNq][4];   // the epilogue's raw x, loaded before the tile's MFMAs
-    auto load_ref = [&](int it) __attribute__((always_inline)) {
-        // the wave's output cells are consecutive (kQ[s] = kQ[0] + s): per row one run of kNq floats
-        if constexpr (kIg && (EPI == 2 || EPI == 3)) {
-            static_assert(R::kQ[R::kNq - 1] == R::kQ[0] + R::kNq - 1, "consecutive output cells");
-            int rows;
-            const __amdgpu_buffer_rsrc_t rx = rsrc_of(a.x, it, rows);
-            const int co = kCt * 16 + (lane & 15);
+        if constexpr (EPI == 2 || EPI == 3) {   // the epilogue's raw x (rows past the batch are loaded as 0)
+            float *xr = reinterpret_cast<float *>(smem + kXr0 + (it & 1) * kXrBytes);
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int row = (lane >> 4) * 4 + rr;
-                const int off = (row * kRow + co * kCells + R::kQ[0]) * 4;
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
-                rv[0][rr] = __uint_as_float(v.x);
-                rv[1][rr] = __uint_as_float(v.y);
-                rv[2][rr] = __uint_as_float(v.z);
-                rv[3][rr] = __uint_as_float(v.w);
-                if constexpr (R::kNq > 4)
-                    rv[4 % kNq][rr] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, off + 16, 0, 0));
-            }
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int i = 0; i < 5; ++i) xr[(rho0 + r) * kXrStride + ch * kCells + c0 + i] = X[r][i];
         }
     };
+    f32x4 acc[kNq];
     auto compute = [&](int it) __attribute__((always_inline)) {
         const unsigned char *dyi = smem + kDy0 + (it & 1) * kImgBytes;
         if constexpr (kVariant & 2) {
@@ -1285,7 +1275,6 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
             // input gradient blocks (q, kCt): acc += sum_p dY_p (16 rows x 32 co) . W'[tap(p, q)][kCt], p ascending
 #pragma unroll
             for (int s = 0; s < kNq; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
-            const uint4 *wl = reinterpret_cast<const uint4 *>(smem + kWl0) + lane;
             const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
             const int tr_sub = 8 * (pp & 1);
 #pragma unroll
@@ -1311,7 +1300,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                 for (int s = 0; s < R::kNq; ++s) {
                     const int tap = tap_of(p, R::kQ[s]);
                     if (tap < 0) continue;
-                    const uint4 Bl = wl[(tap * 2 + kCt) * 64];
+                    const uint4 Bl = wl[tap];
                     f32x4 c = acc[s];
                     c = mfma_bf16(Al, wh[tap], c);   // smallest terms first
                     c = mfma_bf16(Am, wm[tap], c);
@@ -1329,6 +1318,17 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
             int rows;
             const __amdgpu_buffer_rsrc_t ro = rsrc_of(a.gin, it, rows);
             const int co = kCt * 16 + (lane & 15);
+            // the raw x of the wave's output cells, staged in LDS with the tile's images
+            float rv[kNq < 4 ? 4 : kNq][4];
+            if constexpr (EPI == 2 || EPI == 3) {
+                const float *xr = reinterpret_cast<const float *>(smem + kXr0 + (it & 1) * kXrBytes);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int row = (lane >> 4) * 4 + rr;
+#pragma unroll
+                    for (int s = 0; s < R::kNq; ++s) rv[s][rr] = xr[row * kXrStride + co * kCells + R::kQ[s]];
+                }
+            }
             if constexpr (EPI == 2) {   // bn_bwd_reduce_kernel's mask and sums
                 float t1 = 0.f, t2 = 0.f;
 #pragma unroll
@@ -1376,10 +1376,9 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         stage(0);
         issue(1);
     }
-    bar_lds();                                      // weights' l parts and tile 0 in LDS
+    bar_lds();                                      // tile 0 in LDS
     for (int it = 0; it < n_iter; ++it) {
         BB2_STAMP(it, 0);
-        load_ref(it);
         // stage / issue run unconditionally (past the last tile they stage and load zeros that nothing reads):
         // a branch around them makes the compiler's wait for the loaded registers vmcnt(0) at the loop head,
         // which then also waits for the previous iteration's gin stores
@@ -1440,17 +1439,6 @@ __global__ __launch_bounds__(bb2::kThreads) void conv3x3_block_bwd2_kernel(Block
     __shared__ __attribute__((aligned(16))) unsigned char smem[bb2::kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    {   // the weights' l parts: [tap][ct][lane] x 16 bytes (lane l: W'[tap][ci = 8(l>>4) + e][co = 16ct + (l&15)])
-        uint32_t *wl = reinterpret_cast<uint32_t *>(smem + bb2::kWl0);
-        constexpr int kWords = bb2::kWlBytes / 4;
-        for (int i = threadIdx.x; i < kWords; i += bb2::kThreads) {
-            const int d = i & 3, l = (i >> 2) & 63, tc = i >> 8;      // tc = tap*2 + ct
-            const int ci = 8 * (l >> 4) + 2 * d, j = l & 15;
-            const float w0 = a.wpk[(tc * kC + ci) * 16 + j];
-            const float w1 = a.wpk[(tc * kC + ci + 1) * 16 + j];
-            wl[i] = split_part(w0, 2) | (split_part(w1, 2) << 16);
-        }
-    }
     switch (wave) {
     case 0: bb2::run<PRO, EPI, 0>(a, smem, lane); break;
     case 1: bb2::run<PRO, EPI, 1>(a, smem, lane); break;
