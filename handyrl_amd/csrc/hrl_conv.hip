@@ -984,7 +984,7 @@ namespace bb2 {
 
 // diagnostic variants (tools/bb2_variants.sh builds them; the product is 0): bit 1 = no stage VALU (raw bits
 // packed into the images), bit 2 = no MFMA phase, bit 4 = no epilogue / gin store, bit 8 = every wave computes
-// first, bit 16 = no gin store (epilogue kept)
+// first, bit 16 = no gin store (epilogue kept), bit 32 = raised wave priority (s_setprio 2) through the MFMA phase
 #ifndef BB2_VARIANT
 #define BB2_VARIANT 0
 #endif
@@ -1383,7 +1383,9 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         // a branch around them makes the compiler's wait for the loaded registers vmcnt(0) at the loop head,
         // which then also waits for the previous iteration's gin stores
         if constexpr (R::kCFirst || (kVariant & 8)) {
+            if constexpr (kVariant & 32) __builtin_amdgcn_s_setprio(2);
             compute(it);
+            if constexpr (kVariant & 32) __builtin_amdgcn_s_setprio(0);
             epilogue(it);
             BB2_STAMP(it, 1);
             stage(it + 1);
@@ -1393,7 +1395,9 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
             stage(it + 1);
             issue(it + 2);
             BB2_STAMP(it, 1);
+            if constexpr (kVariant & 32) __builtin_amdgcn_s_setprio(2);
             compute(it);
+            if constexpr (kVariant & 32) __builtin_amdgcn_s_setprio(0);
             epilogue(it);
             BB2_STAMP(it, 2);
         }

@@ -500,7 +500,10 @@ class GeisterNet(nn.Module):
         cells = [blk.conv for blk in self.body.blocks]
         cin = cells[0].weight.shape[1] - self.body.blocks[0].hidden_dim
         packed_h = None
-        if hnn._DEFER is not None and hnn.board_conv_ok(h_e[:1], cells[0].weight, cin, cells[0].padding):
+        hd = self.body.blocks[0].hidden_dim
+        if hnn._DEFER is not None and hnn.gboard_conv_ok(h_e[:1, :hd], cells[0].weight, hd, cells[0].padding):
+            packed_h = [hnn.gboard_pack(c.weight.detach(), hd, cin) for c in cells]
+        elif hnn._DEFER is not None and hnn.board_conv_ok(h_e[:1], cells[0].weight, cin, cells[0].padding):
             packed_h = [hnn.board_conv_pack(c.weight.detach(), cin) for c in cells]
         return {'T': T, 'N': N, 'h_e': h_e, 'zx': zx, 'scalar': scalar, 'packed_h': packed_h}
 

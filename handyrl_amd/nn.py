@@ -221,6 +221,13 @@ def gboard_ok(x, groups=1, x2=None):
                and t.data_ptr() % 16 == 0 for t in ts) and x.shape[0] > 0
 
 
+def gboard_conv_ok(x, w, cin_g, pad):
+    """A 'same' 3x3 conv hrl_gboard_forward covers: x (N, cin_g, 6, 6) fp32 CUDA (float4-aligned games), at most 64
+    input channels, any Cout."""
+    return (w.dim() == 4 and tuple(w.shape[2:]) == (3, 3) and tuple(pad) == (1, 1) and w.dtype == torch.float32
+            and x.dim() == 4 and x.shape[1] == cin_g <= 64 and gboard_ok(x))
+
+
 def gboard_pack(w, cin_g=None, ci0=0, out=None):
     """Input channels [ci0, ci0 + cin_g) of the 3x3 weight w (Cout, Cin_total, 3, 3) as hrl_gboard's split
     fragments (written into ``out`` when given: a graph captured over the packed buffer sees the refresh)."""
@@ -276,7 +283,13 @@ class _DeferredConv(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         wv = w if sl is None else w[:, sl[0]:sl[1]]
         ci0 = 0 if sl is None else sl[0]
-        if (sl is None or sl[1] - sl[0] == 32) and board_conv_ok(x, w, ci0, pad):
+        cin_g = wv.shape[1]
+        if gboard_conv_ok(x, w, cin_g, pad):   # the 6x6 board: games as MFMA rows (csrc/hrl_gboard.hip)
+            wpk = gboard_pack(w.detach(), cin_g, ci0) if packed is None else packed
+            y = gboard_conv(x, wpk, w.shape[0], cin_g, bias=None if b is None else b.detach())
+        elif (sl is None or sl[1] - sl[0] == 32) and board_conv_ok(x, w, ci0, pad):
+            if packed is not None and packed.numel() != _native.load().hrl_board_conv_workspace_bytes(w.shape[0]):
+                packed = None   # packed for hrl_gboard (this input missed its alignment): repack for this kernel
             y = board_conv_forward(x, w.detach(), None if b is None else b.detach(), ci0, packed)
         else:
             y = F.conv2d(x, wv, b, padding=pad)
@@ -303,7 +316,8 @@ class _DeferredConv(torch.autograd.Function):
 def conv2d(x, w, b=None, padding=(0, 0), in_slice=None, packed=None):
     """F.conv2d (stride 1) of the env nets; inside deferred_weight_grads() the weight gradient is
     batched over the unroll (DeferredGrads) and the forward of 3x3 32-channel board convs runs on
-    the MFMA board conv (``packed``: its weights packed once for the unroll, board_conv_pack)."""
+    the MFMA board conv (``packed``: its weights packed once for the unroll -- gboard_pack on the 6x6 board
+    (gboard_conv_ok), board_conv_pack otherwise)."""
     if _DEFER is not None and torch.is_grad_enabled() and w.requires_grad:
         return _DeferredConv.apply(x, w, b, in_slice, tuple(padding), _DEFER, packed)
     wv = w if in_slice is None else w[:, in_slice[0]:in_slice[1]]
