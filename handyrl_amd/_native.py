@@ -153,6 +153,8 @@ SIGNATURES = {
                                           _f32p, _f32p, ctypes.c_int, _f32p, _i64, ctypes.c_void_p]),
     'hrl_gboard_pointwise': (ctypes.c_int, [_f32p, _i64, _i64, _f32p, _i64, _i64, _i64, _f32p, _i64, _f32p, _f32p,
                                             ctypes.c_int, _f32p, _i64, ctypes.c_void_p]),
+    'hrl_gboard_lstm_forward': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _i64, ctypes.c_void_p, _f32p, _i64, _f32p,
+                                               _f32p, _f32p, _i64, _f32p, _i64, ctypes.c_void_p]),
     'hrl_torus_head_pool': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, _i64, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_torus_head_unpool': (ctypes.c_int, [_f32p, _f32p, _f32p, _i64, _i64, _i64, _i64, _f32p,
                                              ctypes.c_void_p]),

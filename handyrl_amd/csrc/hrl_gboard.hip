@@ -49,6 +49,15 @@ struct GbArgs {
     int relu;
     float *y;
     int64_t ys;            // floats from one game to the next in y
+    // GATES (hrl_gboard_lstm_forward): the conv is the ConvLSTM cells' h halves (groups = layers, 4H outputs per
+    // layer in i, f, o, g order); the epilogue forms the gates with the x halves zx (+ bias) and the cell state
+    // instead of storing the conv: c' = sig(f) c + sig(i) tanh(g), h' = sig(o) tanh(c') (lstm_fwd_kernel's ops)
+    const float *zx;       // (N, layers*4H, 36), games zxs floats apart
+    int64_t zxs;
+    const float *c_in;     // (N, layers*H, 36), games cs floats apart; c_out may be c_in (same element, same lane)
+    float *c_out, *h_out;  // h_out never aliases x (other workgroups still read it)
+    int64_t cs, hs;
+    int nh;                // H / 16: column tiles per gate
 };
 
 // tap of input cell p for output cell q (-1 off the 3x3 neighbourhood)
@@ -90,10 +99,16 @@ __host__ __device__ constexpr bool band_uses(int NB, int b, int p) {
 constexpr int kPartBytes = 4 * 16 * 32 * 2;   // one split part of one quad's image: [cell][game][channel] bf16
 constexpr int kSlotBytes = 3 * kPartBytes;     // 12 KB per quad
 constexpr int kLdsBytes = 3 * kSlotBytes;      // ring of three quads
+// GATES: the four gate waves exchange a 12-cell chunk of their accumulators [gate][cell][row i][lane] (48 KB)
+constexpr int kGateChunk = 12;
+constexpr int kXchgBytes = 4 * kGateChunk * 4 * 64 * 4;
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }   // lstm_fwd_kernel's
 
 // One wave of gboard_conv_kernel: column tile (task's tile group * NCTW + ctl), output band BAND of NB = 4 / NCTW.
-template <int KC, bool PADC, int NCTW, int BAND>
+template <int KC, bool PADC, int NCTW, int BAND, bool GATES = false>
 __device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem, int lane, int wave, int L) {
+    static_assert(!GATES || (NCTW == 4 && KC == 1 && !PADC), "the gate epilogue: one gate per wave");
     constexpr int NB = 4 / NCTW;
     constexpr int Q0 = band_q0(NB, BAND), Q1 = band_q1(NB, BAND);
     constexpr int NCELL = 4 * (Q1 - Q0);
@@ -108,12 +123,17 @@ __device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem,
     int64_t task = L;
     if (task >= ntasks) return;   // uniform over the workgroup: no barrier is left waiting
     auto tile_of = [&](int64_t t) { return t / n_ctg; };
-    auto ct_of = [&](int64_t t) { return (int)(t % n_ctg) * NCTW + ctl; };
+    // GATES: task group ctg = (layer, hidden block hb); wave ctl takes gate ctl's column tile of that block
+    auto ct_of = [&](int64_t t) {
+        const int ctg = (int)(t % n_ctg);
+        if constexpr (GATES) return (ctg / a.nh) * 4 * a.nh + ctl * a.nh + ctg % a.nh;
+        return ctg * NCTW + ctl;
+    };
     // the staging lane's source row for (task, kc): channels 32kc + 2cp (+1) of game sg of the task's tile
     // (PADC: rows at or past cin_g read row cin_g - 1 and are zeroed)
     auto src = [&](int64_t t, int kc, int &c0, int &c1) -> const float * {
         const int64_t n = min(tile_of(t) * 16 + sg, a.N - 1);
-        const int grp = (ct_of(t) - ctl) * 16 / a.cout_g;   // the group of the task's first column tile
+        const int grp = ct_of(t) * 16 / a.cout_g;   // one group for all the workgroup's column tiles
         c0 = 32 * kc + 2 * cp;
         c1 = c0 + 1;
         if constexpr (PADC) {
@@ -209,9 +229,80 @@ __device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem,
                 bar_lds();
             });
         });
+        const int64_t tile = tile_of(task);
+        if constexpr (GATES) {
+            // wave k holds gate k of hidden channels hb*16 + r for games 4g + i; in chunks of 12 cells every wave
+            // writes its accumulators to LDS, then wave k' forms the cell update of row i = k' from all four gates
+            float *xchg = reinterpret_cast<float *>(smem + kLdsBytes);
+            const int ctg = (int)(task % n_ctg);
+            const int layer = ctg / a.nh, ch = (ctg % a.nh) * 16 + r;
+            const int H = 16 * a.nh;
+            const int64_t n = tile * 16 + 4 * g + wave;   // this wave's row i = wave
+            const int64_t nc = min(n, a.N - 1);
+            const float *zp = a.zx + nc * a.zxs + (int64_t)(layer * 4 * H + ch) * kHW;
+            const float *cp = a.c_in + nc * a.cs + (int64_t)(layer * H + ch) * kHW;
+            float bgate[4];
+            static_for<0, 4>([&](auto k_c) __attribute__((always_inline)) {
+                constexpr int k = decltype(k_c)::value;
+                bgate[k] = a.bias ? a.bias[layer * 4 * H + k * H + ch] : 0.f;
+            });
+            static_for<0, kHW / kGateChunk>([&](auto c_c) __attribute__((always_inline)) {
+                constexpr int C0 = decltype(c_c)::value * kGateChunk;
+                float4 zq[4][kGateChunk / 4], cq[kGateChunk / 4];   // the chunk's x halves and cell state
+                static_for<0, kGateChunk / 4>([&](auto j_c) __attribute__((always_inline)) {
+                    constexpr int j = decltype(j_c)::value;
+                    static_for<0, 4>([&](auto k_c) __attribute__((always_inline)) {
+                        constexpr int k = decltype(k_c)::value;
+                        zq[k][j] = *reinterpret_cast<const float4 *>(zp + (int64_t)k * H * kHW + C0 + 4 * j);
+                    });
+                    cq[j] = *reinterpret_cast<const float4 *>(cp + C0 + 4 * j);
+                });
+                if constexpr (C0 > 0) bar_lds();   // the previous chunk's reads are done
+                static_for<0, kGateChunk>([&](auto q_c) __attribute__((always_inline)) {
+                    constexpr int ql = decltype(q_c)::value;
+                    static_for<0, 4>([&](auto i_c) __attribute__((always_inline)) {
+                        constexpr int i = decltype(i_c)::value;
+                        xchg[((wave * kGateChunk + ql) * 4 + i) * 64 + lane] = acc[C0 + ql][i];
+                    });
+                });
+                bar_lds();
+                if (n < a.N) {
+                    float *ho = a.h_out + n * a.hs + (int64_t)(layer * H + ch) * kHW + C0;
+                    float *co = a.c_out + n * a.cs + (int64_t)(layer * H + ch) * kHW + C0;
+                    static_for<0, kGateChunk / 4>([&](auto j_c) __attribute__((always_inline)) {
+                        constexpr int j = decltype(j_c)::value;
+                        float hv[4], cv[4];
+                        static_for<0, 4>([&](auto u_c) __attribute__((always_inline)) {
+                            constexpr int u = decltype(u_c)::value;
+                            constexpr int ql = 4 * j + u;
+                            float z[4];
+                            static_for<0, 4>([&](auto k_c) __attribute__((always_inline)) {
+                                constexpr int k = decltype(k_c)::value;
+                                const float4 &f = zq[k][j];
+                                const float xv = u == 0 ? f.x : (u == 1 ? f.y : (u == 2 ? f.z : f.w));
+                                const float zh = xchg[((k * kGateChunk + ql) * 4 + wave) * 64 + lane];
+                                z[k] = a.bias ? (xv + bgate[k]) + zh : xv + zh;   // (zx + b) + zh
+                            });
+                            const float c0 = u == 0 ? cq[j].x : (u == 1 ? cq[j].y : (u == 2 ? cq[j].z : cq[j].w));
+                            const float si = sigm(z[0]), sf = sigm(z[1]), so = sigm(z[2]), tg = tanhf(z[3]);
+                            const float fc = sf * c0;
+                            const float ig = si * tg;
+                            const float cc = fc + ig;
+                            cv[u] = cc;
+                            hv[u] = so * tanhf(cc);
+                        });
+                        *reinterpret_cast<float4 *>(co + 4 * j) = make_float4(cv[0], cv[1], cv[2], cv[3]);
+                        *reinterpret_cast<float4 *>(ho + 4 * j) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+                    });
+                }
+            });
+            static_for<0, NCELL>([&](auto q_c) __attribute__((always_inline)) {
+                acc[decltype(q_c)::value] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            });
+            continue;
+        }
         // epilogue: C/D row (game) = 4g + i, column (channel) = r
         const int co = ct * 16 + r;
-        const int64_t tile = tile_of(task);
         if (co < a.cout) {
             const float bv = a.bias ? a.bias[co] : 0.f;
             const float al = a.alpha ? a.alpha[co] : 1.f;
@@ -241,6 +332,16 @@ __device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem,
             acc[decltype(q_c)::value] = (f32x4){0.f, 0.f, 0.f, 0.f};
         });
     }
+}
+
+// The ConvLSTM cells' h halves with the gate update in the epilogue (hrl_gboard_lstm_forward)
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void gboard_lstm_kernel(GbArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[kLdsBytes + kXchgBytes];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int L = (nwg % 8 == 0) ? (b & 7) * (nwg >> 3) + (b >> 3) : b;
+    gboard_run<1, false, 4, 0, true>(a, smem, lane, wave, L);
 }
 
 // A workgroup's 4 waves share one 16-game tile per task: each stages a quarter of every quad (16 games x 32
@@ -415,6 +516,31 @@ int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_
         if (padc) HRL_GB_LAUNCH(2, true); else HRL_GB_LAUNCH(2, false);
     }
 #undef HRL_GB_LAUNCH
+    return status();
+}
+
+int hrl_gboard_lstm_forward(const float *h, int64_t h_stride, int64_t N, int64_t layers, int64_t H, const void *packed,
+                            const float *zx, int64_t zx_stride, const float *bias, const float *c_in, float *c_out,
+                            int64_t c_stride, float *h_out, int64_t hout_stride, void *stream) {
+    if (!h || !packed || !zx || !c_in || !c_out || !h_out || N < 1 || layers < 1 || H < 16 || H > 64 || H % 16)
+        return HRL_EINVAL;
+    if (h_out == h) return HRL_EINVAL;   // other workgroups still read h while this one writes h'
+    if (!aligned16(h) || !aligned16(zx) || !aligned16(c_in) || !aligned16(c_out) || !aligned16(h_out) ||
+        h_stride % 4 || zx_stride % 4 || c_stride % 4 || hout_stride % 4)
+        return HRL_EINVAL;
+    if (h_stride < layers * H * kHW || zx_stride < layers * 4 * H * kHW || c_stride < layers * H * kHW ||
+        hout_stride < layers * H * kHW)
+        return HRL_EINVAL;
+    GbArgs a{};
+    a.x = h; a.x2 = nullptr; a.N = N; a.xs = h_stride; a.xs2 = 0;
+    a.cin_g = (int)H; a.cout_g = (int)(4 * H);
+    a.wpk = static_cast<const uint4 *>(packed);
+    a.nct = (int)(layers * 4 * H / 16); a.cout = (int)(layers * 4 * H);
+    a.bias = bias; a.zx = zx; a.zxs = zx_stride; a.c_in = c_in; a.c_out = c_out; a.h_out = h_out;
+    a.cs = c_stride; a.hs = hout_stride; a.nh = (int)(H / 16);
+    const int64_t tasks = ((N + 15) / 16) * (a.nct / 4);
+    const int grid = (int)(tasks < kCUs ? tasks : kCUs);
+    hipLaunchKernelGGL(gboard_lstm_kernel, dim3(grid), dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
     return status();
 }
 

@@ -258,6 +258,18 @@ def gboard_conv(x, packed, Cout, cin_g, groups=1, x2=None, bias=None, alpha=None
     return y
 
 
+def gboard_lstm(h, packed_h, zx, bias, c_in, c_out, h_out, layers, H):
+    """One DRC repeat of the stacked cells on the 6x6 board (csrc/hrl_gboard.hip, inference only): the grouped
+    h-half conv of h (N, layers*H, 6, 6) with the ConvLSTM gate update in its epilogue, from the x halves zx
+    (N, layers*4H, 6, 6) + bias and the cell state c_in; writes c_out (may be c_in) and h_out (not h)."""
+    P = _native.ptr
+    _native.check(_native.load().hrl_gboard_lstm_forward(
+        P(h), h.stride(0), h.shape[0], layers, H, P(packed_h), P(zx), zx.stride(0), None if bias is None else P(bias),
+        P(c_in), P(c_out), c_in.stride(0), P(h_out), h_out.stride(0), _native.stream_of(h.device)),
+        'hrl_gboard_lstm_forward')
+    assert c_out.stride(0) == c_in.stride(0)
+
+
 def gboard_pointwise(x, w, x2=None, alpha=None, beta=None, relu=False):
     """1x1 conv (no bias) of x (and then x2's channels) on the 6x6 board with weight w (O, C, 1, 1), optional
     BatchNorm apply + ReLU (csrc/hrl_gboard.hip, forward only): F.conv2d(cat([x, x2]), w) without the cat."""

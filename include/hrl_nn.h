@@ -323,6 +323,17 @@ int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_
                        int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
                        const float *beta, int relu, float *y, int64_t y_stride, void *stream);
 
+/* The ConvLSTM cells' h halves of a DRC repeat with the gate update in the epilogue (geister.py:17-63 stacked
+ * over the layers, csrc/hrl_gboard.hip): for every game n, layer l, hidden channel c and cell q
+ *   z_k = (zx[n, l*4H + k*H + c, q] + bias[l*4H + k*H + c]) + conv(h[n, l*H ..], W_l)[k*H + c, q],  k = i, f, o, g
+ *   c_out = sig(z_f) * c_in + sig(z_i) * tanh(z_g),  h_out = sig(z_o) * tanh(c_out)
+ * (hrl_lstm_gates_forward's float operations on hrl_gboard_forward's conv): the conv output never reaches HBM.
+ * packed: hrl_gboard_pack of the stacked h-half weights (layers*4H, H, 3, 3); H a multiple of 16, <= 64; bias
+ * (layers*4H) or NULL.  h, zx, c_in, c_out, h_out: games h_stride, zx_stride, c_stride, c_stride, hout_stride
+ * floats apart, 16-byte aligned.  c_out may be c_in; h_out must not overlap h. */
+int hrl_gboard_lstm_forward(const float *h, int64_t h_stride, int64_t N, int64_t layers, int64_t H, const void *packed,
+                            const float *zx, int64_t zx_stride, const float *bias, const float *c_in, float *c_out,
+                            int64_t c_stride, float *h_out, int64_t hout_stride, void *stream);
 /* A 1x1 convolution on the 6x6 board (no bias; GeisterNet's move-head conv2 and value / return head convs,
  * geister.py:238-264): y[n, o, q] = sum_c W[o, c] x[n, c, q] over x1's C1 channels, then x2's C2 (x2 NULL when
  * C2 = 0), then y*alpha[o] + beta[o] (both or neither) and relu.  weight (O, C1 + C2) row-major, O in

@@ -333,3 +333,36 @@ def test_sequence_unroll_matches_per_step_unroll(cuda):
             assert int(b1[n]) == int(b) == T, n
         else:
             torch.testing.assert_close(b1[n], b, rtol=1e-5, atol=1e-6, msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('inplace', [False, True])
+@pytest.mark.parametrize('repeats', [1, 3])
+def test_fused_gate_repeats_match_unfused(cuda, inplace, repeats):
+    """hrl_gboard_lstm_forward (each DRC repeat's grouped h-half conv with the gate update in its epilogue) gives
+    bit-identically the states of the unfused path (hrl_gboard conv, then the HIP gate kernel): the conv is the
+    same kernel arithmetic and the gate update lstm_fwd_kernel's float operations.  In place (the generator's
+    stacked state, h' through scratch states) and out of place, one and three repeats, ragged game count."""
+    from handyrl_amd.envs.geister import DRC, GeisterNet
+    from handyrl_amd.nn import accelerate
+    torch.manual_seed(5)
+    net = accelerate(GeisterNet().to(cuda)).eval()
+    E = 50
+    x = torch.randn(E, 32, 6, 6, device=cuda)
+    h0 = torch.randn(E, 96, 6, 6, device=cuda)
+    c0 = torch.randn(E, 96, 6, 6, device=cuda)
+    results = []
+    for fuse in (False, True):
+        DRC.fuse_gates = fuse
+        try:
+            h, c = h0.clone(), c0.clone()
+            hs, cs = [h[:, 32 * i:32 * (i + 1)] for i in range(3)], [c[:, 32 * i:32 * (i + 1)] for i in range(3)]
+            with torch.no_grad(), net.body.inference_session(inplace_state=inplace):
+                h_last, (hs2, cs2) = net.body._inference_stacked(x, hs, cs, repeats)
+            if inplace:
+                assert hs2[0].data_ptr() == h.data_ptr() and cs2[0].data_ptr() == c.data_ptr()
+            results.append([t.clone() for t in [h_last] + hs2 + cs2])
+        finally:
+            DRC.fuse_gates = False
+    for a, b in zip(*results):
+        assert torch.equal(a, b)
