@@ -87,6 +87,7 @@ SIGNATURES = {
     'hrl_conv3x3_stats_blocks': (ctypes.c_int64, [_i64]),
     'hrl_conv3x3_set_split': (ctypes.c_int, [ctypes.c_int]),
     'hrl_conv3x3_set_block_form': (ctypes.c_int, [ctypes.c_int]),
+    'hrl_conv3x3_set_fwd_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_torus_set_split': (ctypes.c_int, [ctypes.c_int]),
     'hrl_conv3x3_pack_n': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _f32p, ctypes.c_void_p]),
     'hrl_conv3x3_forward_ex': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_int, _f32p,

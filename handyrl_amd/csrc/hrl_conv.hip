@@ -1088,11 +1088,18 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
     constexpr int kNt = R::kNt > 0 ? R::kNt : 1;
     constexpr int kCt = R::kCt;
     const int ch = lane & 31, hh = lane >> 5;
+    // EPI 1 (kFwd): the forward conv in this form -- the staged image is x' = relu(x a + b) instead of dY, the
+    // input-gradient waves compute the conv with the forward weights, the weight-gradient waves only stage, and the
+    // epilogue emits the BN statistics of the output (conv3x3_kernel<PRO, 1>'s sums)
+    constexpr bool kFwd = EPI == 1;
     // BN_i's backward apply for channel ch (bn_bwd_apply_kernel's per-channel values), the prologue's BN_{i-1}
-    const float mu = a.bn_mean[ch], kk = a.bn_k[ch], gmn = a.bn_gm[ch], is = a.bn_invstd[ch];
-    const float ww = a.bn_w ? a.bn_w[ch] : 1.0f;
-    const float al = is * ww;
-    const float be = (a.bn_b ? a.bn_b[ch] : 0.0f) - mu * al;
+    float mu = 0.f, kk = 0.f, gmn = 0.f, is = 1.f, ww = 1.f, al = 1.f, be = 0.f;
+    if constexpr (!kFwd) {
+        mu = a.bn_mean[ch]; kk = a.bn_k[ch]; gmn = a.bn_gm[ch]; is = a.bn_invstd[ch];
+        ww = a.bn_w ? a.bn_w[ch] : 1.0f;
+        al = is * ww;
+        be = (a.bn_b ? a.bn_b[ch] : 0.0f) - mu * al;
+    }
     float pa = 1.f, pb = 0.f;
     if constexpr (PRO) {
         pa = a.in_alpha[ch];
@@ -1161,7 +1168,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         for (int r = 0; r < 2; ++r) {
             const int off = ldoff + r * kRow * 4;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
+            for (int k = kFwd ? 2 : 0; k < 3; ++k) {
                 const __amdgpu_buffer_rsrc_t rs = k == 0 ? rg : (k == 1 ? ry : rx);
                 float(&d)[5] = k == 0 ? G[r] : (k == 1 ? Y[r] : X[r]);
                 const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
@@ -1197,6 +1204,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                     const float u = xv * pa + pb;
                     xv = u < 0.f ? 0.f : u;
                 }
+                if constexpr (kFwd) d = xv;   // the forward's A operand: x' in the input-gradient waves' image
                 uint32_t h, m, l, xh, xm, xl;
                 if constexpr (kVariant & 1) {
                     h = __float_as_uint(G[r][i]) >> 16; m = h; l = h;
@@ -1222,7 +1230,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
 #pragma unroll
             for (int part = 0; part < 3; ++part) {
                 *reinterpret_cast<uint32_t *>(dyi + part * kPartBytes + o) = dp[part][i];
-                *reinterpret_cast<uint32_t *>(xi + part * kPartBytes + o) = xp[part][i];
+                if constexpr (!kFwd) *reinterpret_cast<uint32_t *>(xi + part * kPartBytes + o) = xp[part][i];
             }
         }
         if constexpr (EPI == 2 || EPI == 3) {   // the epilogue's raw x (rows past the batch are loaded as 0)
@@ -1241,6 +1249,8 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
 #pragma unroll
                 for (int s = 0; s < kNq; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
             }
+        } else if constexpr (!kIg && kFwd) {
+            // the forward has no weight gradient: these waves only stage
         } else if constexpr (!kIg) {
             // weight gradient: dW[tap] += x'_p^T (32 ci x 16 rows) . dY_q (16 rows x 32 co), p ascending
             const unsigned char *xi = smem + kX0 + (it & 1) * kImgBytes;
@@ -1329,6 +1339,21 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                     for (int s = 0; s < R::kNq; ++s) rv[s][rr] = xr[row * kXrStride + co * kCells + R::kQ[s]];
                 }
             }
+            if constexpr (EPI == 1) {   // the output's BN statistics (conv3x3_kernel<PRO, 1>'s sums)
+                float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+                for (int s = 0; s < R::kNq; ++s) {
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int row = (lane >> 4) * 4 + rr;
+                        const float u = row < rows ? acc[s][rr] : 0.f;
+                        t1 += u;
+                        t2 += u * u;
+                    }
+                }
+                s1 += (double)t1;
+                s2 += (double)t2;
+            }
             if constexpr (EPI == 2) {   // bn_bwd_reduce_kernel's mask and sums
                 float t1 = 0.f, t2 = 0.f;
 #pragma unroll
@@ -1406,7 +1431,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
     }
     // weight-gradient partials partial[block][tap][ci][co] (C/D layout of 32x32x16: col = co = lane & 31,
     // row = ci = (i&3) + 8(i>>2) + 4h); each tap has one owner wave: no fold inside the workgroup
-    if constexpr (!kIg) {
+    if constexpr (!kIg && !kFwd) {
         constexpr int kW = kTaps * kC * kC;
         float *outp = a.wpart + (int64_t)blockIdx.x * kW;
         const int h = lane >> 5;
@@ -1418,7 +1443,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                 outp[(R::kTap[s] * kC + ci) * kC + ch] = wacc[s][i];
             }
     }
-    if constexpr (EPI == 2) {   // BN_{i-1}'s sums: waves 0-3 [wave][lane] -> channel (wave&1)*16 + (lane&15)
+    if constexpr (EPI == 1 || EPI == 2) {   // the sums: waves 0-3 [wave][lane] -> channel (wave&1)*16 + (lane&15)
         __syncthreads();
         double *dred = reinterpret_cast<double *>(smem);
         if (kIg) {
@@ -1516,6 +1541,9 @@ int g_split = 1;
 // Chain block backward with an input gradient: 1 = tile-shared conv3x3_block_bwd2_kernel (default),
 // 0 = the per-wave conv3x3_block_bwd_kernel.
 int g_block_form = 1;
+// The chain's forward conv (epilogue 1, packed weights, no bias): 1 = the tile-shared form (bb2, EPI 1),
+// 0 = conv3x3_kernel<PRO, 1>.
+int g_fwd_form = 0;
 
 // One 4-wave workgroup per CU (LDS: 109 KB forward, 145 KB weight gradient);
 // the waves walk row tiles grid-stride so the next tile's loads overlap MFMAs.
@@ -1555,6 +1583,12 @@ int hrl_conv3x3_set_block_form(int form) {
     return prev;
 }
 
+int hrl_conv3x3_set_fwd_form(int form) {
+    const int prev = g_fwd_form;
+    g_fwd_form = form ? 1 : 0;
+    return prev;
+}
+
 int hrl_conv3x3_set_split(int on) {
     const int prev = g_split;
     g_split = on ? 1 : 0;
@@ -1581,6 +1615,14 @@ int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, con
         const int rc = status();
         if (rc) return rc;
         wpk = dst;
+    }
+    if (epilogue == 1 && (flip & 2) && !bias && g_split && g_fwd_form == 1 && M * kRow * 4 <= 0xffffffffLL) {
+        // the chain's forward in the block backward's tile-shared form (bb2, EPI 1)
+        BlockBwdArgs a{};
+        a.x = x; a.in_alpha = in_alpha; a.in_beta = in_beta; a.wpk = wpk; a.gin = y; a.part = part; a.M = M;
+        if (in_alpha) hipLaunchKernelGGL((conv3x3_block_bwd2_kernel<true, 1>), dim3(grid_for(M)), dim3(bb2::kThreads), 0, s, a);
+        else hipLaunchKernelGGL((conv3x3_block_bwd2_kernel<false, 1>), dim3(grid_for(M)), dim3(bb2::kThreads), 0, s, a);
+        return status();
     }
     const dim3 grid(grid_for(M)), block(kThreads);
 #define HRL_CONV_LAUNCH(PRO, EPI)                                                                             \

@@ -173,6 +173,10 @@ int hrl_conv3x3_set_split(int on);
  * gradient and the epilogue are the same in both; the weight gradient sums the tiles in a different
  * association.  Process-wide; returns the previous setting. */
 int hrl_conv3x3_set_block_form(int form);
+/* The chain's forward conv with BN statistics (hrl_conv3x3_forward_ex, epilogue 1, packed weights, no bias):
+ * 1 = the block backward's tile-shared form, 0 (default until measured faster) = the per-wave conv3x3_kernel.
+ * Returns the previous. */
+int hrl_conv3x3_set_fwd_form(int form);
 /* Both packed layouts of n <= 8 weights (32, 32, 3, 3) in one launch: packed[(l*2 + f) * 9216], f = 0 forward,
  * 1 input gradient (host array of device pointers).  hrl_conv3x3_forward_ex with flip | 2 takes `weight`
  * as such a packed layout and skips its own packing launch. */

@@ -459,3 +459,48 @@ def test_block_backward_weight_gradient_exact_on_integer_data(cuda, M, pro):
     assert torch.equal(dw.double().cpu(), ref)
     gref = torch.nn.grad.conv2d_input(xin.shape, w.double().cpu(), dy, padding=1)
     assert torch.equal(gin.double().cpu(), gref.reshape(M, 288))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('M', [37, 20000])
+@pytest.mark.parametrize('pro', [False, True])
+def test_tile_shared_forward_matches_per_wave_conv(cuda, M, pro):
+    """The chain's forward conv with BN statistics (hrl_conv3x3_forward_ex, epilogue 1) in the tile-shared form
+    (the block backward kernel with x' staged in place of dY, default) vs the per-wave conv3x3_kernel: the output
+    is bit-identical (the same split MFMA order on the same x'), the per-channel sums sum(y) and sum(y^2) agree
+    with the fp64 sums to fp32 rounding of a different per-tile grouping.  Ragged M = 37 (rows past the batch
+    contribute nothing) and M = 20000 (several tiles per workgroup); with and without the BN + ReLU prologue."""
+    from handyrl_amd import _native
+    lib = _native.load()
+    P = _native.ptr
+    stream = _native.stream_of(cuda)
+    g0 = torch.Generator(device=cuda).manual_seed(M + 11)
+    rnd = lambda *s: torch.randn(*s, device=cuda, generator=g0)   # noqa: E731
+    x = rnd(M, 288)
+    w = rnd(32, 32, 3, 3) * 0.1
+    alpha, bet = (rnd(32).abs() + 0.5, rnd(32) * 0.3) if pro else (None, None)
+    packed = torch.empty(1, 2, 9216, device=cuda)
+    _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array([w]), 1, P(packed), stream), 'pack')
+    ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+    nblk = lib.hrl_conv3x3_stats_blocks(M)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+    outs = []
+    for form in (0, 1):
+        prev = lib.hrl_conv3x3_set_fwd_form(form)
+        y, part = torch.empty_like(x), torch.full((nblk * 64,), float('nan'), dtype=torch.float64, device=cuda)
+        try:
+            _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(alpha), P(bet), P(packed[0, 0]), None, 2, P(y), 1,
+                                                     None, None, None, None, P(part), P(ws), ws_bytes, stream), 'fwd')
+            torch.cuda.synchronize(cuda)
+        finally:
+            lib.hrl_conv3x3_set_fwd_form(prev)
+        outs.append((y, part))
+    (y0, p0), (y1, p1) = outs
+    assert torch.equal(y1, y0)
+    yd = y0.double().view(M, 32, 9)
+    ref = torch.stack([yd.sum((0, 2)), (yd * yd).sum((0, 2))], 1)
+    scale = torch.stack([yd.abs().sum((0, 2)), (yd * yd).sum((0, 2))], 1)
+    for p in (p0, p1):
+        s = p.view(nblk, 32, 2).sum(0)
+        assert bool(torch.isfinite(s).all())
+        assert float(((s - ref).abs() / scale).max()) < 1e-6
