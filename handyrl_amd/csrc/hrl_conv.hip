@@ -1543,7 +1543,7 @@ int g_split = 1;
 int g_block_form = 1;
 // The chain's forward conv (epilogue 1, packed weights, no bias): 1 = the tile-shared form (bb2, EPI 1),
 // 0 = conv3x3_kernel<PRO, 1>.
-int g_fwd_form = 0;
+int g_fwd_form = 1;
 
 // One 4-wave workgroup per CU (LDS: 109 KB forward, 145 KB weight gradient);
 // the waves walk row tiles grid-stride so the next tile's loads overlap MFMAs.
