@@ -373,10 +373,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
 
 // W (Cout, w_cin_total, 3, 3), input channels [w_ci0, w_ci0 + cin_g) -> split fragments [ct][kc][tap][part][64]
 // x 4 words: lane l of (ct, kc) holds W^T[ci = 32kc + 8(l>>4) + e][co = 16ct + (l&15)], e = 2d, 2d+1 in word d
-// flip: the adjoint (input-gradient) conv of W's input slice, W'[co'][ci'][tap] = W[ci'][w_ci0 + co'][8 - tap]
-// (cout = the slice width, cin_g = W's output channels)
 __global__ void gboard_pack_kernel(const float *__restrict__ w, int cout, int cin_g, int w_cin_total, int w_ci0,
-                                   int KC, int total, int flip, uint32_t *__restrict__ out) {
+                                   int KC, int total, uint32_t *__restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
     const int d = i & 3, l = (i >> 2) & 63;
@@ -389,9 +387,7 @@ __global__ void gboard_pack_kernel(const float *__restrict__ w, int cout, int ci
     const int co = 16 * ct + (l & 15);
     const int ci = 32 * kc + 8 * (l >> 4) + 2 * d;
     auto wv = [&](int c) -> float {
-        if (!(co < cout && c < cin_g)) return 0.f;
-        return flip ? w[((int64_t)c * w_cin_total + w_ci0 + co) * kTaps + (kTaps - 1 - tap)]
-                    : w[((int64_t)co * w_cin_total + w_ci0 + c) * kTaps + tap];
+        return (co < cout && c < cin_g) ? w[((int64_t)co * w_cin_total + w_ci0 + c) * kTaps + tap] : 0.f;
     };
     out[i] = hrl_split::split_part(wv(ci), part) | (hrl_split::split_part(wv(ci + 1), part) << 16);
 }
@@ -453,11 +449,8 @@ bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 
 extern "C" {
 
-// k-steps of 32 input channels: 1, 2 or 4 (Cin_g <= 64 or 97..128)
-bool kc_ok(int64_t Cin_g) { return Cin_g >= 1 && (Cin_g <= 64 || (Cin_g > 96 && Cin_g <= 128)); }
-
 int64_t hrl_gboard_pack_bytes(int64_t Cout, int64_t Cin_g) {
-    if (Cout < 1 || !kc_ok(Cin_g)) return -1;
+    if (Cout < 1 || Cin_g < 1 || Cin_g > 64) return -1;
     return ((Cout + 15) / 16) * ((Cin_g + 31) / 32) * kTaps * 3 * 64 * 16;
 }
 
@@ -469,21 +462,7 @@ int hrl_gboard_pack(const float *weight, int64_t Cout, int64_t Cin_g, int64_t w_
     const int KC = (int)((Cin_g + 31) / 32);
     const int total = (int)(need / 4);
     hipLaunchKernelGGL(gboard_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
-                       weight, (int)Cout, (int)Cin_g, (int)w_cin_total, (int)w_ci0, KC, total, 0,
-                       static_cast<uint32_t *>(packed));
-    return status();
-}
-
-int hrl_gboard_pack_adjoint(const float *weight, int64_t Cout_fwd, int64_t w_cin_total, int64_t w_ci0,
-                            int64_t Cin_slice, void *packed, int64_t packed_bytes, void *stream) {
-    const int64_t need = hrl_gboard_pack_bytes(Cin_slice, Cout_fwd);
-    if (!weight || !packed || need < 0 || packed_bytes < need || w_ci0 < 0 || Cin_slice < 1 ||
-        w_ci0 + Cin_slice > w_cin_total)
-        return HRL_EINVAL;
-    const int KC = (int)((Cout_fwd + 31) / 32);
-    const int total = (int)(need / 4);
-    hipLaunchKernelGGL(gboard_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
-                       weight, (int)Cin_slice, (int)Cout_fwd, (int)w_cin_total, (int)w_ci0, KC, total, 1,
+                       weight, (int)Cout, (int)Cin_g, (int)w_cin_total, (int)w_ci0, KC, total,
                        static_cast<uint32_t *>(packed));
     return status();
 }
@@ -491,11 +470,11 @@ int hrl_gboard_pack_adjoint(const float *weight, int64_t Cout_fwd, int64_t w_cin
 int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_t x2_stride, int64_t N, int64_t Cin_g,
                        int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
                        const float *beta, int relu, float *y, int64_t y_stride, void *stream) {
-    if (!x || !packed || !y || N < 1 || !kc_ok(Cin_g) || groups < 1 || Cout < 1 || Cout % groups)
+    if (!x || !packed || !y || N < 1 || Cin_g < 1 || Cin_g > 64 || groups < 1 || Cout < 1 || Cout % groups)
         return HRL_EINVAL;
     const int64_t cout_g = Cout / groups;
     if (groups > 1 && cout_g % 16) return HRL_EINVAL;        // a column tile never straddles two groups
-    if (x2 && (Cin_g <= 32 || Cin_g > 64 || groups != 1)) return HRL_EINVAL;
+    if (x2 && (Cin_g <= 32 || groups != 1)) return HRL_EINVAL;
     if ((alpha == nullptr) != (beta == nullptr)) return HRL_EINVAL;
     if (!aligned16(x) || (x2 && !aligned16(x2)) || !aligned16(y) || x_stride % 4 || x2_stride % 4 || y_stride % 4)
         return HRL_EINVAL;
@@ -533,10 +512,8 @@ int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_
     } while (0)
     if (KC == 1) {
         if (padc) HRL_GB_LAUNCH(1, true); else HRL_GB_LAUNCH(1, false);
-    } else if (KC == 2) {
-        if (padc) HRL_GB_LAUNCH(2, true); else HRL_GB_LAUNCH(2, false);
     } else {
-        if (padc) HRL_GB_LAUNCH(4, true); else HRL_GB_LAUNCH(4, false);
+        if (padc) HRL_GB_LAUNCH(2, true); else HRL_GB_LAUNCH(2, false);
     }
 #undef HRL_GB_LAUNCH
     return status();

@@ -243,25 +243,6 @@ def gboard_pack(w, cin_g=None, ci0=0, out=None):
     return wpk
 
 
-# the deferred convs' input gradient on hrl_gboard (the adjoint conv, K up to 4 x 32) instead of
-# aten.convolution_backward; off until measured on the GPU
-GBOARD_ADJOINT = False
-
-
-def gboard_pack_adjoint(w, ci0, cin):
-    """The input-gradient conv of input channels [ci0, ci0 + cin) of the 3x3 weight w (Cout, Cin_total, 3, 3),
-    packed for gboard_conv (cin outputs from Cout inputs)."""
-    lib = _native.load()
-    nbytes = lib.hrl_gboard_pack_bytes(cin, w.shape[0])
-    if nbytes < 0:
-        raise ValueError('hrl_gboard_pack_adjoint: unsupported weight %s' % (tuple(w.shape),))
-    wpk = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
-    _native.check(lib.hrl_gboard_pack_adjoint(_native.ptr(w.contiguous()), w.shape[0], w.shape[1], ci0, cin,
-                                              _native.ptr(wpk), nbytes, _native.stream_of(w.device)),
-                  'hrl_gboard_pack_adjoint')
-    return wpk
-
-
 def gboard_conv(x, packed, Cout, cin_g, groups=1, x2=None, bias=None, alpha=None, beta=None, relu=False, out=None):
     """F.conv2d(x, W, bias, padding=1, groups=groups) on the 6x6 board (csrc/hrl_gboard.hip, forward only, no
     autograd), W packed by gboard_pack; optional BatchNorm-apply (y*alpha + beta) and ReLU epilogue.  x may be
@@ -338,14 +319,8 @@ class _DeferredConv(torch.autograd.Function):
         wv = w if sl is None else w[:, sl[0]:sl[1]]
         dx = None
         if ctx.needs_input_grad[0]:
-            Cf = w.shape[0]
-            if (GBOARD_ADJOINT and tuple(pad) == (1, 1) and tuple(w.shape[2:]) == (3, 3) and gboard_ok(dy)
-                    and (Cf <= 64 or 96 < Cf <= 128) and wv.shape[1] == x.shape[1]):
-                ci0 = 0 if sl is None else sl[0]
-                dx = gboard_conv(dy, gboard_pack_adjoint(w.detach(), ci0, wv.shape[1]), wv.shape[1], Cf)
-            else:
-                dx = torch.ops.aten.convolution_backward(dy, x, wv, None, [1, 1], list(pad), [1, 1], False, [0, 0],
-                                                         1, [True, False, False])[0]
+            dx = torch.ops.aten.convolution_backward(dy, x, wv, None, [1, 1], list(pad), [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
         rec.add_conv((w, b, sl, tuple(pad)), x, dy)
         return dx, None, None, None, None, None, None
 

@@ -323,12 +323,6 @@ int hrl_board_conv_forward_packed(const float *x, int64_t N, int64_t Cin, int64_
 int64_t hrl_gboard_pack_bytes(int64_t Cout, int64_t Cin_g);
 int hrl_gboard_pack(const float *weight, int64_t Cout, int64_t Cin_g, int64_t w_cin_total, int64_t w_ci0,
                     void *packed, int64_t packed_bytes, void *stream);
-/* hrl_gboard_pack_adjoint: the input-gradient conv of input channels [w_ci0, w_ci0 + Cin_slice) of weight
- * (Cout_fwd, w_cin_total, 3, 3) -- W'[co'][ci'][tap] = W[ci'][w_ci0 + co'][8 - tap], Cin_slice outputs from Cout_fwd
- * inputs -- packed for hrl_gboard_forward (packed: hrl_gboard_pack_bytes(Cin_slice, Cout_fwd) bytes).
- * Cin_g (input channels per group) may be <= 64 or 97..128 (1, 2 or 4 k-steps of 32). */
-int hrl_gboard_pack_adjoint(const float *weight, int64_t Cout_fwd, int64_t w_cin_total, int64_t w_ci0,
-                            int64_t Cin_slice, void *packed, int64_t packed_bytes, void *stream);
 int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_t x2_stride, int64_t N, int64_t Cin_g,
                        int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
                        const float *beta, int relu, float *y, int64_t y_stride, void *stream);

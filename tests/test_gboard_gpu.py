@@ -147,20 +147,3 @@ def test_gboard_pointwise_matches_conv1x1(cuda, O, C1, C2):
                              alpha=al.to(cuda), beta=be.to(cuda), relu=True).cpu().double()
     ref = (ref * al.double()[None, :, None, None] + be.double()[None, :, None, None]).clamp_min(0)
     assert _close(y, ref)
-
-
-@pytest.mark.parametrize('N,cout_fwd,ci0,cin', [(37, 128, 32, 32), (64, 128, 0, 32), (20, 32, 0, 25), (33, 8, 0, 64)])
-def test_gboard_adjoint_matches_conv_input_gradient(cuda, N, cout_fwd, ci0, cin):
-    """hrl_gboard_pack_adjoint + hrl_gboard_forward == the input gradient of F.conv2d(x, w[:, ci0:ci0+cin], padding=1)
-    (fp64 reference): the ConvLSTM cells' h-half input gradient (128 -> 32, four k-steps), a stem-like ragged slice
-    and the move head's 8 -> 64."""
-    g = torch.Generator().manual_seed(N + cout_fwd + ci0)
-    w = torch.randn(cout_fwd, ci0 + cin + 3, 3, 3, generator=g) * 0.2
-    dy = torch.randn(N, cout_fwd, 6, 6, generator=g)
-    wv = w[:, ci0:ci0 + cin].double()
-    x = torch.zeros(N, cin, 6, 6, dtype=torch.float64, requires_grad=True)
-    F.conv2d(x, wv, padding=1).backward(dy.double())
-    ref = x.grad
-    pk = hnn.gboard_pack_adjoint(w.to(cuda), ci0, cin)
-    y = hnn.gboard_conv(dy.to(cuda), pk, cin, cout_fwd).cpu().double()
-    assert _close(y, ref)
