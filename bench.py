@@ -46,6 +46,7 @@ from handyrl_amd.synthetic import tictactoe_batch, default_args  # noqa: E402
 from handyrl_amd.trainer import LearnerStep            # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SCAN_PMC = 'r03s4_scan_pmc.json'   # PMC passes over the scan kernel the tree ships
 
 
 def scan_bytes_per_launch(B, T, P=2, Pp=1, rewards=False):
@@ -111,51 +112,66 @@ MFMA_BF16_PEAK_TFLOPS = 16 * MFMA_F32_PEAK_TFLOPS   # dense bf16 MFMA: 16x the f
 SPLIT_PRODUCTS = 6   # exact three-way bf16 split of both operands: hh, hm, mh, hl, lh, mm
 
 
-def time_conv(device, M, iters=20):
-    """The step's dominant net kernel: the 32->32 3x3-board MFMA conv (csrc/hrl_conv.hip) at M = B*T rows.
+FWD_KERNEL = {1: 'conv3x3_block_bwd2_kernel<true,1> (the tile-shared form)',
+              2: 'conv3x3_fwd_dma_kernel<true> (the LDS-DMA ring form)'}
 
-    Algorithmic FLOPs per launch: 49 on-board 32x32 tap blocks x 2 per sample
-    (the 32 off-board blocks of the dense 9x9 board matrix are not work).
-    Timed with HIP events on the launch stream over `iters` back-to-back launches.
+
+def time_conv(device, M, iters=20):
+    """The chain's forward conv as the step runs it (hrl_conv3x3_forward_ex: epilogue 1 = the output's BN
+    statistics, packed weights, the previous block's BN + ReLU as prologue; csrc/hrl_conv.hip) at M = B*T rows,
+    HIP events on the launch stream over `iters` back-to-back launches.
+
+    Algorithmic bytes per launch: x read + y written (151 MB each at M = 131,072); FLOPs: 49 on-board 32x32 tap
+    blocks x 2 per sample (the 32 off-board blocks of the dense 9x9 board matrix are not work).
     """
     from handyrl_amd import _native
     lib = _native.load()
+    form = lib.hrl_conv3x3_set_fwd_form(1)
+    lib.hrl_conv3x3_set_fwd_form(form)
     g = torch.Generator(device=device).manual_seed(3)
     x = torch.randn(M, 288, device=device, generator=g)
     w = torch.randn(32, 32, 3, 3, device=device, generator=g) * 0.1
-    b = torch.randn(32, device=device, generator=g)
+    alpha = torch.rand(32, device=device, generator=g) + 0.5
+    beta = torch.randn(32, device=device, generator=g) * 0.3
     y = torch.empty_like(x)
+    P = _native.ptr
+    stream = _native.stream_of(device)
+    packed = torch.empty(1, 2, 9216, device=device)
+    _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array([w]), 1, P(packed), stream), 'pack')
     ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
-    stream = torch.cuda.current_stream(device)
-    P = _native.ptr
+    part = torch.empty(lib.hrl_conv3x3_stats_blocks(M) * 64, dtype=torch.float64, device=device)
+    tstream = torch.cuda.current_stream(device)
 
     def launch():
-        _native.check(lib.hrl_conv3x3_forward(P(x), M, 32, 32, P(w), P(b), 0, P(y), P(ws), ws_bytes,
-                                              _native.stream_of(device)), 'hrl_conv3x3_forward')
+        _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(alpha), P(beta), P(packed[0, 0]), None, 2, P(y), 1,
+                                                 None, None, None, None, P(part), P(ws), ws_bytes, stream),
+                      'hrl_conv3x3_forward_ex')
     for _ in range(3):
         launch()
     start = torch.cuda.Event(enable_timing=True)
     end = torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(device)
-    start.record(stream)
+    start.record(tstream)
     for _ in range(iters):
         launch()
-    end.record(stream)
+    end.record(tstream)
     end.synchronize()
     us = start.elapsed_time(end) * 1e3 / iters
+    nbytes = 2 * M * 288 * 4
+    gbs = nbytes / (us * 1e-6) / 1e9
     flops = 2.0 * M * 49 * 32 * 32
     tf = flops / (us * 1e-6) / 1e12
-    # The kernel runs each fp32 product as six bf16 MFMA partial products (csrc/hrl_conv.hip, split path),
-    # so its MFMA ceiling for fp32-accurate work is the bf16 dense peak / 6.
+    # each fp32 product runs as six bf16 MFMA partial products (the exact split), so the MFMA ceiling for
+    # fp32-accurate work is the bf16 dense peak / 6
     peak = MFMA_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
-    return {'kernel': 'conv3x3_kernel<false,0,split> (+ 2 us weight pack)', 'bound': 'mfma', 'achieved': round(tf, 1),
-            'peak': round(peak, 1), 'unit': 'TFLOP/s', 'frac': round(tf / peak, 4),
-            'flops_per_launch': flops, 'us_per_launch': round(us, 2), 'M': M,
-            'vs_fp32_mfma_peak': round(tf / MFMA_F32_PEAK_TFLOPS, 4),
-            'launches_per_step': '3 forward + 3 input-gradient (same kernel) + 3 weight-gradient',
-            'note': 'achieved = algorithmic fp32 FLOPs / time; peak = bf16 dense MFMA peak / 6 partial products of the '
-                    'exact bf16 split (fp32-accurate); SURVEY D3: reported beside, not instead of, the scan roofline'}
+    return {'kernel': FWD_KERNEL.get(form, 'form %d' % form), 'fwd_form': form, 'bound': 'hbm',
+            'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4),
+            'bytes_per_launch': nbytes, 'us_per_launch': round(us, 2), 'M': M,
+            'mfma_achieved_TFLOPs': round(tf, 1), 'mfma_frac_split': round(tf / peak, 4),
+            'launches_per_step': 3,
+            'note': 'the step\'s chain forward (BN statistics epilogue, BN + ReLU prologue) on random data; bytes = x '
+                    'read + y written; split ceiling = bf16 dense peak / 6 partial products'}
 
 
 def loss_bytes_per_launch(B, T, P=2, Pp=1, A=9):
@@ -294,7 +310,7 @@ def block_traffic():
 
 def pmc_traffic(B, T):
     """HBM bytes per launch of the scan from the committed rocprofv3 PMC passes (profiles/), or None."""
-    path = os.path.join(ROOT, 'profiles', 'r01_scan_pmc.json')
+    path = os.path.join(ROOT, 'profiles', SCAN_PMC)
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -304,14 +320,23 @@ def pmc_traffic(B, T):
     return None
 
 
-def cpu_baseline(B=4096, T=32, steps=3):
-    """The CPU learner oracle on this host, 1 thread (train.py as shipped: model.py:8), at the metric's
-    B=4096 T=32 (about 4 s per step on the GPU box's host cores).  Calibrated against the reference
-    itself in the build container by tools/calibrate_cpu.py (profiles/r02_cpu_calibration.json: the
-    port runs at 0.91-1.07x the reference's time)."""
+def cpu_model():
+    """The host CPU's model name (lscpu's 'Model name', read from /proc/cpuinfo), or None."""
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_learner_rate(B, T, steps, threads):
+    """env-steps/s and seconds of the CPU learner oracle on `threads` torch threads."""
     from oracle.learner import CpuLearner
-    threads = torch.get_num_threads()
-    torch.set_num_threads(1)
+    saved = torch.get_num_threads()
+    torch.set_num_threads(threads)
     try:
         torch.manual_seed(0)
         net = SimpleConv2dModel()
@@ -324,11 +349,27 @@ def cpu_baseline(B=4096, T=32, steps=3):
             learner.step(batch)
         dt = time.perf_counter() - t0
     finally:
-        torch.set_num_threads(threads)
-    return {'value': B * T * steps / dt, 'unit': 'env-steps/s', 'cores': 1, 'kind': 'port',
+        torch.set_num_threads(saved)
+    return B * T * steps / dt, dt
+
+
+def cpu_baseline(B=4096, T=32, steps=3, threads_secondary=8):
+    """The CPU learner oracle on this host, 1 thread (train.py as shipped: model.py:8), at the metric's
+    B=4096 T=32 (about 4 s per step on the GPU box's host cores), and the 8-thread variant as the
+    secondary.  Calibrated against the reference itself in the build container by
+    tools/calibrate_cpu.py (profiles/r02_cpu_calibration.json: the port runs at 0.91-1.07x the
+    reference's time)."""
+    v1, dt1 = cpu_learner_rate(B, T, steps, 1)
+    v8, dt8 = cpu_learner_rate(B, T, steps, threads_secondary)
+    return {'value': v1, 'unit': 'env-steps/s', 'cores': 1, 'kind': 'port',
             'sample': 'oracle.learner.CpuLearner (restates train.py:218-258,382-385), TicTacToe net, '
                       'synthetic B=%d T=%d, %d timed steps after 1 warm-up, torch 1 thread, %.1f s'
-                      % (B, T, steps, dt)}
+                      % (B, T, steps, dt1),
+            'secondary_threads': {'value': v8, 'unit': 'env-steps/s', 'cores': threads_secondary,
+                                  'seconds': round(dt8, 2),
+                                  'note': 'the same sample on %d torch threads (the reference ships 1 thread, '
+                                          'model.py:8)' % threads_secondary},
+            'host': {'cpu_model': cpu_model(), 'os_cpu_count': os.cpu_count()}}
 
 
 def secondary_t9(device, steps=10, warmup=3, B=4096, T=9):
@@ -502,7 +543,8 @@ def main():
     if world != opts.gpus:
         if world == 1 and opts.gpus > 1:
             raise SystemExit('--gpus %d needs torch.distributed.run with %d processes' % (opts.gpus, opts.gpus))
-    device = torch.device('cuda', local)
+    # ranks beyond the visible GPUs share them (HRL_DIST_BACKEND=gloo rehearsal on a one-GPU box)
+    device = torch.device('cuda', local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(device)
     hdist.init_process_group('cuda')
 
@@ -536,6 +578,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     stats, nb = learner.pop_stats()
+    # the roofline line is the step's dominant kernel, timed inside eager learner steps.  With N > 1 those
+    # steps all-reduce their gradient buckets, so EVERY rank runs them (the collectives pair up); rank 0
+    # reports its own timings.
+    us_blk, n_blk = time_block_in_step(learner, batch, device)
+    if world > 1:
+        dist.barrier()
 
     if rank == 0:
         steps_total = world * B * T * opts.steps
@@ -550,7 +598,7 @@ def main():
             'unit': 'GB/s',
             'frac': round(hot['GBps'] / HBM_PEAK_GBS, 4),
             'traffic': pmc_traffic(B, T),
-            'traffic_source': 'profiles/r01_scan_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected)',
+            'traffic_source': 'profiles/%s (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected)' % SCAN_PMC,
             'bytes_per_launch': hot['bytes_per_launch'],
             'us_per_launch': round(hot['us_per_launch'], 3),
             'cold_large_B': {'B': cold['B'], 'T': T, 'achieved': round(cold['GBps'], 1),
@@ -562,7 +610,6 @@ def main():
         loss_roof = time_loss(device, B, T)
         block_roof = time_block_backward(device, B * T)
         # the roofline line is the step's dominant kernel: the chain block backward (3 launches, ~40% of the step)
-        us_blk, n_blk = time_block_in_step(learner, batch, device)
         blk_bytes = block_roof['bytes_per_launch']
         blk_gbs = blk_bytes / (us_blk * 1e-6) / 1e9
         blk_tf = block_roof['flops_per_launch'] / (us_blk * 1e-6) / 1e12

@@ -43,8 +43,11 @@ def init_process_group(device_type):
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         os.environ.setdefault('MASTER_PORT', '29533')
         backend = 'nccl' if device_type == 'cuda' else 'gloo'
+        # HRL_DIST_BACKEND=gloo: several ranks on ONE GPU (RCCL refuses two ranks on one device), the
+        # one-GPU box's rehearsal of the multi-rank bench; gloo all-reduces device tensors via the host
+        backend = os.environ.get('HRL_DIST_BACKEND', backend)
         kwargs = {}
-        if device_type == 'cuda':
+        if device_type == 'cuda' and backend == 'nccl':
             kwargs['device_id'] = torch.device('cuda', local)
         dist.init_process_group(backend, rank=rank, world_size=world, **kwargs)
     return rank, world, local

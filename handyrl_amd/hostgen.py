@@ -39,6 +39,7 @@ and uniform window start (train.py:284-293).
 """
 
 import bz2
+import contextlib
 import pickle
 import random
 
@@ -368,7 +369,12 @@ class HostBatchGenerator:
         saved = random.getstate() if self.sampler == 'reference' else None
         self.games_started, self.failed = 0, 0
         out = {}
+        # a net with per-call inference preparation (GeisterNet: stacked DRC weights, packed conv fragments,
+        # BatchNorm coefficients) prepares once for the whole call instead of once per forward
+        session = getattr(self.net, 'inference_session', None)
+        ctx = session() if session is not None and self.device.type == 'cuda' else contextlib.nullcontext()
         try:
+            ctx.__enter__()
             for s in range(self.E):
                 self._start(s, n)
             for g in self.groups:
@@ -380,6 +386,7 @@ class HostBatchGenerator:
                     self._advance(g, n, out)
                     self._launch(g)
         finally:
+            ctx.__exit__(None, None, None)
             if saved is not None:
                 random.setstate(saved)
             self.net.train(was_training)
@@ -497,7 +504,13 @@ class MomentReplay:
                     if m['action'][p] is not None:
                         act[row, j] = m['action'][p]
                     if m['value'][p] is not None:
-                        val[row, j] = np.asarray(m['value'][p], dtype=np.float32).reshape(-1)[0]
+                        v = np.asarray(m['value'][p], dtype=np.float32).reshape(-1)
+                        if v.size != 1:
+                            # make_batch pads values with the (P, 1) outcome (train.py:94-96), so the reference
+                            # learner takes one value per player; a wider head would be silently truncated here
+                            raise ValueError('MomentReplay: a moment value has %d elements; the learner takes one '
+                                             'value per player' % v.size)
+                        val[row, j] = v[0]
                         omask[row, j] = 1
                     if m['reward'][p] is not None:
                         rew[row, j] = m['reward'][p]

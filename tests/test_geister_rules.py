@@ -138,7 +138,8 @@ def test_gpu_selfplay_2048_games_matches_per_game_loop(cuda):
     """BASELINE.json configs[2]: 2,048 concurrent games in one generate call (HIP graph per ply); three of
     them, first, middle and last, replayed through the reference's per-game loop on the CPU with the same
     weights: every recorded value, every legal policy logit (tolerance 1e-5 absolute + 1e-5 relative: the
-    GPU convolutions run MIOpen's fp32 kernels) and the same recurrent-state plumbing."""
+    GPU convolutions run hrl_gboard's exact-split bf16 MFMA kernels, fp32-accurate but summed in another
+    order than the CPU's) and the same recurrent-state plumbing."""
     from handyrl_amd.nn import accelerate
     from handyrl_amd.rollout import DeviceGenerator
     from handyrl_amd.envs.geister import GeisterNet
