@@ -289,13 +289,19 @@ def time_block_in_step(learner, batch, device, steps=4):
     kernels the graph replays, on the step's own data), after the timed region."""
     from handyrl_amd import nn as hnn
     hnn.BLOCK_TIMING = []
-    try:
+    reducer = learner.reducer
+    if reducer is not None:
+        reducer.enabled = False     # no gradient all-reduce in these steps: nothing to pair across ranks, and
+    try:                            # no collective between the timed launches on the stream
         for _ in range(steps):
             learner._body(batch, None)
         torch.cuda.synchronize(device)
         ts = [s.elapsed_time(e) * 1e3 for s, e in hnn.BLOCK_TIMING[3:]]   # the first eager step warms up
     finally:
         hnn.BLOCK_TIMING = None
+        if reducer is not None:
+            reducer.enabled = True
+            reducer.reset()
     return sum(ts) / max(len(ts), 1), len(ts)
 
 
@@ -495,6 +501,38 @@ def secondary_geese_learner(device, B=2048, T=64, steps=3, warmup=1):
             'vs_cpu_oracle': round(value / cpu_rate, 1)}
 
 
+def secondary_host_rollout(device, E=256):
+    """The host-env generator (hostgen.HostBatchGenerator: any plugin env through the Environment API, one batched
+    GPU forward per ply; generation.py:20-88) on ParallelTicTacToe (simultaneous turns) and Geister with
+    observation=True (every player observes, recurrent state per game and player), E = 256 game slots."""
+    from handyrl_amd.environment import make_env
+    from handyrl_amd.hostgen import HostBatchGenerator
+    from handyrl_amd.nn import accelerate
+    out = {}
+    for name, games, observation in (('ParallelTicTacToe', 2048, False), ('Geister', 256, True)):
+        env_args = {'env': name}
+        torch.manual_seed(0)
+        net = make_env(env_args).net()().to(device)
+        if name == 'Geister':
+            net = accelerate(net)
+        gen = HostBatchGenerator(lambda: make_env(env_args), net, {'observation': observation, 'gamma': 0.8}, E=E)
+        gen.generate(E)                      # warm-up
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        eps = gen.generate(games)
+        dt = time.perf_counter() - t0
+        steps = sum(e['steps'] for e in eps)
+        out[name] = {'value': round(steps / dt, 1), 'unit': 'env-steps/s', 'episodes': len(eps), 'plies': steps,
+                     'seconds': round(dt, 2), 'observation': observation,
+                     'time_split_s': {k: round(v, 3) for k, v in gen.timing.items()}}
+    out['E'] = E
+    out['reference_cpu_worker'] = {'TicTacToe': 1840.0, 'Geister': 349.0}
+    out['note'] = ('one host process; time_split: requests = env observations (the plugin\'s own code), launch = '
+                   'stacking + H2D + forward launch, wait = host blocked on a forward, advance = masks, sampling, '
+                   'env.step/reward and moment records')
+    return out
+
+
 def secondary_geister_rollout(device, E=2048, reps=2):
     """BASELINE.json configs[2]: Geister device self-play, E concurrent games, recurrent GeisterNet inference."""
     from handyrl_amd.envs.geister import GeisterNet, GeisterBatch
@@ -578,9 +616,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     stats, nb = learner.pop_stats()
-    # the roofline line is the step's dominant kernel, timed inside eager learner steps.  With N > 1 those
-    # steps all-reduce their gradient buckets, so EVERY rank runs them (the collectives pair up); rank 0
-    # reports its own timings.
+    # the roofline line is the step's dominant kernel, timed inside eager learner steps after the timed region,
+    # with the gradient all-reduce off (every rank runs them, so the ranks stay in step; rank 0 reports)
     us_blk, n_blk = time_block_in_step(learner, batch, device)
     if world > 1:
         dist.barrier()
@@ -638,6 +675,7 @@ def main():
         gro = secondary_geister_rollout(device) if (opts.secondary and world == 1) else None
         gle = secondary_geister_learner(device) if (opts.secondary and world == 1) else None
         gee = secondary_geese_learner(device) if (opts.secondary and world == 1) else None
+        hro = secondary_host_rollout(device) if (opts.secondary and world == 1) else None
         line = {
             'metric': 'learner env-steps/sec at B=4096 T=32 (TicTacToe net, UPGO/VTRACE)',
             'value': round(value, 1),
@@ -676,6 +714,8 @@ def main():
             line['geister_learner'] = gle
         if gee is not None:
             line['geese_learner'] = gee
+        if hro is not None:
+            line['host_rollout'] = hro
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

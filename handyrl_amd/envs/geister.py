@@ -785,15 +785,125 @@ class GeisterBatch:
         return torch.stack([w, -w], dim=1)
 
 
+class _OneGame:
+    """One game's state in plain Python for the host plugin env: GeisterBatch's rules (same state fields, same
+    operations) with E = 1 and no tensor ops.  A one-game GeisterBatch on the CPU paid ~150 torch launches per
+    ply (≈1.3 ms); this is ≈20-40 µs, so a host Environment steps about as fast as the reference's pure-Python
+    one (geister.py:359-394, 460-535).  tests/test_geister_rules.py replays the reference games through it."""
+
+    TGT = None          # TGT[d][cell]: target cell of absolute direction d, -1 off the board
+    GOAL = None         # GOAL[c][d][cell]: leaving the board that way is colour c's goal
+    LAYOUT = None       # LAYOUT[k][slot]: piece type (0 blue, 1 red) of layout k
+
+    @classmethod
+    def _tables(cls):
+        import itertools
+        if cls.TGT is not None:
+            return
+        tgt = [[-1] * 36 for _ in range(4)]
+        goal = [[[False] * 36 for _ in range(4)] for _ in range(2)]
+        for d, (dx, dy) in enumerate(GeisterBatch.DIRS):
+            for x in range(6):
+                for y in range(6):
+                    nx, ny = x + dx, y + dy
+                    if 0 <= nx < 6 and 0 <= ny < 6:
+                        tgt[d][x * 6 + y] = nx * 6 + ny
+                    else:
+                        for c in range(2):
+                            goal[c][d][x * 6 + y] = (nx, ny) in GeisterBatch.GOALS[c]
+        lay = []
+        for seq in itertools.combinations(range(8), 4):
+            lay.append([0 if i in seq else 1 for i in range(8)])
+        cls.TGT, cls.GOAL, cls.LAYOUT = tgt, goal, lay
+
+    def __init__(self, complete_info=False):
+        self._tables()
+        self.complete_info = complete_info
+        self.reset()
+
+    def reset(self):
+        self.board = [-1] * 36
+        self.color = 0
+        self.turn_count = -2
+        self.win = -1
+        self.cnt = [0, 0, 0, 0]
+
+    def move_legal(self, d, cell):
+        """Absolute move (direction d, cell) of the side to move: GeisterBatch.legal's per-move test."""
+        dst = self.TGT[d][cell]
+        if dst >= 0:
+            t = self.board[dst]
+            return t < 0 or t // 2 != self.color
+        return self.board[cell] % 2 == 0 and self.GOAL[self.color][d][cell]
+
+    def step(self, action):
+        """GeisterBatch.step for one active game."""
+        c = self.color
+        if self.turn_count < 0:                                  # a layout: the mover's 8 pieces
+            types = self.LAYOUT[action - GeisterBatch.MOVES]
+            for cell, t in zip(GeisterBatch.OPOS[c], types):
+                self.board[cell] = c * 2 + t
+            self.cnt[c * 2] += 4
+            self.cnt[c * 2 + 1] += 4
+        else:
+            a = GeisterBatch.MOVES - 1 - action if c == 1 else action
+            d, src = divmod(a, 36)
+            dst = self.TGT[d][src]
+            piece = self.board[src]
+            if dst < 0:                                          # leaves by the goal
+                self.cnt[piece] -= 1
+                self.win = c
+            else:
+                cap = self.board[dst]
+                if cap >= 0:
+                    self.cnt[cap] -= 1
+                    if self.cnt[cap] == 0:
+                        self.win = c if cap % 2 == 0 else 1 - c
+                self.board[dst] = piece
+            self.board[src] = -1
+        moving = self.turn_count >= 0
+        self.color = 1 - c
+        self.turn_count += 1
+        if moving and self.turn_count >= GeisterBatch.MAX_MOVES and self.win < 0:
+            self.win = 2
+
+    def observation(self, player, full=False):
+        """GeisterBatch.observation for one game: {'board': (7, 6, 6), 'scalar': (18,)} float32."""
+        me, opp = player, 1 - player
+        cnt = self.cnt
+        scalar = np.zeros(SCALARS, dtype=np.float32)
+        scalar[0] = me == 0
+        scalar[1] = player == self.color
+        for i, n in enumerate((cnt[me * 2], cnt[me * 2 + 1], cnt[opp * 2], cnt[opp * 2 + 1])):
+            if 1 <= n <= 4:
+                scalar[2 + 4 * i + n - 1] = 1
+        b = np.array(self.board, dtype=np.int8)
+        if me == 1:
+            b = b[::-1]                                          # white: the board rotated 180 degrees
+        planes = np.empty((BOARD_PLANES, 36), dtype=np.float32)
+        planes[0] = 1
+        blue_c, red_c = b == me * 2, b == me * 2 + 1
+        own = blue_c | red_c
+        planes[1] = own
+        planes[2] = (b >= 0) & ~own
+        planes[3] = blue_c
+        planes[4] = red_c
+        if full or self.complete_info:
+            planes[5] = b == opp * 2
+            planes[6] = b == opp * 2 + 1
+        else:
+            planes[5:] = 0
+        return {'board': planes.reshape(BOARD_PLANES, *BOARD), 'scalar': scalar}
+
+
 class Environment(BaseEnvironment):
     """One Geister game behind the reference plugin API (geister.py:170-541).
 
-    The state is a one-game ``GeisterBatch`` on the CPU, so the rules are the
-    same tensor code the device self-play runs (pinned to the reference env by
-    tests/test_geister_rules.py).  Actions and observations are the
-    reference's: 214 labels, ``{'board': (7, 6, 6), 'scalar': (18,)}`` numpy
-    arrays; ``observation(None)`` is the turn player's view with the
-    opponent's colours shown, ``observation(p)`` hides them.
+    The state is a ``_OneGame`` (GeisterBatch's rules in plain Python: the tensor rules the device self-play
+    runs, restated for one game; pinned to the reference env by tests/test_geister_rules.py).  Actions and
+    observations are the reference's: 214 labels, ``{'board': (7, 6, 6), 'scalar': (18,)}`` numpy arrays;
+    ``observation(None)`` is the turn player's view with the opponent's colours shown, ``observation(p)``
+    hides them.
     """
 
     BATCH = GeisterBatch
@@ -801,7 +911,7 @@ class Environment(BaseEnvironment):
 
     def __init__(self, args=None):
         super().__init__(args)
-        self.game = self.BATCH(1, torch.device('cpu'))
+        self.game = _OneGame(self.BATCH.COMPLETE_INFO)
         self.reset()
 
     def reset(self, args=None):
@@ -814,16 +924,17 @@ class Environment(BaseEnvironment):
         self._layouts_set = 0
 
     def __str__(self):
-        b = self.game.board[0].view(6, 6).tolist()
         marks = {-1: '_', 0: 'B', 1: 'R', 2: 'b', 3: 'r'}
-        rows = ['  ' + ' '.join(self.Y)] + [self.X[i] + ' ' + ' '.join(marks[v] for v in b[i]) for i in range(6)]
+        b = self.game.board
+        rows = ['  ' + ' '.join(self.Y)] + [self.X[i] + ' ' + ' '.join(marks[v] for v in b[i * 6:(i + 1) * 6])
+                                           for i in range(6)]
         return '\n'.join(rows) + '\ncolor = ' + 'BW'[self.turn()] + '\nrecord = ' + ' '.join(
             self.action2str(a, i % 2) for i, a in enumerate(self.record))
 
     def play(self, action, _=None):
         action = int(action)
         self._track(action, self.turn())
-        self.game.step(torch.tensor([action]), torch.tensor([True]))
+        self.game.step(action)
         if action < GeisterBatch.MOVES:
             self.record.append(action)
 
@@ -851,36 +962,33 @@ class Environment(BaseEnvironment):
         self._where[piece] = dst
 
     def turn(self):
-        return int(self.game.color[0])
+        return self.game.color
 
     def terminal(self):
-        return bool(self.game.win[0] >= 0)
+        return self.game.win >= 0
 
     def reward(self):
         return {p: -0.01 for p in self.players()}
 
     def outcome(self):
-        o = self.game.outcome()[0].tolist()
-        return {0: o[0], 1: o[1]}
+        w = self.game.win
+        v = 1.0 if w == 0 else (-1.0 if w == 1 else 0.0)       # GeisterBatch.outcome
+        return {0: v, 1: -v}
 
     def legal_actions(self, _=None):
         """In the reference's order (geister.py:472-486): layouts 144..213 before the game, then the mover's
-        pieces by index, each piece's directions 0..3."""
-        legal = self.game.legal()[0].tolist()
-        if legal[GeisterBatch.MOVES]:
-            return [a for a in range(GeisterBatch.MOVES, ACTIONS) if legal[a]]
-        c = self.turn()
+        pieces by index, each piece's directions 0..3 (absolute; white's labels in its rotated frame)."""
+        g = self.game
+        if g.turn_count < 0:
+            return list(range(GeisterBatch.MOVES, ACTIONS))
+        c = g.color
         out = []
         for cell in self._where[c * 8:(c + 1) * 8]:
             if cell < 0:
                 continue
-            x, y = divmod(cell, 6)
-            if c == 1:
-                x, y = 5 - x, 5 - y
             for d in range(4):
-                a = (3 - d if c == 1 else d) * 36 + x * 6 + y
-                if legal[a]:
-                    out.append(a)
+                if g.move_legal(d, cell):
+                    out.append((3 - d) * 36 + 35 - cell if c == 1 else d * 36 + cell)
         return out
 
     def action_length(self):
@@ -891,8 +999,8 @@ class Environment(BaseEnvironment):
 
     def observation(self, player=None):
         who = self.turn() if player is None else player
-        obs = self.game.observation(torch.tensor([who]), full=player is None)
-        return {'scalar': obs['scalar'][0].numpy(), 'board': obs['board'][0].numpy()}
+        obs = self.game.observation(who, full=player is None)
+        return {'scalar': obs['scalar'], 'board': obs['board']}
 
     def net(self):
         return GeisterNet

@@ -42,6 +42,7 @@ import bz2
 import contextlib
 import pickle
 import random
+import time
 
 import numpy as np
 import torch
@@ -130,6 +131,10 @@ class HostBatchGenerator:
         self._hidden_ready = False
         self.games_started = 0
         self.failed = 0
+        # seconds per phase of the last generate(): 'requests' (env observations, the plugin's own cost), 'launch'
+        # (stacking into pinned buffers, H2D, the forward's launch), 'wait' (host blocked on a forward), 'advance'
+        # (masks, sampling, env.step / reward, moment records)
+        self.timing = {}
 
     # -- recurrent state: one per (game slot, player), on the net's device -------------------------------
     def _init_hidden(self):
@@ -217,12 +222,21 @@ class HostBatchGenerator:
     def _launch(self, group):
         """Gather the group's requests and launch their forward; the outputs land in host buffers."""
         rows, obs = [], []
+        t0 = time.perf_counter()
         for s in group.slots:
             if self.slots[s].moments is None:
                 continue
             for p, o in self._requests(s):
                 rows.append((s, self.pidx[p]))
                 obs.append(o)
+        t1 = time.perf_counter()
+        self.timing['requests'] = self.timing.get('requests', 0.0) + (t1 - t0)
+        try:
+            self._launch_rows(group, rows, obs)
+        finally:
+            self.timing['launch'] = self.timing.get('launch', 0.0) + (time.perf_counter() - t1)
+
+    def _launch_rows(self, group, rows, obs):
         if not rows:
             group.pending = None
             return
@@ -286,7 +300,9 @@ class HostBatchGenerator:
             return rows, pol, val
         _, rows, host, ev = group.pending
         if ev is not None:
+            t0 = time.perf_counter()
             ev.synchronize()
+            self.timing['wait'] = self.timing.get('wait', 0.0) + (time.perf_counter() - t0)
         pol = host[0].numpy()
         val = host[1].numpy() if len(host) > 1 else None
         return rows, pol, val
@@ -368,6 +384,7 @@ class HostBatchGenerator:
         self.net.eval()                              # model.py:48
         saved = random.getstate() if self.sampler == 'reference' else None
         self.games_started, self.failed = 0, 0
+        self.timing = {}
         out = {}
         # a net with per-call inference preparation (GeisterNet: stacked DRC weights, packed conv fragments,
         # BatchNorm coefficients) prepares once for the whole call instead of once per forward
@@ -383,7 +400,11 @@ class HostBatchGenerator:
                 for g in self.groups:
                     if g.pending is None:
                         continue
+                    t0 = time.perf_counter()
+                    w0 = self.timing.get('wait', 0.0)
                     self._advance(g, n, out)
+                    self.timing['advance'] = self.timing.get('advance', 0.0) + (
+                        time.perf_counter() - t0 - (self.timing.get('wait', 0.0) - w0))
                     self._launch(g)
         finally:
             ctx.__exit__(None, None, None)
