@@ -166,6 +166,36 @@ def test_geese_learner_full_T_vs_oracle(cuda):
 
 
 @pytest.mark.gpu
+def test_geese_learner_full_size_vs_oracle(cuda):
+    """configs[3] at its full size, B=2048 T=64 (131,072 trajectory cells): one LearnerStep with the HIP torus
+    tower vs one step of the fp32 CPU oracle learner (oracle/learner.py, 16 threads; ≈60 s on one thread) from
+    the same seeded GeeseNet and batch: every loss and the gradient norm at rel 1e-5, the north-star bound."""
+    import os
+    from handyrl_amd.synthetic import geese_batch, geese_args
+    from handyrl_amd.trainer import LearnerStep
+    B, T = 2048, 64
+    args = geese_args(T, B)
+    batch = geese_batch(B, T, cuda, seed=21)
+    torch.manual_seed(4)
+    state = GeeseNet().state_dict()
+    net = GeeseNet()
+    net.load_state_dict(state)
+    step = LearnerStep(net, args, cuda, graph=False)
+    out = {k: float(v) for k, v in step.step(batch).items()}
+    del step, net
+    threads = torch.get_num_threads()
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    try:
+        cpu = GeeseNet()
+        cpu.load_state_dict(state)
+        ref = ol.CpuLearner(cpu, args).step({k: v.cpu() for k, v in batch.items()})
+    finally:
+        torch.set_num_threads(threads)
+    for k in ('p', 'v', 'ent', 'total', 'grad_norm', 'dcnt'):
+        assert abs(out[k] - ref[k]) <= 1e-5 * max(1.0, abs(ref[k])), (k, out[k], ref[k])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('residual,cin,N', [(True, 32, 41), (False, 17, 23), (True, 32, 1500)])
 def test_fused_torus_block_matches_torch(cuda, residual, cin, N):
     """nn.torus_block (conv with BN statistics in its epilogue, residual apply, masked BN backward,

@@ -186,17 +186,27 @@ def test_drc_hip_path_matches_reference_cells(golden, cuda):
     obs, hidden = fwd_inputs(arrays)
     obs = {k: v.to(cuda) for k, v in obs.items()}
     res = []
-    for net in (plain, fast):
-        h = ([t.to(cuda) for t in hidden[0]], [t.to(cuda) for t in hidden[1]])
-        out = net(obs, h)
+    ref64 = seeded_net().double()           # the gradients' exact value (fp64, CPU)
+    for net in (plain, fast, ref64):
+        dev = next(net.parameters()).device
+        dt = next(net.parameters()).dtype
+        h = ([t.to(dev, dt) for t in hidden[0]], [t.to(dev, dt) for t in hidden[1]])
+        out = net({k: v.to(dev, dt) for k, v in obs.items()}, h)
         loss = out['policy'].square().sum() + out['value'].sum() + sum(t.square().sum() for t in out['hidden'][1])
         loss.backward()
-        res.append((out, {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None}))
+        res.append((out, {n: p.grad.detach().cpu().double().clone() for n, p in net.named_parameters()
+                          if p.grad is not None}))
     check_forward(res[1][0], arrays, atol=2e-5)
-    assert set(res[0][1]) == set(res[1][1])
-    # fp32 reassociation (x/h halves summed in the gate kernel, HIP BN): norm-relative 1e-4
-    errs = {n: float((res[1][1][n] - gp).norm() / gp.norm().clamp(min=1e-12)) for n, gp in res[0][1].items()}
-    assert max(errs.values()) < 1e-4, sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    assert set(res[0][1]) == set(res[1][1]) == set(res[2][1])
+    # every gradient against the fp64 one: the HIP path (x/h halves summed in the gate kernel, HIP BN, split
+    # convolutions) within 4x the plain fp32 path's own error, or norm-relative 1e-5 (the north-star bound)
+    for n, g64 in res[2][1].items():
+        den = float(g64.norm())
+        if den == 0.0:
+            continue
+        e_fast = float((res[1][1][n] - g64).norm()) / den
+        e_plain = float((res[0][1][n] - g64).norm()) / den
+        assert e_fast <= max(4 * e_plain, 1e-5), (n, e_fast, e_plain)
 
 
 @pytest.mark.gpu
@@ -270,13 +280,18 @@ def test_gpu_recurrent_learner_matches_cpu_oracle(cuda, graph):
     ref = seeded_net()
     init = {n: p.detach().clone() for n, p in ref.named_parameters()}
     oracle = ol.CpuLearner(ref, args)
+    ref64 = seeded_net().double()           # the same three steps in fp64: the weights' exact trajectory
+    oracle64 = ol.CpuLearner(ref64, args)
+    batch64 = {k: ({kk: vv.double() for kk, vv in v.items()} if isinstance(v, dict) else
+                   (v.double() if v.is_floating_point() else v)) for k, v in cpu_batch.items()}
     net = seeded_net()
     step = LearnerStep(net, args, cuda, graph=graph)
 
-    def zeros(device):
-        return tuple([h.to(device) for h in hs] for hs in net.init_hidden([B, 2]))
+    def zeros(device, dt=torch.float32):
+        return tuple([h.to(device, dt) for h in hs] for hs in net.init_hidden([B, 2]))
     for i in range(3):
         r = oracle.step(cpu_batch, zeros('cpu'))
+        oracle64.step(batch64, zeros('cpu', torch.float64))
         out = step.step(batch, zeros(cuda))
         for k in ('p', 'v', 'r', 'ent', 'total'):
             assert abs(float(out[k]) - r[k]) <= 1e-5 * max(1.0, abs(r[k])), (i, k, float(out[k]), r[k])
@@ -284,12 +299,20 @@ def test_gpu_recurrent_learner_matches_cpu_oracle(cuda, graph):
             (i, float(out['grad_norm']), r['grad_norm'])
     dead = [n for (n, _), live in zip(step.net.named_parameters(), step.live) if not live]
     assert sorted(dead) == sorted('body.blocks.%d.conv.%s' % (i, k) for i in (0, 1) for k in ('weight', 'bias'))
+    # the weights after three updates against the fp64 trajectory: within 4x the fp32 CPU oracle's own distance
+    # from it, or norm-relative 1e-5 (Adam's m / sqrt(v) turns near-zero gradient differences into whole
+    # lr-sized steps in either fp32 implementation, so a fixed elementwise tolerance would bound noise)
     got = dict(step.net.named_parameters())
+    w64 = dict(ref64.named_parameters())
     for n, p in ref.named_parameters():
         if n in dead:
             assert torch.equal(got[n].detach().cpu(), init[n]), n
-        else:
-            torch.testing.assert_close(got[n].detach().cpu(), p.detach(), rtol=1e-4, atol=2e-6, msg=n)
+            continue
+        exact = w64[n].detach()
+        den = max(float(exact.norm()), 1e-12)
+        e_gpu = float((got[n].detach().cpu().double() - exact).norm()) / den
+        e_cpu = float((p.detach().double() - exact).norm()) / den
+        assert e_gpu <= max(4 * e_cpu, 1e-5), (n, e_gpu, e_cpu)
 
 
 @pytest.mark.gpu
