@@ -150,6 +150,12 @@ SIGNATURES = {
                                                      _f32p, ctypes.c_void_p]),
     'hrl_gboard_pack_bytes': (ctypes.c_int64, [_i64, _i64]),
     'hrl_gboard_pack': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _i64, ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_gboard_pack_adjoint': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _i64, ctypes.c_void_p, _i64,
+                                               ctypes.c_void_p]),
+    'hrl_gboard_wgrad_workspace_bytes': (ctypes.c_int64, [_i64, _i64, _i64]),
+    'hrl_gboard_wgrad': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_int, _i64, _i64, _f32p, _i64, _i64, _f32p,
+                                        ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_gboard_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _i64, _i64, _i64, _i64, ctypes.c_void_p, _i64, _f32p,
                                           _f32p, _f32p, ctypes.c_int, _f32p, _i64, ctypes.c_void_p]),
     'hrl_gboard_pointwise': (ctypes.c_int, [_f32p, _i64, _i64, _f32p, _i64, _i64, _i64, _f32p, _i64, _f32p, _f32p,

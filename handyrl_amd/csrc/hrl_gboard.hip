@@ -78,6 +78,13 @@ __device__ __forceinline__ void static_for(F &&f) {
 
 __device__ __forceinline__ float relu_f(float v) { return v < 0.f ? 0.f : v; }   // NaN stays NaN
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x16 mfma32(const uint4 &a, const uint4 &b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+
 __device__ __forceinline__ void bar_lds() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -373,8 +380,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
 
 // W (Cout, w_cin_total, 3, 3), input channels [w_ci0, w_ci0 + cin_g) -> split fragments [ct][kc][tap][part][64]
 // x 4 words: lane l of (ct, kc) holds W^T[ci = 32kc + 8(l>>4) + e][co = 16ct + (l&15)], e = 2d, 2d+1 in word d
+// flip: the adjoint (input-gradient) conv of W's input slice, W'[co'][ci'][tap] = W[ci'][w_ci0 + co'][8 - tap]
+// (cout = the slice width, cin_g = W's output channels)
 __global__ void gboard_pack_kernel(const float *__restrict__ w, int cout, int cin_g, int w_cin_total, int w_ci0,
-                                   int KC, int total, uint32_t *__restrict__ out) {
+                                   int KC, int total, int flip, uint32_t *__restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
     const int d = i & 3, l = (i >> 2) & 63;
@@ -387,7 +396,9 @@ __global__ void gboard_pack_kernel(const float *__restrict__ w, int cout, int ci
     const int co = 16 * ct + (l & 15);
     const int ci = 32 * kc + 8 * (l >> 4) + 2 * d;
     auto wv = [&](int c) -> float {
-        return (co < cout && c < cin_g) ? w[((int64_t)co * w_cin_total + w_ci0 + c) * kTaps + tap] : 0.f;
+        if (!(co < cout && c < cin_g)) return 0.f;
+        return flip ? w[((int64_t)c * w_cin_total + w_ci0 + co) * kTaps + (kTaps - 1 - tap)]
+                    : w[((int64_t)co * w_cin_total + w_ci0 + c) * kTaps + tap];
     };
     out[i] = hrl_split::split_part(wv(ci), part) | (hrl_split::split_part(wv(ci + 1), part) << 16);
 }
@@ -438,6 +449,226 @@ __global__ __launch_bounds__(256) void pointwise_kernel(const float *__restrict_
     }
 }
 
+// ------------------------------------------------------------------ weight gradient, games as the MFMA K
+// gboard_wgrad_kernel: the batched weight (and bias) gradient of a 3x3 'same' conv on the 6x6 board over every use
+// recorded in a recurrent unroll (nn.DeferredGrads.flush; handyrl/train.py:155-174 runs the net T times):
+//     dW[co][ci][tap] = sum_n sum_q dY[n][co][q] X[n][ci][p(q, tap)],   db[co] = sum_n sum_q dY[n][co][q]
+// For a 16-game tile and one (output cell q, tap) pair the sum over the tile's games is one 32x32x16 MFMA block:
+// A = dY_q (32 co x 16 games), B = X_p (16 games x 32 ci), both as the exact bf16 split (six products,
+// fp32-accurate).  A workgroup (4 waves) owns up to four (32-co, 32-ci) units: with 4 units each wave takes one
+// unit and all 9 taps (144 accumulators), with fewer the waves of a unit split its taps.  It walks 16-game tiles
+// (grid-stride over every recorded segment, no concatenation) one board row of output cells at a time: the
+// row's dY cells and the next input row are staged into LDS as part images [cell][part][half][channel][8 games]
+// (a lane's 8 games of one channel are one conflict-free ds_read_b128), input rows in a ring of three.  Each
+// workgroup writes its partial dW / db; gboard_wgrad_reduce_kernel folds them in a fixed order (deterministic)
+// and ADDS the result into the gradient tensor's input-channel slice.
+constexpr int kWgSegs = 64;
+struct WgArgs {
+    const float *x[kWgSegs];
+    const float *dy[kWgSegs];
+    int64_t xs[kWgSegs], dys[kWgSegs];   // floats from one game to the next
+    int64_t n[kWgSegs];
+    int64_t tile0[kWgSegs + 1];          // first global 16-game tile of each segment
+    int nseg;
+    int cout, cin;                       // output channels, input channels of the slice (x holds them contiguous)
+    int cto, cti;                        // 32-channel tiles
+    float *part;                         // [block][cto*cti][9][32][32] then [block][cto*32] bias sums
+    int bias;
+};
+constexpr int kWgCellPart = 1024;                       // one part of one cell: [half][32 ch][8 games] bf16
+constexpr int kWgCell = 3 * kWgCellPart;                // h, m, l
+constexpr int kWgRow = 6 * kWgCell;                     // one board row of one 32-channel tile (18 KB)
+
+template <int CTO, int CTI, int TPH>
+__device__ __forceinline__ void gboard_wgrad_run(const WgArgs &a, unsigned char *smem, int lane, int wave) {
+    // LDS: dY row [cto][6 cells] then the input-row ring [3][cti][6 cells]
+    constexpr int U = CTO * CTI;
+    constexpr int WPU = 4 / U;                            // waves per unit: they split the unit's taps (TPH)
+    const int unit = wave % U;
+    const int uco = unit / CTI, uci = unit % CTI;         // the unit's 32-channel tiles
+    unsigned char *dy_img = smem;
+    unsigned char *x_img = smem + CTO * kWgRow;
+    const int64_t ntiles = a.tile0[a.nseg];
+    f32x16 acc[9];
+    static_for<0, 9>([&](auto t_c) __attribute__((always_inline)) {
+        constexpr int t = decltype(t_c)::value;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    });
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};                 // bias partials of the staging items' channels
+    // staging item k of this thread: (channel c, game pair jp) over nch channels x 8 pairs
+    auto stage_rows = [&](const float *base, int64_t gs, int64_t n_in_tile, int nch_valid, auto ntile_c,
+                          int cell0, unsigned char *img, auto is_dy_c) __attribute__((always_inline)) {
+        // base: game 0 of the tile, channel 0, cell cell0 (6 cells of one board row)
+        constexpr int ntile_ch = decltype(ntile_c)::value, nitems = ntile_ch;
+        constexpr bool is_dy = decltype(is_dy_c)::value;
+#pragma unroll
+        for (int k = 0; k < nitems; ++k) {
+            const int item = (int)threadIdx.x + 256 * k;
+            const int c = item % (32 * ntile_ch), jp = item / (32 * ntile_ch);
+            float v[2][6];
+#pragma unroll
+            for (int gi = 0; gi < 2; ++gi) {
+                const int g = 2 * jp + gi;
+                if (g < n_in_tile && c < nch_valid) {
+                    const float *p = base + g * gs + (int64_t)c * kHW + cell0;
+                    const float2 a0 = *reinterpret_cast<const float2 *>(p);
+                    const float2 a1 = *reinterpret_cast<const float2 *>(p + 2);
+                    const float2 a2 = *reinterpret_cast<const float2 *>(p + 4);
+                    v[gi][0] = a0.x; v[gi][1] = a0.y; v[gi][2] = a1.x; v[gi][3] = a1.y; v[gi][4] = a2.x; v[gi][5] = a2.y;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 6; ++e) v[gi][e] = 0.f;
+                }
+            }
+            if constexpr (is_dy) {
+#pragma unroll
+                for (int e = 0; e < 6; ++e) bsum[k] += v[0][e] + v[1][e];
+            }
+            const int tile_ch = c >> 5, ch = c & 31, half = jp >> 2, sub = jp & 3;
+            unsigned char *dst = img + tile_ch * kWgRow + ((half * 32 + ch) * 16 + 4 * sub);
+#pragma unroll
+            for (int e = 0; e < 6; ++e) {
+                uint32_t h0, m0, l0, h1, m1, l1;
+                hrl_split::split3(v[0][e], h0, m0, l0);
+                hrl_split::split3(v[1][e], h1, m1, l1);
+                *reinterpret_cast<uint32_t *>(dst + e * kWgCell + 0 * kWgCellPart) = h0 | (h1 << 16);
+                *reinterpret_cast<uint32_t *>(dst + e * kWgCell + 1 * kWgCellPart) = m0 | (m1 << 16);
+                *reinterpret_cast<uint32_t *>(dst + e * kWgCell + 2 * kWgCellPart) = l0 | (l1 << 16);
+            }
+        }
+    };
+    constexpr int nitems_dy = CTO, nitems_x = CTI;       // items per thread (32 channels x 8 pairs per 256)
+    const int h = lane >> 5, cl = lane & 31;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        int sg = 0;
+        while (sg + 1 < a.nseg && a.tile0[sg + 1] <= tile) ++sg;
+        const int64_t n0 = (tile - a.tile0[sg]) * 16;
+        const int64_t nin = min<int64_t>(16, a.n[sg] - n0);
+        const float *xb = a.x[sg] + n0 * a.xs[sg];
+        const float *db = a.dy[sg] + n0 * a.dys[sg];
+        // input rows 0 and 1 into ring slots 0 and 1
+        stage_rows(xb, a.xs[sg], nin, a.cin, IC<CTI>{}, 0, x_img + 0 * CTI * kWgRow, std::false_type{});
+        stage_rows(xb, a.xs[sg], nin, a.cin, IC<CTI>{}, 6, x_img + 1 * CTI * kWgRow, std::false_type{});
+        for (int r = 0; r < 6; ++r) {
+            stage_rows(db, a.dys[sg], nin, a.cout, IC<CTO>{}, 6 * r, dy_img, std::true_type{});
+            if (r + 1 < 6)
+                stage_rows(xb, a.xs[sg], nin, a.cin, IC<CTI>{}, 6 * (r + 1), x_img + ((r + 1) % 3) * CTI * kWgRow,
+                           std::false_type{});
+            __syncthreads();
+            // the row's (q, tap) pairs: A = dY_q (co = lane & 31, games 8h..8h+7), B = X_p (ci = lane & 31)
+            const unsigned char *arow = dy_img + uco * kWgRow + (h * 32 + cl) * 16;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                const uint4 Ah = *reinterpret_cast<const uint4 *>(arow + c * kWgCell + 0 * kWgCellPart);
+                const uint4 Am = *reinterpret_cast<const uint4 *>(arow + c * kWgCell + 1 * kWgCellPart);
+                const uint4 Al = *reinterpret_cast<const uint4 *>(arow + c * kWgCell + 2 * kWgCellPart);
+                static_for<0, 9>([&](auto t_c) __attribute__((always_inline)) {
+                    constexpr int t = decltype(t_c)::value;
+                    if constexpr (t % WPU != TPH) return;
+                    const int pr = r + t / 3 - 1, pc = c + t % 3 - 1;
+                    if (pr < 0 || pr > 5 || pc < 0 || pc > 5) return;
+                    const unsigned char *b = x_img + (pr % 3) * CTI * kWgRow + uci * kWgRow + pc * kWgCell +
+                                             (h * 32 + cl) * 16;
+                    const uint4 Bh = *reinterpret_cast<const uint4 *>(b + 0 * kWgCellPart);
+                    const uint4 Bm = *reinterpret_cast<const uint4 *>(b + 1 * kWgCellPart);
+                    const uint4 Bl = *reinterpret_cast<const uint4 *>(b + 2 * kWgCellPart);
+                    f32x16 cc = acc[t];
+                    cc = mfma32(Al, Bh, cc);   // smallest terms first
+                    cc = mfma32(Am, Bm, cc);
+                    cc = mfma32(Ah, Bl, cc);
+                    cc = mfma32(Am, Bh, cc);
+                    cc = mfma32(Ah, Bm, cc);
+                    cc = mfma32(Ah, Bh, cc);
+                    acc[t] = cc;
+                });
+            }
+            __syncthreads();
+        }
+    }
+    // partials: [block][unit][tap][co 32][ci 32]; C/D of 32x32x16: row (co) = (i&3) + 8(i>>2) + 4h, col (ci) = lane&31
+    constexpr int nunits = U;
+    float *outp = a.part + (int64_t)blockIdx.x * nunits * 9 * 1024 + (int64_t)unit * 9 * 1024;
+    static_for<0, 9>([&](auto t_c) __attribute__((always_inline)) {
+        constexpr int t = decltype(t_c)::value;
+        if constexpr (t % WPU != TPH) return;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int co = (i & 3) + 8 * (i >> 2) + 4 * h;
+            outp[(t * 32 + co) * 32 + cl] = acc[t][i];
+        }
+    });
+    if (a.bias) {   // bias partials per channel: the staging threads' sums, folded through LDS in a fixed order
+        __syncthreads();
+        float *red = reinterpret_cast<float *>(smem);
+#pragma unroll
+        for (int k = 0; k < nitems_dy; ++k) red[threadIdx.x + 256 * k] = bsum[k];
+        __syncthreads();
+        const int nch = 32 * CTO;
+        float *bp = a.part + (int64_t)gridDim.x * nunits * 9 * 1024 + (int64_t)blockIdx.x * nch;
+        for (int c = threadIdx.x; c < nch; c += 256) {
+            float t = 0.f;
+            for (int i = c; i < 256 * nitems_dy; i += nch) t += red[i];   // items with channel c, pair order
+            bp[c] = t;
+        }
+    }
+}
+
+template <int CTO, int CTI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gboard_wgrad_kernel(WgArgs a) {
+    static_assert((CTO + 3 * CTI) * kWgRow <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[(CTO + 3 * CTI) * kWgRow];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int U = CTO * CTI;
+    const int tph = wave / U;
+    if constexpr (U == 4) {
+        gboard_wgrad_run<CTO, CTI, 0>(a, smem, lane, wave);
+    } else if constexpr (U == 2) {
+        if (tph == 0) gboard_wgrad_run<CTO, CTI, 0>(a, smem, lane, wave);
+        else gboard_wgrad_run<CTO, CTI, 1>(a, smem, lane, wave);
+    } else {
+        switch (tph) {
+        case 0: gboard_wgrad_run<CTO, CTI, 0>(a, smem, lane, wave); break;
+        case 1: gboard_wgrad_run<CTO, CTI, 1>(a, smem, lane, wave); break;
+        case 2: gboard_wgrad_run<CTO, CTI, 2>(a, smem, lane, wave); break;
+        default: gboard_wgrad_run<CTO, CTI, 3>(a, smem, lane, wave); break;
+        }
+    }
+}
+
+// fold the per-workgroup partials in block order and add into dst (the gradient of weight (Cout, w_cin_total, 3,
+// 3), input channels [ci0, ci0 + cin)) and, with a bias, into dbias
+__global__ __launch_bounds__(256) void gboard_wgrad_reduce_kernel(const float *__restrict__ part, int blocks, int cto,
+                                                                  int cti, int cout, int cin, int w_cin_total,
+                                                                  int ci0, float *__restrict__ dst,
+                                                                  float *__restrict__ dbias) {
+    const int nunits = cto * cti;
+    const int total = cout * cin * 9;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < total) {
+        const int tap = i % 9, ci = (i / 9) % cin, co = i / (9 * cin);
+        const int unit = (co >> 5) * cti + (ci >> 5);
+        const int64_t off = ((int64_t)unit * 9 + tap) * 1024 + (co & 31) * 32 + (ci & 31);
+        float s0 = 0.f, s1 = 0.f;
+        int b = 0;
+        for (; b + 1 < blocks; b += 2) {
+            s0 += part[(int64_t)b * nunits * 9 * 1024 + off];
+            s1 += part[(int64_t)(b + 1) * nunits * 9 * 1024 + off];
+        }
+        if (b < blocks) s0 += part[(int64_t)b * nunits * 9 * 1024 + off];
+        float *d = dst + ((int64_t)co * w_cin_total + ci0 + ci) * 9 + tap;
+        *d = *d + (s0 + s1);
+    }
+    if (dbias && i < cout) {
+        const float *bp = part + (int64_t)blocks * nunits * 9 * 1024;
+        const int nch = 32 * cto;
+        float t = 0.f;
+        for (int b = 0; b < blocks; ++b) t += bp[(int64_t)b * nch + i];
+        dbias[i] = dbias[i] + t;
+    }
+}
+
 int status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
@@ -449,8 +680,11 @@ bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 
 extern "C" {
 
+// k-steps of 32 input channels: 1, 2 or 4 (Cin_g <= 64 or 97..128)
+bool kc_ok(int64_t Cin_g) { return Cin_g >= 1 && (Cin_g <= 64 || (Cin_g > 96 && Cin_g <= 128)); }
+
 int64_t hrl_gboard_pack_bytes(int64_t Cout, int64_t Cin_g) {
-    if (Cout < 1 || Cin_g < 1 || Cin_g > 64) return -1;
+    if (Cout < 1 || !kc_ok(Cin_g)) return -1;
     return ((Cout + 15) / 16) * ((Cin_g + 31) / 32) * kTaps * 3 * 64 * 16;
 }
 
@@ -462,7 +696,21 @@ int hrl_gboard_pack(const float *weight, int64_t Cout, int64_t Cin_g, int64_t w_
     const int KC = (int)((Cin_g + 31) / 32);
     const int total = (int)(need / 4);
     hipLaunchKernelGGL(gboard_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
-                       weight, (int)Cout, (int)Cin_g, (int)w_cin_total, (int)w_ci0, KC, total,
+                       weight, (int)Cout, (int)Cin_g, (int)w_cin_total, (int)w_ci0, KC, total, 0,
+                       static_cast<uint32_t *>(packed));
+    return status();
+}
+
+int hrl_gboard_pack_adjoint(const float *weight, int64_t Cout_fwd, int64_t w_cin_total, int64_t w_ci0,
+                            int64_t Cin_slice, void *packed, int64_t packed_bytes, void *stream) {
+    const int64_t need = hrl_gboard_pack_bytes(Cin_slice, Cout_fwd);
+    if (!weight || !packed || need < 0 || packed_bytes < need || w_ci0 < 0 || Cin_slice < 1 ||
+        w_ci0 + Cin_slice > w_cin_total)
+        return HRL_EINVAL;
+    const int KC = (int)((Cout_fwd + 31) / 32);
+    const int total = (int)(need / 4);
+    hipLaunchKernelGGL(gboard_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       weight, (int)Cin_slice, (int)Cout_fwd, (int)w_cin_total, (int)w_ci0, KC, total, 1,
                        static_cast<uint32_t *>(packed));
     return status();
 }
@@ -470,11 +718,11 @@ int hrl_gboard_pack(const float *weight, int64_t Cout, int64_t Cin_g, int64_t w_
 int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_t x2_stride, int64_t N, int64_t Cin_g,
                        int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
                        const float *beta, int relu, float *y, int64_t y_stride, void *stream) {
-    if (!x || !packed || !y || N < 1 || Cin_g < 1 || Cin_g > 64 || groups < 1 || Cout < 1 || Cout % groups)
+    if (!x || !packed || !y || N < 1 || !kc_ok(Cin_g) || groups < 1 || Cout < 1 || Cout % groups)
         return HRL_EINVAL;
     const int64_t cout_g = Cout / groups;
     if (groups > 1 && cout_g % 16) return HRL_EINVAL;        // a column tile never straddles two groups
-    if (x2 && (Cin_g <= 32 || groups != 1)) return HRL_EINVAL;
+    if (x2 && (Cin_g <= 32 || Cin_g > 64 || groups != 1)) return HRL_EINVAL;
     if ((alpha == nullptr) != (beta == nullptr)) return HRL_EINVAL;
     if (!aligned16(x) || (x2 && !aligned16(x2)) || !aligned16(y) || x_stride % 4 || x2_stride % 4 || y_stride % 4)
         return HRL_EINVAL;
@@ -512,8 +760,10 @@ int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_
     } while (0)
     if (KC == 1) {
         if (padc) HRL_GB_LAUNCH(1, true); else HRL_GB_LAUNCH(1, false);
-    } else {
+    } else if (KC == 2) {
         if (padc) HRL_GB_LAUNCH(2, true); else HRL_GB_LAUNCH(2, false);
+    } else {
+        if (padc) HRL_GB_LAUNCH(4, true); else HRL_GB_LAUNCH(4, false);
     }
 #undef HRL_GB_LAUNCH
     return status();
@@ -541,6 +791,57 @@ int hrl_gboard_lstm_forward(const float *h, int64_t h_stride, int64_t N, int64_t
     const int64_t tasks = ((N + 15) / 16) * (a.nct / 4);
     const int grid = (int)(tasks < kCUs ? tasks : kCUs);
     hipLaunchKernelGGL(gboard_lstm_kernel, dim3(grid), dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+    return status();
+}
+
+int64_t hrl_gboard_wgrad_workspace_bytes(int64_t Cout, int64_t Cin, int64_t total_games) {
+    if (Cout < 1 || Cin < 1 || total_games < 1) return -1;
+    const int64_t cto = (Cout + 31) / 32, cti = (Cin + 31) / 32;
+    // the instantiated (32-channel) tile shapes: (co, ci) tiles 4x1, 2x2, 2x1, 1x2, 1x1
+    if (!((cto == 4 && cti == 1) || (cto <= 2 && cti <= 2))) return -1;
+    const int64_t tiles = (total_games + 15) / 16;
+    const int64_t blocks = tiles < kCUs ? tiles : kCUs;
+    return blocks * (cto * cti * 9 * 1024 + 32 * cto) * 4;
+}
+
+int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const float *const *dys,
+                     const int64_t *dy_strides, const int64_t *ns, int nseg, int64_t Cout, int64_t Cin,
+                     float *dweight, int64_t w_cin_total, int64_t w_ci0, float *dbias, void *workspace,
+                     int64_t workspace_bytes, void *stream) {
+    if (nseg < 1 || nseg > kWgSegs || !xs || !dys || !ns || !x_strides || !dy_strides || !dweight || !workspace)
+        return HRL_EINVAL;
+    if (w_ci0 < 0 || w_ci0 + Cin > w_cin_total) return HRL_EINVAL;
+    WgArgs a{};
+    int64_t tiles = 0, games = 0;
+    for (int i = 0; i < nseg; ++i) {
+        if (!xs[i] || !dys[i] || ns[i] < 1 || (reinterpret_cast<uintptr_t>(xs[i]) & 7) ||
+            (reinterpret_cast<uintptr_t>(dys[i]) & 7) || x_strides[i] % 2 || dy_strides[i] % 2 ||
+            x_strides[i] < Cin * kHW || dy_strides[i] < Cout * kHW)
+            return HRL_EINVAL;
+        a.x[i] = xs[i]; a.dy[i] = dys[i]; a.xs[i] = x_strides[i]; a.dys[i] = dy_strides[i]; a.n[i] = ns[i];
+        a.tile0[i] = tiles;
+        tiles += (ns[i] + 15) / 16;
+        games += ns[i];
+    }
+    a.tile0[nseg] = tiles;
+    const int64_t need = hrl_gboard_wgrad_workspace_bytes(Cout, Cin, games);
+    if (need < 0 || workspace_bytes < need) return HRL_EINVAL;
+    a.nseg = nseg; a.cout = (int)Cout; a.cin = (int)Cin;
+    a.cto = (int)((Cout + 31) / 32); a.cti = (int)((Cin + 31) / 32);
+    a.part = static_cast<float *>(workspace);
+    a.bias = dbias != nullptr;
+    const int blocks = (int)(tiles < kCUs ? tiles : kCUs);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (a.cto == 4 && a.cti == 1) hipLaunchKernelGGL((gboard_wgrad_kernel<4, 1>), dim3(blocks), dim3(256), 0, s, a);
+    else if (a.cto == 2 && a.cti == 2) hipLaunchKernelGGL((gboard_wgrad_kernel<2, 2>), dim3(blocks), dim3(256), 0, s, a);
+    else if (a.cto == 2 && a.cti == 1) hipLaunchKernelGGL((gboard_wgrad_kernel<2, 1>), dim3(blocks), dim3(256), 0, s, a);
+    else if (a.cto == 1 && a.cti == 2) hipLaunchKernelGGL((gboard_wgrad_kernel<1, 2>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((gboard_wgrad_kernel<1, 1>), dim3(blocks), dim3(256), 0, s, a);
+    int rc = status();
+    if (rc) return rc;
+    const int total = (int)(Cout * Cin * 9);
+    hipLaunchKernelGGL(gboard_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, a.part, blocks, a.cto,
+                       a.cti, (int)Cout, (int)Cin, (int)w_cin_total, (int)w_ci0, dweight, dbias);
     return status();
 }
 

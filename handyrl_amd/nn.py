@@ -27,6 +27,8 @@ if libhrl.so is missing that raises (no silent fallback).
 
 import operator
 
+import os
+
 import torch
 import torch.fx
 import torch.nn as nn
@@ -56,6 +58,16 @@ class DeferredGrads:
     def __init__(self):
         self.conv = {}     # (param, bias param, in slice, padding) -> [(x, dy)]
         self.affine = {}   # (weight, bias) -> [(dweight, dbias)]
+        self.adjoint = {}  # (param, in slice) -> the input-gradient conv's packed weights, packed once per step
+
+    def adjoint_pack(self, w, ci0, cin):
+        """gboard_pack_adjoint(w, ci0, cin), once per step: the weights do not change inside a step, and the
+        unroll calls a cell's input gradient 3T times."""
+        key = (id(w), ci0, cin)
+        pk = self.adjoint.get(key)
+        if pk is None:
+            pk = self.adjoint[key] = gboard_pack_adjoint(w.detach(), ci0, cin)
+        return pk
 
     def add_conv(self, key, x, dy):
         self.conv.setdefault(key, []).append((x, dy))
@@ -69,9 +81,26 @@ class DeferredGrads:
         (a ConvLSTM h-conv weight is recorded once per input slice)."""
         touched = {}
         for (w, b, sl, pad), rec in self.conv.items():
+            wv = w if sl is None else w[:, sl[0]:sl[1]]
+            if GBOARD_WGRAD and _gboard_wgrad_ok(rec, wv, pad):
+                # the 6x6 board: games as the MFMA K over every recorded use, no concatenation (hrl_gboard_wgrad)
+                gboard_wgrad(rec, w, b, sl)
+                touched[id(w)] = w
+                if b is not None:
+                    touched[id(b)] = b
+                continue
             X = torch.cat([r[0] for r in rec]) if len(rec) > 1 else rec[0][0]
             DY = torch.cat([r[1] for r in rec]) if len(rec) > 1 else rec[0][1]
-            wv = w if sl is None else w[:, sl[0]:sl[1]]
+            if _pointwise_ok(X, wv, pad):
+                # a 1x1 conv: dW[o, c] = sum over games and cells of dy[n, o, q] x[n, c, q], one GEMM
+                N, C, O = X.shape[0], X.shape[1], DY.shape[1]
+                dw = torch.tensordot(DY.reshape(N, O, -1), X.reshape(N, C, -1), dims=([0, 2], [0, 2]))
+                _add_grad(w, dw.view(O, C, 1, 1), sl)
+                touched[id(w)] = w
+                if b is not None:
+                    _add_grad(b, DY.sum((0, 2, 3)), None)
+                    touched[id(b)] = b
+                continue
             _, dw, db = torch.ops.aten.convolution_backward(
                 DY, X, wv, [wv.shape[0]] if b is not None else None, [1, 1], list(pad), [1, 1], False, [0, 0], 1,
                 [False, True, b is not None])
@@ -89,7 +118,60 @@ class DeferredGrads:
                 touched[id(b)] = b
         self.conv.clear()
         self.affine.clear()
+        self.adjoint.clear()
         return list(touched.values())
+
+
+# the deferred 3x3 board convs' weight gradient on hrl_gboard_wgrad (games as the MFMA K) instead of
+# aten.convolution_backward over the concatenated records
+GBOARD_WGRAD = os.environ.get('HRL_GBOARD_WGRAD', '1') == '1'
+
+
+def _gboard_wgrad_ok(rec, wv, pad):
+    """Records hrl_gboard_wgrad covers: 3x3 'same' on the 6x6 board, fp32 CUDA, channel-contiguous games."""
+    if tuple(pad) != (1, 1) or tuple(wv.shape[2:]) != (3, 3) or wv.dtype != torch.float32 or not wv.is_cuda:
+        return False
+    cout, cin = wv.shape[0], wv.shape[1]
+    cto, cti = (cout + 31) // 32, (cin + 31) // 32
+    if not ((cto == 4 and cti == 1) or (cto <= 2 and cti <= 2)):
+        return False
+    for x, dy in rec:
+        for t, c in ((x, cin), (dy, cout)):
+            if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 4 and tuple(t.shape[1:]) == (c, 6, 6)
+                    and t.stride(1) == 36 and t.stride(2) == 6 and t.stride(3) == 1 and t.stride(0) % 2 == 0
+                    and t.data_ptr() % 8 == 0 and t.shape[0] > 0):
+                return False
+    return True
+
+
+def gboard_wgrad(rec, w, b, sl):
+    """Add the weight (and bias) gradient of the recorded (x, dy) uses of conv weight w (input-channel slice sl)
+    into w.grad / b.grad with csrc/hrl_gboard.hip's games-as-K kernel, up to 64 records per launch."""
+    import ctypes
+    lib = _native.load()
+    ci0, cin = (0, w.shape[1]) if sl is None else (sl[0], sl[1] - sl[0])
+    cout = w.shape[0]
+    for p in (w, b):
+        if p is not None and p.grad is None:
+            p.grad = torch.zeros_like(p)
+    assert w.grad.is_contiguous() and (b is None or b.grad.is_contiguous())
+    stream = _native.stream_of(w.device)
+    for k in range(0, len(rec), 64):
+        chunk = rec[k:k + 64]
+        n = len(chunk)
+        xs = (ctypes.c_void_p * n)(*[r[0].data_ptr() for r in chunk])
+        dys = (ctypes.c_void_p * n)(*[r[1].data_ptr() for r in chunk])
+        xst = (ctypes.c_int64 * n)(*[r[0].stride(0) for r in chunk])
+        dyst = (ctypes.c_int64 * n)(*[r[1].stride(0) for r in chunk])
+        ns = (ctypes.c_int64 * n)(*[r[0].shape[0] for r in chunk])
+        games = sum(r[0].shape[0] for r in chunk)
+        nbytes = lib.hrl_gboard_wgrad_workspace_bytes(cout, cin, games)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+        _native.check(lib.hrl_gboard_wgrad(
+            ctypes.cast(xs, ctypes.c_void_p), ctypes.cast(xst, ctypes.c_void_p), ctypes.cast(dys, ctypes.c_void_p),
+            ctypes.cast(dyst, ctypes.c_void_p), ctypes.cast(ns, ctypes.c_void_p), n, cout, cin,
+            _native.ptr(w.grad), w.shape[1], ci0, None if b is None else _native.ptr(b.grad), _native.ptr(ws),
+            nbytes, stream), 'hrl_gboard_wgrad')
 
 
 def _add_grad(p, g, sl):
@@ -221,6 +303,13 @@ def gboard_ok(x, groups=1, x2=None):
                and t.data_ptr() % 16 == 0 for t in ts) and x.shape[0] > 0
 
 
+def _pointwise_ok(x, wv, pad):
+    """A 1x1 conv (no padding) the deferred path runs as plain GEMMs (forward, input gradient, batched weight
+    gradient) instead of the vendor convolution."""
+    return (wv.dim() == 4 and tuple(wv.shape[2:]) == (1, 1) and tuple(pad) == (0, 0) and x.dim() == 4
+            and x.is_cuda and x.is_contiguous() and x.dtype == torch.float32 and wv.dtype == torch.float32)
+
+
 def gboard_conv_ok(x, w, cin_g, pad):
     """A 'same' 3x3 conv hrl_gboard_forward covers: x (N, cin_g, 6, 6) fp32 CUDA (float4-aligned games), at most 64
     input channels, any Cout."""
@@ -240,6 +329,25 @@ def gboard_pack(w, cin_g=None, ci0=0, out=None):
     wpk = torch.empty(nbytes, dtype=torch.uint8, device=w.device) if out is None else out
     _native.check(lib.hrl_gboard_pack(_native.ptr(w.contiguous()), Cout, cin_g, cin_total, ci0, _native.ptr(wpk),
                                       wpk.numel(), _native.stream_of(w.device)), 'hrl_gboard_pack')
+    return wpk
+
+
+# the deferred convs' input gradient on hrl_gboard (the adjoint conv, K up to 4 x 32) instead of
+# aten.convolution_backward; off until measured on the GPU
+GBOARD_ADJOINT = os.environ.get('HRL_GBOARD_ADJOINT', '0') == '1'
+
+
+def gboard_pack_adjoint(w, ci0, cin):
+    """The input-gradient conv of input channels [ci0, ci0 + cin) of the 3x3 weight w (Cout, Cin_total, 3, 3),
+    packed for gboard_conv (cin outputs from Cout inputs)."""
+    lib = _native.load()
+    nbytes = lib.hrl_gboard_pack_bytes(cin, w.shape[0])
+    if nbytes < 0:
+        raise ValueError('hrl_gboard_pack_adjoint: unsupported weight %s' % (tuple(w.shape),))
+    wpk = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+    _native.check(lib.hrl_gboard_pack_adjoint(_native.ptr(w.contiguous()), w.shape[0], w.shape[1], ci0, cin,
+                                              _native.ptr(wpk), nbytes, _native.stream_of(w.device)),
+                  'hrl_gboard_pack_adjoint')
     return wpk
 
 
@@ -299,6 +407,11 @@ class _DeferredConv(torch.autograd.Function):
         if gboard_conv_ok(x, w, cin_g, pad):   # the 6x6 board: games as MFMA rows (csrc/hrl_gboard.hip)
             wpk = gboard_pack(w.detach(), cin_g, ci0) if packed is None else packed
             y = gboard_conv(x, wpk, w.shape[0], cin_g, bias=None if b is None else b.detach())
+        elif _pointwise_ok(x, wv, pad):          # a 1x1 conv: per game one (Cout x Cin) . (Cin x cells) GEMM
+            N, C = x.shape[0], x.shape[1]
+            y = torch.matmul(wv.detach().reshape(wv.shape[0], C), x.reshape(N, C, -1)).view(N, -1, *x.shape[2:])
+            if b is not None:
+                y = y + b.detach().view(1, -1, 1, 1)
         elif (sl is None or sl[1] - sl[0] == 32) and board_conv_ok(x, w, ci0, pad):
             if packed is not None and packed.numel() != _native.load().hrl_board_conv_workspace_bytes(w.shape[0]):
                 packed = None   # packed for hrl_gboard (this input missed its alignment): repack for this kernel
@@ -319,8 +432,18 @@ class _DeferredConv(torch.autograd.Function):
         wv = w if sl is None else w[:, sl[0]:sl[1]]
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.ops.aten.convolution_backward(dy, x, wv, None, [1, 1], list(pad), [1, 1], False, [0, 0], 1,
-                                                     [True, False, False])[0]
+            Cf = w.shape[0]
+            if (GBOARD_ADJOINT and tuple(pad) == (1, 1) and tuple(w.shape[2:]) == (3, 3) and gboard_ok(dy)
+                    and (Cf <= 64 or 96 < Cf <= 128) and wv.shape[1] == x.shape[1]):
+                # the adjoint conv on hrl_gboard: K = the forward's Cout (up to 4 x 32), Cout = the slice width
+                ci0 = 0 if sl is None else sl[0]
+                dx = gboard_conv(dy, rec.adjoint_pack(w, ci0, wv.shape[1]), wv.shape[1], Cf)
+            elif _pointwise_ok(x, wv, pad):
+                N, O = dy.shape[0], dy.shape[1]
+                dx = torch.matmul(wv.detach().reshape(O, -1).t(), dy.reshape(N, O, -1)).view_as(x)
+            else:
+                dx = torch.ops.aten.convolution_backward(dy, x, wv, None, [1, 1], list(pad), [1, 1], False, [0, 0],
+                                                         1, [True, False, False])[0]
         rec.add_conv((w, b, sl, tuple(pad)), x, dy)
         return dx, None, None, None, None, None, None
 

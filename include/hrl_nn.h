@@ -323,6 +323,23 @@ int hrl_board_conv_forward_packed(const float *x, int64_t N, int64_t Cin, int64_
 int64_t hrl_gboard_pack_bytes(int64_t Cout, int64_t Cin_g);
 int hrl_gboard_pack(const float *weight, int64_t Cout, int64_t Cin_g, int64_t w_cin_total, int64_t w_ci0,
                     void *packed, int64_t packed_bytes, void *stream);
+/* hrl_gboard_pack_adjoint: the input-gradient conv of input channels [w_ci0, w_ci0 + Cin_slice) of weight
+ * (Cout_fwd, w_cin_total, 3, 3) -- W'[co'][ci'][tap] = W[ci'][w_ci0 + co'][8 - tap], Cin_slice outputs from Cout_fwd
+ * inputs -- packed for hrl_gboard_forward (packed: hrl_gboard_pack_bytes(Cin_slice, Cout_fwd) bytes).
+ * Cin_g (input channels per group) may be <= 64 or 97..128 (1, 2 or 4 k-steps of 32). */
+int hrl_gboard_pack_adjoint(const float *weight, int64_t Cout_fwd, int64_t w_cin_total, int64_t w_ci0,
+                            int64_t Cin_slice, void *packed, int64_t packed_bytes, void *stream);
+/* hrl_gboard_wgrad: the weight (and bias) gradient of a 3x3 'same' conv on the 6x6 board summed over nseg (<= 64)
+ * recorded uses (x_i: ns[i] games of Cin input channels, x_strides[i] floats apart; dy_i: ns[i] games of Cout
+ * output gradients), ADDED into input channels [w_ci0, w_ci0 + Cin) of dweight (Cout, w_cin_total, 3, 3) and, when
+ * dbias is given, into dbias (Cout).  Games are the MFMA K (exact bf16 split, fp32-accurate); deterministic.
+ * Replaces the deferred weight gradient's aten.convolution_backward (nn.DeferredGrads.flush).  32-channel tiles
+ * (Cout, Cin): 4x1, 2x2, 2x1, 1x2, 1x1.  workspace: hrl_gboard_wgrad_workspace_bytes(Cout, Cin, sum ns) bytes. */
+int64_t hrl_gboard_wgrad_workspace_bytes(int64_t Cout, int64_t Cin, int64_t total_games);
+int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const float *const *dys,
+                     const int64_t *dy_strides, const int64_t *ns, int nseg, int64_t Cout, int64_t Cin,
+                     float *dweight, int64_t w_cin_total, int64_t w_ci0, float *dbias, void *workspace,
+                     int64_t workspace_bytes, void *stream);
 int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_t x2_stride, int64_t N, int64_t Cin_g,
                        int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
                        const float *beta, int relu, float *y, int64_t y_stride, void *stream);

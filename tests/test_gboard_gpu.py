@@ -147,3 +147,68 @@ def test_gboard_pointwise_matches_conv1x1(cuda, O, C1, C2):
                              alpha=al.to(cuda), beta=be.to(cuda), relu=True).cpu().double()
     ref = (ref * al.double()[None, :, None, None] + be.double()[None, :, None, None]).clamp_min(0)
     assert _close(y, ref)
+
+
+@pytest.mark.parametrize('N,cout_fwd,ci0,cin', [(37, 128, 32, 32), (64, 128, 0, 32), (20, 32, 0, 25), (33, 8, 0, 64)])
+def test_gboard_adjoint_matches_conv_input_gradient(cuda, N, cout_fwd, ci0, cin):
+    """hrl_gboard_pack_adjoint + hrl_gboard_forward == the input gradient of F.conv2d(x, w[:, ci0:ci0+cin], padding=1)
+    (fp64 reference): the ConvLSTM cells' h-half input gradient (128 -> 32, four k-steps), a stem-like ragged slice
+    and the move head's 8 -> 64."""
+    g = torch.Generator().manual_seed(N + cout_fwd + ci0)
+    w = torch.randn(cout_fwd, ci0 + cin + 3, 3, 3, generator=g) * 0.2
+    dy = torch.randn(N, cout_fwd, 6, 6, generator=g)
+    wv = w[:, ci0:ci0 + cin].double()
+    x = torch.zeros(N, cin, 6, 6, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x, wv, padding=1).backward(dy.double())
+    ref = x.grad
+    pk = hnn.gboard_pack_adjoint(w.to(cuda), ci0, cin)
+    y = hnn.gboard_conv(dy.to(cuda), pk, cin, cout_fwd).cpu().double()
+    assert _close(y, ref)
+
+
+@pytest.mark.parametrize('cout,cin_total,ci0,cin,ns,bias', [
+    (128, 64, 32, 32, (37, 256, 5), True),      # a ConvLSTM cell's h half: three recorded uses, ragged
+    (128, 64, 0, 32, (4096,), True),            # its x half over a whole unroll (T*N games at once)
+    (32, 25, 0, 25, (300,), False),             # the stem: 25 input planes (a padded channel tile)
+    (8, 64, 0, 64, (17, 100), False),           # the move head's 64 -> 8 (a padded output tile)
+])
+@pytest.mark.parametrize('integer', [True, False])
+def test_gboard_wgrad_matches_conv_weight_gradient(cuda, cout, cin_total, ci0, cin, ns, bias, integer):
+    """hrl_gboard_wgrad (games as the MFMA K, every recorded use in one launch, no concatenation) ADDS the weight
+    (and bias) gradient of F.conv2d(x_i, w[:, ci0:ci0+cin], padding=1) summed over the records into the slice of
+    an existing gradient: exactly the fp64 sum on integer data (pins the image layouts, every (cell, tap) pair,
+    the padded channel tiles, ragged game counts and the segment table), within 4e-6 of the gradient's scale on
+    random data; the rest of the gradient tensor is untouched."""
+    g = torch.Generator().manual_seed(cout * 7 + cin + len(ns) + int(integer))
+    mk = ((lambda *s: torch.randint(-3, 4, s, generator=g).float()) if integer else
+          (lambda *s: torch.randn(*s, generator=g)))
+    w = torch.nn.Parameter(torch.zeros(cout, cin_total, 3, 3, device=cuda))
+    b = torch.nn.Parameter(torch.zeros(cout, device=cuda)) if bias else None
+    w.grad = mk(cout, cin_total, 3, 3).to(cuda)          # an existing gradient: the kernel adds into its slice
+    before = w.grad.clone()
+    if b is not None:
+        b.grad = mk(cout).to(cuda)
+        bbefore = b.grad.clone()
+    rec = [(mk(n, cin, 6, 6).to(cuda), mk(n, cout, 6, 6).to(cuda)) for n in ns]
+    sl = None if (ci0 == 0 and cin == cin_total) else (ci0, ci0 + cin)
+    hnn.gboard_wgrad(rec, w, b, sl)
+    torch.cuda.synchronize(cuda)
+    X = torch.cat([r[0] for r in rec]).double().cpu()
+    DY = torch.cat([r[1] for r in rec]).double().cpu()
+    dw = torch.nn.grad.conv2d_weight(X, (cout, cin, 3, 3), DY, padding=1)
+    ref = before.double().cpu()
+    ref[:, ci0:ci0 + cin] += dw
+    got = w.grad.double().cpu()
+    if integer:
+        assert torch.equal(got, ref)
+    else:
+        assert (got - ref).abs().max().item() <= 4e-6 * dw.abs().max().item()
+        outside = torch.ones(cin_total, dtype=torch.bool)
+        outside[ci0:ci0 + cin] = False
+        assert torch.equal(got[:, outside], before.double().cpu()[:, outside])
+    if b is not None:
+        bref = bbefore.double().cpu() + DY.sum((0, 2, 3))
+        if integer:
+            assert torch.equal(b.grad.double().cpu(), bref)
+        else:
+            assert (b.grad.double().cpu() - bref).abs().max().item() <= 4e-6 * DY.abs().sum((0, 2, 3)).max().item()
