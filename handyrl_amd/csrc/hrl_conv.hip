@@ -1543,6 +1543,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         bb2::bar_lds();   // the stagers' prologue: the first tiles landed,
         bb2::bar_lds();   // tile 0's image staged
         for (int it = 0; it < n_iter; ++it) {
+            BB2_STAMP(it, 0);
             const unsigned char *img = smem + kImg0 + (it & 1) * bb2::kImgBytes;
             f32x4 acc[kNq];
 #pragma unroll
@@ -1580,6 +1581,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                     acc[s] = c;
                 }
             }
+            BB2_STAMP(it, 1);
             // epilogue: the output's BN statistics (bb2 EPI 1's sums, same order), y from the accumulators
             const int64_t t = t0 + (int64_t)it * step;
             const int rows = (int)min<int64_t>(kTile, a.M - t * kTile);
@@ -1610,7 +1612,9 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                 if constexpr (R::kNq > 4)
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[4 % kNq][rr]), ro, off + 16, 0, 0);
             }
+            BB2_STAMP(it, 2);
             bb2::bar_lds();   // tile it+1's image staged, tile it's image free
+            BB2_STAMP(it, 3);
         }
         // the sums: waves 0-3 [wave][lane] -> channel (wave&1)*16 + (lane&15), bb2's fold order
         __syncthreads();
@@ -1696,12 +1700,17 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         bb2::bar_lds();
         int slot = 0;                    // ring slot of tile it (= it % kSlots)
         for (int it = 0; it < n_iter; ++it) {
+            BB2_STAMP(it, 0);
             // tile it's slot was read by stage(it) before the last barrier: tile it + kSlots goes there
             dma(it + kSlots, slot);
+            BB2_STAMP(it, 1);
             const int next = slot + 1 == kSlots ? 0 : slot + 1;
             stage(it + 1, next);
+            BB2_STAMP(it, 2);
             vm_wait<(kSlots - 2) * NP>();   // tile it+2 landed (it+3 .. it+kSlots stay in flight)
+            BB2_STAMP(it, 3);
             bb2::bar_lds();
+            BB2_STAMP(it, 4);
             slot = next;
         }
         vm_wait<0>();
