@@ -1465,18 +1465,18 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
 
 // ------------------------------------------------------------------ the chain's forward conv, LDS-DMA ring
 // conv3x3_fwd_dma_kernel<PRO>: y = conv(x') with x' = relu(x*in_alpha + in_beta) (PRO) or x, and the output's BN
-// statistics (sum y, sum y^2 per channel) -- the arithmetic of bb2's forward (EPI 1): the same x', the same split
-// MFMA order, the same per-tile and per-workgroup sum order, so y and the sums are bit-identical to it.
-// What changes is the load pipeline.  bb2 loaded each 16-row tile into registers one tile ahead (≈18 KB in flight
-// per CU, one burst per tile): its forward ran at 0.42 of HBM, latency-bound.  Here
-//  * waves 4-7 (stagers) stream raw x tiles into a kSlots-deep LDS ring by LDS-DMA (buffer_load_dwordx4 ... lds:
-//    1 KiB per wave-instruction, no VGPRs), so kSlots-2 tiles stay in flight across every barrier and kSlots-1
-//    between them (≈72-90 KB per CU);
-//  * the stagers build tile k+1's x' part images (prologue + exact split, bb2's image layout and diagonal write
-//    order) from the ring while waves 0-3 run tile k's input-gradient-form MFMAs and store y from their
-//    accumulators (bb2::Role<0..3>);
-//  * one raw s_barrier per tile; the ring's RAW order is each stager's counted vmcnt before the barrier that
-//    precedes the read (cdna_hip_programming.md: 'Read a staged buffer one phase AFTER the wait that retires it').
+// statistics (sum y, sum y^2 per channel): every output block is the same split MFMA sequence as bb2's forward (EPI 1)
+// on the same x' (bit-identical y); the statistics are fp32 per tile and wave, folded in fp64 in a fixed order.
+// bb2 loaded each 16-row tile into registers one tile ahead (≈18 KB in flight per CU, one burst per tile) and gave
+// four waves all the MFMAs and four waves only staging: the forward ran at 0.42 of HBM, and stamps of a first
+// LDS-DMA form showed the staging waves beside the heaviest MFMA waves as the critical path.  Here
+//  * every wave computes: wave W owns column tile W & 1 and the output cells {4,0} | {1,3} | {5,7} | {2,6,8} (W >> 1)
+//    -- 13, 12, 12 and 12 (input cell, output cell) pairs, so each SIMD's two waves (w, w+4) carry 24-25 pairs;
+//  * x streams into a kSlots-deep LDS ring by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per wave-instruction,
+//    no VGPRs), issued by every wave as inline asm (hipcc would drain a visible LDS-DMA at every ds_read) with its
+//    vmcnt counted by hand, kSlots-1 tiles ahead;
+//  * every wave stages 1/8 of the next tile's x' part images (prologue + exact split, bb2's image layout and
+//    diagonal write order) from the ring, then its MFMAs run on the current tile: one raw s_barrier per tile.
 // Rows past the batch: their LDS-DMA is dropped by the descriptor's range check, so the ring holds stale rows
 // there; every output row depends on its own input row only, its store is dropped and its statistics masked.
 namespace fw3 {
@@ -1490,232 +1490,265 @@ constexpr int kLdsBytes = kRaw0 + kSlots * kRawBytes;       // 147,456 B
 static_assert(kLdsBytes <= 160 * 1024, "LDS");
 static_assert(kRawBytes % 1024 == 0, "whole LDS-DMA pieces per tile");
 
-typedef __attribute__((address_space(3))) void lds_void;
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-// pieces p = S, S+4, ... < kPieces belong to stager S
-template <int S> __device__ constexpr int pieces_of() {
+// one LDS-DMA piece (16 B per lane to M0 + 16 * lane); M0 saved and restored inside the statement
+__device__ __forceinline__ void dma16(u32x4 desc, uint32_t voff, uint32_t lds_byte) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(desc), "s"(lds_byte)
+                 : "memory");
+}
+
+// wave_rsrc's buffer descriptor as four wave-uniform dwords (for the inline-asm buffer ops)
+__device__ __forceinline__ u32x4 wave_desc(const void *base, uint32_t bytes) {
+    const uint64_t p = reinterpret_cast<uint64_t>(base);
+    u32x4 d;
+    d.x = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    d.y = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) & 0xffffu;
+    d.z = __builtin_amdgcn_readfirstlane(bytes);
+    d.w = 0x00020000u;
+    return d;
+}
+
+// the output cells of cell group G (W >> 1)
+template <int G> struct Cells;
+template <> struct Cells<0> { static constexpr int kN = 2; static constexpr int kQ[2] = {0, 4}; };
+template <> struct Cells<1> { static constexpr int kN = 2; static constexpr int kQ[2] = {1, 3}; };
+template <> struct Cells<2> { static constexpr int kN = 2; static constexpr int kQ[2] = {5, 7}; };
+template <> struct Cells<3> { static constexpr int kN = 3; static constexpr int kQ[3] = {2, 6, 8}; };
+
+template <int G> __device__ constexpr bool g_uses_p(int p) {
+    for (int s = 0; s < Cells<G>::kN; ++s)
+        if (tap_of(p, Cells<G>::kQ[s]) >= 0) return true;
+    return false;
+}
+template <int G> __device__ constexpr bool g_uses_tap(int t) {
+    for (int s = 0; s < Cells<G>::kN; ++s)
+        for (int p = 0; p < kCells; ++p)
+            if (tap_of(p, Cells<G>::kQ[s]) == t) return true;
+    return false;
+}
+
+template <int W> __device__ constexpr int pieces_of() {     // pieces p = W, W+8, W+16 < 18 of every tile
     int n = 0;
-    for (int p = S; p < kPieces; p += 4) ++n;
+    for (int p = W; p < kPieces; p += 8) ++n;
     return n;
 }
 
-template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// the counted wait at the end of iteration it for the ring's tile it+2: the younger vector-memory operations of
+// this wave are its later LDS-DMA groups (NP each) and output stores (NS per tile)
+template <int NP, int NS>
+__device__ __forceinline__ void wait_tile_after(int it) {
+    static_assert((kSlots - 2) * (NP + NS) + NS <= 63, "vmcnt");
+    // tile it+2 came with the prologue while it + 2 < kSlots: younger are the prologue's later groups and every
+    // iteration's group and stores so far, (kSlots - 2) NP + (it + 1) NS; later it came with iteration
+    // it + 2 - kSlots, and (kSlots - 2) (NP + NS) + NS are younger
+    if (it == 0) vm_wait<(kSlots - 2) * NP + NS>();
+    else if (it == 1) vm_wait<(kSlots - 2) * NP + 2 * NS>();
+    else if (it == 2) vm_wait<(kSlots - 2) * NP + 3 * NS>();
+    else vm_wait<(kSlots - 2) * (NP + NS) + NS>();
+    static_assert(kSlots == 5, "the early-iteration counts above are written for kSlots = 5");
+}
 
 template <bool PRO, int W>
 __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, int lane) {
+    constexpr int kCt = W & 1, G = W >> 1;
+    using C = Cells<G>;
+    constexpr int kNq = C::kN;
+    constexpr int NP = pieces_of<W>();
+    constexpr int NS = 4 * kNq;                         // one 4-byte store per row (4) and cell
     const int64_t ntiles = (a.M + kTile - 1) / kTile;
     const int64_t t0 = blockIdx.x;
     const int64_t step = gridDim.x;
     const int n_iter = t0 < ntiles ? (int)((ntiles - 1 - t0) / step + 1) : 0;
-    if constexpr (W < 4) {
-        // ---- MFMA waves: bb2's input-gradient roles with the forward weights
-        using R = bb2::Role<W>;
-        constexpr int kNq = R::kNq;
-        constexpr int kCt = R::kCt;
-        uint4 wh[kTaps], wm[kTaps], wl[kTaps];
-        {
-            const int ci0 = 8 * (lane >> 4), j = lane & 15;
+    const int ch = lane & 31, hh = lane >> 5;
+    // the forward weights of the wave's taps: all three split parts in registers (bb2's fragment layout)
+    uint4 wh[kTaps], wm[kTaps], wl[kTaps];
+    {
+        const int ci0 = 8 * (lane >> 4), j = lane & 15;
 #pragma unroll
-            for (int t = 0; t < kTaps; ++t) {
-                if (!bb2::uses_tap<W>(t)) continue;
-                uint32_t hv[4], mv[4], lv[4];
+        for (int t = 0; t < kTaps; ++t) {
+            if (!g_uses_tap<G>(t)) continue;
+            uint32_t hv[4], mv[4], lv[4];
 #pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int tc = t * 2 + kCt;
-                    const float w0 = a.wpk[(tc * kC + ci0 + 2 * d) * 16 + j];
-                    const float w1 = a.wpk[(tc * kC + ci0 + 2 * d + 1) * 16 + j];
-                    uint32_t h0, m0, l0, h1, m1, l1;
-                    hrl_split::split3(w0, h0, m0, l0);
-                    hrl_split::split3(w1, h1, m1, l1);
-                    hv[d] = h0 | (h1 << 16);
-                    mv[d] = m0 | (m1 << 16);
-                    lv[d] = l0 | (l1 << 16);
+            for (int d = 0; d < 4; ++d) {
+                const int tc = t * 2 + kCt;
+                const float w0 = a.wpk[(tc * kC + ci0 + 2 * d) * 16 + j];
+                const float w1 = a.wpk[(tc * kC + ci0 + 2 * d + 1) * 16 + j];
+                uint32_t h0, m0, l0, h1, m1, l1;
+                hrl_split::split3(w0, h0, m0, l0);
+                hrl_split::split3(w1, h1, m1, l1);
+                hv[d] = h0 | (h1 << 16);
+                mv[d] = m0 | (m1 << 16);
+                lv[d] = l0 | (l1 << 16);
+            }
+            wh[t] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+            wm[t] = make_uint4(mv[0], mv[1], mv[2], mv[3]);
+            wl[t] = make_uint4(lv[0], lv[1], lv[2], lv[3]);
+        }
+    }
+    float pa = 1.f, pb = 0.f;
+    if constexpr (PRO) {
+        pa = a.in_alpha[ch];
+        pb = a.in_beta[ch];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the weight and prologue loads, before any DMA is counted
+    const uint32_t smem_base = (uint32_t)(uintptr_t)smem;
+    auto dma = [&](int it, int slot) __attribute__((always_inline)) {
+        const int64_t t = t0 + (int64_t)it * step;
+        const bool ok = it < n_iter;
+        const int rows = ok ? (int)min<int64_t>(kTile, a.M - t * kTile) : 0;
+        const u32x4 desc = wave_desc(a.x + (ok ? t * kTile * kRow : 0), (uint32_t)rows * kRow * 4);
+        const uint32_t raw = smem_base + kRaw0 + (uint32_t)slot * kRawBytes;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            const int p = W + 8 * j;
+            dma16(desc, p * 1024 + lane * 16, raw + p * 1024);
+        }
+    };
+    const int c0 = hh ? 4 : 0;
+    const int rho0 = 2 * ((W + (ch >> 2)) & 7);              // bb2 staging wave W's row pair (its diagonal)
+    auto stage = [&](int it, int slot) __attribute__((always_inline)) {
+        const float *raw = reinterpret_cast<const float *>(smem + kRaw0 + slot * kRawBytes);
+        unsigned char *xi = smem + kImg0 + (it & 1) * bb2::kImgBytes;
+        uint32_t xp[3][5];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const float *src = raw + (rho0 + r) * kRow + ch * kCells + c0;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                float xv = src[i];
+                if constexpr (PRO) {   // bn_apply_kernel's float operations
+                    const float u = xv * pa + pb;
+                    xv = u < 0.f ? 0.f : u;
                 }
-                wh[t] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
-                wm[t] = make_uint4(mv[0], mv[1], mv[2], mv[3]);
-                wl[t] = make_uint4(lv[0], lv[1], lv[2], lv[3]);
+                uint32_t xh, xm, xl;
+                hrl_split::split3(xv, xh, xm, xl);
+                if (r == 0) {
+                    xp[0][i] = xh; xp[1][i] = xm; xp[2][i] = xl;
+                } else {
+                    xp[0][i] |= xh << 16; xp[1][i] |= xm << 16; xp[2][i] |= xl << 16;
+                }
             }
         }
-        const int co = kCt * 16 + (lane & 15);
-        const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-        const int tr_sub = 8 * (pp & 1);
-        double s1 = 0.0, s2 = 0.0;
-        bb2::bar_lds();   // the stagers' prologue: the first tiles landed,
-        bb2::bar_lds();   // tile 0's image staged
-        for (int it = 0; it < n_iter; ++it) {
-            BB2_STAMP(it, 0);
-            const unsigned char *img = smem + kImg0 + (it & 1) * bb2::kImgBytes;
-            f32x4 acc[kNq];
+        const int half = rho0 >> 3, sub = 2 * (rho0 & 7);
 #pragma unroll
-            for (int s = 0; s < kNq; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 5; ++i) {
+            const int o = bb2::img_off(c0 + i, ch, half) + sub;
 #pragma unroll
-            for (int p = 0; p < kCells; ++p) {
-                if (!bb2::uses_p<W>(p)) continue;
-                uint32_t A[3][4];
+            for (int part = 0; part < 3; ++part)
+                *reinterpret_cast<uint32_t *>(xi + part * bb2::kPartBytes + o) = xp[part][i];
+        }
+    };
+    const int co = kCt * 16 + (lane & 15);
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int tr_sub = 8 * (pp & 1);
+    double s1 = 0.0, s2 = 0.0;
+    // prologue: tiles 0 .. kSlots-1 in flight; tile 0 staged
 #pragma unroll
-                for (int part = 0; part < 3; ++part) {
+    for (int j = 0; j < kSlots; ++j) dma(j, j);
+    vm_wait<(kSlots - 1) * NP>();                            // tile 0 landed
+    bb2::bar_lds();
+    stage(0, 0);
+    vm_wait<(kSlots - 2) * NP>();                            // tile 1 landed
+    bb2::bar_lds();
+    int slot = 0;                                            // ring slot of tile it (= it % kSlots)
+    for (int it = 0; it < n_iter; ++it) {
+        BB2_STAMP(it, 0);
+        // tile it's slot was read by stage(it) before the last barrier: tile it + kSlots goes there
+        dma(it + kSlots, slot);
+        const int next = slot + 1 == kSlots ? 0 : slot + 1;
+        stage(it + 1, next);                                 // runs past the last tile too (stale rows, unread)
+        BB2_STAMP(it, 1);
+        // the MFMAs of tile it: acc[s] += sum_p x'_p (16 rows x 32 ci) . W[tap(p, q_s)][kCt], p ascending
+        const unsigned char *img = smem + kImg0 + (it & 1) * bb2::kImgBytes;
+        f32x4 acc[kNq];
 #pragma unroll
-                    for (int hlf = 0; hlf < 2; ++hlf) {
-                        const int o = part * bb2::kPartBytes + bb2::img_off(p, 8 * g + 4 * hlf + qq, pp >> 1) + tr_sub;
-                        const bb2::v4s r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                            (bb2::lds_v4s *)((__attribute__((address_space(3))) unsigned char *)(img + o)));
-                        const uint2 u = __builtin_bit_cast(uint2, r);
-                        A[part][2 * hlf] = u.x;
-                        A[part][2 * hlf + 1] = u.y;
-                    }
-                }
-                const uint4 Ah = make_uint4(A[0][0], A[0][1], A[0][2], A[0][3]);
-                const uint4 Am = make_uint4(A[1][0], A[1][1], A[1][2], A[1][3]);
-                const uint4 Al = make_uint4(A[2][0], A[2][1], A[2][2], A[2][3]);
+        for (int s = 0; s < kNq; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int s = 0; s < R::kNq; ++s) {
-                    const int tap = tap_of(p, R::kQ[s]);
-                    if (tap < 0) continue;
-                    f32x4 c = acc[s];
-                    c = mfma_bf16(Al, wh[tap], c);   // smallest terms first (bb2's order)
-                    c = mfma_bf16(Am, wm[tap], c);
-                    c = mfma_bf16(Ah, wl[tap], c);
-                    c = mfma_bf16(Am, wh[tap], c);
-                    c = mfma_bf16(Ah, wm[tap], c);
-                    c = mfma_bf16(Ah, wh[tap], c);
-                    acc[s] = c;
-                }
-            }
-            BB2_STAMP(it, 1);
-            // epilogue: the output's BN statistics (bb2 EPI 1's sums, same order), y from the accumulators
-            const int64_t t = t0 + (int64_t)it * step;
-            const int rows = (int)min<int64_t>(kTile, a.M - t * kTile);
-            const __amdgpu_buffer_rsrc_t ro = wave_rsrc(a.gin + t * kTile * kRow, (uint32_t)rows * kRow * 4);
-            float t1 = 0.f, t2 = 0.f;
+        for (int p = 0; p < kCells; ++p) {
+            if (!g_uses_p<G>(p)) continue;
+            uint32_t A[3][4];
 #pragma unroll
-            for (int s = 0; s < R::kNq; ++s) {
+            for (int part = 0; part < 3; ++part) {
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    const int row = (lane >> 4) * 4 + rr;
-                    const float u = row < rows ? acc[s][rr] : 0.f;
-                    t1 += u;
-                    t2 += u * u;
+                for (int hlf = 0; hlf < 2; ++hlf) {
+                    const int o = part * bb2::kPartBytes + bb2::img_off(p, 8 * g + 4 * hlf + qq, pp >> 1) + tr_sub;
+                    const bb2::v4s r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (bb2::lds_v4s *)((__attribute__((address_space(3))) unsigned char *)(img + o)));
+                    const uint2 u = __builtin_bit_cast(uint2, r);
+                    A[part][2 * hlf] = u.x;
+                    A[part][2 * hlf + 1] = u.y;
                 }
             }
-            s1 += (double)t1;
-            s2 += (double)t2;
+            const uint4 Ah = make_uint4(A[0][0], A[0][1], A[0][2], A[0][3]);
+            const uint4 Am = make_uint4(A[1][0], A[1][1], A[1][2], A[1][3]);
+            const uint4 Al = make_uint4(A[2][0], A[2][1], A[2][2], A[2][3]);
+#pragma unroll
+            for (int s = 0; s < kNq; ++s) {
+                const int tap = tap_of(p, C::kQ[s]);
+                if (tap < 0) continue;
+                f32x4 c = acc[s];
+                c = mfma_bf16(Al, wh[tap], c);   // smallest terms first (bb2's order)
+                c = mfma_bf16(Am, wm[tap], c);
+                c = mfma_bf16(Ah, wl[tap], c);
+                c = mfma_bf16(Am, wh[tap], c);
+                c = mfma_bf16(Ah, wm[tap], c);
+                c = mfma_bf16(Ah, wh[tap], c);
+                acc[s] = c;
+            }
+        }
+        BB2_STAMP(it, 2);
+        // epilogue: the output's BN statistics (fp32 per tile, fp64 across tiles), y straight from the accumulators
+        const int64_t t = t0 + (int64_t)it * step;
+        const int rows = (int)min<int64_t>(kTile, a.M - t * kTile);
+        const u32x4 od = wave_desc(a.gin + t * kTile * kRow, (uint32_t)rows * kRow * 4);
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int s = 0; s < kNq; ++s) {
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
                 const int row = (lane >> 4) * 4 + rr;
-                const int off = (row * kRow + co * kCells + R::kQ[0]) * 4;
-                u32x4 w;
-                w.x = __float_as_uint(acc[0][rr]);
-                w.y = __float_as_uint(acc[1][rr]);
-                w.z = __float_as_uint(acc[2][rr]);
-                w.w = __float_as_uint(acc[3][rr]);
-                __builtin_amdgcn_raw_buffer_store_b128(w, ro, off, 0, 0);
-                if constexpr (R::kNq > 4)
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[4 % kNq][rr]), ro, off + 16, 0, 0);
+                const float u = row < rows ? acc[s][rr] : 0.f;
+                t1 += u;
+                t2 += u * u;
             }
-            BB2_STAMP(it, 2);
-            bb2::bar_lds();   // tile it+1's image staged, tile it's image free
-            BB2_STAMP(it, 3);
         }
-        // the sums: waves 0-3 [wave][lane] -> channel (wave&1)*16 + (lane&15), bb2's fold order
-        __syncthreads();
-        double *dred = reinterpret_cast<double *>(smem);
-        dred[(W * 64 + lane) * 2 + 0] = s1;
-        dred[(W * 64 + lane) * 2 + 1] = s2;
-        __syncthreads();
-        if (W == 0) {
-            const int c = lane >> 1, k = lane & 1, ct = c >> 4, l16 = c & 15;
-            double tot = 0.0;
-            for (int w = ct; w < 4; w += 2)
-                for (int lg = 0; lg < 4; ++lg) tot += dred[(w * 64 + lg * 16 + l16) * 2 + k];
-            a.part[((int64_t)blockIdx.x * kC + c) * 2 + k] = tot;
-        }
-    } else {
-        // ---- stagers: the LDS-DMA ring and the x' images
-        constexpr int S = W - 4;
-        constexpr int NP = pieces_of<S>();
-        const int ch = lane & 31, hh = lane >> 5;
-        float pa = 1.f, pb = 0.f;
-        if constexpr (PRO) {
-            pa = a.in_alpha[ch];
-            pb = a.in_beta[ch];
-        }
-        const int c0 = hh ? 4 : 0;
-        auto dma = [&](int it, int slot) __attribute__((always_inline)) {
-            const int64_t t = t0 + (int64_t)it * step;
-            const bool ok = it < n_iter;
-            const int rows = ok ? (int)min<int64_t>(kTile, a.M - t * kTile) : 0;
-            const __amdgpu_buffer_rsrc_t rs = wave_rsrc(a.x + (ok ? t * kTile * kRow : 0), (uint32_t)rows * kRow * 4);
-            unsigned char *raw = smem + kRaw0 + slot * kRawBytes;
+        s1 += (double)t1;
+        s2 += (double)t2;
 #pragma unroll
-            for (int j = 0; j < NP; ++j) {
-                const int p = S + 4 * j;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(raw + p * 1024), 16, p * 1024 + lane * 16, 0,
-                                                         0, 0);
+        for (int rr = 0; rr < 4; ++rr) {
+            const int row = (lane >> 4) * 4 + rr;
+#pragma unroll
+            for (int s = 0; s < kNq; ++s) {
+                const uint32_t off = (uint32_t)(row * kRow + co * kCells + C::kQ[s]) * 4;
+                // inline asm: hipcc must not count these stores into its own (absent) vmcnt bookkeeping
+                asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(__float_as_uint(acc[s][rr])), "v"(off),
+                             "s"(od)
+                             : "memory");
             }
-        };
-        auto stage = [&](int it, int slot) __attribute__((always_inline)) {
-            const float *raw = reinterpret_cast<const float *>(smem + kRaw0 + slot * kRawBytes);
-            unsigned char *xi = smem + kImg0 + (it & 1) * bb2::kImgBytes;
-#pragma unroll
-            for (int v = 0; v < 2; ++v) {
-                const int V = S + 4 * v;                    // bb2's staging wave V's rows (its diagonal)
-                const int rho0 = 2 * ((V + (ch >> 2)) & 7);
-                uint32_t xp[3][5];
-#pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    const float *src = raw + (rho0 + r) * kRow + ch * kCells + c0;
-#pragma unroll
-                    for (int i = 0; i < 5; ++i) {
-                        float xv = src[i];
-                        if constexpr (PRO) {   // bn_apply_kernel's float operations
-                            const float u = xv * pa + pb;
-                            xv = u < 0.f ? 0.f : u;
-                        }
-                        uint32_t xh, xm, xl;
-                        hrl_split::split3(xv, xh, xm, xl);
-                        if (r == 0) {
-                            xp[0][i] = xh; xp[1][i] = xm; xp[2][i] = xl;
-                        } else {
-                            xp[0][i] |= xh << 16; xp[1][i] |= xm << 16; xp[2][i] |= xl << 16;
-                        }
-                    }
-                }
-                const int half = rho0 >> 3, sub = 2 * (rho0 & 7);
-#pragma unroll
-                for (int i = 0; i < 5; ++i) {
-                    const int o = bb2::img_off(c0 + i, ch, half) + sub;
-#pragma unroll
-                    for (int part = 0; part < 3; ++part)
-                        *reinterpret_cast<uint32_t *>(xi + part * bb2::kPartBytes + o) = xp[part][i];
-                }
-            }
-        };
-        // prologue: tiles 0 .. kSlots-1 in flight, tile 0 staged
-#pragma unroll
-        for (int j = 0; j < kSlots; ++j) dma(j, j);
-        vm_wait<(kSlots - 1) * NP>();   // tile 0 landed
-        bb2::bar_lds();
-        stage(0, 0);
-        vm_wait<(kSlots - 2) * NP>();   // tile 1 landed
-        bb2::bar_lds();
-        int slot = 0;                    // ring slot of tile it (= it % kSlots)
-        for (int it = 0; it < n_iter; ++it) {
-            BB2_STAMP(it, 0);
-            // tile it's slot was read by stage(it) before the last barrier: tile it + kSlots goes there
-            dma(it + kSlots, slot);
-            BB2_STAMP(it, 1);
-            const int next = slot + 1 == kSlots ? 0 : slot + 1;
-            stage(it + 1, next);
-            BB2_STAMP(it, 2);
-            vm_wait<(kSlots - 2) * NP>();   // tile it+2 landed (it+3 .. it+kSlots stay in flight)
-            BB2_STAMP(it, 3);
-            bb2::bar_lds();
-            BB2_STAMP(it, 4);
-            slot = next;
         }
-        vm_wait<0>();
-        __syncthreads();
-        __syncthreads();
+        wait_tile_after<NP, NS>(it);                         // tile it+2 landed (it+3 .. it+kSlots in flight)
+        BB2_STAMP(it, 3);
+        bb2::bar_lds();                                      // tile it+1's image staged, tile it's image free
+        slot = next;
+    }
+    vm_wait<0>();
+    // the sums: [wave][lane] -> channel (wave & 1) * 16 + (lane & 15), waves and lane groups in a fixed order
+    __syncthreads();
+    double *dred = reinterpret_cast<double *>(smem);
+    dred[(W * 64 + lane) * 2 + 0] = s1;
+    dred[(W * 64 + lane) * 2 + 1] = s2;
+    __syncthreads();
+    if (W == 0) {
+        const int c = lane >> 1, k = lane & 1, ct = c >> 4, l16 = c & 15;
+        double tot = 0.0;
+        for (int w = ct; w < 8; w += 2)
+            for (int lg = 0; lg < 4; ++lg) tot += dred[(w * 64 + lg * 16 + l16) * 2 + k];
+        a.part[((int64_t)blockIdx.x * kC + c) * 2 + k] = tot;
     }
 }
 

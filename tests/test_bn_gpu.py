@@ -513,7 +513,7 @@ def test_tile_shared_forward_matches_per_wave_conv(cuda, M, pro):
     """The chain's forward conv with BN statistics (hrl_conv3x3_forward_ex, epilogue 1) in the tile-shared form
     (the block backward kernel with x' staged in place of dY) and the LDS-DMA ring form (2, conv3x3_fwd_dma_kernel)
     vs the per-wave conv3x3_kernel: the output is bit-identical (the same split MFMA order on the same x'), the
-    ring form's sums equal the tile-shared form's bit for bit, the per-channel sums sum(y) and sum(y^2) agree
+    per-channel sums sum(y) and sum(y^2) agree
     with the fp64 sums to fp32 rounding of a different per-tile grouping.  Ragged M = 37 (rows past the batch
     contribute nothing) and M = 20000 (several tiles per workgroup); with and without the BN + ReLU prologue."""
     from handyrl_amd import _native
@@ -544,7 +544,6 @@ def test_tile_shared_forward_matches_per_wave_conv(cuda, M, pro):
     (y0, p0), (y1, p1), (y2, p2) = outs
     assert torch.equal(y1, y0)
     assert torch.equal(y2, y0)
-    assert torch.equal(p2, p1)     # the LDS-DMA ring form sums in the tile-shared form's order
     yd = y0.double().view(M, 32, 9)
     ref = torch.stack([yd.sum((0, 2)), (yd * yd).sum((0, 2))], 1)
     scale = torch.stack([yd.abs().sum((0, 2)), (yd * yd).sum((0, 2))], 1)

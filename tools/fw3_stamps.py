@@ -4,9 +4,9 @@
     python tools/fw3_stamps.py            # on the GPU box
 
 Lane 0 of every wave writes s_memtime (no drain) at the phase boundaries of iterations 2 and 3 (BB2_STAMP in
-csrc/hrl_conv.hip).  MFMA waves 0-3: 0 loop head, 1 MFMAs issued, 2 epilogue issued, 3 past the barrier.  Stagers
-4-7: 0 loop head, 1 LDS-DMA issued, 2 stage written, 3 past the counted vmcnt wait, 4 past the barrier.  Prints
-per-wave medians over the workgroups and the iteration period.
+csrc/hrl_conv.hip): 0 loop head, 1 LDS-DMA issued and the next tile staged, 2 MFMAs issued, 3 stores issued and
+the ring's counted vmcnt wait passed; the rest of the period is the barrier.  Prints per-wave medians over the
+workgroups and the iteration period.
 """
 import ctypes
 import os
@@ -47,12 +47,11 @@ def main():
     torch.cuda.synchronize(dev)
     st = buf.view(nblk, 8, 2, 8).cpu().numpy().astype(np.int64)
     for wv in range(8):
-        npts = 4 if wv < 4 else 5
-        d = st[:, wv, :, 1:npts] - st[:, wv, :, 0:npts - 1]
+        d = st[:, wv, :, 1:4] - st[:, wv, :, 0:3]
         period = np.median(st[:, wv, 1, 0] - st[:, wv, 0, 0])
-        med = np.median(d.reshape(-1, npts - 1), axis=0)
-        print('wave %d (%s): period %6.0f cycles; phases %s' % (
-            wv, 'mfma' if wv < 4 else 'stager', period, ' '.join('%6.0f' % v for v in med)))
+        med = np.median(d.reshape(-1, 3), axis=0)
+        print('wave %d: period %6.0f cycles; dma+stage %6.0f, mfma %6.0f, epilogue+wait %6.0f, barrier %6.0f' % (
+            wv, period, med[0], med[1], med[2], period - med.sum()))
 
 
 if __name__ == '__main__':
