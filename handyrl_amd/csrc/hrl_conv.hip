@@ -1705,7 +1705,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         // epilogue: the output's BN statistics (fp32 per tile, fp64 across tiles), y straight from the accumulators
         const int64_t t = t0 + (int64_t)it * step;
         const int rows = (int)min<int64_t>(kTile, a.M - t * kTile);
-        const u32x4 od = wave_desc(a.gin + t * kTile * kRow, (uint32_t)rows * kRow * 4);
+        const __amdgpu_buffer_rsrc_t od = wave_rsrc(a.gin + t * kTile * kRow, (uint32_t)rows * kRow * 4);
         float t1 = 0.f, t2 = 0.f;
 #pragma unroll
         for (int s = 0; s < kNq; ++s) {
@@ -1724,11 +1724,10 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
             const int row = (lane >> 4) * 4 + rr;
 #pragma unroll
             for (int s = 0; s < kNq; ++s) {
-                const uint32_t off = (uint32_t)(row * kRow + co * kCells + C::kQ[s]) * 4;
-                // inline asm: hipcc must not count these stores into its own (absent) vmcnt bookkeeping
-                asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(__float_as_uint(acc[s][rr])), "v"(off),
-                             "s"(od)
-                             : "memory");
+                // a compiler-visible store: hipcc then keeps the MFMA -> store-data wait states (an inline-asm store
+                // read some accumulators before their MFMA had written them); vmcnt is still counted by hand
+                const int off = (row * kRow + co * kCells + C::kQ[s]) * 4;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[s][rr]), od, off, 0, 0);
             }
         }
         wait_tile_after<NP, NS>(it);                         // tile it+2 landed (it+3 .. it+kSlots in flight)
