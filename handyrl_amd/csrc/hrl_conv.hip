@@ -1470,8 +1470,9 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
 // bb2 loaded each 16-row tile into registers one tile ahead (≈18 KB in flight per CU, one burst per tile) and gave
 // four waves all the MFMAs and four waves only staging: the forward ran at 0.42 of HBM, and stamps of a first
 // LDS-DMA form showed the staging waves beside the heaviest MFMA waves as the critical path.  Here
-//  * every wave computes: wave W owns column tile W & 1 and the output cells {4,0} | {1,3} | {5,7} | {2,6,8} (W >> 1)
-//    -- 13, 12, 12 and 12 (input cell, output cell) pairs, so each SIMD's two waves (w, w+4) carry 24-25 pairs;
+//  * every wave computes: wave W owns column tile W & 1 and the output cells {0,1,2} | {3,4} | {5,6} | {7,8} (W >> 1)
+//    -- 14, 15, 10 and 10 (input cell, output cell) pairs, so each SIMD's two waves (w, w+4) carry 24-25 pairs,
+//    and a row's cells leave as one store;
 //  * x streams into a kSlots-deep LDS ring by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per wave-instruction,
 //    no VGPRs), issued by every wave as inline asm (hipcc would drain a visible LDS-DMA at every ds_read) with its
 //    vmcnt counted by hand, kSlots-1 tiles ahead;
@@ -1513,12 +1514,13 @@ __device__ __forceinline__ u32x4 wave_desc(const void *base, uint32_t bytes) {
     return d;
 }
 
-// the output cells of cell group G (W >> 1)
+// the output cells of cell group G (W >> 1): runs of consecutive cells, so a row's cells leave in one store
+// (14, 15, 10 and 10 (input, output) cell pairs: the SIMD pairs (w, w+4) carry 24 and 25)
 template <int G> struct Cells;
-template <> struct Cells<0> { static constexpr int kN = 2; static constexpr int kQ[2] = {0, 4}; };
-template <> struct Cells<1> { static constexpr int kN = 2; static constexpr int kQ[2] = {1, 3}; };
-template <> struct Cells<2> { static constexpr int kN = 2; static constexpr int kQ[2] = {5, 7}; };
-template <> struct Cells<3> { static constexpr int kN = 3; static constexpr int kQ[3] = {2, 6, 8}; };
+template <> struct Cells<0> { static constexpr int kN = 3; static constexpr int kQ[3] = {0, 1, 2}; };
+template <> struct Cells<1> { static constexpr int kN = 2; static constexpr int kQ[2] = {3, 4}; };
+template <> struct Cells<2> { static constexpr int kN = 2; static constexpr int kQ[2] = {5, 6}; };
+template <> struct Cells<3> { static constexpr int kN = 2; static constexpr int kQ[2] = {7, 8}; };
 
 template <int G> __device__ constexpr bool g_uses_p(int p) {
     for (int s = 0; s < Cells<G>::kN; ++s)
@@ -1559,7 +1561,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
     using C = Cells<G>;
     constexpr int kNq = C::kN;
     constexpr int NP = pieces_of<W>();
-    constexpr int NS = 4 * kNq;                         // one 4-byte store per row (4) and cell
+    constexpr int NS = 4;                               // one store per row: the group's run of cells
     const int64_t ntiles = (a.M + kTile - 1) / kTile;
     const int64_t t0 = blockIdx.x;
     const int64_t step = gridDim.x;
@@ -1719,15 +1721,23 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         }
         s1 += (double)t1;
         s2 += (double)t2;
+        // compiler-visible stores: hipcc then keeps the MFMA -> store-data wait states (inline-asm stores read some
+        // accumulators before their MFMA had written them); vmcnt is still counted by hand
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
             const int row = (lane >> 4) * 4 + rr;
-#pragma unroll
-            for (int s = 0; s < kNq; ++s) {
-                // a compiler-visible store: hipcc then keeps the MFMA -> store-data wait states (an inline-asm store
-                // read some accumulators before their MFMA had written them); vmcnt is still counted by hand
-                const int off = (row * kRow + co * kCells + C::kQ[s]) * 4;
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[s][rr]), od, off, 0, 0);
+            const int off = (row * kRow + co * kCells + C::kQ[0]) * 4;
+            if constexpr (kNq == 3) {
+                u32x3 v;
+                v.x = __float_as_uint(acc[0][rr]);
+                v.y = __float_as_uint(acc[1][rr]);
+                v.z = __float_as_uint(acc[2 % kNq][rr]);
+                __builtin_amdgcn_raw_buffer_store_b96(v, od, off, 0, 0);
+            } else {
+                u32x2 v;
+                v.x = __float_as_uint(acc[0][rr]);
+                v.y = __float_as_uint(acc[1][rr]);
+                __builtin_amdgcn_raw_buffer_store_b64(v, od, off, 0, 0);
             }
         }
         wait_tile_after<NP, NS>(it);                         // tile it+2 landed (it+3 .. it+kSlots in flight)
