@@ -2279,9 +2279,9 @@ int g_split = 1;
 // Chain block backward with an input gradient: 2 = the LDS-DMA ring conv3x3_block_bwd3_kernel, 1 = tile-shared
 // conv3x3_block_bwd2_kernel (default), 0 = the per-wave conv3x3_block_bwd_kernel.
 int g_block_form = 1;
-// The chain's forward conv (epilogue 1, packed weights, no bias): 1 = the tile-shared form (bb2, EPI 1),
-// 0 = conv3x3_kernel<PRO, 1>.
-int g_fwd_form = 1;
+// The chain's forward conv (epilogue 1, packed weights, no bias): 2 = the LDS-DMA ring form (fw3, default),
+// 1 = the tile-shared form (bb2, EPI 1), 0 = conv3x3_kernel<PRO, 1>.
+int g_fwd_form = 2;
 
 // One 4-wave workgroup per CU (LDS: 109 KB forward, 145 KB weight gradient);
 // the waves walk row tiles grid-stride so the next tile's loads overlap MFMAs.
