@@ -42,6 +42,8 @@ constexpr int kCUs = 256;         // one 4-wave workgroup per CU (one wave per S
 struct GbArgs {
     const float *x, *x2;   // x2 (optional): input channels 32.. (the move head's [h_e, h_last] without a copy)
     int64_t N, xs, xs2;    // games; floats from one game to the next in x / x2
+    const float *xg[4];    // per-group inputs (hrl_gboard_forward_groups: the DRC layers' separate states), or NULL
+    int64_t xgs[4];        // floats from one game to the next in xg[g]
     int cin_g, cout_g;     // input / output channels per group
     const uint4 *wpk;      // split weight fragments [ct][kc][tap][part][64]
     int nct, cout;         // 16-channel column tiles; output channels stored
@@ -148,6 +150,7 @@ __device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem,
             c1 = min(c1, a.cin_g - 1);
         }
         if (KC > 1 && kc >= 1 && a.x2) return a.x2 + n * a.xs2 + (int64_t)(-32) * kHW;
+        if (a.xg[0]) return a.xg[grp] + n * a.xgs[grp];
         return a.x + n * a.xs + (int64_t)(grp * a.cin_g) * kHW;
     };
     float4 raw[3][2];
@@ -669,6 +672,74 @@ __global__ __launch_bounds__(256) void gboard_wgrad_reduce_kernel(const float *_
     }
 }
 
+// The weight gradient of a 1x1 conv on the board (the heads' pointwise convs in the learner):
+//     dW[o][c] = sum over games n and cells q of dy[n][o][q] * x[n][c][q]
+// HBM-bound (x is read once).  Thread (slot, c) of a workgroup walks games slot, slot + slots, ... of the
+// workgroup's range, summing each game's 36-cell dot products in cell order; the slots are folded in LDS and each
+// workgroup writes its O x C partial, which pw_wgrad_reduce_kernel folds in block order (deterministic).
+constexpr int kPwMaxO = 8;
+__global__ __launch_bounds__(256) void pw_wgrad_kernel(const float *__restrict__ x, int64_t xs,
+                                                       const float *__restrict__ dy, int64_t dys, int64_t N, int C,
+                                                       int O, int64_t games_per_block, float *__restrict__ part) {
+    __shared__ float red[256 * kPwMaxO];
+    const int t = threadIdx.x;
+    const int slots = 256 / C;
+    const int slot = t / C, c = t % C;
+    float acc[kPwMaxO];
+#pragma unroll
+    for (int o = 0; o < kPwMaxO; ++o) acc[o] = 0.f;
+    const int64_t n0 = (int64_t)blockIdx.x * games_per_block;
+    const int64_t n1 = min(n0 + games_per_block, N);
+    if (slot < slots) {
+        for (int64_t n = n0 + slot; n < n1; n += slots) {
+            const float4 *xr = reinterpret_cast<const float4 *>(x + n * xs + (int64_t)c * kHW);
+            float4 xv[kQuads];
+#pragma unroll
+            for (int k = 0; k < kQuads; ++k) xv[k] = xr[k];
+#pragma unroll
+            for (int o = 0; o < kPwMaxO; ++o) {
+                if (o < O) {
+                    const float4 *dr = reinterpret_cast<const float4 *>(dy + n * dys + (int64_t)o * kHW);
+                    float d = 0.f;
+#pragma unroll
+                    for (int k = 0; k < kQuads; ++k) {
+                        const float4 g = dr[k];
+                        d += g.x * xv[k].x;
+                        d += g.y * xv[k].y;
+                        d += g.z * xv[k].z;
+                        d += g.w * xv[k].w;
+                    }
+                    acc[o] += d;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < kPwMaxO; ++o) red[o * 256 + t] = acc[o];
+    __syncthreads();
+    if (t < C) {
+        for (int o = 0; o < O; ++o) {
+            float v = 0.f;
+            for (int sl = 0; sl < slots; ++sl) v += red[o * 256 + sl * C + t];
+            part[((int64_t)blockIdx.x * O + o) * C + t] = v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void pw_wgrad_reduce_kernel(const float *__restrict__ part, int blocks, int OC,
+                                                              float *__restrict__ dw) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= OC) return;
+    float s0 = 0.f, s1 = 0.f;
+    int b = 0;
+    for (; b + 1 < blocks; b += 2) {
+        s0 += part[(int64_t)b * OC + i];
+        s1 += part[(int64_t)(b + 1) * OC + i];
+    }
+    if (b < blocks) s0 += part[(int64_t)b * OC + i];
+    dw[i] = dw[i] + (s0 + s1);
+}
+
 int status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
@@ -715,6 +786,29 @@ int hrl_gboard_pack_adjoint(const float *weight, int64_t Cout_fwd, int64_t w_cin
     return status();
 }
 
+int gboard_launch(GbArgs a, int64_t Cin_g, int64_t groups, hipStream_t s);
+
+int hrl_gboard_forward_groups(const float *const *xs, const int64_t *x_strides, int64_t N, int64_t Cin_g,
+                              int64_t groups, const void *packed, int64_t Cout, float *y, int64_t y_stride,
+                              void *stream) {
+    if (!xs || !x_strides || !packed || !y || N < 1 || Cin_g < 1 || Cin_g > 32 || groups < 1 || groups > 4 ||
+        Cout < 1 || Cout % groups || (Cout / groups) % 16)
+        return HRL_EINVAL;
+    if (!aligned16(y) || y_stride % 4 || y_stride < Cout * kHW) return HRL_EINVAL;
+    GbArgs a{};
+    for (int g = 0; g < groups; ++g) {
+        if (!xs[g] || !aligned16(xs[g]) || x_strides[g] % 4 || x_strides[g] < Cin_g * kHW) return HRL_EINVAL;
+        a.xg[g] = xs[g];
+        a.xgs[g] = x_strides[g];
+    }
+    a.x = xs[0]; a.N = N; a.xs = x_strides[0];
+    a.cin_g = (int)Cin_g; a.cout_g = (int)(Cout / groups);
+    a.wpk = static_cast<const uint4 *>(packed);
+    a.nct = (int)((Cout + 15) / 16); a.cout = (int)Cout;
+    a.y = y; a.ys = y_stride;
+    return gboard_launch(a, Cin_g, groups, static_cast<hipStream_t>(stream));
+}
+
 int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_t x2_stride, int64_t N, int64_t Cin_g,
                        int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
                        const float *beta, int relu, float *y, int64_t y_stride, void *stream) {
@@ -734,6 +828,11 @@ int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_
     a.wpk = static_cast<const uint4 *>(packed);
     a.nct = (int)((Cout + 15) / 16); a.cout = (int)Cout;
     a.bias = bias; a.alpha = alpha; a.beta = beta; a.relu = relu; a.y = y; a.ys = y_stride;
+    return gboard_launch(a, Cin_g, groups, static_cast<hipStream_t>(stream));
+}
+
+int gboard_launch(GbArgs a, int64_t Cin_g, int64_t groups, hipStream_t s) {
+    const int64_t N = a.N, cout_g = a.cout_g;
     const int64_t ntiles = (N + 15) / 16;
     // column tiles per workgroup (NCTW = 4, 2, 1; the other waves split the output cells into 4 / NCTW bands):
     // the fewest task rounds per band over the chip's 256 CUs (one 4-wave workgroup each), ties to the wider
@@ -749,7 +848,6 @@ int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_
     const int64_t tasks = ntiles * (a.nct / nctw);
     int grid = (int)(tasks < kCUs ? tasks : kCUs);
     const dim3 block(kThreads);
-    hipStream_t s = static_cast<hipStream_t>(stream);
     const int KC = (int)((Cin_g + 31) / 32);
     const bool padc = Cin_g % 32 != 0;
 #define HRL_GB_LAUNCH(KC_, PADC_)                                                                                  \
@@ -842,6 +940,34 @@ int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const flo
     const int total = (int)(Cout * Cin * 9);
     hipLaunchKernelGGL(gboard_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, a.part, blocks, a.cto,
                        a.cti, (int)Cout, (int)Cin, (int)w_cin_total, (int)w_ci0, dweight, dbias);
+    return status();
+}
+
+int64_t hrl_gboard_pointwise_wgrad_workspace_bytes(int64_t C, int64_t O, int64_t N) {
+    if (C < 1 || C > 256 || O < 1 || O > kPwMaxO || N < 1) return -1;
+    const int64_t blocks = N < 2 * kCUs ? N : 2 * kCUs;
+    return blocks * O * C * 4;
+}
+
+int hrl_gboard_pointwise_wgrad(const float *x, int64_t x_stride, const float *dy, int64_t dy_stride, int64_t N,
+                               int64_t C, int64_t O, float *dweight, void *workspace, int64_t workspace_bytes,
+                               void *stream) {
+    const int64_t need = hrl_gboard_pointwise_wgrad_workspace_bytes(C, O, N);
+    if (!x || !dy || !dweight || !workspace || need < 0 || workspace_bytes < need) return HRL_EINVAL;
+    if (!aligned16(x) || !aligned16(dy) || x_stride % 4 || dy_stride % 4 || x_stride < C * kHW ||
+        dy_stride < O * kHW)
+        return HRL_EINVAL;
+    const int64_t blocks = N < 2 * kCUs ? N : 2 * kCUs;
+    const int64_t per = (N + blocks - 1) / blocks;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    float *part = static_cast<float *>(workspace);
+    hipLaunchKernelGGL(pw_wgrad_kernel, dim3((int)blocks), dim3(256), 0, s, x, x_stride, dy, dy_stride, N, (int)C,
+                       (int)O, per, part);
+    int rc = status();
+    if (rc) return rc;
+    const int OC = (int)(O * C);
+    hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3((OC + 255) / 256), dim3(256), 0, s, part, (int)blocks, OC,
+                       dweight);
     return status();
 }
 

@@ -148,6 +148,69 @@ __global__ void lstm_fwd_kernel(const float *__restrict__ zx, const float *__res
     }
 }
 
+// The layers of one DRC repeat in one launch (hrl_lstm_gates_forward_grouped): layer l's zh is a channel slice of
+// one grouped convolution's output (per-sample stride zhs), its zx, c and outputs have their own pointers.  Each
+// element runs lstm_fwd_kernel's float operations (z = zx + zh), so the outputs equal L separate launches.
+constexpr int kMaxLayers = 4;
+struct LayerTable {
+    const float *zx[kMaxLayers];
+    int64_t zxs[kMaxLayers];
+    const float *c[kMaxLayers];
+    float *h_out[kMaxLayers], *c_out[kMaxLayers], *gates[kMaxLayers];
+};
+
+template <int VW>
+__global__ void lstm_fwd_grouped_kernel(const float *__restrict__ zh, int64_t zhs, LayerTable t, int L, Geo g) {
+    using V = typename Vec<VW>::T;
+    const int64_t per = g.N * g.H * g.nq;
+    const int64_t total = per * L;
+    for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e0 < total;
+         e0 += (int64_t)gridDim.x * blockDim.x) {
+        const int l = (int)(e0 / per);
+        const int64_t e = e0 - (int64_t)l * per;
+        const int q = (int)(e % g.nq);
+        const int64_t nc = e / g.nq;
+        const int ch = (int)(nc % g.H);
+        const int64_t n = nc / g.H;
+        const int64_t plane = (int64_t)g.HW;
+        const int64_t gstep = (int64_t)g.H * plane;
+        const int64_t hoff = n * zhs + (int64_t)l * 4 * gstep + (int64_t)ch * plane + (int64_t)q * VW;
+        const int64_t zoff = n * 4 * gstep + (int64_t)ch * plane + (int64_t)q * VW;
+        const int64_t xoff = n * t.zxs[l] + (int64_t)ch * plane + (int64_t)q * VW;
+        const int64_t soff = nc * plane + (int64_t)q * VW;
+        const V zi = ld<VW>(zh + hoff), zf = ld<VW>(zh + hoff + gstep), zo = ld<VW>(zh + hoff + 2 * gstep),
+                zg = ld<VW>(zh + hoff + 3 * gstep);
+        const float *zx = t.zx[l];
+        const V xi = ld<VW>(zx + xoff), xf = ld<VW>(zx + xoff + gstep), xo = ld<VW>(zx + xoff + 2 * gstep),
+                xg = ld<VW>(zx + xoff + 3 * gstep);
+        const V cv = ld<VW>(t.c[l] + soff);
+        V gi, gf, go, gg, cn, hn;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+            const float a_i = get<VW>(xi, j) + get<VW>(zi, j), a_f = get<VW>(xf, j) + get<VW>(zf, j),
+                        a_o = get<VW>(xo, j) + get<VW>(zo, j), a_g = get<VW>(xg, j) + get<VW>(zg, j);
+            const float si = sigm(a_i), sf = sigm(a_f), so = sigm(a_o), tg = tanhf(a_g);
+            const float fc = sf * get<VW>(cv, j);
+            const float ig = si * tg;
+            const float cc = fc + ig;
+            put<VW>(gi, j, si);
+            put<VW>(gf, j, sf);
+            put<VW>(go, j, so);
+            put<VW>(gg, j, tg);
+            put<VW>(cn, j, cc);
+            put<VW>(hn, j, so * tanhf(cc));
+        }
+        if (float *gates = t.gates[l]) {
+            st<VW>(gates + zoff, gi);
+            st<VW>(gates + zoff + gstep, gf);
+            st<VW>(gates + zoff + 2 * gstep, go);
+            st<VW>(gates + zoff + 3 * gstep, gg);
+        }
+        st<VW>(t.c_out[l] + soff, cn);
+        st<VW>(t.h_out[l] + soff, hn);
+    }
+}
+
 template <int VW>
 __global__ void lstm_bwd_kernel(const float *__restrict__ gates, const float *__restrict__ c,
                                 const float *__restrict__ c_out, const float *__restrict__ dh,
@@ -227,6 +290,30 @@ int hrl_lstm_gates_forward(const float *zx, int64_t zx_stride, const float *zh, 
     else
         hipLaunchKernelGGL(lstm_fwd_kernel<1>, dim3(grid_for(total)), dim3(256), 0, s, zx, zh, c, g, h_out, c_out,
                            gates);
+    return status();
+}
+
+int hrl_lstm_gates_forward_grouped(int L, const float *zh, int64_t zh_stride, const float *const *zx,
+                                   const int64_t *zx_strides, const float *const *c, int64_t N, int64_t H, int64_t HW,
+                                   float *const *h_out, float *const *c_out, float *const *gates, void *stream) {
+    if (N == 0) return HRL_OK;
+    if (L < 1 || L > kMaxLayers || !zh || !zx || !zx_strides || !c || !h_out || !c_out || N < 0 || H < 1 || HW < 1)
+        return HRL_EINVAL;
+    if (zh_stride < L * 4 * H * HW) return HRL_EINVAL;
+    LayerTable t{};
+    bool vec = HW % 4 == 0 && zh_stride % 4 == 0 && aligned(zh);
+    for (int l = 0; l < L; ++l) {
+        if (!zx[l] || !c[l] || !h_out[l] || !c_out[l] || zx_strides[l] < 4 * H * HW) return HRL_EINVAL;
+        t.zx[l] = zx[l]; t.zxs[l] = zx_strides[l]; t.c[l] = c[l];
+        t.h_out[l] = h_out[l]; t.c_out[l] = c_out[l]; t.gates[l] = gates ? gates[l] : nullptr;
+        vec = vec && zx_strides[l] % 4 == 0 && aligned(zx[l]) && aligned(c[l]) && aligned(h_out[l]) &&
+              aligned(c_out[l]) && aligned(t.gates[l]);
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Geo g{N, (int)H, (int)HW, (int)(vec ? HW / 4 : HW), 0, nullptr, 1};
+    const int64_t total = N * H * g.nq * L;
+    if (vec) hipLaunchKernelGGL(lstm_fwd_grouped_kernel<4>, dim3(grid_for(total)), dim3(256), 0, s, zh, zh_stride, t, L, g);
+    else hipLaunchKernelGGL(lstm_fwd_grouped_kernel<1>, dim3(grid_for(total)), dim3(256), 0, s, zh, zh_stride, t, L, g);
     return status();
 }
 

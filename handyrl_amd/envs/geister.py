@@ -25,6 +25,7 @@ Observation format
 """
 
 import contextlib
+import os
 
 import numpy as np
 import torch
@@ -125,6 +126,9 @@ class DRC(nn.Module):
     # unfused at 2,048 games: the epilogue's loads and transcendentals run serially after the MFMAs at one
     # wave per SIMD), so off by default
     fuse_gates = False
+    # the learner's unroll: each repeat's layers as one grouped h-half conv + one grouped gate launch
+    # (nn.drc_repeat) instead of a conv and a gate launch per layer
+    group_repeat = os.environ.get('HRL_DRC_GROUPED', '1') == '1'
     _inplace = False  # the session advances a stacked state in place (DeviceGenerator)
 
     def _stacked_weights(self, out=None):
@@ -257,6 +261,12 @@ class DRC(nn.Module):
                 return (conv2d(x, ws[layers[0]], bias[layers[0]], pad, in_slice=(0, cin)),)
             w_x = torch.cat([ws[i][:, :cin] for i in layers])
             b_x = None if bias[0] is None else torch.cat([bias[i] for i in layers])
+            if deferred and n > 1 and layers[-1] < n - 1 and hnn.gboard_conv_ok(x, w_x, cin, pad):
+                # the learner's layers that reach no output (see below): forward only, on hrl_gboard
+                with torch.no_grad():
+                    z = hnn.gboard_conv(x, hnn.gboard_pack(w_x), w_x.shape[0], cin,
+                                        bias=None if b_x is None else b_x.detach())
+                return z.chunk(len(layers), dim=-3)
             return F.conv2d(x, w_x, b_x, padding=pad).chunk(len(layers), dim=-3)
         if torch.is_grad_enabled() and n > 1:
             # Only the last layer reaches the output (every cell reads x and its own state), so the
@@ -276,6 +286,14 @@ class DRC(nn.Module):
         cin = c_all - self.blocks[0].hidden_dim
         deferred = hnn._DEFER is not None
         w_h = None if deferred else [w[:, cin:].contiguous() for w in ws]
+        if (deferred and isinstance(packed_h, dict) and self.group_repeat
+                and hnn.drc_repeat_ok(zx, hs, cs, ws, pad)):
+            # every repeat's layers in two launches (the grouped h-half conv and the grouped gates)
+            for _ in range(num_repeats):
+                hs, cs = hnn.drc_repeat(zx, hs, cs, ws, (cin, c_all), pad, packed_h['grouped'])
+            return hs[-1], (hs, cs)
+        if isinstance(packed_h, dict):
+            packed_h = packed_h['layers']
         for _ in range(num_repeats):
             for i in range(len(self.blocks)):
                 if deferred:
@@ -532,7 +550,9 @@ class GeisterNet(nn.Module):
         packed_h = None
         hd = self.body.blocks[0].hidden_dim
         if hnn._DEFER is not None and hnn.gboard_conv_ok(h_e[:1, :hd], cells[0].weight, hd, cells[0].padding):
-            packed_h = [hnn.gboard_pack(c.weight.detach(), hd, cin) for c in cells]
+            w_h = torch.cat([c.weight.detach()[:, cin:] for c in cells])
+            packed_h = {'layers': [hnn.gboard_pack(c.weight.detach(), hd, cin) for c in cells],
+                        'grouped': hnn.gboard_pack(w_h)}
         elif hnn._DEFER is not None and hnn.board_conv_ok(h_e[:1], cells[0].weight, cin, cells[0].padding):
             packed_h = [hnn.board_conv_pack(c.weight.detach(), cin) for c in cells]
         return {'T': T, 'N': N, 'h_e': h_e, 'zx': zx, 'scalar': scalar, 'packed_h': packed_h}

@@ -60,13 +60,14 @@ class DeferredGrads:
         self.affine = {}   # (weight, bias) -> [(dweight, dbias)]
         self.adjoint = {}  # (param, in slice) -> the input-gradient conv's packed weights, packed once per step
 
-    def adjoint_pack(self, w, ci0, cin):
-        """gboard_pack_adjoint(w, ci0, cin), once per step: the weights do not change inside a step, and the
-        unroll calls a cell's input gradient 3T times."""
-        key = (id(w), ci0, cin)
+    def adjoint_pack(self, w, ci0, cin, split=False):
+        """gboard_pack_adjoint(w, ci0, cin) (split: gboard_pack_adjoint_split), once per step: the weights do not
+        change inside a step, and the unroll calls a cell's input gradient 3T times."""
+        key = (id(w), ci0, cin, split)
         pk = self.adjoint.get(key)
         if pk is None:
-            pk = self.adjoint[key] = gboard_pack_adjoint(w.detach(), ci0, cin)
+            fn = gboard_pack_adjoint_split if split else gboard_pack_adjoint
+            pk = self.adjoint[key] = fn(w.detach(), ci0, cin)
         return pk
 
     def add_conv(self, key, x, dy):
@@ -88,6 +89,11 @@ class DeferredGrads:
                 touched[id(w)] = w
                 if b is not None:
                     touched[id(b)] = b
+                continue
+            if b is None and _pointwise_board_ok(rec, wv, pad):
+                # a 1x1 conv on the 6x6 board: one HBM pass over each recorded input (hrl_gboard_pointwise_wgrad)
+                gboard_pointwise_wgrad(rec, w, sl)
+                touched[id(w)] = w
                 continue
             X = torch.cat([r[0] for r in rec]) if len(rec) > 1 else rec[0][0]
             DY = torch.cat([r[1] for r in rec]) if len(rec) > 1 else rec[0][1]
@@ -172,6 +178,38 @@ def gboard_wgrad(rec, w, b, sl):
             ctypes.cast(dyst, ctypes.c_void_p), ctypes.cast(ns, ctypes.c_void_p), n, cout, cin,
             _native.ptr(w.grad), w.shape[1], ci0, None if b is None else _native.ptr(b.grad), _native.ptr(ws),
             nbytes, stream), 'hrl_gboard_wgrad')
+
+
+def _pointwise_board_ok(rec, wv, pad):
+    """Records hrl_gboard_pointwise_wgrad covers: a 1x1 conv (O <= 8 outputs, C <= 256 inputs) on the 6x6 board,
+    fp32 CUDA, float4-aligned channel-contiguous games."""
+    if (tuple(pad) != (0, 0) or tuple(wv.shape[2:]) != (1, 1) or wv.dtype != torch.float32 or not wv.is_cuda
+            or wv.shape[0] > 8 or wv.shape[1] > 256):
+        return False
+    return all(gboard_ok(x) and gboard_ok(dy) and x.shape[1] == wv.shape[1] and dy.shape[1] == wv.shape[0]
+               and x.shape[0] == dy.shape[0] for x, dy in rec)
+
+
+def gboard_pointwise_wgrad(rec, w, sl):
+    """Add the weight gradient of the recorded (x, dy) uses of 1x1 conv weight w (input-channel slice sl) into
+    w.grad (csrc/hrl_gboard.hip, one launch pair per record)."""
+    lib = _native.load()
+    O = w.shape[0]
+    C = w.shape[1] if sl is None else sl[1] - sl[0]
+    if w.grad is None:
+        w.grad = torch.zeros_like(w)
+    g = w.grad if sl is None else w.grad[:, sl[0]:sl[1]]
+    dst = g if g.is_contiguous() else torch.zeros(O, C, 1, 1, device=w.device)
+    stream = _native.stream_of(w.device)
+    for x, dy in rec:
+        N = x.shape[0]
+        nbytes = lib.hrl_gboard_pointwise_wgrad_workspace_bytes(C, O, N)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+        _native.check(lib.hrl_gboard_pointwise_wgrad(
+            _native.ptr(x), x.stride(0), _native.ptr(dy), dy.stride(0), N, C, O, _native.ptr(dst), _native.ptr(ws),
+            nbytes, stream), 'hrl_gboard_pointwise_wgrad')
+    if dst is not g:
+        g.add_(dst)
 
 
 def _add_grad(p, g, sl):
@@ -351,6 +389,31 @@ def gboard_pack_adjoint(w, ci0, cin):
     return wpk
 
 
+def gboard_pack_adjoint_split(w, ci0, cin):
+    """The input-gradient conv of input channels [ci0, ci0 + cin) of the 3x3 weight w (Cout, Cin_total, 3, 3) split
+    over its K = Cout in 32-channel pieces: packed for gboard_conv(dy, ., S * cin, 32, groups=S), S = Cout / 32, whose
+    group s is the adjoint conv of dy's channels [32s, 32s + 32) -- the S partial input gradients, summed after."""
+    Cf = w.shape[0]
+    S = Cf // 32
+    adj = w[:, ci0:ci0 + cin].flip(2, 3).transpose(0, 1)                     # (cin, Cf, 3, 3): W'[co'][ci'][tap]
+    w_grp = adj.reshape(cin, S, 32, 3, 3).transpose(0, 1).reshape(S * cin, 32, 3, 3).contiguous()
+    return gboard_pack(w_grp)
+
+
+# the deferred 3x3 convs' input gradient with K = 64..128 (the ConvLSTM h halves' 128 -> 32) on hrl_gboard as
+# K-split partial convs (S groups of 32, one launch with S times the workgroups) + a sum, instead of
+# aten.convolution_backward
+GBOARD_ADJOINT_SPLIT = os.environ.get('HRL_GBOARD_ADJOINT_SPLIT', '1') == '1'
+
+
+def gboard_adjoint_split(dy, w, ci0, cin, rec):
+    """dx of the deferred conv (input channels [ci0, ci0 + cin) of w) for output gradient dy on hrl_gboard."""
+    N, Cf = dy.shape[0], dy.shape[1]
+    S = Cf // 32
+    part = gboard_conv(dy, rec.adjoint_pack(w, ci0, cin, split=True), S * cin, 32, groups=S)
+    return part.view(N, S, cin, 6, 6).sum(1)
+
+
 def gboard_conv(x, packed, Cout, cin_g, groups=1, x2=None, bias=None, alpha=None, beta=None, relu=False, out=None):
     """F.conv2d(x, W, bias, padding=1, groups=groups) on the 6x6 board (csrc/hrl_gboard.hip, forward only, no
     autograd), W packed by gboard_pack; optional BatchNorm-apply (y*alpha + beta) and ReLU epilogue.  x may be
@@ -430,22 +493,115 @@ class _DeferredConv(torch.autograd.Function):
         sl, pad, rec, b = ctx.meta
         dy = dy.contiguous()
         wv = w if sl is None else w[:, sl[0]:sl[1]]
-        dx = None
-        if ctx.needs_input_grad[0]:
-            Cf = w.shape[0]
-            if (GBOARD_ADJOINT and tuple(pad) == (1, 1) and tuple(w.shape[2:]) == (3, 3) and gboard_ok(dy)
-                    and (Cf <= 64 or 96 < Cf <= 128) and wv.shape[1] == x.shape[1]):
-                # the adjoint conv on hrl_gboard: K = the forward's Cout (up to 4 x 32), Cout = the slice width
-                ci0 = 0 if sl is None else sl[0]
-                dx = gboard_conv(dy, rec.adjoint_pack(w, ci0, wv.shape[1]), wv.shape[1], Cf)
-            elif _pointwise_ok(x, wv, pad):
-                N, O = dy.shape[0], dy.shape[1]
-                dx = torch.matmul(wv.detach().reshape(O, -1).t(), dy.reshape(N, O, -1)).view_as(x)
-            else:
-                dx = torch.ops.aten.convolution_backward(dy, x, wv, None, [1, 1], list(pad), [1, 1], False, [0, 0],
-                                                         1, [True, False, False])[0]
+        dx = _deferred_conv_dx(dy, x, w, sl, pad, rec) if ctx.needs_input_grad[0] else None
         rec.add_conv((w, b, sl, tuple(pad)), x, dy)
         return dx, None, None, None, None, None, None
+
+
+def _deferred_conv_dx(dy, x, w, sl, pad, rec):
+    """The input gradient of a deferred conv (input-channel slice sl of w) for output gradient dy."""
+    wv = w if sl is None else w[:, sl[0]:sl[1]]
+    Cf = w.shape[0]
+    if (GBOARD_ADJOINT_SPLIT and tuple(pad) == (1, 1) and tuple(w.shape[2:]) == (3, 3) and gboard_ok(dy)
+            and Cf % 32 == 0 and 2 <= Cf // 32 <= 8 and wv.shape[1] % 16 == 0 and wv.shape[1] == x.shape[1]
+            and dy.shape[1] == Cf):
+        return gboard_adjoint_split(dy, w, 0 if sl is None else sl[0], wv.shape[1], rec)
+    if (GBOARD_ADJOINT and tuple(pad) == (1, 1) and tuple(w.shape[2:]) == (3, 3) and gboard_ok(dy)
+            and (Cf <= 64 or 96 < Cf <= 128) and wv.shape[1] == x.shape[1]):
+        # the adjoint conv on hrl_gboard: K = the forward's Cout (up to 4 x 32), Cout = the slice width
+        ci0 = 0 if sl is None else sl[0]
+        return gboard_conv(dy, rec.adjoint_pack(w, ci0, wv.shape[1]), wv.shape[1], Cf)
+    if _pointwise_ok(x, wv, pad):
+        N, O = dy.shape[0], dy.shape[1]
+        return torch.matmul(wv.detach().reshape(O, -1).t(), dy.reshape(N, O, -1)).view_as(x)
+    return torch.ops.aten.convolution_backward(dy, x, wv, None, [1, 1], list(pad), [1, 1], False, [0, 0], 1,
+                                               [True, False, False])[0]
+
+
+class _DRCRepeat(torch.autograd.Function):
+    """One repeat of a DRC's L ConvLSTM cells in a deferred-gradient unroll (GeisterNet's learner), in two
+    launches for all L layers: the h halves as ONE grouped hrl_gboard conv over the layers' separate states
+    (hrl_gboard_forward_groups) and the gates as one hrl_lstm_gates_forward_grouped.  Both compute each layer's
+    values with the per-layer kernels' float operations (_DeferredConv + lstm_gates), so the outputs are the
+    same bits.  Backward, per layer whose outputs carry a gradient (GeisterNet: the last one): the gate
+    backward, the h half's input gradient, and the (h, dz) record of the deferred weight gradient.
+
+    apply(meta, *zx, *h, *c) -> (*h', *c'); meta = (ws, h slice of the weights, pad, packed, DeferredGrads)."""
+
+    @staticmethod
+    def forward(ctx, meta, *args):
+        ctx.set_materialize_grads(False)
+        ws, sl, pad, packed, rec = meta
+        L = len(ws)
+        zx, hs, cs = args[:L], args[L:2 * L], args[2 * L:]
+        N, H = hs[0].shape[0], hs[0].shape[1]
+        lib = _native.load()
+        stream = _native.stream_of(hs[0].device)
+        P = _native.ptr
+        zh = torch.empty(N, L * 4 * H, 6, 6, device=hs[0].device)
+        _native.check(lib.hrl_gboard_forward_groups(
+            _native.ptr_array(hs), _native.i64_array([h.stride(0) for h in hs]), N, H, L, P(packed), L * 4 * H,
+            P(zh), zh.stride(0), stream), 'hrl_gboard_forward_groups')
+        h_out = [torch.empty_like(c) for c in cs]
+        c_out = [torch.empty_like(c) for c in cs]
+        gates = [torch.empty(N, 4 * H, 6, 6, device=zh.device) for _ in range(L)]
+        _native.check(lib.hrl_lstm_gates_forward_grouped(
+            L, P(zh), zh.stride(0), _native.ptr_array(zx), _native.i64_array([z.stride(0) for z in zx]),
+            _native.ptr_array(cs), N, H, 36, _native.ptr_array(h_out), _native.ptr_array(c_out),
+            _native.ptr_array(gates), stream), 'hrl_lstm_gates_forward_grouped')
+        ctx.save_for_backward(*hs, *cs, *c_out, *gates)
+        ctx.meta = meta
+        return (*h_out, *c_out)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        ws, sl, pad, packed, rec = ctx.meta
+        L = len(ws)
+        saved = ctx.saved_tensors
+        hs, cs, c_out, gates = saved[:L], saved[L:2 * L], saved[2 * L:3 * L], saved[3 * L:]
+        dzx, dh, dc = [None] * L, [None] * L, [None] * L
+        lib = _native.load()
+        for i in range(L):
+            gh, gc = grads[i], grads[L + i]
+            if gh is None and gc is None:
+                continue
+            N, G = gates[i].shape[0], gates[i].shape[1]
+            dz = torch.empty_like(gates[i])
+            dci = torch.empty_like(cs[i])
+            gh = None if gh is None else gh.contiguous()
+            gc = None if gc is None else gc.contiguous()
+            _native.check(lib.hrl_lstm_gates_backward(
+                _native.ptr(gates[i]), _native.ptr(cs[i]), _native.ptr(c_out[i]), _native.ptr(gh), _native.ptr(gc),
+                N, G // 4, 36, _native.ptr(dz), _native.ptr(dci), _native.stream_of(dz.device)),
+                'hrl_lstm_gates_backward')
+            if ctx.needs_input_grad[1 + i]:
+                dzx[i] = dz
+            if ctx.needs_input_grad[1 + L + i]:
+                dh[i] = _deferred_conv_dx(dz, hs[i], ws[i], sl, pad, rec)
+            if ctx.needs_input_grad[1 + 2 * L + i]:
+                dc[i] = dci
+            rec.add_conv((ws[i], None, sl, tuple(pad)), hs[i], dz)
+        return (None, *dzx, *dh, *dc)
+
+
+def drc_repeat_ok(zx, hs, cs, ws, pad):
+    """_DRCRepeat covers: 1..4 layers of 3x3 'same' cells on the 6x6 board, H = 32 hidden channels, fp32 CUDA
+    float4-aligned games (zx may be channel slices of a wider tensor)."""
+    L = len(ws)
+    if not (1 <= L <= 4 and tuple(pad) == (1, 1)):
+        return False
+    H = hs[0].shape[1]
+    return (H == 32 and all(tuple(w.shape[2:]) == (3, 3) and w.shape[0] == 4 * H for w in ws)
+            and all(gboard_ok(t) for t in hs) and all(gboard_ok(t) and t.is_contiguous() for t in cs)
+            and all(gboard_ok(z) and z.shape[1] == 4 * H for z in zx)
+            and all(t.shape[0] == hs[0].shape[0] for t in (*zx, *hs, *cs)))
+
+
+def drc_repeat(zx, hs, cs, ws, sl, pad, packed):
+    """One repeat of the DRC cells in a deferred unroll (_DRCRepeat); returns (hs', cs')."""
+    L = len(ws)
+    out = _DRCRepeat.apply((ws, sl, tuple(pad), packed, _DEFER), *zx, *hs, *cs)
+    return list(out[:L]), list(out[L:])
 
 
 def conv2d(x, w, b=None, padding=(0, 0), in_slice=None, packed=None):

@@ -223,6 +223,13 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
 int hrl_lstm_gates_forward(const float *zx, int64_t zx_stride, const float *zh, const float *c, int64_t N, int64_t H,
                            int64_t HW, const float *bias, int64_t bias_rows, float *h_out, float *c_out, float *gates,
                            void *stream);
+/* hrl_lstm_gates_forward_grouped: the L (<= 4) cells of one DRC repeat in one launch; layer l's zh is channels
+ * [l*4H, (l+1)*4H) of one grouped convolution's output (per-sample stride zh_stride floats), zx[l] its x half
+ * (per-sample stride zx_strides[l]), c[l] its state; writes h_out[l], c_out[l] (contiguous (N, H, HW)) and, when
+ * gates is given, gates[l] (N, 4H, HW).  hrl_lstm_gates_forward's float operations (z = zx + zh). */
+int hrl_lstm_gates_forward_grouped(int L, const float *zh, int64_t zh_stride, const float *const *zx,
+                                   const int64_t *zx_strides, const float *const *c, int64_t N, int64_t H, int64_t HW,
+                                   float *const *h_out, float *const *c_out, float *const *gates, void *stream);
 int hrl_lstm_gates_backward(const float *gates, const float *c, const float *c_out, const float *dh,
                             const float *dc_out, int64_t N, int64_t H, int64_t HW, float *dz, float *dc,
                             void *stream);
@@ -335,11 +342,25 @@ int hrl_gboard_pack_adjoint(const float *weight, int64_t Cout_fwd, int64_t w_cin
  * dbias is given, into dbias (Cout).  Games are the MFMA K (exact bf16 split, fp32-accurate); deterministic.
  * Replaces the deferred weight gradient's aten.convolution_backward (nn.DeferredGrads.flush).  32-channel tiles
  * (Cout, Cin): 4x1, 2x2, 2x1, 1x2, 1x1.  workspace: hrl_gboard_wgrad_workspace_bytes(Cout, Cin, sum ns) bytes. */
+/* hrl_gboard_pointwise_wgrad: dweight (O, C) += sum over N games and the 36 cells of dy[n][o][q] x[n][c][q] -- the
+ * weight gradient of a 1x1 conv on the 6x6 board (O <= 8, C <= 256; games x_stride / dy_stride floats apart,
+ * float4-aligned).  Deterministic (per-workgroup partials folded in order).  workspace:
+ * hrl_gboard_pointwise_wgrad_workspace_bytes(C, O, N) bytes. */
+int64_t hrl_gboard_pointwise_wgrad_workspace_bytes(int64_t C, int64_t O, int64_t N);
+int hrl_gboard_pointwise_wgrad(const float *x, int64_t x_stride, const float *dy, int64_t dy_stride, int64_t N,
+                               int64_t C, int64_t O, float *dweight, void *workspace, int64_t workspace_bytes,
+                               void *stream);
 int64_t hrl_gboard_wgrad_workspace_bytes(int64_t Cout, int64_t Cin, int64_t total_games);
 int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const float *const *dys,
                      const int64_t *dy_strides, const int64_t *ns, int nseg, int64_t Cout, int64_t Cin,
                      float *dweight, int64_t w_cin_total, int64_t w_ci0, float *dbias, void *workspace,
                      int64_t workspace_bytes, void *stream);
+/* hrl_gboard_forward_groups: a grouped conv (groups <= 4, Cin_g <= 32 per group) whose groups read separate
+ * inputs xs[g] (N games, x_strides[g] floats apart): the DRC layers' h halves of one repeat without stacking
+ * their states.  No bias / epilogue. */
+int hrl_gboard_forward_groups(const float *const *xs, const int64_t *x_strides, int64_t N, int64_t Cin_g,
+                              int64_t groups, const void *packed, int64_t Cout, float *y, int64_t y_stride,
+                              void *stream);
 int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_t x2_stride, int64_t N, int64_t Cin_g,
                        int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
                        const float *beta, int relu, float *y, int64_t y_stride, void *stream);

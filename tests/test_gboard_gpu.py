@@ -212,3 +212,83 @@ def test_gboard_wgrad_matches_conv_weight_gradient(cuda, cout, cin_total, ci0, c
             assert torch.equal(b.grad.double().cpu(), bref)
         else:
             assert (b.grad.double().cpu() - bref).abs().max().item() <= 4e-6 * DY.abs().sum((0, 2, 3)).max().item()
+
+
+@pytest.mark.parametrize('N,cout_fwd,ci0,cin', [(37, 128, 32, 32), (256, 128, 32, 32), (20, 64, 0, 32),
+                                                (9, 96, 16, 48)])
+def test_gboard_adjoint_split_matches_conv_input_gradient(cuda, N, cout_fwd, ci0, cin):
+    """The K-split input gradient (nn.gboard_adjoint_split: S = Cout / 32 partial adjoint convs as one grouped
+    hrl_gboard launch, then their sum) == the input gradient of F.conv2d(x, w[:, ci0:ci0+cin], padding=1): exactly
+    the fp64 result on integer data, within 4e-6 of its scale on random data."""
+    for integer in (True, False):
+        g = torch.Generator().manual_seed(N + cout_fwd + ci0 + int(integer))
+        mk = ((lambda *s: torch.randint(-3, 4, s, generator=g).float()) if integer else
+              (lambda *s: torch.randn(*s, generator=g)))
+        w = mk(cout_fwd, ci0 + cin + 3, 3, 3)
+        dy = mk(N, cout_fwd, 6, 6)
+        x = torch.zeros(N, cin, 6, 6, dtype=torch.float64, requires_grad=True)
+        F.conv2d(x, w[:, ci0:ci0 + cin].double(), padding=1).backward(dy.double())
+        ref = x.grad
+        rec = hnn.DeferredGrads()
+        y = hnn.gboard_adjoint_split(dy.to(cuda), w.to(cuda), ci0, cin, rec).cpu().double()
+        if integer:
+            assert torch.equal(y, ref)
+        else:
+            assert _close(y, ref)
+
+
+def test_gboard_forward_groups_and_grouped_gates(cuda):
+    """hrl_gboard_forward_groups (each group reads its own input tensor) == the grouped conv of the stacked inputs,
+    bit for bit; hrl_lstm_gates_forward_grouped == one lstm_gates per layer on the conv's channel slices, bit for
+    bit (zx a channel slice of a wider tensor, ragged game count)."""
+    from handyrl_amd import _native
+    lib = _native.load()
+    g = torch.Generator().manual_seed(11)
+    N, H, L = 45, 32, 3
+    hs = [torch.randn(N, H, 6, 6, generator=g).to(cuda) for _ in range(L)]
+    cs = [torch.randn(N, H, 6, 6, generator=g).to(cuda) for _ in range(L)]
+    wide = torch.randn(N, 4 * H * L + 32, 6, 6, generator=g).to(cuda)
+    zx = [wide[:, 4 * H * i:4 * H * (i + 1)] for i in range(L)]
+    w = (torch.randn(4 * H * L, H, 3, 3, generator=g) * 0.2).to(cuda)
+    pk = hnn.gboard_pack(w)
+    ref = hnn.gboard_conv(torch.cat(hs, 1), pk, 4 * H * L, H, groups=L)
+    zh = torch.empty_like(ref)
+    P = _native.ptr
+    stream = _native.stream_of(cuda)
+    _native.check(lib.hrl_gboard_forward_groups(_native.ptr_array(hs), _native.i64_array([h.stride(0) for h in hs]),
+                                                N, H, L, P(pk), 4 * H * L, P(zh), zh.stride(0), stream), 'groups')
+    assert torch.equal(zh, ref)
+    h_out = [torch.empty_like(c) for c in cs]
+    c_out = [torch.empty_like(c) for c in cs]
+    gates = [torch.empty(N, 4 * H, 6, 6, device=cuda) for _ in range(L)]
+    _native.check(lib.hrl_lstm_gates_forward_grouped(
+        L, P(zh), zh.stride(0), _native.ptr_array(zx), _native.i64_array([z.stride(0) for z in zx]),
+        _native.ptr_array(cs), N, H, 36, _native.ptr_array(h_out), _native.ptr_array(c_out), _native.ptr_array(gates),
+        stream), 'gates')
+    for i in range(L):
+        hn, cn = hnn.lstm_gates(zx[i], zh[:, 4 * H * i:4 * H * (i + 1)], cs[i])
+        assert torch.equal(h_out[i], hn) and torch.equal(c_out[i], cn), i
+
+
+@pytest.mark.parametrize('O,C,ns', [(1, 64, (300,)), (4, 8, (37, 5)), (8, 256, (64,))])
+def test_gboard_pointwise_wgrad_matches_conv1x1_weight_gradient(cuda, O, C, ns):
+    """hrl_gboard_pointwise_wgrad ADDS the 1x1 conv's weight gradient sum_{n,q} dy[n,o,q] x[n,c,q] over the records
+    into an existing gradient: exactly the fp64 sum on integer data, within 4e-6 of its scale on random data."""
+    for integer in (True, False):
+        g = torch.Generator().manual_seed(O * 31 + C + int(integer))
+        mk = ((lambda *s: torch.randint(-3, 4, s, generator=g).float()) if integer else
+              (lambda *s: torch.randn(*s, generator=g)))
+        w = torch.nn.Parameter(torch.zeros(O, C, 1, 1, device=cuda))
+        w.grad = mk(O, C, 1, 1).to(cuda)
+        before = w.grad.double().cpu()
+        rec = [(mk(n, C, 6, 6).to(cuda), mk(n, O, 6, 6).to(cuda)) for n in ns]
+        hnn.gboard_pointwise_wgrad(rec, w, None)
+        X = torch.cat([r[0] for r in rec]).double().cpu()
+        DY = torch.cat([r[1] for r in rec]).double().cpu()
+        dw = torch.einsum('noq,ncq->oc', DY.reshape(DY.shape[0], O, 36), X.reshape(X.shape[0], C, 36))
+        ref = before + dw.view(O, C, 1, 1)
+        got = w.grad.double().cpu()
+        if integer:
+            assert torch.equal(got, ref)
+        else:
+            assert (got - ref).abs().max().item() <= 4e-6 * dw.abs().max().item()

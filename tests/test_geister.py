@@ -389,3 +389,42 @@ def test_fused_gate_repeats_match_unfused(cuda, inplace, repeats):
             DRC.fuse_gates = False
     for a, b in zip(*results):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('graph', [False, True])
+def test_grouped_drc_repeat_matches_per_layer_unroll(cuda, graph):
+    """The learner's unroll with each DRC repeat as one grouped h-half conv + one grouped gate launch
+    (nn.drc_repeat: hrl_gboard_forward_groups, hrl_lstm_gates_forward_grouped) against the per-layer launches
+    (_DeferredConv + lstm_gates): two LearnerSteps from the same seeded net on the same batch (ragged game
+    count) give the same losses, grad norms and updated weights, bit for bit -- each layer's values are the
+    per-layer kernels' float operations and the backward records the same (h, dz) pairs in the same order.
+    (The stem's weights aside: see below.)"""
+    from handyrl_amd.envs.geister import DRC
+    from handyrl_amd.synthetic import geister_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    B, T = 13, 5
+    args = default_args(T, B)
+    batch = geister_batch(B, T, cuda, seed=7)
+    res = []
+    prev = DRC.group_repeat
+    try:
+        for grouped in (False, True):
+            DRC.group_repeat = grouped
+            net = seeded_net()
+            step = LearnerStep(net, args, cuda, graph=graph)
+            outs = []
+            for _ in range(2):
+                hidden = tuple([h.to(cuda) for h in hs] for hs in net.init_hidden([B, 2]))
+                out = step.step(batch, hidden)
+                outs.append({k: float(out[k]) for k in ('p', 'v', 'r', 'ent', 'total', 'grad_norm')})
+            res.append((outs, {n: p.detach().clone() for n, p in step.net.named_parameters()}))
+    finally:
+        DRC.group_repeat = prev
+    (o0, w0), (o1, w1) = res
+    assert o0 == o1, (o0, o1)
+    # the stem's weights see the vendor convolution backward (MIOpen), which is not run-to-run deterministic
+    # itself (the per-layer unroll twice differs there by ~1e-9): those within 1e-7, everything else exact
+    stem = ('conv1.weight', 'bn1.weight', 'bn1.bias')
+    diff = {n: float((w1[n] - w0[n]).abs().max()) for n in w0 if not torch.equal(w0[n], w1[n])}
+    assert all(n in stem and d < 1e-7 for n, d in diff.items()), diff
