@@ -156,11 +156,14 @@ SIGNATURES = {
     'hrl_gboard_wgrad': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_int, _i64, _i64, _f32p, _i64, _i64, _f32p,
                                         ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_gboard_set_whole_ring': (ctypes.c_int, [ctypes.c_int]),
     'hrl_gboard_pointwise_wgrad_workspace_bytes': (_i64, [_i64, _i64, _i64]),
     'hrl_gboard_pointwise_wgrad': (ctypes.c_int, [_f32p, _i64, _f32p, _i64, _i64, _i64, _i64, _f32p, ctypes.c_void_p,
                                                   _i64, ctypes.c_void_p]),
     'hrl_gboard_forward_groups': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, _i64, _i64, _i64, ctypes.c_void_p,
                                                  _i64, _f32p, _i64, ctypes.c_void_p]),
+    'hrl_lstm_gates_backward_ex': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _i64, ctypes.c_int, _i64, _f32p, _i64,
+                                                  _i64, _i64, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_void_p]),
     'hrl_lstm_gates_forward_grouped': (ctypes.c_int, [ctypes.c_int, _f32p, _i64, ctypes.c_void_p, ctypes.c_void_p,
                                                       ctypes.c_void_p, _i64, _i64, _i64, ctypes.c_void_p,
                                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -168,8 +171,6 @@ SIGNATURES = {
                                           _f32p, _f32p, ctypes.c_int, _f32p, _i64, ctypes.c_void_p]),
     'hrl_gboard_pointwise': (ctypes.c_int, [_f32p, _i64, _i64, _f32p, _i64, _i64, _i64, _f32p, _i64, _f32p, _f32p,
                                             ctypes.c_int, _f32p, _i64, ctypes.c_void_p]),
-    'hrl_gboard_lstm_forward': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _i64, ctypes.c_void_p, _f32p, _i64, _f32p,
-                                               _f32p, _f32p, _i64, _f32p, _i64, ctypes.c_void_p]),
     'hrl_torus_head_pool': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, _i64, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_torus_head_unpool': (ctypes.c_int, [_f32p, _f32p, _f32p, _i64, _i64, _i64, _i64, _f32p,
                                              ctypes.c_void_p]),

@@ -1780,427 +1780,6 @@ __global__ __launch_bounds__(bb2::kThreads) void conv3x3_fwd_dma_kernel(BlockBwd
     }
 }
 
-// ------------------------------------------------------------------ one chain block's backward, LDS-DMA ring
-// conv3x3_block_bwd3_kernel<PRO, EPI> (EPI 0, 2, 3): bb2's arithmetic -- the same dY (bn_bwd_apply_kernel's float
-// operations), the same x', the same split MFMA orders, so gin is bit-identical to bb2 and the weight gradient sums
-// the same pairs in the same per-tile order -- on a pipeline with more bytes in flight.  bb2 kept every tile's g, y
-// and x in registers one tile ahead (≈55 KB per CU, issued in one burst per tile) and its no-MFMA variant alone ran
-// at ≈4.5 TB/s.  Here
-//  * x streams into a kSlots-deep LDS ring by LDS-DMA, issued by the input-gradient waves 0-3 (which issue no
-//    ordinary loads: hipcc drains every LDS-DMA at the first use of an ordinary load's result in the same wave),
-//    kSlots-1 tiles ahead; the ring also feeds the epilogue's raw x (bb2's separate x region is gone);
-//  * waves 4-7 load g and y into registers one tile ahead and stage BOTH images of the next tile (dY and x');
-//  * the x' image is single-buffered, which is what makes the ring fit in LDS beside the double-buffered dY
-//    images, so each tile has two phases: A) the weight-gradient waves read x'(k), dY(k) and run their MFMAs;
-//    B) the input-gradient waves run theirs on dY(k) and store gin while the weight-gradient waves overwrite x'
-//    with x'(k+1) and stage dY(k+1) into the other buffer.  Each SIMD hosts one wave of each kind (w, w+4), so
-//    one wave's MFMAs run beside the other's idle phase or its staging VALU in both phases.
-// Rows past the batch: their LDS-DMA is dropped (stale ring rows), so the stagers write x' = 0 and dY = 0 there
-// and the epilogue selects them out before any arithmetic on the raw x.
-namespace bb3 {
-
-constexpr int kSlots = 4;
-constexpr int kRawBytes = kTile * kRow * 4;                 // 18,432
-constexpr int kPieces = kRawBytes / 1024;                   // 18
-constexpr int kDy0 = 0;                                     // dY images, buffers 0/1
-constexpr int kXp0 = 2 * bb2::kImgBytes;                    // the x' image (one buffer)
-constexpr int kRaw0 = kXp0 + bb2::kImgBytes;                // the raw-x ring
-constexpr int kLdsBytes = kRaw0 + kSlots * kRawBytes;       // 156,672 B
-static_assert(kLdsBytes <= 160 * 1024, "LDS");
-
-// One LDS-DMA piece, buffer_load_dwordx4 ... lds (16 B per lane to M0 + 16 * lane), written as inline asm so that
-// hipcc does not see it: the compiler tracks a builtin LDS-DMA as a pending LDS write and waits vmcnt(0) before
-// the next ds_read of ANY LDS address (it drained the ring every tile); the waves issuing these count their own
-// vmcnt by hand (fw3::vm_wait).  M0 is saved and restored inside the statement (cdna_hip_programming.md).
-__device__ __forceinline__ void dma16(u32x4 desc, uint32_t voff, uint32_t lds_byte) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(voff), "s"(desc), "s"(lds_byte)
-                 : "memory");
-}
-
-// the buffer descriptor of wave_rsrc as four wave-uniform dwords (for the inline-asm buffer ops)
-__device__ __forceinline__ u32x4 wave_desc(const void *base, uint32_t bytes) {
-    const uint64_t p = reinterpret_cast<uint64_t>(base);
-    u32x4 d;
-    d.x = __builtin_amdgcn_readfirstlane((uint32_t)p);
-    d.y = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) & 0xffffu;
-    d.z = __builtin_amdgcn_readfirstlane(bytes);
-    d.w = 0x00020000u;
-    return d;
-}
-
-template <int W> __device__ constexpr int pieces_of() {     // pieces p = W, W+4, ... of a tile: issued by IG wave W
-    int n = 0;
-    for (int p = W; p < kPieces; p += 4) ++n;
-    return n;
-}
-
-template <bool PRO, int EPI, int W>
-__device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, int lane) {
-    using R = bb2::Role<W>;
-    constexpr bool kIg = R::kIg;
-    const int ch = lane & 31;
-    const int64_t ntiles = (a.M + kTile - 1) / kTile;
-    const int64_t t0 = blockIdx.x;
-    const int64_t step = gridDim.x;
-    const int n_iter = t0 < ntiles ? (int)((ntiles - 1 - t0) / step + 1) : 0;
-    auto rows_of = [&](int it) __attribute__((always_inline)) {
-        const int64_t t = t0 + (int64_t)it * step;
-        return it < n_iter ? (int)min<int64_t>(kTile, a.M - t * kTile) : 0;
-    };
-    auto rsrc_of = [&](const float *base, int it) __attribute__((always_inline)) {
-        const int64_t t = t0 + (int64_t)it * step;
-        const int rows = rows_of(it);
-        return wave_rsrc(base + (it < n_iter ? t * kTile * kRow : 0), (uint32_t)rows * kRow * 4);
-    };
-    double s1 = 0.0, s2 = 0.0;
-    if constexpr (kIg) {
-        // ---- input-gradient waves: the x ring's LDS-DMA, the input gradient, the epilogue
-        constexpr int kNq = R::kNq;
-        constexpr int kCt = R::kCt;
-        constexpr int NP = pieces_of<W>();
-        constexpr int NS = kNq > 4 ? 8 : 4;                 // gin stores per tile
-        uint4 wh[kTaps], wm[kTaps], wl[kTaps];
-        {
-            const int ci0 = 8 * (lane >> 4), j = lane & 15;
-#pragma unroll
-            for (int t = 0; t < kTaps; ++t) {
-                if (!bb2::uses_tap<W>(t)) continue;
-                uint32_t hv[4], mv[4], lv[4];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int tc = t * 2 + kCt;
-                    const float w0 = a.wpk[(tc * kC + ci0 + 2 * d) * 16 + j];
-                    const float w1 = a.wpk[(tc * kC + ci0 + 2 * d + 1) * 16 + j];
-                    uint32_t h0, m0, l0, h1, m1, l1;
-                    hrl_split::split3(w0, h0, m0, l0);
-                    hrl_split::split3(w1, h1, m1, l1);
-                    hv[d] = h0 | (h1 << 16);
-                    mv[d] = m0 | (m1 << 16);
-                    lv[d] = l0 | (l1 << 16);
-                }
-                wh[t] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
-                wm[t] = make_uint4(mv[0], mv[1], mv[2], mv[3]);
-                wl[t] = make_uint4(lv[0], lv[1], lv[2], lv[3]);
-            }
-        }
-        float em = 0.f, ea = 1.f, eb = 0.f;     // epilogue 2: BN_{i-1} of this lane's output channel
-        if constexpr (EPI == 2) {
-            em = a.ep_mean[kCt * 16 + (lane & 15)];
-            ea = a.ep_alpha[kCt * 16 + (lane & 15)];
-            eb = a.ep_beta[kCt * 16 + (lane & 15)];
-        }
-        const uint32_t smem_base = (uint32_t)(uintptr_t)smem;
-        auto dma = [&](int it) __attribute__((always_inline)) {
-            const int64_t t = t0 + (int64_t)it * step;
-            const u32x4 desc = wave_desc(a.x + (it < n_iter ? t * kTile * kRow : 0), (uint32_t)rows_of(it) * kRow * 4);
-            const uint32_t raw = smem_base + kRaw0 + (uint32_t)(it % kSlots) * kRawBytes;
-#pragma unroll
-            for (int j = 0; j < NP; ++j) {
-                const int p = W + 4 * j;
-                dma16(desc, p * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(raw + p * 1024));
-            }
-        };
-        const int co = kCt * 16 + (lane & 15);
-        const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-        const int tr_sub = 8 * (pp & 1);
-        // prologue: tiles 0 .. kSlots-2 in flight; tile 0 landed before the stagers' first barrier
-#pragma unroll
-        for (int j = 0; j < kSlots - 1; ++j) dma(j);
-        fw3::vm_wait<(kSlots - 2) * NP>();
-        bb2::bar_lds();                                     // P1: tile 0 in the ring
-        bb2::bar_lds();                                     // P2: tile 0's images staged
-        for (int it = 0; it < n_iter; ++it) {
-            // ---- phase A: the weight-gradient waves' MFMAs; here the ring's next tile
-            dma(it + kSlots - 1);                           // into tile it-1's slot (free since the last barrier)
-            // tile it+1 must have landed before the stagers read it in phase B: the younger VMEM operations are
-            // this wave's later DMA groups and gin stores (2 of each in the steady state)
-            if (it >= 2) fw3::vm_wait<2 * (NP + NS)>();
-            else if (it == 1) fw3::vm_wait<2 * NP + NS>();
-            else fw3::vm_wait<2 * NP>();
-            bb2::bar_lds();                                 // mid: x'(it) read, tile it+1 in the ring
-            // ---- phase B: input gradient of tile it
-            const unsigned char *dyi = smem + kDy0 + (it & 1) * bb2::kImgBytes;
-            f32x4 acc[kNq];
-#pragma unroll
-            for (int s = 0; s < kNq; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int p = 0; p < kCells; ++p) {
-                if (!bb2::uses_p<W>(p)) continue;
-                uint32_t A[3][4];
-#pragma unroll
-                for (int part = 0; part < 3; ++part) {
-#pragma unroll
-                    for (int hlf = 0; hlf < 2; ++hlf) {
-                        const int o = part * bb2::kPartBytes + bb2::img_off(p, 8 * g + 4 * hlf + qq, pp >> 1) + tr_sub;
-                        const bb2::v4s r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                            (bb2::lds_v4s *)((__attribute__((address_space(3))) unsigned char *)(dyi + o)));
-                        const uint2 u = __builtin_bit_cast(uint2, r);
-                        A[part][2 * hlf] = u.x;
-                        A[part][2 * hlf + 1] = u.y;
-                    }
-                }
-                const uint4 Ah = make_uint4(A[0][0], A[0][1], A[0][2], A[0][3]);
-                const uint4 Am = make_uint4(A[1][0], A[1][1], A[1][2], A[1][3]);
-                const uint4 Al = make_uint4(A[2][0], A[2][1], A[2][2], A[2][3]);
-#pragma unroll
-                for (int s = 0; s < R::kNq; ++s) {
-                    const int tap = tap_of(p, R::kQ[s]);
-                    if (tap < 0) continue;
-                    f32x4 c = acc[s];
-                    c = mfma_bf16(Al, wh[tap], c);   // smallest terms first (bb2's order)
-                    c = mfma_bf16(Am, wm[tap], c);
-                    c = mfma_bf16(Ah, wl[tap], c);
-                    c = mfma_bf16(Am, wh[tap], c);
-                    c = mfma_bf16(Ah, wm[tap], c);
-                    c = mfma_bf16(Ah, wh[tap], c);
-                    acc[s] = c;
-                }
-            }
-            // epilogue (bb2's): BN_{i-1}'s sums / the stem ReLU mask from the raw x in the ring, gin stores
-            const int rows = rows_of(it);
-            const __amdgpu_buffer_rsrc_t ro = rsrc_of(a.gin, it);
-            float rv[kNq < 4 ? 4 : kNq][4];
-            if constexpr (EPI == 2 || EPI == 3) {
-                const float *xr = reinterpret_cast<const float *>(smem + kRaw0 + (it % kSlots) * kRawBytes);
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    const int row = (lane >> 4) * 4 + rr;
-#pragma unroll
-                    for (int s = 0; s < R::kNq; ++s) rv[s][rr] = xr[row * kRow + co * kCells + R::kQ[s]];
-                }
-            }
-            if constexpr (EPI == 2) {   // bn_bwd_reduce_kernel's mask and sums (rows past the batch selected out)
-                float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-                for (int s = 0; s < R::kNq; ++s) {
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        const int row = (lane >> 4) * 4 + rr;
-                        const bool ok = row < rows;
-                        const float x0 = ok ? rv[s][rr] : 0.f;
-                        const float gm = (x0 * ea + eb > 0.f && ok) ? acc[s][rr] : 0.f;
-                        t1 += gm;
-                        t2 += gm * (x0 - em);
-                    }
-                }
-                s1 += (double)t1;
-                s2 += (double)t2;
-            }
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int row = (lane >> 4) * 4 + rr;
-                const int off = (row * kRow + co * kCells + R::kQ[0]) * 4;
-                float v[kNq];
-#pragma unroll
-                for (int s = 0; s < R::kNq; ++s) {
-                    v[s] = acc[s][rr];
-                    if constexpr (EPI == 3)
-                        if (!(rv[s][rr] > 0.f)) v[s] = 0.f;
-                }
-                u32x4 w;
-                w.x = __float_as_uint(v[0]);
-                w.y = __float_as_uint(v[1]);
-                w.z = __float_as_uint(v[2]);
-                w.w = __float_as_uint(v[3]);
-                __builtin_amdgcn_raw_buffer_store_b128(w, ro, off, 0, 0);
-                if constexpr (R::kNq > 4)
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[4 % kNq]), ro, off + 16, 0, 0);
-            }
-            bb2::bar_lds();                                 // end: dY(it) read, tile it's slot free
-        }
-        fw3::vm_wait<0>();
-    } else {
-        // ---- weight-gradient waves: g, y loads one tile ahead; both images of the next tile; the weight gradient
-        constexpr int S = W - 4;
-        const int hh = lane >> 5;
-        const float mu = a.bn_mean[ch], kk = a.bn_k[ch], gmn = a.bn_gm[ch], is = a.bn_invstd[ch];
-        const float ww = a.bn_w ? a.bn_w[ch] : 1.0f;
-        const float al = is * ww;
-        const float be = (a.bn_b ? a.bn_b[ch] : 0.0f) - mu * al;
-        float pa = 1.f, pb = 0.f;
-        if constexpr (PRO) {
-            pa = a.in_alpha[ch];
-            pb = a.in_beta[ch];
-        }
-        f32x16 wacc[R::kNt];
-#pragma unroll
-        for (int t = 0; t < R::kNt; ++t)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) wacc[t][i] = 0.f;
-        const int c0 = hh ? 4 : 0;
-        int rho[2];
-#pragma unroll
-        for (int v = 0; v < 2; ++v) rho[v] = 2 * ((S + 4 * v + (ch >> 2)) & 7);   // bb2 staging wave S+4v's rows
-        float G[2][2][5], Y[2][2][5];
-        auto issue = [&](int it) __attribute__((always_inline)) {   // g, y of tile it (zeros past the end)
-            const __amdgpu_buffer_rsrc_t rg = rsrc_of(a.g, it), ry = rsrc_of(a.y, it);
-#pragma unroll
-            for (int v = 0; v < 2; ++v)
-#pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    const int off = ((rho[v] + r) * kRow + ch * kCells + c0) * 4;
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        float(&d)[5] = k == 0 ? G[v][r] : Y[v][r];
-                        const __amdgpu_buffer_rsrc_t rs = k == 0 ? rg : ry;
-                        const u32x3 u3 = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
-                        const u32x2 u2 = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 12, 0, 0);
-                        d[0] = __uint_as_float(u3.x);
-                        d[1] = __uint_as_float(u3.y);
-                        d[2] = __uint_as_float(u3.z);
-                        d[3] = __uint_as_float(u2.x);
-                        d[4] = __uint_as_float(u2.y);
-                    }
-                }
-        };
-        auto stage = [&](int it) __attribute__((always_inline)) {   // dY(it) -> buffer it & 1, x'(it) -> the x' image
-            const int rows = rows_of(it);
-            const float *raw = reinterpret_cast<const float *>(smem + kRaw0 + (it % kSlots) * kRawBytes);
-            unsigned char *dyi = smem + kDy0 + (it & 1) * bb2::kImgBytes;
-            unsigned char *xi = smem + kXp0;
-#pragma unroll
-            for (int v = 0; v < 2; ++v) {
-                uint32_t dp[3][5], xp[3][5];
-#pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    const bool valid = rho[v] + r < rows;
-                    const float *src = raw + (rho[v] + r) * kRow + ch * kCells + c0;
-#pragma unroll
-                    for (int i = 0; i < 5; ++i) {
-                        // dY = BN_i backward apply (bn_bwd_apply_kernel's float operations); rows past the batch 0
-                        const float yv = Y[v][r][i];
-                        float gv = G[v][r][i];
-                        if (!(yv * al + be > 0.f)) gv = 0.f;
-                        const float tt = (yv - mu) * kk;
-                        float d = (((gv - gmn) - tt) * is) * ww;
-                        d = valid ? d : 0.f;
-                        float xv = src[i];
-                        if constexpr (PRO) {   // bn_apply_kernel's float operations
-                            const float u = xv * pa + pb;
-                            xv = u < 0.f ? 0.f : u;
-                        }
-                        xv = valid ? xv : 0.f;
-                        uint32_t h, m, l, xh, xm, xl;
-                        hrl_split::split3(d, h, m, l);
-                        hrl_split::split3(xv, xh, xm, xl);
-                        if (r == 0) {
-                            dp[0][i] = h; dp[1][i] = m; dp[2][i] = l;
-                            xp[0][i] = xh; xp[1][i] = xm; xp[2][i] = xl;
-                        } else {
-                            dp[0][i] |= h << 16; dp[1][i] |= m << 16; dp[2][i] |= l << 16;
-                            xp[0][i] |= xh << 16; xp[1][i] |= xm << 16; xp[2][i] |= xl << 16;
-                        }
-                    }
-                }
-                const int half = rho[v] >> 3, sub = 2 * (rho[v] & 7);
-#pragma unroll
-                for (int i = 0; i < 5; ++i) {
-                    const int o = bb2::img_off(c0 + i, ch, half) + sub;
-#pragma unroll
-                    for (int part = 0; part < 3; ++part) {
-                        *reinterpret_cast<uint32_t *>(dyi + part * bb2::kPartBytes + o) = dp[part][i];
-                        *reinterpret_cast<uint32_t *>(xi + part * bb2::kPartBytes + o) = xp[part][i];
-                    }
-                }
-            }
-        };
-        issue(0);
-        bb2::bar_lds();                                     // P1: tile 0 in the ring
-        stage(0);
-        issue(1);
-        bb2::bar_lds();                                     // P2: tile 0's images staged
-        for (int it = 0; it < n_iter; ++it) {
-            // ---- phase A: weight gradient of tile it, dW[tap] += x'_p^T (32 ci x 16 rows) . dY_q, p ascending
-            {
-                const unsigned char *dyi = smem + kDy0 + (it & 1) * bb2::kImgBytes;
-                const unsigned char *xi = smem + kXp0;
-                const int kg = lane >> 5;
-#pragma unroll
-                for (int p = 0; p < kCells; ++p) {
-                    if (!bb2::uses_p<W>(p)) continue;
-                    const int o = bb2::img_off(p, ch, kg);
-                    const uint4 Ah = *reinterpret_cast<const uint4 *>(xi + o);
-                    const uint4 Am = *reinterpret_cast<const uint4 *>(xi + bb2::kPartBytes + o);
-                    const uint4 Al = *reinterpret_cast<const uint4 *>(xi + 2 * bb2::kPartBytes + o);
-#pragma unroll
-                    for (int s = 0; s < R::kNt; ++s) {
-                        const int dy = R::kTap[s] / 3, dx = R::kTap[s] % 3;
-                        const int qy = p / 3 - dy + 1, qx = p % 3 - dx + 1;
-                        if (qy < 0 || qy > 2 || qx < 0 || qx > 2) continue;
-                        const int ob = bb2::img_off(qy * 3 + qx, ch, kg);
-                        const uint4 Bh = *reinterpret_cast<const uint4 *>(dyi + ob);
-                        const uint4 Bm = *reinterpret_cast<const uint4 *>(dyi + bb2::kPartBytes + ob);
-                        const uint4 Bl = *reinterpret_cast<const uint4 *>(dyi + 2 * bb2::kPartBytes + ob);
-                        f32x16 c = wacc[s];
-                        c = mfma32(Al, Bh, c);   // smallest terms first
-                        c = mfma32(Am, Bm, c);
-                        c = mfma32(Ah, Bl, c);
-                        c = mfma32(Am, Bh, c);
-                        c = mfma32(Ah, Bm, c);
-                        c = mfma32(Ah, Bh, c);
-                        wacc[s] = c;
-                    }
-                }
-            }
-            bb2::bar_lds();                                 // mid: x'(it) read, tile it+1 in the ring
-            // ---- phase B: the next tile's images (runs unconditionally: past the last tile it stages zeros)
-            stage(it + 1);
-            issue(it + 2);
-            bb2::bar_lds();                                 // end
-        }
-        // weight-gradient partials partial[block][tap][ci][co] (bb2's layout; one owner wave per tap)
-        constexpr int kW = kTaps * kC * kC;
-        float *outp = a.wpart + (int64_t)blockIdx.x * kW;
-        const int h = lane >> 5;
-#pragma unroll
-        for (int s = 0; s < R::kNt; ++s)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int ci = (i & 3) + 8 * (i >> 2) + 4 * h;
-                outp[(R::kTap[s] * kC + ci) * kC + ch] = wacc[s][i];
-            }
-    }
-    if constexpr (EPI == 2) {   // the sums: waves 0-3 [wave][lane] -> channel (wave&1)*16 + (lane&15), bb2's order
-        __syncthreads();
-        double *dred = reinterpret_cast<double *>(smem);
-        if (kIg) {
-            dred[(W * 64 + lane) * 2 + 0] = s1;
-            dred[(W * 64 + lane) * 2 + 1] = s2;
-        }
-        __syncthreads();
-        if (W == 0) {
-            const int c = lane >> 1, k = lane & 1, ct = c >> 4, l16 = c & 15;
-            double tot = 0.0;
-            for (int w = ct; w < 4; w += 2)
-                for (int lg = 0; lg < 4; ++lg) tot += dred[(w * 64 + lg * 16 + l16) * 2 + k];
-            a.part[((int64_t)blockIdx.x * kC + c) * 2 + k] = tot;
-        }
-    }
-}
-
-}  // namespace bb3
-
-template <bool PRO, int EPI>
-__global__ __launch_bounds__(bb2::kThreads) void conv3x3_block_bwd3_kernel(BlockBwdArgs a) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[bb3::kLdsBytes];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    switch (wave) {
-    case 0: bb3::run<PRO, EPI, 0>(a, smem, lane); break;
-    case 1: bb3::run<PRO, EPI, 1>(a, smem, lane); break;
-    case 2: bb3::run<PRO, EPI, 2>(a, smem, lane); break;
-    case 3: bb3::run<PRO, EPI, 3>(a, smem, lane); break;
-    case 4: bb3::run<PRO, EPI, 4>(a, smem, lane); break;
-    case 5: bb3::run<PRO, EPI, 5>(a, smem, lane); break;
-    case 6: bb3::run<PRO, EPI, 6>(a, smem, lane); break;
-    default: bb3::run<PRO, EPI, 7>(a, smem, lane); break;
-    }
-}
-
 template <bool PRO, int EPI>
 __global__ __launch_bounds__(bb2::kThreads) void conv3x3_block_bwd2_kernel(BlockBwdArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[bb2::kLdsBytes];
@@ -2276,8 +1855,8 @@ __global__ void conv3x3_pack_n_kernel(WeightList wl, int n, float *__restrict__ 
 
 // Forward / input-gradient arithmetic: exact-split bf16 MFMA (1, default) or fp32 MFMA (0).
 int g_split = 1;
-// Chain block backward with an input gradient: 2 = the LDS-DMA ring conv3x3_block_bwd3_kernel, 1 = tile-shared
-// conv3x3_block_bwd2_kernel (default), 0 = the per-wave conv3x3_block_bwd_kernel.
+// Chain block backward with an input gradient: 1 = tile-shared conv3x3_block_bwd2_kernel (default), 0 = the
+// per-wave conv3x3_block_bwd_kernel (the tests' reference form).
 int g_block_form = 1;
 // The chain's forward conv (epilogue 1, packed weights, no bias): 2 = the LDS-DMA ring form (fw3, default),
 // 1 = the tile-shared form (bb2, EPI 1), 0 = conv3x3_kernel<PRO, 1>.
@@ -2317,7 +1896,7 @@ int64_t hrl_conv3x3_stats_blocks(int64_t M) { return M < 1 ? -1 : grid_for(M); }
 
 int hrl_conv3x3_set_block_form(int form) {
     const int prev = g_block_form;
-    g_block_form = form < 0 ? 0 : (form > 2 ? 2 : form);
+    g_block_form = form < 0 ? 0 : (form > 1 ? 1 : form);
     return prev;
 }
 
@@ -2461,8 +2040,6 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
     hipLaunchKernelGGL((conv3x3_block_bwd_kernel<PRO, EPI, DG>), dim3(grid), dim3(kThreads), 0, s, a)
 #define HRL_BLOCK2_LAUNCH(PRO, EPI) \
     hipLaunchKernelGGL((conv3x3_block_bwd2_kernel<PRO, EPI>), dim3(grid), dim3(bb2::kThreads), 0, s, a)
-#define HRL_BLOCK3_LAUNCH(PRO, EPI) \
-    hipLaunchKernelGGL((conv3x3_block_bwd3_kernel<PRO, EPI>), dim3(grid), dim3(bb2::kThreads), 0, s, a)
     if (!gin) {
         if (pro) HRL_BLOCK_LAUNCH(true, 0, false); else HRL_BLOCK_LAUNCH(false, 0, false);
     } else if (g_block_form == 0) {   // the per-wave form (kept for comparison)
@@ -2473,14 +2050,6 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
         } else {
             if (pro) HRL_BLOCK_LAUNCH(true, 0, true); else HRL_BLOCK_LAUNCH(false, 0, true);
         }
-    } else if (g_block_form == 2) {   // the LDS-DMA ring form
-        if (epilogue == 2) {
-            if (pro) HRL_BLOCK3_LAUNCH(true, 2); else HRL_BLOCK3_LAUNCH(false, 2);
-        } else if (epilogue == 3) {
-            if (pro) HRL_BLOCK3_LAUNCH(true, 3); else HRL_BLOCK3_LAUNCH(false, 3);
-        } else {
-            if (pro) HRL_BLOCK3_LAUNCH(true, 0); else HRL_BLOCK3_LAUNCH(false, 0);
-        }
     } else if (epilogue == 2) {
         if (pro) HRL_BLOCK2_LAUNCH(true, 2); else HRL_BLOCK2_LAUNCH(false, 2);
     } else if (epilogue == 3) {
@@ -2490,7 +2059,6 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
     }
 #undef HRL_BLOCK_LAUNCH
 #undef HRL_BLOCK2_LAUNCH
-#undef HRL_BLOCK3_LAUNCH
     int rc = status();
     if (rc) return rc;
     hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, wpart, grid,

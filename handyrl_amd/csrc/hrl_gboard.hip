@@ -51,15 +51,6 @@ struct GbArgs {
     int relu;
     float *y;
     int64_t ys;            // floats from one game to the next in y
-    // GATES (hrl_gboard_lstm_forward): the conv is the ConvLSTM cells' h halves (groups = layers, 4H outputs per
-    // layer in i, f, o, g order); the epilogue forms the gates with the x halves zx (+ bias) and the cell state
-    // instead of storing the conv: c' = sig(f) c + sig(i) tanh(g), h' = sig(o) tanh(c') (lstm_fwd_kernel's ops)
-    const float *zx;       // (N, layers*4H, 36), games zxs floats apart
-    int64_t zxs;
-    const float *c_in;     // (N, layers*H, 36), games cs floats apart; c_out may be c_in (same element, same lane)
-    float *c_out, *h_out;  // h_out never aliases x (other workgroups still read it)
-    int64_t cs, hs;
-    int nh;                // H / 16: column tiles per gate
 };
 
 // tap of input cell p for output cell q (-1 off the 3x3 neighbourhood)
@@ -108,16 +99,12 @@ __host__ __device__ constexpr bool band_uses(int NB, int b, int p) {
 constexpr int kPartBytes = 4 * 16 * 32 * 2;   // one split part of one quad's image: [cell][game][channel] bf16
 constexpr int kSlotBytes = 3 * kPartBytes;     // 12 KB per quad
 constexpr int kLdsBytes = 3 * kSlotBytes;      // ring of three quads
-// GATES: the four gate waves exchange a 12-cell chunk of their accumulators [gate][cell][row i][lane] (48 KB)
-constexpr int kGateChunk = 12;
-constexpr int kXchgBytes = 4 * kGateChunk * 4 * 64 * 4;
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }   // lstm_fwd_kernel's
 
 // One wave of gboard_conv_kernel: column tile (task's tile group * NCTW + ctl), output band BAND of NB = 4 / NCTW.
-template <int KC, bool PADC, int NCTW, int BAND, bool GATES = false>
+template <int KC, bool PADC, int NCTW, int BAND, int R = 3>
 __device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem, int lane, int wave, int L) {
-    static_assert(!GATES || (NCTW == 4 && KC == 1 && !PADC), "the gate epilogue: one gate per wave");
     constexpr int NB = 4 / NCTW;
     constexpr int Q0 = band_q0(NB, BAND), Q1 = band_q1(NB, BAND);
     constexpr int NCELL = 4 * (Q1 - Q0);
@@ -132,12 +119,7 @@ __device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem,
     int64_t task = L;
     if (task >= ntasks) return;   // uniform over the workgroup: no barrier is left waiting
     auto tile_of = [&](int64_t t) { return t / n_ctg; };
-    // GATES: task group ctg = (layer, hidden block hb); wave ctl takes gate ctl's column tile of that block
-    auto ct_of = [&](int64_t t) {
-        const int ctg = (int)(t % n_ctg);
-        if constexpr (GATES) return (ctg / a.nh) * 4 * a.nh + ctl * a.nh + ctg % a.nh;
-        return ctg * NCTW + ctl;
-    };
+    auto ct_of = [&](int64_t t) { return (int)(t % n_ctg) * NCTW + ctl; };
     // the staging lane's source row for (task, kc): channels 32kc + 2cp (+1) of game sg of the task's tile
     // (PADC: rows at or past cin_g read row cin_g - 1 and are zeroed)
     auto src = [&](int64_t t, int kc, int &c0, int &c1) -> const float * {
@@ -153,7 +135,7 @@ __device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem,
         if (a.xg[0]) return a.xg[grp] + n * a.xgs[grp];
         return a.x + n * a.xs + (int64_t)(grp * a.cin_g) * kHW;
     };
-    float4 raw[3][2];
+    float4 raw[R][2];
     auto issue = [&](int64_t t, int kc, int quad, auto slot_c) __attribute__((always_inline)) {
         constexpr int slot = decltype(slot_c)::value;
         int c0, c1;
@@ -196,121 +178,76 @@ __device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem,
     });
 
     const int64_t step = gridDim.x;
-    // prologue: quad 0 staged, quad 1 in flight
-    issue(task, 0, 0, IC<0>{});
-    issue(task, 0, 1, IC<1>{});
-    stage(0, IC<0>{});
+    // compute quad j of the current task from LDS slot `slot`
+    auto compute = [&](auto j_c, auto slot_c) __attribute__((always_inline)) {
+        constexpr int j = decltype(j_c)::value;
+        const unsigned char *img = smem + decltype(slot_c)::value * kSlotBytes + r * 64 + g * 16;
+        static_for<0, 4>([&](auto u_c) __attribute__((always_inline)) {
+            constexpr int u = decltype(u_c)::value;
+            constexpr int p = 4 * j + u;
+            if constexpr (band_uses(NB, BAND, p)) {
+                const uint4 Ah = *reinterpret_cast<const uint4 *>(img + (0 * 4 + u) * 1024);
+                const uint4 Am = *reinterpret_cast<const uint4 *>(img + (1 * 4 + u) * 1024);
+                const uint4 Al = *reinterpret_cast<const uint4 *>(img + (2 * 4 + u) * 1024);
+                static_for<4 * Q0, 4 * Q1>([&](auto q_c) __attribute__((always_inline)) {
+                    constexpr int q = decltype(q_c)::value;
+                    constexpr int t = tap_pq(p, q);
+                    if constexpr (t >= 0)
+                        acc[q - 4 * Q0] = mfma_split(Ah, Am, Al, Bw[t][0], Bw[t][1], Bw[t][2], acc[q - 4 * Q0]);
+                });
+            }
+        });
+    };
+    // WHOLE (R = 9, one k-step, one task per workgroup): the tile's nine quads are loaded and staged at once
+    // and the waves then compute without a barrier per quad -- the output bands need different input quads,
+    // so a per-quad lockstep idles the waves of one band while the other's are busy
+    constexpr bool WHOLE = R == kQuads && KC == 1;
     int ct_b = -1;
+    if constexpr (WHOLE) {
+        static_for<0, kQuads>([&](auto i_c) __attribute__((always_inline)) {
+            issue(task, 0, decltype(i_c)::value, i_c);
+        });
+        static_for<0, kQuads>([&](auto i_c) __attribute__((always_inline)) { stage(0, i_c); });
+        ct_b = ct_of(task);
+        load_b(ct_b, 0);   // after the staging: the raw quads' registers are free again
+    } else {
+        // prologue: quad 0 staged, quads 1 .. R - 2 in flight
+        static_assert((KC * kQuads) % R == 0 && R - 1 <= KC * kQuads, "the ring's slots repeat per task");
+        static_for<0, R - 1>([&](auto i_c) __attribute__((always_inline)) {
+            constexpr int i = decltype(i_c)::value;
+            issue(task, i / kQuads, i % kQuads, IC<i>{});
+        });
+        stage(0, IC<0>{});
+    }
     bar_lds();
     for (; task < ntasks; task += step) {
         const int64_t nxt = task + step < ntasks ? task + step : task;   // loads past the end: re-read
         const int ct = ct_of(task);
         if (KC == 1 && ct != ct_b) load_b(ct, 0);
         ct_b = ct;
+        if constexpr (WHOLE) {
+            static_for<0, kQuads>([&](auto j_c) __attribute__((always_inline)) {
+                compute(j_c, j_c);
+                __builtin_amdgcn_sched_barrier(0);   // keeps the quads' LDS reads from being hoisted (spills)
+            });
+        } else
         static_for<0, KC>([&](auto kc_c) __attribute__((always_inline)) {
             constexpr int kc = decltype(kc_c)::value;
             if constexpr (KC > 1) load_b(ct, kc);
             static_for<0, kQuads>([&](auto j_c) __attribute__((always_inline)) {
                 constexpr int j = decltype(j_c)::value;
-                constexpr int s = kc * kQuads + j;   // step within the task; slots are s % 3 (kQuads % 3 == 0)
-                // loads two quads ahead into the slot staged last step, then stage the next quad
-                constexpr int s2 = s + 2, s1 = s + 1;
-                if constexpr (s2 < KC * kQuads) issue(task, s2 / kQuads, s2 % kQuads, IC<s2 % 3>{});
-                else issue(nxt, (s2 - KC * kQuads) / kQuads, (s2 - KC * kQuads) % kQuads, IC<s2 % 3>{});
-                // compute quad j from slot s % 3
-                const unsigned char *img = smem + (s % 3) * kSlotBytes + r * 64 + g * 16;
-                static_for<0, 4>([&](auto u_c) __attribute__((always_inline)) {
-                    constexpr int u = decltype(u_c)::value;
-                    constexpr int p = 4 * j + u;
-                    if constexpr (band_uses(NB, BAND, p)) {
-                        const uint4 Ah = *reinterpret_cast<const uint4 *>(img + (0 * 4 + u) * 1024);
-                        const uint4 Am = *reinterpret_cast<const uint4 *>(img + (1 * 4 + u) * 1024);
-                        const uint4 Al = *reinterpret_cast<const uint4 *>(img + (2 * 4 + u) * 1024);
-                        static_for<4 * Q0, 4 * Q1>([&](auto q_c) __attribute__((always_inline)) {
-                            constexpr int q = decltype(q_c)::value;
-                            constexpr int t = tap_pq(p, q);
-                            if constexpr (t >= 0)
-                                acc[q - 4 * Q0] = mfma_split(Ah, Am, Al, Bw[t][0], Bw[t][1], Bw[t][2], acc[q - 4 * Q0]);
-                        });
-                    }
-                });
-                if constexpr (s1 < KC * kQuads) stage(s1 / kQuads, IC<s1 % 3>{});
-                else stage(0, IC<s1 % 3>{});   // the next task's quad 0
+                constexpr int s = kc * kQuads + j;   // step within the task; slots are s % R
+                // loads R - 1 quads ahead into the slot staged last step, then stage the next quad
+                constexpr int s2 = s + R - 1, s1 = s + 1;
+                if constexpr (s2 < KC * kQuads) issue(task, s2 / kQuads, s2 % kQuads, IC<s2 % R>{});
+                else issue(nxt, (s2 - KC * kQuads) / kQuads, (s2 - KC * kQuads) % kQuads, IC<s2 % R>{});
+                compute(j_c, IC<s % R>{});   // quad j from slot s % R
+                if constexpr (s1 < KC * kQuads) stage(s1 / kQuads, IC<s1 % R>{});
+                else stage(0, IC<s1 % R>{});   // the next task's quad 0
                 bar_lds();
             });
         });
         const int64_t tile = tile_of(task);
-        if constexpr (GATES) {
-            // wave k holds gate k of hidden channels hb*16 + r for games 4g + i; in chunks of 12 cells every wave
-            // writes its accumulators to LDS, then wave k' forms the cell update of row i = k' from all four gates
-            float *xchg = reinterpret_cast<float *>(smem + kLdsBytes);
-            const int ctg = (int)(task % n_ctg);
-            const int layer = ctg / a.nh, ch = (ctg % a.nh) * 16 + r;
-            const int H = 16 * a.nh;
-            const int64_t n = tile * 16 + 4 * g + wave;   // this wave's row i = wave
-            const int64_t nc = min(n, a.N - 1);
-            const float *zp = a.zx + nc * a.zxs + (int64_t)(layer * 4 * H + ch) * kHW;
-            const float *cp = a.c_in + nc * a.cs + (int64_t)(layer * H + ch) * kHW;
-            float bgate[4];
-            static_for<0, 4>([&](auto k_c) __attribute__((always_inline)) {
-                constexpr int k = decltype(k_c)::value;
-                bgate[k] = a.bias ? a.bias[layer * 4 * H + k * H + ch] : 0.f;
-            });
-            static_for<0, kHW / kGateChunk>([&](auto c_c) __attribute__((always_inline)) {
-                constexpr int C0 = decltype(c_c)::value * kGateChunk;
-                float4 zq[4][kGateChunk / 4], cq[kGateChunk / 4];   // the chunk's x halves and cell state
-                static_for<0, kGateChunk / 4>([&](auto j_c) __attribute__((always_inline)) {
-                    constexpr int j = decltype(j_c)::value;
-                    static_for<0, 4>([&](auto k_c) __attribute__((always_inline)) {
-                        constexpr int k = decltype(k_c)::value;
-                        zq[k][j] = *reinterpret_cast<const float4 *>(zp + (int64_t)k * H * kHW + C0 + 4 * j);
-                    });
-                    cq[j] = *reinterpret_cast<const float4 *>(cp + C0 + 4 * j);
-                });
-                if constexpr (C0 > 0) bar_lds();   // the previous chunk's reads are done
-                static_for<0, kGateChunk>([&](auto q_c) __attribute__((always_inline)) {
-                    constexpr int ql = decltype(q_c)::value;
-                    static_for<0, 4>([&](auto i_c) __attribute__((always_inline)) {
-                        constexpr int i = decltype(i_c)::value;
-                        xchg[((wave * kGateChunk + ql) * 4 + i) * 64 + lane] = acc[C0 + ql][i];
-                    });
-                });
-                bar_lds();
-                if (n < a.N) {
-                    float *ho = a.h_out + n * a.hs + (int64_t)(layer * H + ch) * kHW + C0;
-                    float *co = a.c_out + n * a.cs + (int64_t)(layer * H + ch) * kHW + C0;
-                    static_for<0, kGateChunk / 4>([&](auto j_c) __attribute__((always_inline)) {
-                        constexpr int j = decltype(j_c)::value;
-                        float hv[4], cv[4];
-                        static_for<0, 4>([&](auto u_c) __attribute__((always_inline)) {
-                            constexpr int u = decltype(u_c)::value;
-                            constexpr int ql = 4 * j + u;
-                            float z[4];
-                            static_for<0, 4>([&](auto k_c) __attribute__((always_inline)) {
-                                constexpr int k = decltype(k_c)::value;
-                                const float4 &f = zq[k][j];
-                                const float xv = u == 0 ? f.x : (u == 1 ? f.y : (u == 2 ? f.z : f.w));
-                                const float zh = xchg[((k * kGateChunk + ql) * 4 + wave) * 64 + lane];
-                                z[k] = a.bias ? (xv + bgate[k]) + zh : xv + zh;   // (zx + b) + zh
-                            });
-                            const float c0 = u == 0 ? cq[j].x : (u == 1 ? cq[j].y : (u == 2 ? cq[j].z : cq[j].w));
-                            const float si = sigm(z[0]), sf = sigm(z[1]), so = sigm(z[2]), tg = tanhf(z[3]);
-                            const float fc = sf * c0;
-                            const float ig = si * tg;
-                            const float cc = fc + ig;
-                            cv[u] = cc;
-                            hv[u] = so * tanhf(cc);
-                        });
-                        *reinterpret_cast<float4 *>(co + 4 * j) = make_float4(cv[0], cv[1], cv[2], cv[3]);
-                        *reinterpret_cast<float4 *>(ho + 4 * j) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-                    });
-                }
-            });
-            static_for<0, NCELL>([&](auto q_c) __attribute__((always_inline)) {
-                acc[decltype(q_c)::value] = (f32x4){0.f, 0.f, 0.f, 0.f};
-            });
-            continue;
-        }
         // epilogue: C/D row (game) = 4g + i, column (channel) = r
         const int co = ct * 16 + r;
         if (co < a.cout) {
@@ -344,21 +281,14 @@ __device__ __forceinline__ void gboard_run(const GbArgs &a, unsigned char *smem,
     }
 }
 
-// The ConvLSTM cells' h halves with the gate update in the epilogue (hrl_gboard_lstm_forward)
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void gboard_lstm_kernel(GbArgs a) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[kLdsBytes + kXchgBytes];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nwg = gridDim.x, b = blockIdx.x;
-    const int L = (nwg % 8 == 0) ? (b & 7) * (nwg >> 3) + (b >> 3) : b;
-    gboard_run<1, false, 4, 0, true>(a, smem, lane, wave, L);
-}
-
 // A workgroup's 4 waves share one 16-game tile per task: each stages a quarter of every quad (16 games x 32
 // channels x 4 cells, split once into the LDS ring) and computes NCTW column tiles x (4 / NCTW) output bands.
-template <int KC, bool PADC, int NCTW>
+// R: the ring's quads (loads R - 1 quads ahead).  3 when workgroups walk several tasks (the next task's loads
+// overlap this one's MFMAs); 9 -- a whole 32-channel k-step (108 KB) -- when every workgroup has one task (few
+// games: the learner's per-step 256), so all of it is in flight at once instead of one HBM latency per quad.
+template <int KC, bool PADC, int NCTW, int R>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void gboard_conv_kernel(GbArgs a) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[kLdsBytes];
+    __shared__ __attribute__((aligned(16))) unsigned char smem[R * kSlotBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nwg = gridDim.x, b = blockIdx.x;
@@ -367,16 +297,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, 1))
     constexpr int NB = 4 / NCTW;
     const int band = wave / NCTW;
     if constexpr (NB == 1) {
-        gboard_run<KC, PADC, NCTW, 0>(a, smem, lane, wave, L);
+        gboard_run<KC, PADC, NCTW, 0, R>(a, smem, lane, wave, L);
     } else if constexpr (NB == 2) {
-        if (band == 0) gboard_run<KC, PADC, NCTW, 0>(a, smem, lane, wave, L);
-        else gboard_run<KC, PADC, NCTW, 1>(a, smem, lane, wave, L);
+        if (band == 0) gboard_run<KC, PADC, NCTW, 0, R>(a, smem, lane, wave, L);
+        else gboard_run<KC, PADC, NCTW, 1, R>(a, smem, lane, wave, L);
     } else {
         switch (band) {
-        case 0: gboard_run<KC, PADC, NCTW, 0>(a, smem, lane, wave, L); break;
-        case 1: gboard_run<KC, PADC, NCTW, 1>(a, smem, lane, wave, L); break;
-        case 2: gboard_run<KC, PADC, NCTW, 2>(a, smem, lane, wave, L); break;
-        default: gboard_run<KC, PADC, NCTW, 3>(a, smem, lane, wave, L); break;
+        case 0: gboard_run<KC, PADC, NCTW, 0, R>(a, smem, lane, wave, L); break;
+        case 1: gboard_run<KC, PADC, NCTW, 1, R>(a, smem, lane, wave, L); break;
+        case 2: gboard_run<KC, PADC, NCTW, 2, R>(a, smem, lane, wave, L); break;
+        default: gboard_run<KC, PADC, NCTW, 3, R>(a, smem, lane, wave, L); break;
         }
     }
 }
@@ -740,6 +670,8 @@ __global__ __launch_bounds__(256) void pw_wgrad_reduce_kernel(const float *__res
     dw[i] = dw[i] + (s0 + s1);
 }
 
+int g_gboard_whole = 1;   // hrl_gboard_set_whole_ring
+
 int status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
@@ -850,12 +782,19 @@ int gboard_launch(GbArgs a, int64_t Cin_g, int64_t groups, hipStream_t s) {
     const dim3 block(kThreads);
     const int KC = (int)((Cin_g + 31) / 32);
     const bool padc = Cin_g % 32 != 0;
-#define HRL_GB_LAUNCH(KC_, PADC_)                                                                                  \
+#define HRL_GB_LAUNCH_R(KC_, PADC_, R_)                                                                          \
     do {                                                                                                         \
-        if (nctw == 4) hipLaunchKernelGGL((gboard_conv_kernel<KC_, PADC_, 4>), dim3(grid), block, 0, s, a);      \
-        else if (nctw == 2) hipLaunchKernelGGL((gboard_conv_kernel<KC_, PADC_, 2>), dim3(grid), block, 0, s, a); \
-        else hipLaunchKernelGGL((gboard_conv_kernel<KC_, PADC_, 1>), dim3(grid), block, 0, s, a);                \
+        if (nctw == 4) hipLaunchKernelGGL((gboard_conv_kernel<KC_, PADC_, 4, R_>), dim3(grid), block, 0, s, a);  \
+        else if (nctw == 2)                                                                                      \
+            hipLaunchKernelGGL((gboard_conv_kernel<KC_, PADC_, 2, R_>), dim3(grid), block, 0, s, a);             \
+        else hipLaunchKernelGGL((gboard_conv_kernel<KC_, PADC_, 1, R_>), dim3(grid), block, 0, s, a);            \
     } while (0)
+#define HRL_GB_LAUNCH(KC_, PADC_)                                                                                \
+    do {                                                                                                         \
+        if (whole) HRL_GB_LAUNCH_R(KC_, PADC_, ((KC_) == 1 ? 9 : 3)); else HRL_GB_LAUNCH_R(KC_, PADC_, 3);      \
+    } while (0)
+    // one task per workgroup: the whole k-step ring (see gboard_conv_kernel)
+    const bool whole = tasks <= kCUs && g_gboard_whole && KC == 1;
     if (KC == 1) {
         if (padc) HRL_GB_LAUNCH(1, true); else HRL_GB_LAUNCH(1, false);
     } else if (KC == 2) {
@@ -863,32 +802,8 @@ int gboard_launch(GbArgs a, int64_t Cin_g, int64_t groups, hipStream_t s) {
     } else {
         if (padc) HRL_GB_LAUNCH(4, true); else HRL_GB_LAUNCH(4, false);
     }
+#undef HRL_GB_LAUNCH_R
 #undef HRL_GB_LAUNCH
-    return status();
-}
-
-int hrl_gboard_lstm_forward(const float *h, int64_t h_stride, int64_t N, int64_t layers, int64_t H, const void *packed,
-                            const float *zx, int64_t zx_stride, const float *bias, const float *c_in, float *c_out,
-                            int64_t c_stride, float *h_out, int64_t hout_stride, void *stream) {
-    if (!h || !packed || !zx || !c_in || !c_out || !h_out || N < 1 || layers < 1 || H < 16 || H > 64 || H % 16)
-        return HRL_EINVAL;
-    if (h_out == h) return HRL_EINVAL;   // other workgroups still read h while this one writes h'
-    if (!aligned16(h) || !aligned16(zx) || !aligned16(c_in) || !aligned16(c_out) || !aligned16(h_out) ||
-        h_stride % 4 || zx_stride % 4 || c_stride % 4 || hout_stride % 4)
-        return HRL_EINVAL;
-    if (h_stride < layers * H * kHW || zx_stride < layers * 4 * H * kHW || c_stride < layers * H * kHW ||
-        hout_stride < layers * H * kHW)
-        return HRL_EINVAL;
-    GbArgs a{};
-    a.x = h; a.x2 = nullptr; a.N = N; a.xs = h_stride; a.xs2 = 0;
-    a.cin_g = (int)H; a.cout_g = (int)(4 * H);
-    a.wpk = static_cast<const uint4 *>(packed);
-    a.nct = (int)(layers * 4 * H / 16); a.cout = (int)(layers * 4 * H);
-    a.bias = bias; a.zx = zx; a.zxs = zx_stride; a.c_in = c_in; a.c_out = c_out; a.h_out = h_out;
-    a.cs = c_stride; a.hs = hout_stride; a.nh = (int)(H / 16);
-    const int64_t tasks = ((N + 15) / 16) * (a.nct / 4);
-    const int grid = (int)(tasks < kCUs ? tasks : kCUs);
-    hipLaunchKernelGGL(gboard_lstm_kernel, dim3(grid), dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
     return status();
 }
 
@@ -941,6 +856,12 @@ int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const flo
     hipLaunchKernelGGL(gboard_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, a.part, blocks, a.cto,
                        a.cti, (int)Cout, (int)Cin, (int)w_cin_total, (int)w_ci0, dweight, dbias);
     return status();
+}
+
+int hrl_gboard_set_whole_ring(int on) {
+    const int prev = g_gboard_whole;
+    g_gboard_whole = on ? 1 : 0;
+    return prev;
 }
 
 int64_t hrl_gboard_pointwise_wgrad_workspace_bytes(int64_t C, int64_t O, int64_t N) {

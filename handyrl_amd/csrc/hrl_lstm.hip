@@ -256,6 +256,84 @@ __global__ void lstm_bwd_kernel(const float *__restrict__ gates, const float *__
     }
 }
 
+// lstm_bwd_kernel for a recurrent unroll step's repeats (hrl_lstm_gates_backward_ex): dh may be the sum of S
+// partial input gradients (the K-split adjoint conv's groups, summed here in s order instead of by a separate
+// pass), and the x half's gradient dzx accumulates over the repeats (dzx = dz on the first, dzx += dz after)
+struct BwdEx {
+    const float *dh;
+    int64_t dhs, dps;   // floats from one game to the next in dh / from one partial to the next
+    int S;
+    float *dzx;
+    int dzx_init;
+};
+
+template <int VW>
+__global__ void lstm_bwd_ex_kernel(const float *__restrict__ gates, const float *__restrict__ c,
+                                   const float *__restrict__ c_out, BwdEx x, const float *__restrict__ dc_out, Geo g,
+                                   float *__restrict__ dz, float *__restrict__ dc) {
+    using V = typename Vec<VW>::T;
+    const int64_t total = g.N * g.H * g.nq;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int q = (int)(e % g.nq);
+        const int64_t nc = e / g.nq;
+        const int ch = (int)(nc % g.H);
+        const int64_t n = nc / g.H;
+        const int64_t plane = (int64_t)g.HW;
+        const int64_t zoff = n * 4 * g.H * plane + (int64_t)ch * plane + (int64_t)q * VW;
+        const int64_t soff = nc * plane + (int64_t)q * VW;
+        const int64_t hoff = n * x.dhs + (int64_t)ch * plane + (int64_t)q * VW;
+        const int64_t gstep = (int64_t)g.H * plane;
+        const V gi = ld<VW>(gates + zoff), gf = ld<VW>(gates + zoff + gstep), go = ld<VW>(gates + zoff + 2 * gstep),
+                gg = ld<VW>(gates + zoff + 3 * gstep);
+        const V cv = ld<VW>(c + soff), cn = ld<VW>(c_out + soff);
+        V dhv = {}, dcv = {};
+        if (x.dh) {
+            dhv = ld<VW>(x.dh + hoff);
+            for (int sp = 1; sp < x.S; ++sp) {
+                const V p = ld<VW>(x.dh + hoff + sp * x.dps);
+#pragma unroll
+                for (int j = 0; j < VW; ++j) put<VW>(dhv, j, get<VW>(dhv, j) + get<VW>(p, j));
+            }
+        }
+        if (dc_out) dcv = ld<VW>(dc_out + soff);
+        V di, df, dout, dg, dprev;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+            const float si = get<VW>(gi, j), sf = get<VW>(gf, j), so = get<VW>(go, j), tg = get<VW>(gg, j);
+            const float tc = tanhf(get<VW>(cn, j));
+            const float d_h = x.dh ? get<VW>(dhv, j) : 0.f;
+            const float d_c = dc_out ? get<VW>(dcv, j) : 0.f;
+            const float dct = d_c + d_h * so * (1.f - tc * tc);
+            put<VW>(di, j, dct * tg * (si * (1.f - si)));
+            put<VW>(df, j, dct * get<VW>(cv, j) * (sf * (1.f - sf)));
+            put<VW>(dout, j, d_h * tc * (so * (1.f - so)));
+            put<VW>(dg, j, dct * si * (1.f - tg * tg));
+            put<VW>(dprev, j, dct * sf);
+        }
+        st<VW>(dz + zoff, di);
+        st<VW>(dz + zoff + gstep, df);
+        st<VW>(dz + zoff + 2 * gstep, dout);
+        st<VW>(dz + zoff + 3 * gstep, dg);
+        st<VW>(dc + soff, dprev);
+        if (x.dzx) {
+            const V d4[4] = {di, df, dout, dg};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float *p = x.dzx + zoff + k * gstep;
+                if (x.dzx_init) {
+                    st<VW>(p, d4[k]);
+                } else {
+                    V a = ld<VW>(p);
+#pragma unroll
+                    for (int j = 0; j < VW; ++j) put<VW>(a, j, get<VW>(a, j) + get<VW>(d4[k], j));
+                    st<VW>(p, a);
+                }
+            }
+        }
+    }
+}
+
 int status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
@@ -332,6 +410,29 @@ int hrl_lstm_gates_backward(const float *gates, const float *c, const float *c_o
                            g, dz, dc);
     else
         hipLaunchKernelGGL(lstm_bwd_kernel<1>, dim3(grid_for(total)), dim3(256), 0, s, gates, c, c_out, dh, dc_out,
+                           g, dz, dc);
+    return status();
+}
+
+int hrl_lstm_gates_backward_ex(const float *gates, const float *c, const float *c_out, const float *dh,
+                               int64_t dh_stride, int dh_parts, int64_t dh_part_stride, const float *dc_out,
+                               int64_t N, int64_t H, int64_t HW, float *dz, float *dc, float *dzx, int dzx_init,
+                               void *stream) {
+    if (N == 0) return HRL_OK;
+    if (!gates || !c || !c_out || !dz || !dc || N < 0 || H < 1 || HW < 1 || dh_parts < 1) return HRL_EINVAL;
+    if (dh && (dh_stride < H * HW || (dh_parts > 1 && dh_part_stride < H * HW))) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool vec = HW % 4 == 0 && aligned(gates) && aligned(c) && aligned(c_out) && aligned(dh) &&
+                     aligned(dc_out) && aligned(dz) && aligned(dc) && aligned(dzx) && dh_stride % 4 == 0 &&
+                     dh_part_stride % 4 == 0;
+    Geo g{N, (int)H, (int)HW, (int)(vec ? HW / 4 : HW), 0};
+    BwdEx x{dh, dh_stride, dh_part_stride, dh ? dh_parts : 1, dzx, dzx_init};
+    const int64_t total = N * H * g.nq;
+    if (vec)
+        hipLaunchKernelGGL(lstm_bwd_ex_kernel<4>, dim3(grid_for(total)), dim3(256), 0, s, gates, c, c_out, x, dc_out,
+                           g, dz, dc);
+    else
+        hipLaunchKernelGGL(lstm_bwd_ex_kernel<1>, dim3(grid_for(total)), dim3(256), 0, s, gates, c, c_out, x, dc_out,
                            g, dz, dc);
     return status();
 }

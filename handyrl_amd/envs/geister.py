@@ -121,13 +121,8 @@ class DRC(nn.Module):
         return self.step_hip(self.x_halves(x), hs, cs, num_repeats)
 
     _session = None   # the stacked weights of an inference session (DRC.inference_session)
-    # on hrl_gboard, run each repeat as ONE launch with the gate update in the h-half conv's epilogue
-    # (hrl_gboard_lstm_forward): bit-identical, but measured slower (136 us per repeat against 83 + 48 us
-    # unfused at 2,048 games: the epilogue's loads and transcendentals run serially after the MFMAs at one
-    # wave per SIMD), so off by default
-    fuse_gates = False
     # the learner's unroll: each repeat's layers as one grouped h-half conv + one grouped gate launch
-    # (nn.drc_repeat) instead of a conv and a gate launch per layer
+    # (nn.drc_step) instead of a conv and a gate launch per layer
     group_repeat = os.environ.get('HRL_DRC_GROUPED', '1') == '1'
     _inplace = False  # the session advances a stacked state in place (DeviceGenerator)
 
@@ -206,31 +201,6 @@ class DRC(nn.Module):
         # the old one: h is consumed by the convolution before, c read and written at the same index
         inplace = (self._inplace and h.is_contiguous() and c.is_contiguous()
                    and h.data_ptr() == hs[0].data_ptr() and c.data_ptr() == cs[0].data_ptr())
-        if (gb and self.fuse_gates and hd % 16 == 0 and hnn.gboard_ok(h) and hnn.gboard_ok(c) and hnn.gboard_ok(z)
-                and (cache['b_x'] is None or cache['b_x'].is_contiguous())):
-            # each repeat is ONE launch: the grouped h-half conv with the gate update in its epilogue (the conv
-            # output never reaches HBM).  h' cannot overwrite h (other workgroups still read it), so the repeats
-            # alternate between two scratch states and the last one writes the caller's state (in place) or a
-            # new tensor; c is updated in place from the first repeat on (each element by the lane that reads it)
-            h0, c_state = h, (c if inplace else torch.empty_like(c))
-            tmp = [torch.empty_like(h) for _ in range(min(2, num_repeats))] if (num_repeats > 1 or inplace) else []
-            c_in = c
-            for rep in range(num_repeats):
-                last = rep == num_repeats - 1
-                if last and not (inplace and num_repeats > 1):
-                    h_out = tmp[rep % 2] if inplace else torch.empty_like(h)
-                elif last:
-                    h_out = h0
-                else:
-                    h_out = tmp[rep % 2]
-                hnn.gboard_lstm(h, cache['pk_h'], z, cache['b_x'], c_in, c_state, h_out, n, hd)
-                h, c_in = h_out, c_state
-            if inplace and num_repeats == 1:
-                h0.copy_(h)
-                h = h0
-            c = c_state
-            hs, cs = list(h.split(hd, 1)), list(c.split(hd, 1))
-            return hs[-1], (hs, cs)
         zx = z.view(E * n, 4 * hd, *HW)
         for _ in range(num_repeats):
             if gb and hnn.gboard_ok(h):
@@ -287,10 +257,10 @@ class DRC(nn.Module):
         deferred = hnn._DEFER is not None
         w_h = None if deferred else [w[:, cin:].contiguous() for w in ws]
         if (deferred and isinstance(packed_h, dict) and self.group_repeat
-                and hnn.drc_repeat_ok(zx, hs, cs, ws, pad)):
-            # every repeat's layers in two launches (the grouped h-half conv and the grouped gates)
-            for _ in range(num_repeats):
-                hs, cs = hnn.drc_repeat(zx, hs, cs, ws, (cin, c_all), pad, packed_h['grouped'])
+                and hnn.drc_step_ok(zx, hs, cs, ws, pad)):
+            # every repeat's layers in two launches (the grouped h-half conv and the grouped gates), the step's
+            # repeats under one autograd node (nn.drc_step)
+            hs, cs = hnn.drc_step(zx, hs, cs, ws, (cin, c_all), pad, packed_h['grouped'], num_repeats)
             return hs[-1], (hs, cs)
         if isinstance(packed_h, dict):
             packed_h = packed_h['layers']

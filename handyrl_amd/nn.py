@@ -429,18 +429,6 @@ def gboard_conv(x, packed, Cout, cin_g, groups=1, x2=None, bias=None, alpha=None
     return y
 
 
-def gboard_lstm(h, packed_h, zx, bias, c_in, c_out, h_out, layers, H):
-    """One DRC repeat of the stacked cells on the 6x6 board (csrc/hrl_gboard.hip, inference only): the grouped
-    h-half conv of h (N, layers*H, 6, 6) with the ConvLSTM gate update in its epilogue, from the x halves zx
-    (N, layers*4H, 6, 6) + bias and the cell state c_in; writes c_out (may be c_in) and h_out (not h)."""
-    P = _native.ptr
-    _native.check(_native.load().hrl_gboard_lstm_forward(
-        P(h), h.stride(0), h.shape[0], layers, H, P(packed_h), P(zx), zx.stride(0), None if bias is None else P(bias),
-        P(c_in), P(c_out), c_in.stride(0), P(h_out), h_out.stride(0), _native.stream_of(h.device)),
-        'hrl_gboard_lstm_forward')
-    assert c_out.stride(0) == c_in.stride(0)
-
-
 def gboard_pointwise(x, w, x2=None, alpha=None, beta=None, relu=False):
     """1x1 conv (no bias) of x (and then x2's channels) on the 6x6 board with weight w (O, C, 1, 1), optional
     BatchNorm apply + ReLU (csrc/hrl_gboard.hip, forward only): F.conv2d(cat([x, x2]), w) without the cat."""
@@ -506,6 +494,11 @@ def _deferred_conv_dx(dy, x, w, sl, pad, rec):
             and Cf % 32 == 0 and 2 <= Cf // 32 <= 8 and wv.shape[1] % 16 == 0 and wv.shape[1] == x.shape[1]
             and dy.shape[1] == Cf):
         return gboard_adjoint_split(dy, w, 0 if sl is None else sl[0], wv.shape[1], rec)
+    if ((GBOARD_ADJOINT_SPLIT or GBOARD_ADJOINT) and tuple(pad) == (1, 1) and tuple(w.shape[2:]) == (3, 3)
+            and gboard_ok(dy) and Cf <= 32 and wv.shape[1] == x.shape[1] and dy.shape[1] == Cf):
+        # a K of one k-step (the move head's 64 -> 8: K = 8): the plain adjoint conv on hrl_gboard
+        ci0 = 0 if sl is None else sl[0]
+        return gboard_conv(dy, rec.adjoint_pack(w, ci0, wv.shape[1]), wv.shape[1], Cf)
     if (GBOARD_ADJOINT and tuple(pad) == (1, 1) and tuple(w.shape[2:]) == (3, 3) and gboard_ok(dy)
             and (Cf <= 64 or 96 < Cf <= 128) and wv.shape[1] == x.shape[1]):
         # the adjoint conv on hrl_gboard: K = the forward's Cout (up to 4 x 32), Cout = the slice width
@@ -518,74 +511,115 @@ def _deferred_conv_dx(dy, x, w, sl, pad, rec):
                                                [True, False, False])[0]
 
 
-class _DRCRepeat(torch.autograd.Function):
-    """One repeat of a DRC's L ConvLSTM cells in a deferred-gradient unroll (GeisterNet's learner), in two
-    launches for all L layers: the h halves as ONE grouped hrl_gboard conv over the layers' separate states
-    (hrl_gboard_forward_groups) and the gates as one hrl_lstm_gates_forward_grouped.  Both compute each layer's
-    values with the per-layer kernels' float operations (_DeferredConv + lstm_gates), so the outputs are the
-    same bits.  Backward, per layer whose outputs carry a gradient (GeisterNet: the last one): the gate
-    backward, the h half's input gradient, and the (h, dz) record of the deferred weight gradient.
+class _DRCStep(torch.autograd.Function):
+    """The R repeats of a DRC's L ConvLSTM cells at one time step of a deferred-gradient unroll (GeisterNet's
+    learner), each repeat in two launches for all L layers: the h halves as ONE grouped hrl_gboard conv over the
+    layers' separate states (hrl_gboard_forward_groups) and the gates as one hrl_lstm_gates_forward_grouped (the
+    per-layer kernels' float operations, so the states are those of _DeferredConv + lstm_gates bit for bit).
 
-    apply(meta, *zx, *h, *c) -> (*h', *c'); meta = (ws, h slice of the weights, pad, packed, DeferredGrads)."""
+    Backward, per layer whose outputs carry a gradient (GeisterNet: the last one), repeats in reverse: the gate
+    backward (hrl_lstm_gates_backward_ex) reads the h input gradient of the repeat after it as the S partials of
+    the K-split adjoint conv (gboard_adjoint_split's grouped launch, summed in the gate kernel) and accumulates the
+    x half's gradient over the repeats; each repeat records its (h, dz) for the deferred weight gradient.
+
+    apply(meta, *zx, *h, *c) -> (*h', *c'); meta = (ws, h slice of the weights, pad, packed, DeferredGrads, R)."""
 
     @staticmethod
     def forward(ctx, meta, *args):
         ctx.set_materialize_grads(False)
-        ws, sl, pad, packed, rec = meta
+        ws, sl, pad, packed, rec, R = meta
         L = len(ws)
-        zx, hs, cs = args[:L], args[L:2 * L], args[2 * L:]
+        zx, hs, cs = args[:L], list(args[L:2 * L]), list(args[2 * L:])
         N, H = hs[0].shape[0], hs[0].shape[1]
         lib = _native.load()
         stream = _native.stream_of(hs[0].device)
         P = _native.ptr
-        zh = torch.empty(N, L * 4 * H, 6, 6, device=hs[0].device)
-        _native.check(lib.hrl_gboard_forward_groups(
-            _native.ptr_array(hs), _native.i64_array([h.stride(0) for h in hs]), N, H, L, P(packed), L * 4 * H,
-            P(zh), zh.stride(0), stream), 'hrl_gboard_forward_groups')
-        h_out = [torch.empty_like(c) for c in cs]
-        c_out = [torch.empty_like(c) for c in cs]
-        gates = [torch.empty(N, 4 * H, 6, 6, device=zh.device) for _ in range(L)]
-        _native.check(lib.hrl_lstm_gates_forward_grouped(
-            L, P(zh), zh.stride(0), _native.ptr_array(zx), _native.i64_array([z.stride(0) for z in zx]),
-            _native.ptr_array(cs), N, H, 36, _native.ptr_array(h_out), _native.ptr_array(c_out),
-            _native.ptr_array(gates), stream), 'hrl_lstm_gates_forward_grouped')
-        ctx.save_for_backward(*hs, *cs, *c_out, *gates)
+        # a layer whose x half is outside autograd (DRC.x_halves: the layers that reach no output) gets no
+        # backward: its gate activations are not stored
+        live = [z.requires_grad for z in zx]
+        zx_ptrs = _native.ptr_array(zx)
+        zx_strides = _native.i64_array([z.stride(0) for z in zx])
+        saved = []
+        for _ in range(R):
+            zh = torch.empty(N, L * 4 * H, 6, 6, device=hs[0].device)
+            _native.check(lib.hrl_gboard_forward_groups(
+                _native.ptr_array(hs), _native.i64_array([h.stride(0) for h in hs]), N, H, L, P(packed), L * 4 * H,
+                P(zh), zh.stride(0), stream), 'hrl_gboard_forward_groups')
+            h_out = [torch.empty_like(c) for c in cs]
+            c_out = [torch.empty_like(c) for c in cs]
+            gates = [torch.empty(N, 4 * H, 6, 6, device=zh.device) if lv else None for lv in live]
+            _native.check(lib.hrl_lstm_gates_forward_grouped(
+                L, P(zh), zh.stride(0), zx_ptrs, zx_strides, _native.ptr_array(cs), N, H, 36,
+                _native.ptr_array(h_out), _native.ptr_array(c_out), _native.ptr_array(gates), stream),
+                'hrl_lstm_gates_forward_grouped')
+            for i in range(L):
+                if live[i]:
+                    saved += [hs[i], cs[i], c_out[i], gates[i]]
+            hs, cs = h_out, c_out
+        ctx.save_for_backward(*saved)
         ctx.meta = meta
-        return (*h_out, *c_out)
+        ctx.live = live
+        return (*hs, *cs)
 
     @staticmethod
     def backward(ctx, *grads):
-        ws, sl, pad, packed, rec = ctx.meta
+        ws, sl, pad, packed, rec, R = ctx.meta
         L = len(ws)
+        live = ctx.live
+        nl = sum(live)
         saved = ctx.saved_tensors
-        hs, cs, c_out, gates = saved[:L], saved[L:2 * L], saved[2 * L:3 * L], saved[3 * L:]
         dzx, dh, dc = [None] * L, [None] * L, [None] * L
         lib = _native.load()
+        k = -1
         for i in range(L):
+            if not live[i]:
+                if grads[i] is not None or grads[L + i] is not None:
+                    raise RuntimeError('DRC step: a gradient reached layer %d, whose x half was computed without '
+                                       'autograd (DRC.x_halves)' % i)
+                continue
+            k += 1
             gh, gc = grads[i], grads[L + i]
             if gh is None and gc is None:
                 continue
-            N, G = gates[i].shape[0], gates[i].shape[1]
-            dz = torch.empty_like(gates[i])
-            dci = torch.empty_like(cs[i])
+            w = ws[i]
             gh = None if gh is None else gh.contiguous()
             gc = None if gc is None else gc.contiguous()
-            _native.check(lib.hrl_lstm_gates_backward(
-                _native.ptr(gates[i]), _native.ptr(cs[i]), _native.ptr(c_out[i]), _native.ptr(gh), _native.ptr(gc),
-                N, G // 4, 36, _native.ptr(dz), _native.ptr(dci), _native.stream_of(dz.device)),
-                'hrl_lstm_gates_backward')
-            if ctx.needs_input_grad[1 + i]:
-                dzx[i] = dz
+            N = saved[4 * k].shape[0]
+            H = saved[4 * k].shape[1]
+            G = 4 * H
+            Cf = w.shape[0]
+            split = (GBOARD_ADJOINT_SPLIT and Cf % 32 == 0 and 2 <= Cf // 32 <= 8 and H % 16 == 0
+                     and tuple(pad) == (1, 1) and tuple(w.shape[2:]) == (3, 3))
+            S = Cf // 32 if split else 1
+            acc = torch.empty(N, G, 6, 6, device=w.device) if ctx.needs_input_grad[1 + i] else None
+            dh_t, dh_stride, dh_parts = gh, H * 36, 1
+            for r in range(R - 1, -1, -1):
+                h_r, c_r, co_r, g_r = saved[4 * (r * nl + k):4 * (r * nl + k) + 4]
+                dz = torch.empty_like(g_r)
+                dcr = torch.empty_like(c_r)
+                _native.check(lib.hrl_lstm_gates_backward_ex(
+                    _native.ptr(g_r), _native.ptr(c_r), _native.ptr(co_r), _native.ptr(dh_t), dh_stride, dh_parts,
+                    H * 36, _native.ptr(gc), N, H, 36, _native.ptr(dz), _native.ptr(dcr), _native.ptr(acc),
+                    int(r == R - 1), _native.stream_of(dz.device)), 'hrl_lstm_gates_backward_ex')
+                rec.add_conv((w, None, sl, tuple(pad)), h_r, dz)
+                gc = dcr
+                if r == 0 and not ctx.needs_input_grad[1 + L + i]:
+                    break
+                if split:   # the S partial input gradients, summed by the next gate backward (or below)
+                    dh_t = gboard_conv(dz, rec.adjoint_pack(w, sl[0], H, split=True), S * H, 32, groups=S)
+                    dh_stride, dh_parts = S * H * 36, S
+                else:
+                    dh_t = _deferred_conv_dx(dz, h_r, w, sl, pad, rec)
+                    dh_stride, dh_parts = H * 36, 1
+            dzx[i] = acc
             if ctx.needs_input_grad[1 + L + i]:
-                dh[i] = _deferred_conv_dx(dz, hs[i], ws[i], sl, pad, rec)
-            if ctx.needs_input_grad[1 + 2 * L + i]:
-                dc[i] = dci
-            rec.add_conv((ws[i], None, sl, tuple(pad)), hs[i], dz)
+                dh[i] = dh_t.view(N, S, H, 6, 6).sum(1) if dh_parts > 1 else dh_t
+            dc[i] = gc if ctx.needs_input_grad[1 + 2 * L + i] else None
         return (None, *dzx, *dh, *dc)
 
 
-def drc_repeat_ok(zx, hs, cs, ws, pad):
-    """_DRCRepeat covers: 1..4 layers of 3x3 'same' cells on the 6x6 board, H = 32 hidden channels, fp32 CUDA
+def drc_step_ok(zx, hs, cs, ws, pad):
+    """_DRCStep covers: 1..4 layers of 3x3 'same' cells on the 6x6 board, H = 32 hidden channels, fp32 CUDA
     float4-aligned games (zx may be channel slices of a wider tensor)."""
     L = len(ws)
     if not (1 <= L <= 4 and tuple(pad) == (1, 1)):
@@ -597,10 +631,10 @@ def drc_repeat_ok(zx, hs, cs, ws, pad):
             and all(t.shape[0] == hs[0].shape[0] for t in (*zx, *hs, *cs)))
 
 
-def drc_repeat(zx, hs, cs, ws, sl, pad, packed):
-    """One repeat of the DRC cells in a deferred unroll (_DRCRepeat); returns (hs', cs')."""
+def drc_step(zx, hs, cs, ws, sl, pad, packed, repeats):
+    """The repeats of the DRC cells at one time step of a deferred unroll (_DRCStep); returns (hs', cs')."""
     L = len(ws)
-    out = _DRCRepeat.apply((ws, sl, tuple(pad), packed, _DEFER), *zx, *hs, *cs)
+    out = _DRCStep.apply((ws, sl, tuple(pad), packed, _DEFER, repeats), *zx, *hs, *cs)
     return list(out[:L]), list(out[L:])
 
 

@@ -103,9 +103,18 @@ class LearnerStep:
         if self.reducer is not None:
             self.reducer.enabled = False    # its hooks neither count nor launch during the probe
         try:
-            outputs = forward_prediction(self.net, small_hidden, small, self.args)
-            losses, _ = self.loss_fn(outputs, small, self.args)
-            backward_total(losses)
+            if hidden is not None and self.defer:
+                # the step's own kernels (deferred weight gradients, flushed into .grad): no vendor-conv path
+                # runs just for the probe
+                with deferred_weight_grads() as deferred:
+                    outputs = forward_prediction(self.net, small_hidden, small, self.args)
+                    losses, _ = self.loss_fn(outputs, small, self.args)
+                    backward_total(losses)
+                deferred.flush()
+            else:
+                outputs = forward_prediction(self.net, small_hidden, small, self.args)
+                losses, _ = self.loss_fn(outputs, small, self.args)
+                backward_total(losses)
             live = [p.grad is not None for p in self.params]
         finally:
             for p, v in zip(self.params, views):

@@ -174,8 +174,8 @@ int hrl_conv3x3_set_split(int on);
  * association.  Process-wide; returns the previous setting. */
 int hrl_conv3x3_set_block_form(int form);
 /* The chain's forward conv with BN statistics (hrl_conv3x3_forward_ex, epilogue 1, packed weights, no bias):
- * 1 (default) = the block backward's tile-shared form, 0 = the per-wave conv3x3_kernel (1.17 vs 1.19 ms per
- * B=4096 T=32 learner step, tools/fwd_form_bench.py).  Returns the previous. */
+ * 2 (default) = the LDS-DMA ring form (every wave computes, x' staged from a raw ring), 1 = the block backward's
+ * tile-shared form, 0 = the per-wave conv3x3_kernel (tools/fwd_form_bench.py).  Returns the previous. */
 int hrl_conv3x3_set_fwd_form(int form);
 /* Both packed layouts of n <= 8 weights (32, 32, 3, 3) in one launch: packed[(l*2 + f) * 9216], f = 0 forward,
  * 1 input gradient (host array of device pointers).  hrl_conv3x3_forward_ex with flip | 2 takes `weight`
@@ -230,6 +230,13 @@ int hrl_lstm_gates_forward(const float *zx, int64_t zx_stride, const float *zh, 
 int hrl_lstm_gates_forward_grouped(int L, const float *zh, int64_t zh_stride, const float *const *zx,
                                    const int64_t *zx_strides, const float *const *c, int64_t N, int64_t H, int64_t HW,
                                    float *const *h_out, float *const *c_out, float *const *gates, void *stream);
+/* hrl_lstm_gates_backward_ex: hrl_lstm_gates_backward for the repeats of a recurrent unroll step -- dh (games
+ * dh_stride floats apart) is the sum of dh_parts partial gradients dh_part_stride floats apart (added in order),
+ * and with dzx given the gate gradient is also written (dzx_init) or added (else) into dzx (N, 4H, HW). */
+int hrl_lstm_gates_backward_ex(const float *gates, const float *c, const float *c_out, const float *dh,
+                               int64_t dh_stride, int dh_parts, int64_t dh_part_stride, const float *dc_out,
+                               int64_t N, int64_t H, int64_t HW, float *dz, float *dc, float *dzx, int dzx_init,
+                               void *stream);
 int hrl_lstm_gates_backward(const float *gates, const float *c, const float *c_out, const float *dh,
                             const float *dc_out, int64_t N, int64_t H, int64_t HW, float *dz, float *dc,
                             void *stream);
@@ -346,6 +353,9 @@ int hrl_gboard_pack_adjoint(const float *weight, int64_t Cout_fwd, int64_t w_cin
  * weight gradient of a 1x1 conv on the 6x6 board (O <= 8, C <= 256; games x_stride / dy_stride floats apart,
  * float4-aligned).  Deterministic (per-workgroup partials folded in order).  workspace:
  * hrl_gboard_pointwise_wgrad_workspace_bytes(C, O, N) bytes. */
+/* hrl_gboard_set_whole_ring: 1 (default) = launches with one task per workgroup stage a whole 32-channel k-step
+ * (9 quads) at once, 0 = the 3-quad ring always (measurement); returns the previous setting. */
+int hrl_gboard_set_whole_ring(int on);
 int64_t hrl_gboard_pointwise_wgrad_workspace_bytes(int64_t C, int64_t O, int64_t N);
 int hrl_gboard_pointwise_wgrad(const float *x, int64_t x_stride, const float *dy, int64_t dy_stride, int64_t N,
                                int64_t C, int64_t O, float *dweight, void *workspace, int64_t workspace_bytes,
@@ -365,17 +375,6 @@ int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_
                        int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
                        const float *beta, int relu, float *y, int64_t y_stride, void *stream);
 
-/* The ConvLSTM cells' h halves of a DRC repeat with the gate update in the epilogue (geister.py:17-63 stacked
- * over the layers, csrc/hrl_gboard.hip): for every game n, layer l, hidden channel c and cell q
- *   z_k = (zx[n, l*4H + k*H + c, q] + bias[l*4H + k*H + c]) + conv(h[n, l*H ..], W_l)[k*H + c, q],  k = i, f, o, g
- *   c_out = sig(z_f) * c_in + sig(z_i) * tanh(z_g),  h_out = sig(z_o) * tanh(c_out)
- * (hrl_lstm_gates_forward's float operations on hrl_gboard_forward's conv): the conv output never reaches HBM.
- * packed: hrl_gboard_pack of the stacked h-half weights (layers*4H, H, 3, 3); H a multiple of 16, <= 64; bias
- * (layers*4H) or NULL.  h, zx, c_in, c_out, h_out: games h_stride, zx_stride, c_stride, c_stride, hout_stride
- * floats apart, 16-byte aligned.  c_out may be c_in; h_out must not overlap h. */
-int hrl_gboard_lstm_forward(const float *h, int64_t h_stride, int64_t N, int64_t layers, int64_t H, const void *packed,
-                            const float *zx, int64_t zx_stride, const float *bias, const float *c_in, float *c_out,
-                            int64_t c_stride, float *h_out, int64_t hout_stride, void *stream);
 /* A 1x1 convolution on the 6x6 board (no bias; GeisterNet's move-head conv2 and value / return head convs,
  * geister.py:238-264): y[n, o, q] = sum_c W[o, c] x[n, c, q] over x1's C1 channels, then x2's C2 (x2 NULL when
  * C2 = 0), then y*alpha[o] + beta[o] (both or neither) and relu.  weight (O, C1 + C2) row-major, O in

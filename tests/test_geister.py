@@ -359,47 +359,14 @@ def test_sequence_unroll_matches_per_step_unroll(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('inplace', [False, True])
-@pytest.mark.parametrize('repeats', [1, 3])
-def test_fused_gate_repeats_match_unfused(cuda, inplace, repeats):
-    """hrl_gboard_lstm_forward (each DRC repeat's grouped h-half conv with the gate update in its epilogue) gives
-    bit-identically the states of the unfused path (hrl_gboard conv, then the HIP gate kernel): the conv is the
-    same kernel arithmetic and the gate update lstm_fwd_kernel's float operations.  In place (the generator's
-    stacked state, h' through scratch states) and out of place, one and three repeats, ragged game count."""
-    from handyrl_amd.envs.geister import DRC, GeisterNet
-    from handyrl_amd.nn import accelerate
-    torch.manual_seed(5)
-    net = accelerate(GeisterNet().to(cuda)).eval()
-    E = 50
-    x = torch.randn(E, 32, 6, 6, device=cuda)
-    h0 = torch.randn(E, 96, 6, 6, device=cuda)
-    c0 = torch.randn(E, 96, 6, 6, device=cuda)
-    results = []
-    for fuse in (False, True):
-        DRC.fuse_gates = fuse
-        try:
-            h, c = h0.clone(), c0.clone()
-            hs, cs = [h[:, 32 * i:32 * (i + 1)] for i in range(3)], [c[:, 32 * i:32 * (i + 1)] for i in range(3)]
-            with torch.no_grad(), net.body.inference_session(inplace_state=inplace):
-                h_last, (hs2, cs2) = net.body._inference_stacked(x, hs, cs, repeats)
-            if inplace:
-                assert hs2[0].data_ptr() == h.data_ptr() and cs2[0].data_ptr() == c.data_ptr()
-            results.append([t.clone() for t in [h_last] + hs2 + cs2])
-        finally:
-            DRC.fuse_gates = False
-    for a, b in zip(*results):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize('graph', [False, True])
-def test_grouped_drc_repeat_matches_per_layer_unroll(cuda, graph):
-    """The learner's unroll with each DRC repeat as one grouped h-half conv + one grouped gate launch
-    (nn.drc_repeat: hrl_gboard_forward_groups, hrl_lstm_gates_forward_grouped) against the per-layer launches
-    (_DeferredConv + lstm_gates): two LearnerSteps from the same seeded net on the same batch (ragged game
-    count) give the same losses, grad norms and updated weights, bit for bit -- each layer's values are the
-    per-layer kernels' float operations and the backward records the same (h, dz) pairs in the same order.
-    (The stem's weights aside: see below.)"""
+def test_grouped_drc_step_matches_per_layer_unroll(cuda, graph):
+    """The learner's unroll with each time step's DRC repeats under one autograd node (nn.drc_step: per repeat one
+    grouped h-half conv + one grouped gate launch, hrl_gboard_forward_groups / hrl_lstm_gates_forward_grouped;
+    backward with the K-split adjoint's partials summed inside hrl_lstm_gates_backward_ex) against the per-layer
+    launches (_DeferredConv + lstm_gates): from the same seeded net on the same batch (ragged game count) the
+    forward -- every loss -- is bit-identical (the per-layer kernels' float operations); the gradient (its norm)
+    and the updated weights agree to 1e-6 (the partial input gradients are added in a different order)."""
     from handyrl_amd.envs.geister import DRC
     from handyrl_amd.synthetic import geister_batch, default_args
     from handyrl_amd.trainer import LearnerStep
@@ -413,18 +380,16 @@ def test_grouped_drc_repeat_matches_per_layer_unroll(cuda, graph):
             DRC.group_repeat = grouped
             net = seeded_net()
             step = LearnerStep(net, args, cuda, graph=graph)
-            outs = []
-            for _ in range(2):
-                hidden = tuple([h.to(cuda) for h in hs] for hs in net.init_hidden([B, 2]))
-                out = step.step(batch, hidden)
-                outs.append({k: float(out[k]) for k in ('p', 'v', 'r', 'ent', 'total', 'grad_norm')})
-            res.append((outs, {n: p.detach().clone() for n, p in step.net.named_parameters()}))
+            hidden = tuple([h.to(cuda) for h in hs] for hs in net.init_hidden([B, 2]))
+            out = step.step(batch, hidden)
+            res.append(({k: float(out[k]) for k in ('p', 'v', 'r', 'ent', 'total', 'grad_norm')},
+                        {n: p.detach().clone() for n, p in step.net.named_parameters()}))
     finally:
         DRC.group_repeat = prev
     (o0, w0), (o1, w1) = res
-    assert o0 == o1, (o0, o1)
-    # the stem's weights see the vendor convolution backward (MIOpen), which is not run-to-run deterministic
-    # itself (the per-layer unroll twice differs there by ~1e-9): those within 1e-7, everything else exact
-    stem = ('conv1.weight', 'bn1.weight', 'bn1.bias')
-    diff = {n: float((w1[n] - w0[n]).abs().max()) for n in w0 if not torch.equal(w0[n], w1[n])}
-    assert all(n in stem and d < 1e-7 for n, d in diff.items()), diff
+    for k in ('p', 'v', 'r', 'ent', 'total'):
+        assert o0[k] == o1[k], (k, o0[k], o1[k])
+    assert abs(o1['grad_norm'] - o0['grad_norm']) <= 1e-6 * o0['grad_norm'], (o0['grad_norm'], o1['grad_norm'])
+    for n in w0:
+        den = max(float(w0[n].norm()), 1e-12)
+        assert float((w1[n] - w0[n]).norm()) / den <= 1e-6, n

@@ -1,5 +1,5 @@
-"""Time one chain block's backward: the fused hrl_conv3x3_block_backward (the default form, the LDS-DMA ring form
-2, the tile-shared form 1 and the per-wave form 0) vs the three launches it replaces.
+"""Time one chain block's backward: the fused hrl_conv3x3_block_backward (the default tile-shared form 1 and
+the per-wave form 0) vs the three launches it replaces.
 
     python tools/block_bench.py [--M 131072] [--iters 20]
 HRL_LIB_PATH selects another build of libhrl.so (diagnostic variants).  HIP events on the launch stream.
@@ -60,7 +60,7 @@ def main():
             fused()
             lib.hrl_conv3x3_set_block_form(prev)
         return run
-    for name, fn in (('fused_us', fused), ('fused_ring_us', form(2)), ('fused_tile_shared_us', form(1)),
+    for name, fn in (('fused_us', fused), ('fused_tile_shared_us', form(1)),
                      ('fused_per_wave_us', form(0)), ('three_launches_us', three)):
         for _ in range(3):
             fn()

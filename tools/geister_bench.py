@@ -57,6 +57,9 @@ def main():
     ap.add_argument('--flat', type=int, nargs='+', default=[1], help='train.FLAT_HIDDEN values to compare')
     opts = ap.parse_args()
     device = torch.device('cuda', 0)
+    if 'HRL_GBOARD_WHOLE' in os.environ:   # hrl_gboard's whole-k-step ring on (default) / off
+        from handyrl_amd import _native
+        _native.load().hrl_gboard_set_whole_ring(int(os.environ['HRL_GBOARD_WHOLE']))
     import handyrl_amd.train as train_mod
     for flat in opts.flat:
         train_mod.FLAT_HIDDEN = bool(flat)
