@@ -837,7 +837,9 @@ int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const flo
         games += ns[i];
     }
     a.tile0[nseg] = tiles;
-    const int64_t need = hrl_gboard_wgrad_workspace_bytes(Cout, Cin, games);
+    // one partial per workgroup, one workgroup per 16-game tile of a segment (each segment rounds up on its own)
+    (void)games;
+    const int64_t need = hrl_gboard_wgrad_workspace_bytes(Cout, Cin, tiles * 16);
     if (need < 0 || workspace_bytes < need) return HRL_EINVAL;
     a.nseg = nseg; a.cout = (int)Cout; a.cin = (int)Cin;
     a.cto = (int)((Cout + 31) / 32); a.cti = (int)((Cin + 31) / 32);

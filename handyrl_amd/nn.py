@@ -170,7 +170,7 @@ def gboard_wgrad(rec, w, b, sl):
         xst = (ctypes.c_int64 * n)(*[r[0].stride(0) for r in chunk])
         dyst = (ctypes.c_int64 * n)(*[r[1].stride(0) for r in chunk])
         ns = (ctypes.c_int64 * n)(*[r[0].shape[0] for r in chunk])
-        games = sum(r[0].shape[0] for r in chunk)
+        games = sum((r[0].shape[0] + 15) // 16 * 16 for r in chunk)   # one partial per 16-game tile of a record
         nbytes = lib.hrl_gboard_wgrad_workspace_bytes(cout, cin, games)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
         _native.check(lib.hrl_gboard_wgrad(

@@ -348,7 +348,13 @@ int hrl_gboard_pack_adjoint(const float *weight, int64_t Cout_fwd, int64_t w_cin
  * output gradients), ADDED into input channels [w_ci0, w_ci0 + Cin) of dweight (Cout, w_cin_total, 3, 3) and, when
  * dbias is given, into dbias (Cout).  Games are the MFMA K (exact bf16 split, fp32-accurate); deterministic.
  * Replaces the deferred weight gradient's aten.convolution_backward (nn.DeferredGrads.flush).  32-channel tiles
- * (Cout, Cin): 4x1, 2x2, 2x1, 1x2, 1x1.  workspace: hrl_gboard_wgrad_workspace_bytes(Cout, Cin, sum ns) bytes. */
+ * (Cout, Cin): 4x1, 2x2, 2x1, 1x2, 1x1.  workspace: hrl_gboard_wgrad_workspace_bytes(Cout, Cin, G) bytes, G = the
+ * sum over the segments of ns[i] rounded up to a multiple of 16 (one workgroup partial per 16-game tile). */
+int64_t hrl_gboard_wgrad_workspace_bytes(int64_t Cout, int64_t Cin, int64_t total_games);
+int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const float *const *dys,
+                     const int64_t *dy_strides, const int64_t *ns, int nseg, int64_t Cout, int64_t Cin,
+                     float *dweight, int64_t w_cin_total, int64_t w_ci0, float *dbias, void *workspace,
+                     int64_t workspace_bytes, void *stream);
 /* hrl_gboard_pointwise_wgrad: dweight (O, C) += sum over N games and the 36 cells of dy[n][o][q] x[n][c][q] -- the
  * weight gradient of a 1x1 conv on the 6x6 board (O <= 8, C <= 256; games x_stride / dy_stride floats apart,
  * float4-aligned).  Deterministic (per-workgroup partials folded in order).  workspace:
@@ -360,11 +366,6 @@ int64_t hrl_gboard_pointwise_wgrad_workspace_bytes(int64_t C, int64_t O, int64_t
 int hrl_gboard_pointwise_wgrad(const float *x, int64_t x_stride, const float *dy, int64_t dy_stride, int64_t N,
                                int64_t C, int64_t O, float *dweight, void *workspace, int64_t workspace_bytes,
                                void *stream);
-int64_t hrl_gboard_wgrad_workspace_bytes(int64_t Cout, int64_t Cin, int64_t total_games);
-int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const float *const *dys,
-                     const int64_t *dy_strides, const int64_t *ns, int nseg, int64_t Cout, int64_t Cin,
-                     float *dweight, int64_t w_cin_total, int64_t w_ci0, float *dbias, void *workspace,
-                     int64_t workspace_bytes, void *stream);
 /* hrl_gboard_forward_groups: a grouped conv (groups <= 4, Cin_g <= 32 per group) whose groups read separate
  * inputs xs[g] (N games, x_strides[g] floats apart): the DRC layers' h halves of one repeat without stacking
  * their states.  No bias / epilogue. */

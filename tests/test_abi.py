@@ -74,3 +74,21 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_native, 'LIB_PATH', str(tmp_path / 'nope.so'))
     with pytest.raises(RuntimeError, match='no CPU fallback'):
         _native.load()
+
+
+def test_gboard_wgrad_rejects_workspace_sized_by_games_not_tiles():
+    """hrl_gboard_wgrad runs one workgroup partial per 16-game tile of each record, so 24 records of 2 games need
+    24 partials, not ceil(48 / 16) = 3: a workspace sized from the game total is rejected before any launch."""
+    lib = _native.load()
+    n = 24
+    ptrs = (ctypes.c_void_p * n)(*[4096 * (i + 1) for i in range(n)])
+    strides = (ctypes.c_int64 * n)(*[32 * 36] * n)
+    dstrides = (ctypes.c_int64 * n)(*[128 * 36] * n)
+    ns = (ctypes.c_int64 * n)(*[2] * n)
+    cast = lambda a: ctypes.cast(a, ctypes.c_void_p)   # noqa: E731
+    small = lib.hrl_gboard_wgrad_workspace_bytes(128, 32, 2 * n)
+    enough = lib.hrl_gboard_wgrad_workspace_bytes(128, 32, 16 * n)
+    assert 0 < small < enough
+    code = lib.hrl_gboard_wgrad(cast(ptrs), cast(strides), cast(ptrs), cast(dstrides), cast(ns), n, 128, 32,
+                                ctypes.c_void_p(16), 64, 32, None, ctypes.c_void_p(16), small, None)
+    assert code == _native.HRL_EINVAL

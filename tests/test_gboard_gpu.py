@@ -171,7 +171,8 @@ def test_gboard_adjoint_matches_conv_input_gradient(cuda, N, cout_fwd, ci0, cin)
     (128, 64, 0, 32, (4096,), True),            # its x half over a whole unroll (T*N games at once)
     (32, 25, 0, 25, (300,), False),             # the stem: 25 input planes (a padded channel tile)
     (8, 64, 0, 64, (17, 100), False),           # the move head's 64 -> 8 (a padded output tile)
-])
+    (128, 64, 32, 32, (2,) * 24 + (5,), True),  # many tiny records (the learner's liveness probe): one partial
+])                                              # per record tile, far more than sum(ns) / 16
 @pytest.mark.parametrize('integer', [True, False])
 def test_gboard_wgrad_matches_conv_weight_gradient(cuda, cout, cin_total, ci0, cin, ns, bias, integer):
     """hrl_gboard_wgrad (games as the MFMA K, every recorded use in one launch, no concatenation) ADDS the weight
