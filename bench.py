@@ -46,7 +46,9 @@ from handyrl_amd.synthetic import tictactoe_batch, default_args  # noqa: E402
 from handyrl_amd.trainer import LearnerStep            # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-SCAN_PMC = 'r03s4_scan_pmc.json'   # PMC passes over the scan kernel the tree ships
+SCAN_PMC = 'r03s4_scan_pmc.json'   # PMC passes over the scan kernel the tree ships (unchanged since round 3)
+BLOCK_PMC = 'r04_block_pmc.json'   # the chain block backward (tools/block_pmc.py)
+FWD_PMC = 'r04_fwd_pmc.json'       # the ring forward conv, fwd form 2 (tools/conv_pmc.py fwd 2)
 
 
 def scan_bytes_per_launch(B, T, P=2, Pp=1, rewards=False):
@@ -170,6 +172,9 @@ def time_conv(device, M, iters=20):
             'bytes_per_launch': nbytes, 'us_per_launch': round(us, 2), 'M': M,
             'mfma_achieved_TFLOPs': round(tf, 1), 'mfma_frac_split': round(tf / peak, 4),
             'launches_per_step': 3,
+            'traffic': _pmc_bytes(FWD_PMC) if form == 2 else None,
+            'traffic_source': ('profiles/%s (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected)' % FWD_PMC
+                               if form == 2 else None),
             'note': 'the step\'s chain forward (BN statistics epilogue, BN + ReLU prologue) on random data; bytes = x '
                     'read + y written; split ceiling = bf16 dense peak / 6 partial products'}
 
@@ -307,7 +312,11 @@ def time_block_in_step(learner, batch, device, steps=4):
 
 def block_traffic():
     """HBM bytes per chain block backward launch from the committed rocprofv3 PMC passes (profiles/), or None."""
-    path = os.path.join(ROOT, 'profiles', 'r03_block_pmc.json')
+    return _pmc_bytes(BLOCK_PMC)
+
+
+def _pmc_bytes(name):
+    path = os.path.join(ROOT, 'profiles', name)
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -659,8 +668,8 @@ def main():
             'unit': 'GB/s',
             'frac': round(blk_gbs / HBM_PEAK_GBS, 4),
             'traffic': block_traffic(),
-            'traffic_source': 'profiles/r03_block_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes over '
-                              'tools/block_bench.py, gfx950-corrected)',
+            'traffic_source': 'profiles/%s (rocprofv3 FETCH_SIZE/WRITE_SIZE passes over '
+                              'tools/block_bench.py, gfx950-corrected)' % BLOCK_PMC,
             'bytes_per_launch': blk_bytes,
             'us_per_launch': round(us_blk, 2),
             'launches_timed': n_blk,
