@@ -521,9 +521,7 @@ def secondary_host_rollout(device, E=256):
     for name, games, observation in (('ParallelTicTacToe', 2048, False), ('Geister', 256, True)):
         env_args = {'env': name}
         torch.manual_seed(0)
-        net = make_env(env_args).net()().to(device)
-        if name == 'Geister':
-            net = accelerate(net)
+        net = accelerate(make_env(env_args).net()().to(device))   # HIP inference BatchNorm etc., as self-play
         gen = HostBatchGenerator(lambda: make_env(env_args), net, {'observation': observation, 'gamma': 0.8}, E=E)
         gen.generate(E)                      # warm-up
         torch.cuda.synchronize(device)

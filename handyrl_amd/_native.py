@@ -196,7 +196,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 _lib = None
 
