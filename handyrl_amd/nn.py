@@ -414,11 +414,21 @@ def gboard_adjoint_split(dy, w, ci0, cin, rec):
     return part.view(N, S, cin, 6, 6).sum(1)
 
 
+def _check_gboard_packed(packed, Cout, cin_g):
+    """hrl_gboard_forward reads hrl_gboard_pack_bytes(Cout, cin_g) bytes of split weights and cannot check them
+    itself: a buffer packed for another shape (or for the torus board conv) is refused here."""
+    need = _native.load().hrl_gboard_pack_bytes(Cout, cin_g)
+    if need < 0 or packed.dtype != torch.uint8 or packed.numel() < need:
+        raise ValueError('hrl_gboard: packed weights of %d bytes, (Cout %d, Cin_g %d) needs %d'
+                         % (packed.numel() * packed.element_size(), Cout, cin_g, need))
+
+
 def gboard_conv(x, packed, Cout, cin_g, groups=1, x2=None, bias=None, alpha=None, beta=None, relu=False, out=None):
     """F.conv2d(x, W, bias, padding=1, groups=groups) on the 6x6 board (csrc/hrl_gboard.hip, forward only, no
     autograd), W packed by gboard_pack; optional BatchNorm-apply (y*alpha + beta) and ReLU epilogue.  x may be
     a channel slice of a wider tensor; x2: channels 32.. of a two-source input (x then holds channels 0..31)."""
     N = x.shape[0]
+    _check_gboard_packed(packed, Cout, cin_g)
     y = torch.empty(N, Cout, 6, 6, device=x.device, dtype=torch.float32) if out is None else out
     P = _native.ptr
     _native.check(_native.load().hrl_gboard_forward(
@@ -456,6 +466,8 @@ class _DeferredConv(torch.autograd.Function):
         ci0 = 0 if sl is None else sl[0]
         cin_g = wv.shape[1]
         if gboard_conv_ok(x, w, cin_g, pad):   # the 6x6 board: games as MFMA rows (csrc/hrl_gboard.hip)
+            if packed is not None and packed.numel() != _native.load().hrl_gboard_pack_bytes(w.shape[0], cin_g):
+                packed = None   # packed for the torus board conv or another shape: repack for this kernel
             wpk = gboard_pack(w.detach(), cin_g, ci0) if packed is None else packed
             y = gboard_conv(x, wpk, w.shape[0], cin_g, bias=None if b is None else b.detach())
         elif _pointwise_ok(x, wv, pad):          # a 1x1 conv: per game one (Cout x Cin) . (Cin x cells) GEMM
@@ -540,6 +552,7 @@ class _DRCStep(torch.autograd.Function):
         zx_ptrs = _native.ptr_array(zx)
         zx_strides = _native.i64_array([z.stride(0) for z in zx])
         saved = []
+        _check_gboard_packed(packed, L * 4 * H, H)
         for _ in range(R):
             zh = torch.empty(N, L * 4 * H, 6, 6, device=hs[0].device)
             _native.check(lib.hrl_gboard_forward_groups(

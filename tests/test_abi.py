@@ -92,3 +92,17 @@ def test_gboard_wgrad_rejects_workspace_sized_by_games_not_tiles():
     code = lib.hrl_gboard_wgrad(cast(ptrs), cast(strides), cast(ptrs), cast(dstrides), cast(ns), n, 128, 32,
                                 ctypes.c_void_p(16), 64, 32, None, ctypes.c_void_p(16), small, None)
     assert code == _native.HRL_EINVAL
+
+
+def test_gboard_conv_refuses_packed_weights_of_another_shape():
+    """hrl_gboard_forward cannot see the packed buffer's size; the Python boundary refuses a buffer smaller than
+    hrl_gboard_pack_bytes(Cout, Cin_g) before any launch (no GPU needed)."""
+    import torch
+    from handyrl_amd import nn as hnn
+    lib = _native.load()
+    need = lib.hrl_gboard_pack_bytes(64, 32)
+    x = torch.zeros(1, 32, 6, 6)
+    with pytest.raises(ValueError):
+        hnn.gboard_conv(x, torch.zeros(need - 16, dtype=torch.uint8), 64, 32)
+    with pytest.raises(ValueError):
+        hnn.gboard_conv(x, torch.zeros(need // 4, dtype=torch.float32), 64, 32)

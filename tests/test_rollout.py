@@ -253,3 +253,52 @@ def test_sample_record_hip_matches_torch(cuda, A):
     assert bool((a[:7] == 0).all())
     for k in ('policy', 'amask', 'action', 'value', 'turn', 'reward'):
         assert torch.equal(a_st[k], b_st[k]), k
+
+
+@pytest.mark.gpu
+def test_state_dependent_reward_is_read_after_the_step(cuda):
+    """A batched env whose reward depends on the state (no REWARD_STATELESS) has it read after env.step, as
+    generation.py:55-60 reads env.reward() after env.step: with a GeisterBatch whose reward is 0.001 x its ply
+    counter, slot t of the reward record holds the reward of the state AFTER ply t for every game running at ply t
+    (0 otherwise), and the returns are the fp64 discounted sums of those records (generation.py:73-77)."""
+    from handyrl_amd.envs.geister import GeisterNet, GeisterBatch
+    from handyrl_amd.rollout import DeviceGenerator
+    from handyrl_amd.nn import accelerate
+
+    class PlyReward(GeisterBatch):
+        REWARD_STATELESS = False
+        seen = None
+
+        def reward(self):
+            return (0.001 * (self.turn_count + 2).double()).view(-1, 1).expand(-1, 2).contiguous()
+
+        def step(self, action, active):
+            before = self.reward().clone()
+            super().step(action, active)
+            self.seen.append((before, self.reward().clone(), active.clone()))
+
+    torch.manual_seed(3)
+    net = accelerate(GeisterNet().to(cuda))
+    E = 32
+    env = PlyReward(E, cuda)
+    env.seen = []
+    gen = DeviceGenerator(env, net, graph=False, gamma=0.8)
+    ep = gen.generate(generator=torch.Generator(device=cuda).manual_seed(0))
+    reward = ep['reward'].cpu()          # the episode record's dtype (recorded in fp64, like the reference's floats)
+    T = reward.shape[1]
+    expect = torch.zeros(reward.shape, dtype=torch.float64)
+    moved = False
+    for t, (before, after, active) in enumerate(env.seen[:T]):
+        a = active.cpu().view(-1, 1)
+        expect[:, t] = torch.where(a, after.cpu(), 0.0)
+        moved = moved or bool((a & (after.cpu() != before.cpu())).any())
+    assert moved   # the reward does change with the step, so reading it before would differ
+    bad = (reward != expect.to(reward.dtype)).any(-1).nonzero().tolist()
+    assert not bad, (len(env.seen), T, ep['length'].tolist(),
+                     [(n, t, reward[n, t].tolist(), expect[n, t].tolist()) for n, t in bad[:6]])
+    ret = torch.zeros(E, 2, dtype=torch.float64)
+    rets = torch.zeros(E, T, 2, dtype=torch.float64)
+    for k in range(T - 1, -1, -1):
+        ret = expect[:, k] + 0.8 * ret
+        rets[:, k] = ret
+    assert torch.equal(ep['return'].cpu(), rets.to(ep['return'].dtype))   # fp64 sums, stored as the record's dtype
