@@ -193,6 +193,68 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
     const int nbg = nblocks / G;
     const float w = weight ? weight[c] : 1.0f;
     float dw = 0.f, db = 0.f;
+    // group grp's statistics -> its outputs (one thread; groups in order: the running statistics advance as G
+    // sequential calls would)
+    auto fin = [&](int grp, double S0, double S1) {
+        const int gc = grp * C + c;
+        if (mode == 0) {
+            const double mean = S0 / M;
+            double var = S1 / M - mean * mean;
+            if (var < 0.0) var = 0.0;
+            const float meanf = (float)mean;
+            const float invstd = (float)(1.0 / sqrt(var + eps));
+            save_mean[gc] = meanf;
+            save_invstd[gc] = invstd;
+            const float alpha = invstd * w;
+            coef_a[gc] = alpha;
+            coef_b[gc] = (bias ? bias[c] : 0.0f) - meanf * alpha;
+            if (running_mean) running_mean[c] = momentum * meanf + (1.0f - momentum) * running_mean[c];
+            if (running_var) {
+                const float unbiased = (float)(M > 1.0 ? var * M / (M - 1.0) : var);
+                running_var[c] = momentum * unbiased + (1.0f - momentum) * running_var[c];
+            }
+        } else {
+            const float invstd = save_invstd[gc];
+            const float sum_dy = (float)S0, dot = (float)S1;
+            dw = grp == 0 ? dot * invstd : dw + dot * invstd;
+            db = grp == 0 ? sum_dy : db + sum_dy;
+            coef_a[gc] = dot * invstd * invstd / (float)M;   // k
+            coef_b[gc] = sum_dy / (float)M;                   // mean(dy)
+        }
+    };
+    if (G > 1 && G <= kThreads / 2) {
+        // the groups' partial sums fold in parallel (tpg threads per group, a power of two, fixed tree order),
+        // then one thread finalizes the groups in order: one reduction round instead of G
+        int tpg = 1;
+        while (tpg * 2 * G <= kThreads) tpg *= 2;
+        const int grp = threadIdx.x / tpg, sub = threadIdx.x % tpg;
+        double s0 = 0.0, s1 = 0.0;
+        if (grp < G) {
+            for (int i = sub; i < nbg; i += tpg) {
+                const int64_t b = (int64_t)grp * nbg + i;
+                s0 += part[(b * C + c) * 2 + 0];
+                s1 += part[(b * C + c) * 2 + 1];
+            }
+        }
+        red[0][threadIdx.x] = s0;
+        red[1][threadIdx.x] = s1;
+        __syncthreads();
+        for (int wd = tpg / 2; wd > 0; wd >>= 1) {
+            if (grp < G && sub < wd) {
+                red[0][threadIdx.x] += red[0][threadIdx.x + wd];
+                red[1][threadIdx.x] += red[1][threadIdx.x + wd];
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            for (int g2 = 0; g2 < G; ++g2) fin(g2, red[0][g2 * tpg], red[1][g2 * tpg]);
+            if (mode == 1) {
+                if (dweight) dweight[c] = dw;
+                if (dbias) dbias[c] = db;
+            }
+        }
+        return;
+    }
     for (int grp = 0; grp < G; ++grp) {
         double s0 = 0.0, s1 = 0.0;
         for (int i = threadIdx.x; i < nbg; i += kThreads) {
@@ -210,34 +272,7 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
             }
             __syncthreads();
         }
-        if (threadIdx.x == 0) {
-            const double S0 = red[0][0], S1 = red[1][0];
-            const int gc = grp * C + c;
-            if (mode == 0) {
-                const double mean = S0 / M;
-                double var = S1 / M - mean * mean;
-                if (var < 0.0) var = 0.0;
-                const float meanf = (float)mean;
-                const float invstd = (float)(1.0 / sqrt(var + eps));
-                save_mean[gc] = meanf;
-                save_invstd[gc] = invstd;
-                const float alpha = invstd * w;
-                coef_a[gc] = alpha;
-                coef_b[gc] = (bias ? bias[c] : 0.0f) - meanf * alpha;
-                if (running_mean) running_mean[c] = momentum * meanf + (1.0f - momentum) * running_mean[c];
-                if (running_var) {
-                    const float unbiased = (float)(M > 1.0 ? var * M / (M - 1.0) : var);
-                    running_var[c] = momentum * unbiased + (1.0f - momentum) * running_var[c];
-                }
-            } else {
-                const float invstd = save_invstd[gc];
-                const float sum_dy = (float)S0, dot = (float)S1;
-                dw = grp == 0 ? dot * invstd : dw + dot * invstd;
-                db = grp == 0 ? sum_dy : db + sum_dy;
-                coef_a[gc] = dot * invstd * invstd / (float)M;   // k
-                coef_b[gc] = sum_dy / (float)M;                   // mean(dy)
-            }
-        }
+        if (threadIdx.x == 0) fin(grp, red[0][0], red[1][0]);
         __syncthreads();   // red is reused by the next group
     }
     if (mode == 1 && threadIdx.x == 0) {

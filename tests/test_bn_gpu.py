@@ -507,3 +507,30 @@ def test_tile_shared_forward_matches_per_wave_conv(cuda, M, pro):
         s = p.view(nblk, 32, 2).sum(0)
         assert bool(torch.isfinite(s).all())
         assert float(((s - ref).abs() / scale).max()) < 1e-6
+
+
+@pytest.mark.parametrize('G,N,C,HW', [(16, 8, 32, 36), (2, 50, 8, 36), (64, 4, 1, 36), (200, 2, 4, 9)])
+def test_grouped_batch_norm_matches_sequential_calls(cuda, G, N, C, HW):
+    """nn.batch_norm_train(groups=G) (one launch per direction, the groups' statistics folded in parallel for
+    G <= 128 and finalized in group order) vs G sequential calls on the row blocks: outputs, input / weight / bias
+    gradients and the running statistics after all G updates, to fp64-level rounding (1e-6 relative)."""
+    from handyrl_amd.nn import batch_norm_train
+    g0 = torch.Generator(device=cuda).manual_seed(G * 7 + C)
+    x = torch.randn(G * N, C, HW, device=cuda, generator=g0) * 2 + 0.5
+    dy = torch.randn(G * N, C, HW, device=cuda, generator=g0)
+    outs = []
+    for grouped in (True, False):
+        w = (torch.rand(C, device=cuda, generator=torch.Generator(device=cuda).manual_seed(1)) + 0.5).requires_grad_()
+        b = torch.zeros(C, device=cuda, requires_grad=True)
+        rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+        xi = x.clone().requires_grad_()
+        if grouped:
+            y = batch_norm_train(xi, w, b, rm, rv, 0.1, 1e-5, relu=True, groups=G)
+        else:
+            y = torch.cat([batch_norm_train(xi[k * N:(k + 1) * N], w, b, rm, rv, 0.1, 1e-5, relu=True)
+                           for k in range(G)])
+        y.backward(dy)
+        outs.append((y.detach(), xi.grad, w.grad, b.grad, rm, rv))
+    for a, r in zip(*outs):
+        scale = max(float(r.abs().max()), 1e-30)
+        assert float((a - r).abs().max()) <= 1e-6 * scale
