@@ -571,34 +571,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 }
 
 // fold the per-workgroup partials in block order and add into dst (the gradient of weight (Cout, w_cin_total, 3,
-// 3), input channels [ci0, ci0 + cin)) and, with a bias, into dbias
+// 3), input channels [ci0, ci0 + cin)) and, with a bias, into dbias.  Thread i reads element i of every
+// workgroup's [unit][tap][32 co][32 ci] slab (consecutive threads, consecutive addresses), four workgroup ranges
+// per element over the block's waves, folded in range order through LDS (deterministic).
 __global__ __launch_bounds__(256) void gboard_wgrad_reduce_kernel(const float *__restrict__ part, int blocks, int cto,
                                                                   int cti, int cout, int cin, int w_cin_total,
                                                                   int ci0, float *__restrict__ dst,
                                                                   float *__restrict__ dbias) {
+    __shared__ float red[4][64];
     const int nunits = cto * cti;
-    const int total = cout * cin * 9;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < total) {
-        const int tap = i % 9, ci = (i / 9) % cin, co = i / (9 * cin);
-        const int unit = (co >> 5) * cti + (ci >> 5);
-        const int64_t off = ((int64_t)unit * 9 + tap) * 1024 + (co & 31) * 32 + (ci & 31);
-        float s0 = 0.f, s1 = 0.f;
-        int b = 0;
-        for (; b + 1 < blocks; b += 2) {
-            s0 += part[(int64_t)b * nunits * 9 * 1024 + off];
-            s1 += part[(int64_t)(b + 1) * nunits * 9 * 1024 + off];
+    const int64_t slab = (int64_t)nunits * 9 * 1024;
+    const int lane = threadIdx.x & 63, r = threadIdx.x >> 6;
+    const int64_t e = (int64_t)blockIdx.x * 64 + lane;   // element of the slab
+    const int per = (blocks + 3) / 4;
+    const int b0 = r * per, b1 = min(blocks, b0 + per);
+    float s0 = 0.f, s1 = 0.f;
+    if (e < slab) {
+        int b = b0;
+        for (; b + 1 < b1; b += 2) {
+            s0 += part[(int64_t)b * slab + e];
+            s1 += part[(int64_t)(b + 1) * slab + e];
         }
-        if (b < blocks) s0 += part[(int64_t)b * nunits * 9 * 1024 + off];
-        float *d = dst + ((int64_t)co * w_cin_total + ci0 + ci) * 9 + tap;
-        *d = *d + (s0 + s1);
+        if (b < b1) s0 += part[(int64_t)b * slab + e];
     }
-    if (dbias && i < cout) {
-        const float *bp = part + (int64_t)blocks * nunits * 9 * 1024;
+    red[r][lane] = s0 + s1;
+    __syncthreads();
+    if (r == 0 && e < slab) {
+        const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+        const int ci_l = (int)(e & 31), co_l = (int)((e >> 5) & 31);
+        const int tap = (int)((e >> 10) % 9), unit = (int)(e / (9 * 1024));
+        const int co = (unit / cti) * 32 + co_l, ci = (unit % cti) * 32 + ci_l;
+        if (co < cout && ci < cin) {
+            float *d = dst + ((int64_t)co * w_cin_total + ci0 + ci) * 9 + tap;
+            *d = *d + v;
+        }
+    }
+    if (dbias && blockIdx.x == 0) {
+        const float *bp = part + (int64_t)blocks * slab;
         const int nch = 32 * cto;
-        float t = 0.f;
-        for (int b = 0; b < blocks; ++b) t += bp[(int64_t)b * nch + i];
-        dbias[i] = dbias[i] + t;
+        for (int i = threadIdx.x; i < cout; i += 256) {
+            float t = 0.f;
+            for (int b = 0; b < blocks; ++b) t += bp[(int64_t)b * nch + i];
+            dbias[i] = dbias[i] + t;
+        }
     }
 }
 
@@ -658,16 +673,24 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const float *__restrict__
 
 __global__ __launch_bounds__(256) void pw_wgrad_reduce_kernel(const float *__restrict__ part, int blocks, int OC,
                                                               float *__restrict__ dw) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= OC) return;
+    // element i = blockIdx.x * 64 + lane; the block's four waves sum four workgroup ranges, folded in order
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, r = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + lane;
+    const int per = (blocks + 3) / 4;
+    const int b0 = r * per, b1 = min(blocks, b0 + per);
     float s0 = 0.f, s1 = 0.f;
-    int b = 0;
-    for (; b + 1 < blocks; b += 2) {
-        s0 += part[(int64_t)b * OC + i];
-        s1 += part[(int64_t)(b + 1) * OC + i];
+    if (i < OC) {
+        int b = b0;
+        for (; b + 1 < b1; b += 2) {
+            s0 += part[(int64_t)b * OC + i];
+            s1 += part[(int64_t)(b + 1) * OC + i];
+        }
+        if (b < b1) s0 += part[(int64_t)b * OC + i];
     }
-    if (b < blocks) s0 += part[(int64_t)b * OC + i];
-    dw[i] = dw[i] + (s0 + s1);
+    red[r][lane] = s0 + s1;
+    __syncthreads();
+    if (r == 0 && i < OC) dw[i] = dw[i] + (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
 }
 
 int g_gboard_whole = 1;   // hrl_gboard_set_whole_ring
@@ -854,8 +877,8 @@ int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const flo
     else hipLaunchKernelGGL((gboard_wgrad_kernel<1, 1>), dim3(blocks), dim3(256), 0, s, a);
     int rc = status();
     if (rc) return rc;
-    const int total = (int)(Cout * Cin * 9);
-    hipLaunchKernelGGL(gboard_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, a.part, blocks, a.cto,
+    const int64_t slab = (int64_t)a.cto * a.cti * 9 * 1024;
+    hipLaunchKernelGGL(gboard_wgrad_reduce_kernel, dim3((unsigned)((slab + 63) / 64)), dim3(256), 0, s, a.part, blocks, a.cto,
                        a.cti, (int)Cout, (int)Cin, (int)w_cin_total, (int)w_ci0, dweight, dbias);
     return status();
 }
@@ -889,7 +912,7 @@ int hrl_gboard_pointwise_wgrad(const float *x, int64_t x_stride, const float *dy
     int rc = status();
     if (rc) return rc;
     const int OC = (int)(O * C);
-    hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3((OC + 255) / 256), dim3(256), 0, s, part, (int)blocks, OC,
+    hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3((OC + 63) / 64), dim3(256), 0, s, part, (int)blocks, OC,
                        dweight);
     return status();
 }
