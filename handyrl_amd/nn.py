@@ -470,6 +470,10 @@ class _DeferredConv(torch.autograd.Function):
                 packed = None   # packed for the torus board conv or another shape: repack for this kernel
             wpk = gboard_pack(w.detach(), cin_g, ci0) if packed is None else packed
             y = gboard_conv(x, wpk, w.shape[0], cin_g, bias=None if b is None else b.detach())
+        elif (b is None and _pointwise_ok(x, wv, pad) and wv.shape[0] in (1, 2, 4, 8) and x.shape[1] <= 128
+              and gboard_ok(x)):
+            # a 1x1 conv with a few outputs on the 6x6 board (the heads): one HIP pass over x (hrl_gboard_pointwise)
+            y = gboard_pointwise(x, wv.detach())
         elif _pointwise_ok(x, wv, pad):          # a 1x1 conv: per game one (Cout x Cin) . (Cin x cells) GEMM
             N, C = x.shape[0], x.shape[1]
             y = torch.matmul(wv.detach().reshape(wv.shape[0], C), x.reshape(N, C, -1)).view(N, -1, *x.shape[2:])
@@ -518,6 +522,8 @@ def _deferred_conv_dx(dy, x, w, sl, pad, rec):
         return gboard_conv(dy, rec.adjoint_pack(w, ci0, wv.shape[1]), wv.shape[1], Cf)
     if _pointwise_ok(x, wv, pad):
         N, O = dy.shape[0], dy.shape[1]
+        if O == 1:   # one output channel: dx = w[c] * dy, an outer product (the same single products as the GEMM)
+            return wv.detach().reshape(1, -1, 1, 1) * dy
         return torch.matmul(wv.detach().reshape(O, -1).t(), dy.reshape(N, O, -1)).view_as(x)
     return torch.ops.aten.convolution_backward(dy, x, wv, None, [1, 1], list(pad), [1, 1], False, [0, 0], 1,
                                                [True, False, False])[0]
