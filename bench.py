@@ -636,6 +636,10 @@ def main():
         cold = time_scan(device, 1 << 18, T, 60, cold=True)
         scan_roof = {
             'kernel': 'targets_kernel<VTRACE,UPGO> value head (hrl_compute_targets_fused)',
+            'in_step': False,
+            'in_step_note': 'the B1 operator boundary (compute_target, losses.py:61) on the step-size batch; the '
+                            'learner step runs the same scan code (hrl_scan.h recur_chunk) inside '
+                            'loss_fused_kernel (loss_roofline), so this kernel is not in the step sequence',
             'bound': 'hbm',
             'achieved': round(hot['GBps'], 1),
             'peak': HBM_PEAK_GBS,
