@@ -157,6 +157,7 @@ SIGNATURES = {
                                         ctypes.c_void_p, ctypes.c_int, _i64, _i64, _f32p, _i64, _i64, _f32p,
                                         ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_gboard_set_whole_ring': (ctypes.c_int, [ctypes.c_int]),
+    'hrl_gboard_set_nctw': (ctypes.c_int, [ctypes.c_int]),
     'hrl_gboard_pointwise_wgrad_workspace_bytes': (_i64, [_i64, _i64, _i64]),
     'hrl_gboard_pointwise_wgrad': (ctypes.c_int, [_f32p, _i64, _f32p, _i64, _i64, _i64, _i64, _f32p, ctypes.c_void_p,
                                                   _i64, ctypes.c_void_p]),

@@ -694,6 +694,7 @@ __global__ __launch_bounds__(256) void pw_wgrad_reduce_kernel(const float *__res
 }
 
 int g_gboard_whole = 1;   // hrl_gboard_set_whole_ring
+int g_gboard_nctw = 0;    // hrl_gboard_set_nctw: 0 = the launcher's choice
 
 int status() {
     const hipError_t e = hipGetLastError();
@@ -800,6 +801,8 @@ int gboard_launch(GbArgs a, int64_t Cin_g, int64_t groups, hipStream_t s) {
         const double rounds = (double)((tasks + kCUs - 1) / kCUs) * c / 4.0;
         if (rounds < best - 1e-9) { best = rounds; nctw = c; }
     }
+    if (g_gboard_nctw > 0 && a.nct % g_gboard_nctw == 0 && !(groups > 1 && (cout_g / 16) % g_gboard_nctw))
+        nctw = g_gboard_nctw;   // hrl_gboard_set_nctw (measurement)
     const int64_t tasks = ntiles * (a.nct / nctw);
     int grid = (int)(tasks < kCUs ? tasks : kCUs);
     const dim3 block(kThreads);
@@ -881,6 +884,12 @@ int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const flo
     hipLaunchKernelGGL(gboard_wgrad_reduce_kernel, dim3((unsigned)((slab + 63) / 64)), dim3(256), 0, s, a.part, blocks, a.cto,
                        a.cti, (int)Cout, (int)Cin, (int)w_cin_total, (int)w_ci0, dweight, dbias);
     return status();
+}
+
+int hrl_gboard_set_nctw(int nctw) {
+    const int prev = g_gboard_nctw;
+    g_gboard_nctw = (nctw == 1 || nctw == 2 || nctw == 4) ? nctw : 0;
+    return prev;
 }
 
 int hrl_gboard_set_whole_ring(int on) {

@@ -362,6 +362,9 @@ int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const flo
 /* hrl_gboard_set_whole_ring: 1 (default) = launches with one task per workgroup stage a whole 32-channel k-step
  * (9 quads) at once, 0 = the 3-quad ring always (measurement); returns the previous setting. */
 int hrl_gboard_set_whole_ring(int on);
+/* hrl_gboard_set_nctw: force the column tiles per workgroup (1, 2, 4; 0 = the launcher's choice), measurement
+ * only; returns the previous setting. */
+int hrl_gboard_set_nctw(int nctw);
 int64_t hrl_gboard_pointwise_wgrad_workspace_bytes(int64_t C, int64_t O, int64_t N);
 int hrl_gboard_pointwise_wgrad(const float *x, int64_t x_stride, const float *dy, int64_t dy_stride, int64_t N,
                                int64_t C, int64_t O, float *dweight, void *workspace, int64_t workspace_bytes,

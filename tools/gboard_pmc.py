@@ -21,9 +21,11 @@ def main():
     ap.add_argument('--N', type=int, default=256)
     ap.add_argument('--iters', type=int, default=20)
     ap.add_argument('--whole', type=int, default=1)
+    ap.add_argument('--nctw', type=int, default=0)
     opts = ap.parse_args()
     dev = torch.device('cuda', 0)
     _native.load().hrl_gboard_set_whole_ring(opts.whole)
+    _native.load().hrl_gboard_set_nctw(opts.nctw)
     g = torch.Generator(device=dev).manual_seed(1)
     N = opts.N
     if opts.which == 'h':
@@ -46,7 +48,7 @@ def main():
         launch()
     e.record()
     e.synchronize()
-    print('%s N=%d whole=%d: %.2f us per launch' % (opts.which, N, opts.whole, s.elapsed_time(e) * 1e3 / opts.iters))
+    print('%s N=%d whole=%d nctw=%d: %.2f us per launch' % (opts.which, N, opts.whole, opts.nctw, s.elapsed_time(e) * 1e3 / opts.iters))
 
 
 if __name__ == '__main__':
