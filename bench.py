@@ -295,6 +295,9 @@ def time_block_in_step(learner, batch, device, steps=4):
     from handyrl_amd import nn as hnn
     hnn.BLOCK_TIMING = []
     reducer = learner.reducer
+    # each rank's update would use its own un-reduced gradients: the training state is put back afterwards, so
+    # the replicas stay identical (and equal to the state after the timed steps)
+    snap = learner.snapshot()
     if reducer is not None:
         reducer.enabled = False     # no gradient all-reduce in these steps: nothing to pair across ranks, and
     try:                            # no collective between the timed launches on the stream
@@ -304,6 +307,7 @@ def time_block_in_step(learner, batch, device, steps=4):
         ts = [s.elapsed_time(e) * 1e3 for s, e in hnn.BLOCK_TIMING[3:]]   # the first eager step warms up
     finally:
         hnn.BLOCK_TIMING = None
+        learner.restore(snap)
         if reducer is not None:
             reducer.enabled = True
             reducer.reset()

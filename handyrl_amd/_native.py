@@ -158,18 +158,19 @@ SIGNATURES = {
                                         ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_gboard_set_whole_ring': (ctypes.c_int, [ctypes.c_int]),
     'hrl_gboard_set_nctw': (ctypes.c_int, [ctypes.c_int]),
+    'hrl_gboard_launch_stats': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     'hrl_gboard_pointwise_wgrad_workspace_bytes': (_i64, [_i64, _i64, _i64]),
     'hrl_gboard_pointwise_wgrad': (ctypes.c_int, [_f32p, _i64, _f32p, _i64, _i64, _i64, _i64, _f32p, ctypes.c_void_p,
                                                   _i64, ctypes.c_void_p]),
     'hrl_gboard_forward_groups': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, _i64, _i64, _i64, ctypes.c_void_p,
-                                                 _i64, _f32p, _i64, ctypes.c_void_p]),
+                                                 _i64, _i64, _f32p, _i64, ctypes.c_void_p]),
     'hrl_lstm_gates_backward_ex': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _i64, ctypes.c_int, _i64, _f32p, _i64,
                                                   _i64, _i64, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_void_p]),
     'hrl_lstm_gates_forward_grouped': (ctypes.c_int, [ctypes.c_int, _f32p, _i64, ctypes.c_void_p, ctypes.c_void_p,
                                                       ctypes.c_void_p, _i64, _i64, _i64, ctypes.c_void_p,
                                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
-    'hrl_gboard_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _i64, _i64, _i64, _i64, ctypes.c_void_p, _i64, _f32p,
-                                          _f32p, _f32p, ctypes.c_int, _f32p, _i64, ctypes.c_void_p]),
+    'hrl_gboard_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _i64, _i64, _i64, _i64, ctypes.c_void_p, _i64, _i64,
+                                          _f32p, _f32p, _f32p, ctypes.c_int, _f32p, _i64, ctypes.c_void_p]),
     'hrl_gboard_pointwise': (ctypes.c_int, [_f32p, _i64, _i64, _f32p, _i64, _i64, _i64, _f32p, _i64, _f32p, _f32p,
                                             ctypes.c_int, _f32p, _i64, ctypes.c_void_p]),
     'hrl_torus_head_pool': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, _i64, _f32p, _f32p, ctypes.c_void_p]),
@@ -197,7 +198,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 _lib = None
 

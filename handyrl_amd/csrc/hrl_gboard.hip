@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "../../include/hrl_nn.h"
@@ -695,6 +696,10 @@ __global__ __launch_bounds__(256) void pw_wgrad_reduce_kernel(const float *__res
 
 int g_gboard_whole = 1;   // hrl_gboard_set_whole_ring
 int g_gboard_nctw = 0;    // hrl_gboard_set_nctw: 0 = the launcher's choice
+// hrl_gboard_launch_stats: which forms the launchers chose since the last reset (host-side counters, one thread)
+enum { kStConv, kStWhole, kStNctw1, kStNctw2, kStNctw4, kStGroups4, kStFwdGroups, kStWgrad, kStWgradMaxSegs,
+       kStWgradMaxTiles, kStWgradMultiTile, kStCount };
+int64_t g_gboard_stats[kStCount] = {};
 
 int status() {
     const hipError_t e = hipGetLastError();
@@ -745,11 +750,14 @@ int hrl_gboard_pack_adjoint(const float *weight, int64_t Cout_fwd, int64_t w_cin
 int gboard_launch(GbArgs a, int64_t Cin_g, int64_t groups, hipStream_t s);
 
 int hrl_gboard_forward_groups(const float *const *xs, const int64_t *x_strides, int64_t N, int64_t Cin_g,
-                              int64_t groups, const void *packed, int64_t Cout, float *y, int64_t y_stride,
-                              void *stream) {
+                              int64_t groups, const void *packed, int64_t packed_bytes, int64_t Cout, float *y,
+                              int64_t y_stride, void *stream) {
     if (!xs || !x_strides || !packed || !y || N < 1 || Cin_g < 1 || Cin_g > 32 || groups < 1 || groups > 4 ||
         Cout < 1 || Cout % groups || (Cout / groups) % 16)
         return HRL_EINVAL;
+    // the kernel reads hrl_gboard_pack_bytes(Cout, Cin_g) bytes of split fragments: refuse a smaller buffer
+    const int64_t need = hrl_gboard_pack_bytes(Cout, Cin_g);
+    if (need < 0 || packed_bytes < need) return HRL_EINVAL;
     if (!aligned16(y) || y_stride % 4 || y_stride < Cout * kHW) return HRL_EINVAL;
     GbArgs a{};
     for (int g = 0; g < groups; ++g) {
@@ -766,10 +774,12 @@ int hrl_gboard_forward_groups(const float *const *xs, const int64_t *x_strides, 
 }
 
 int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_t x2_stride, int64_t N, int64_t Cin_g,
-                       int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
-                       const float *beta, int relu, float *y, int64_t y_stride, void *stream) {
+                       int64_t groups, const void *packed, int64_t packed_bytes, int64_t Cout, const float *bias,
+                       const float *alpha, const float *beta, int relu, float *y, int64_t y_stride, void *stream) {
     if (!x || !packed || !y || N < 1 || !kc_ok(Cin_g) || groups < 1 || Cout < 1 || Cout % groups)
         return HRL_EINVAL;
+    const int64_t need = hrl_gboard_pack_bytes(Cout, Cin_g);   // the split fragments the kernel reads
+    if (need < 0 || packed_bytes < need) return HRL_EINVAL;
     const int64_t cout_g = Cout / groups;
     if (groups > 1 && cout_g % 16) return HRL_EINVAL;        // a column tile never straddles two groups
     if (x2 && (Cin_g <= 32 || Cin_g > 64 || groups != 1)) return HRL_EINVAL;
@@ -821,6 +831,10 @@ int gboard_launch(GbArgs a, int64_t Cin_g, int64_t groups, hipStream_t s) {
     } while (0)
     // one task per workgroup: the whole k-step ring (see gboard_conv_kernel)
     const bool whole = tasks <= kCUs && g_gboard_whole && KC == 1;
+    ++g_gboard_stats[kStConv];
+    g_gboard_stats[kStWhole] += whole;
+    ++g_gboard_stats[nctw == 1 ? kStNctw1 : (nctw == 2 ? kStNctw2 : kStNctw4)];
+    g_gboard_stats[kStGroups4] += groups == 4;
     if (KC == 1) {
         if (padc) HRL_GB_LAUNCH(1, true); else HRL_GB_LAUNCH(1, false);
     } else if (KC == 2) {
@@ -872,6 +886,10 @@ int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const flo
     a.part = static_cast<float *>(workspace);
     a.bias = dbias != nullptr;
     const int blocks = (int)(tiles < kCUs ? tiles : kCUs);
+    ++g_gboard_stats[kStWgrad];
+    g_gboard_stats[kStWgradMaxSegs] = std::max<int64_t>(g_gboard_stats[kStWgradMaxSegs], nseg);
+    g_gboard_stats[kStWgradMaxTiles] = std::max<int64_t>(g_gboard_stats[kStWgradMaxTiles], tiles);
+    g_gboard_stats[kStWgradMultiTile] += tiles > blocks;   // workgroups carrying accumulators over several tiles
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (a.cto == 4 && a.cti == 1) hipLaunchKernelGGL((gboard_wgrad_kernel<4, 1>), dim3(blocks), dim3(256), 0, s, a);
     else if (a.cto == 2 && a.cti == 2) hipLaunchKernelGGL((gboard_wgrad_kernel<2, 2>), dim3(blocks), dim3(256), 0, s, a);
@@ -890,6 +908,14 @@ int hrl_gboard_set_nctw(int nctw) {
     const int prev = g_gboard_nctw;
     g_gboard_nctw = (nctw == 1 || nctw == 2 || nctw == 4) ? nctw : 0;
     return prev;
+}
+
+int hrl_gboard_launch_stats(int64_t *counts, int n, int reset) {
+    const int m = counts ? std::min(n, (int)kStCount) : 0;
+    for (int i = 0; i < m; ++i) counts[i] = g_gboard_stats[i];
+    if (reset)
+        for (int i = 0; i < kStCount; ++i) g_gboard_stats[i] = 0;
+    return kStCount;
 }
 
 int hrl_gboard_set_whole_ring(int on) {

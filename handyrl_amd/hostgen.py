@@ -391,27 +391,31 @@ class HostBatchGenerator:
         session = getattr(self.net, 'inference_session', None)
         ctx = session() if session is not None and self.device.type == 'cuda' else contextlib.nullcontext()
         try:
-            ctx.__enter__()
-            for s in range(self.E):
-                self._start(s, n)
-            for g in self.groups:
-                self._launch(g)
-            while any(g.pending is not None for g in self.groups):
-                for g in self.groups:
-                    if g.pending is None:
-                        continue
-                    t0 = time.perf_counter()
-                    w0 = self.timing.get('wait', 0.0)
-                    self._advance(g, n, out)
-                    self.timing['advance'] = self.timing.get('advance', 0.0) + (
-                        time.perf_counter() - t0 - (self.timing.get('wait', 0.0) - w0))
-                    self._launch(g)
+            with ctx:   # entered and exited as a pair; an exception in the body reaches __exit__ and propagates
+                self._run(n, out)
         finally:
-            ctx.__exit__(None, None, None)
             if saved is not None:
                 random.setstate(saved)
             self.net.train(was_training)
         return [out[k] for k in sorted(out)]
+
+    def _run(self, n, out):
+        """generate()'s body inside the net's inference session: start every slot, then advance and relaunch the
+        slot groups until none has a forward pending."""
+        for s in range(self.E):
+            self._start(s, n)
+        for g in self.groups:
+            self._launch(g)
+        while any(g.pending is not None for g in self.groups):
+            for g in self.groups:
+                if g.pending is None:
+                    continue
+                t0 = time.perf_counter()
+                w0 = self.timing.get('wait', 0.0)
+                self._advance(g, n, out)
+                self.timing['advance'] = self.timing.get('advance', 0.0) + (
+                    time.perf_counter() - t0 - (self.timing.get('wait', 0.0) - w0))
+                self._launch(g)
 
 
 class MomentReplay:

@@ -433,7 +433,8 @@ def gboard_conv(x, packed, Cout, cin_g, groups=1, x2=None, bias=None, alpha=None
     P = _native.ptr
     _native.check(_native.load().hrl_gboard_forward(
         P(x), x.stride(0), None if x2 is None else P(x2), 0 if x2 is None else x2.stride(0), N, cin_g, groups,
-        P(packed), Cout, None if bias is None else P(bias), None if alpha is None else P(alpha),
+        P(packed), packed.numel() * packed.element_size(), Cout, None if bias is None else P(bias),
+        None if alpha is None else P(alpha),
         None if beta is None else P(beta), int(relu), P(y), y.stride(0), _native.stream_of(x.device)),
         'hrl_gboard_forward')
     return y
@@ -562,8 +563,9 @@ class _DRCStep(torch.autograd.Function):
         for _ in range(R):
             zh = torch.empty(N, L * 4 * H, 6, 6, device=hs[0].device)
             _native.check(lib.hrl_gboard_forward_groups(
-                _native.ptr_array(hs), _native.i64_array([h.stride(0) for h in hs]), N, H, L, P(packed), L * 4 * H,
-                P(zh), zh.stride(0), stream), 'hrl_gboard_forward_groups')
+                _native.ptr_array(hs), _native.i64_array([h.stride(0) for h in hs]), N, H, L, P(packed),
+                packed.numel() * packed.element_size(), L * 4 * H, P(zh), zh.stride(0), stream),
+                'hrl_gboard_forward_groups')
             h_out = [torch.empty_like(c) for c in cs]
             c_out = [torch.empty_like(c) for c in cs]
             gates = [torch.empty(N, 4 * H, 6, 6, device=zh.device) if lv else None for lv in live]

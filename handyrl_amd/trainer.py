@@ -167,6 +167,25 @@ class LearnerStep:
         out['grad_norm'] = gnorm
         return out
 
+    def snapshot(self):
+        """A copy of the training state (parameters, buffers, Adam's state tensors) that restore() puts back in
+        place, so captured graphs keep pointing at the same tensors."""
+        with torch.no_grad():
+            return ([p.detach().clone() for p in self.net.parameters()],
+                    [b.detach().clone() for b in self.net.buffers()],
+                    [(v, v.detach().clone()) for st in self.optimizer.state.values() for v in st.values()
+                     if isinstance(v, torch.Tensor)])
+
+    def restore(self, snap):
+        params, buffers, opt = snap
+        with torch.no_grad():
+            for p, v in zip(self.net.parameters(), params):
+                p.copy_(v)
+            for b, v in zip(self.net.buffers(), buffers):
+                b.copy_(v)
+            for t, v in opt:
+                t.copy_(v)
+
     def _body(self, batch, hidden):
         losses, dcnt = self._grads(batch, hidden)
         if self.reducer is not None:

@@ -333,7 +333,9 @@ int hrl_board_conv_forward_packed(const float *x, int64_t N, int64_t Cin, int64_
  *   (channel c at + c * 36); x2 (or NULL; groups 1, Cin_g > 32 only): channels 32.. read from x2 instead
  *   (the head's [h_e, h_last] without the concatenation).  y: game n at y + n * y_stride.  Epilogue, in order:
  *   + bias[co] (or NULL), * alpha[co] + beta[co] (a BatchNorm's inference coefficients, or both NULL),
- *   relu.  x, x2, y 16-byte aligned, strides multiples of 4. */
+ *   relu.  x, x2, y 16-byte aligned, strides multiples of 4.  packed_bytes: the size of `packed` (hrl_gboard_forward
+ *   and hrl_gboard_forward_groups return HRL_EINVAL before any launch when it is below
+ *   hrl_gboard_pack_bytes(Cout, Cin_g), e.g. a buffer packed for another shape; ABI 19). */
 int64_t hrl_gboard_pack_bytes(int64_t Cout, int64_t Cin_g);
 int hrl_gboard_pack(const float *weight, int64_t Cout, int64_t Cin_g, int64_t w_cin_total, int64_t w_ci0,
                     void *packed, int64_t packed_bytes, void *stream);
@@ -355,16 +357,24 @@ int hrl_gboard_wgrad(const float *const *xs, const int64_t *x_strides, const flo
                      const int64_t *dy_strides, const int64_t *ns, int nseg, int64_t Cout, int64_t Cin,
                      float *dweight, int64_t w_cin_total, int64_t w_ci0, float *dbias, void *workspace,
                      int64_t workspace_bytes, void *stream);
-/* hrl_gboard_pointwise_wgrad: dweight (O, C) += sum over N games and the 36 cells of dy[n][o][q] x[n][c][q] -- the
- * weight gradient of a 1x1 conv on the 6x6 board (O <= 8, C <= 256; games x_stride / dy_stride floats apart,
- * float4-aligned).  Deterministic (per-workgroup partials folded in order).  workspace:
- * hrl_gboard_pointwise_wgrad_workspace_bytes(C, O, N) bytes. */
 /* hrl_gboard_set_whole_ring: 1 (default) = launches with one task per workgroup stage a whole 32-channel k-step
  * (9 quads) at once, 0 = the 3-quad ring always (measurement); returns the previous setting. */
 int hrl_gboard_set_whole_ring(int on);
 /* hrl_gboard_set_nctw: force the column tiles per workgroup (1, 2, 4; 0 = the launcher's choice), measurement
  * only; returns the previous setting. */
 int hrl_gboard_set_nctw(int nctw);
+/* hrl_gboard_launch_stats: the launch forms the gboard launchers chose since the last reset (host-side counters; a
+ * graph replay does not count), so a test can assert which kernels a learner step at a given size ran.  Copies
+ * min(n, total) counters into counts (NULL: none) and returns the total; reset != 0 zeroes them afterwards.  Order:
+ * 0 conv launches, 1 of them whole-tile (one task per workgroup, the k-step staged at once), 2/3/4 with 1/2/4 column
+ * tiles per workgroup, 5 with groups == 4 (the h halves' K-split adjoint), 6 hrl_gboard_forward_groups calls,
+ * 7 hrl_gboard_wgrad launches, 8 the most segments in one, 9 the most 16-game tiles in one, 10 wgrad launches in
+ * which workgroups carry their accumulators over several tiles (tiles > 256). */
+int hrl_gboard_launch_stats(int64_t *counts, int n, int reset);
+/* hrl_gboard_pointwise_wgrad: dweight (O, C) += sum over N games and the 36 cells of dy[n][o][q] x[n][c][q] -- the
+ * weight gradient of a 1x1 conv on the 6x6 board (O <= 8, C <= 256; games x_stride / dy_stride floats apart,
+ * float4-aligned).  Deterministic (per-workgroup partials folded in order).  workspace:
+ * hrl_gboard_pointwise_wgrad_workspace_bytes(C, O, N) bytes. */
 int64_t hrl_gboard_pointwise_wgrad_workspace_bytes(int64_t C, int64_t O, int64_t N);
 int hrl_gboard_pointwise_wgrad(const float *x, int64_t x_stride, const float *dy, int64_t dy_stride, int64_t N,
                                int64_t C, int64_t O, float *dweight, void *workspace, int64_t workspace_bytes,
@@ -373,11 +383,11 @@ int hrl_gboard_pointwise_wgrad(const float *x, int64_t x_stride, const float *dy
  * inputs xs[g] (N games, x_strides[g] floats apart): the DRC layers' h halves of one repeat without stacking
  * their states.  No bias / epilogue. */
 int hrl_gboard_forward_groups(const float *const *xs, const int64_t *x_strides, int64_t N, int64_t Cin_g,
-                              int64_t groups, const void *packed, int64_t Cout, float *y, int64_t y_stride,
-                              void *stream);
+                              int64_t groups, const void *packed, int64_t packed_bytes, int64_t Cout, float *y,
+                              int64_t y_stride, void *stream);
 int hrl_gboard_forward(const float *x, int64_t x_stride, const float *x2, int64_t x2_stride, int64_t N, int64_t Cin_g,
-                       int64_t groups, const void *packed, int64_t Cout, const float *bias, const float *alpha,
-                       const float *beta, int relu, float *y, int64_t y_stride, void *stream);
+                       int64_t groups, const void *packed, int64_t packed_bytes, int64_t Cout, const float *bias,
+                       const float *alpha, const float *beta, int relu, float *y, int64_t y_stride, void *stream);
 
 /* A 1x1 convolution on the 6x6 board (no bias; GeisterNet's move-head conv2 and value / return head convs,
  * geister.py:238-264): y[n, o, q] = sum_c W[o, c] x[n, c, q] over x1's C1 channels, then x2's C2 (x2 NULL when

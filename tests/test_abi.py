@@ -94,9 +94,37 @@ def test_gboard_wgrad_rejects_workspace_sized_by_games_not_tiles():
     assert code == _native.HRL_EINVAL
 
 
+def test_gboard_forward_rejects_undersized_packed_buffer():
+    """hrl_gboard_forward / hrl_gboard_forward_groups take the packed buffer's size (ABI 19) and return HRL_EINVAL,
+    before any launch, when it is below hrl_gboard_pack_bytes(Cout, Cin_g): a C caller binding the ABI directly
+     cannot make the kernel read past the fragments.  Only argument validation runs here."""
+    lib = _native.load()
+    dummy = ctypes.c_void_p(4096)
+    N, Cout, cin = 8, 64, 32
+    need = lib.hrl_gboard_pack_bytes(Cout, cin)
+    assert need > 0
+    for size in (need - 16, need // 2, 0):
+        code = lib.hrl_gboard_forward(dummy, cin * 36, None, 0, N, cin, 1, dummy, size, Cout, None, None, None, 0,
+                                      dummy, Cout * 36, None)
+        assert code == _native.HRL_EINVAL
+    # the adjoint packing of the move head's 64 <- 8 input gradient (K = 8): Cout 64, Cin_g 8
+    need_adj = lib.hrl_gboard_pack_bytes(64, 8)
+    code = lib.hrl_gboard_forward(dummy, 8 * 36, None, 0, N, 8, 1, dummy, need_adj - 1, 64, None, None, None, 0,
+                                  dummy, 64 * 36, None)
+    assert code == _native.HRL_EINVAL
+    L, H = 3, 32
+    xs = (ctypes.c_void_p * L)(*[4096 * (i + 1) for i in range(L)])
+    strides = (ctypes.c_int64 * L)(*[H * 36] * L)
+    cast = lambda a: ctypes.cast(a, ctypes.c_void_p)   # noqa: E731
+    need_g = lib.hrl_gboard_pack_bytes(4 * H * L, H)
+    code = lib.hrl_gboard_forward_groups(cast(xs), cast(strides), N, H, L, dummy, need_g - 16, 4 * H * L, dummy,
+                                         4 * H * L * 36, None)
+    assert code == _native.HRL_EINVAL
+
+
 def test_gboard_conv_refuses_packed_weights_of_another_shape():
-    """hrl_gboard_forward cannot see the packed buffer's size; the Python boundary refuses a buffer smaller than
-    hrl_gboard_pack_bytes(Cout, Cin_g) before any launch (no GPU needed)."""
+    """The Python boundary refuses a packed buffer smaller than hrl_gboard_pack_bytes(Cout, Cin_g) (or of another
+    dtype) before any launch (no GPU needed); the C entry checks the size again."""
     import torch
     from handyrl_amd import nn as hnn
     lib = _native.load()

@@ -172,7 +172,12 @@ def test_gboard_adjoint_matches_conv_input_gradient(cuda, N, cout_fwd, ci0, cin)
     (32, 25, 0, 25, (300,), False),             # the stem: 25 input planes (a padded channel tile)
     (8, 64, 0, 64, (17, 100), False),           # the move head's 64 -> 8 (a padded output tile)
     (128, 64, 32, 32, (2,) * 24 + (5,), True),  # many tiny records (the learner's liveness probe): one partial
-])                                              # per record tile, far more than sum(ns) / 16
+                                                # per record tile, far more than sum(ns) / 16
+    (128, 64, 32, 32, (300,) * 20, True),       # 380 tiles over 256 workgroups: accumulators carried across
+                                                # tiles, the segment search restarting inside a workgroup's range
+    (128, 64, 32, 32, (512,) * 40, True),       # 1,280 tiles in 40 segments (the bench learner's h halves: 48 x 16)
+    (32, 25, 0, 25, (4100, 3000), False),       # the stem over a whole unroll and more: 445 ragged tiles
+])
 @pytest.mark.parametrize('integer', [True, False])
 def test_gboard_wgrad_matches_conv_weight_gradient(cuda, cout, cin_total, ci0, cin, ns, bias, integer):
     """hrl_gboard_wgrad (games as the MFMA K, every recorded use in one launch, no concatenation) ADDS the weight
@@ -257,7 +262,8 @@ def test_gboard_forward_groups_and_grouped_gates(cuda):
     P = _native.ptr
     stream = _native.stream_of(cuda)
     _native.check(lib.hrl_gboard_forward_groups(_native.ptr_array(hs), _native.i64_array([h.stride(0) for h in hs]),
-                                                N, H, L, P(pk), 4 * H * L, P(zh), zh.stride(0), stream), 'groups')
+                                                N, H, L, P(pk), pk.numel(), 4 * H * L, P(zh), zh.stride(0), stream),
+                  'groups')
     assert torch.equal(zh, ref)
     h_out = [torch.empty_like(c) for c in cs]
     c_out = [torch.empty_like(c) for c in cs]

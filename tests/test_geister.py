@@ -393,3 +393,71 @@ def test_grouped_drc_step_matches_per_layer_unroll(cuda, graph):
     for n in w0:
         den = max(float(w0[n].norm()), 1e-12)
         assert float((w1[n] - w0[n]).norm()) / den <= 1e-6, n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('graph', [False, True])
+def test_recurrent_learner_step_at_bench_size_vs_oracle(cuda, graph):
+    """One LearnerStep of GeisterNet at the size the bench's geister_learner leg and the reference's stock learner
+    run (config.yaml:13,18: B = 256, forward_steps = 16; train.py:155-174 for the recurrent unroll) against
+    oracle.learner.CpuLearner on the same batch from the same seeded weights: losses and the clipped gradient norm
+    at rel 1e-5 against the fp32 oracle, every live parameter's clipped gradient against the same step in fp64
+    (check_grads_vs_fp64), the dead DRC blocks untouched.  At this size the gboard launchers pick forms the small
+    oracle tests never reach; hrl_gboard_launch_stats asserts they ran: whole-tile launches (one task per workgroup),
+    the h halves' K-split adjoint (groups = 4), and games-as-K weight gradients over many recorded uses (segments)
+    whose workgroups carry their accumulators over several 16-game tiles (> 256 tiles)."""
+    import ctypes
+    from handyrl_amd import _native
+    from handyrl_amd.synthetic import geister_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    from tests.test_learner_gpu import check_grads_vs_fp64
+    B, T = 256, 16
+    args = default_args(T, B)
+    batch = geister_batch(B, T, cuda, seed=17)
+    cpu_batch = {k: ({kk: vv.cpu() for kk, vv in v.items()} if isinstance(v, dict) else v.cpu())
+                 for k, v in batch.items()}
+    state = seeded_net().state_dict()
+    res = {}
+    threads = torch.get_num_threads()
+    torch.set_num_threads(8)
+    try:
+        for dt in (torch.float32, torch.float64):
+            net = seeded_net().to(dt)
+            net.load_state_dict(state)
+            b = {k: ({kk: vv.to(dt) for kk, vv in v.items()} if isinstance(v, dict) else
+                     (v.to(dt) if v.is_floating_point() else v)) for k, v in cpu_batch.items()}
+            hidden = tuple([h.to(dt) for h in hs] for hs in net.init_hidden([B, 2]))
+            r = ol.CpuLearner(net, args).step(b, hidden)
+            r['grads'] = {n: p.grad.double().clone() for n, p in net.named_parameters() if p.grad is not None}
+            res[dt] = r
+    finally:
+        torch.set_num_threads(threads)
+    r32, r64 = res[torch.float32], res[torch.float64]
+    lib = _native.load()
+    n_stats = lib.hrl_gboard_launch_stats(None, 0, 1)            # reset
+    net = seeded_net()
+    net.load_state_dict(state)
+    init = {n: p.detach().clone() for n, p in net.named_parameters()}
+    step = LearnerStep(net, args, cuda, graph=graph)
+    hidden = tuple([h.to(cuda) for h in hs] for hs in net.init_hidden([B, 2]))
+    out = step.step(batch, hidden)
+    torch.cuda.synchronize()
+    stats = (ctypes.c_int64 * n_stats)()
+    lib.hrl_gboard_launch_stats(ctypes.cast(stats, ctypes.c_void_p), n_stats, 0)
+    st = list(stats)
+    for k in ('p', 'v', 'r', 'ent', 'total'):
+        assert abs(float(out[k]) - r32[k]) <= 1e-5 * max(1.0, abs(r32[k])), (k, float(out[k]), r32[k])
+    assert abs(float(out['grad_norm']) - r32['grad_norm']) <= 1e-5 * r32['grad_norm'], \
+        (float(out['grad_norm']), r32['grad_norm'])
+    dead = {n for (n, _), live in zip(step.net.named_parameters(), step.live) if not live}
+    assert dead == set(init) - set(r32['grads'])
+    got = {n: p.grad.detach().cpu().double() for n, p in step.net.named_parameters() if n not in dead}
+    check_grads_vs_fp64(got, r32, r64)
+    for n in dead:
+        assert torch.equal(dict(step.net.named_parameters())[n].detach().cpu(), init[n]), n
+    # the launch forms of the bench-size step (counted once per captured / eager launch)
+    assert st[1] > 0, st                   # whole-tile launches: B = 256 games are 16 tiles, one task per workgroup
+    assert st[5] > 0, st                   # the h halves' input gradient as the K-split adjoint (S = 4 groups)
+    assert st[6] > 0, st                   # each repeat's h halves as one grouped launch over the layers' states
+    assert st[7] > 0 and st[8] >= 3 * T, st    # weight gradients over the unroll's recorded uses (3T for the cell)
+    assert st[9] > 256 and st[10] > 0, st  # > 256 tiles: workgroups carry accumulators over several tiles
