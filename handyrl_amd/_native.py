@@ -124,9 +124,11 @@ SIGNATURES = {
     'hrl_stem_forward': (ctypes.c_int, [_f32p, _i64, _i64, _f32p, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_stem_wgrad': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _f32p, _f32p, ctypes.c_void_p, _i64,
                                       ctypes.c_void_p]),
+    'hrl_stem_set_wgrad_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_clip_grad_norm': (ctypes.c_int, [_f32p, _i64, _dbl, _f32p, ctypes.c_void_p]),
     'hrl_heads_workspace_bytes': (ctypes.c_int64, [_i64]),
     'hrl_heads_bn_parts': (ctypes.c_int64, [_i64]),
+    'hrl_heads_set_bwd_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_heads_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
                                          _f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_void_p]),
     'hrl_heads_backward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,

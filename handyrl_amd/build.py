@@ -40,18 +40,31 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.hip'))
 
 
-def _deps_mtime():
-    paths = sources() + [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)]
-    paths += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
-    return max(os.path.getmtime(p) for p in paths)
+def _obj_of(src):
+    return os.path.join(OBJ_DIR, os.path.basename(src) + '.o')
 
 
 def up_to_date():
-    return os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime()
+    """The library is newer than every object and every object newer than its source and the headers (a source
+    edited while a build ran leaves its object older than the source, so the next build recompiles it)."""
+    if not os.path.exists(LIB):
+        return False
+    hdrs = [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)]
+    hdrs += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
+    deps = max(os.path.getmtime(h) for h in hdrs)
+    lib_t = os.path.getmtime(LIB)
+    for src in sources():
+        obj = _obj_of(src)
+        if not os.path.exists(obj):
+            return False
+        t = os.path.getmtime(obj)
+        if t < max(deps, os.path.getmtime(src)) or t > lib_t:
+            return False
+    return True
 
 
 def _compile(src):
-    obj = os.path.join(OBJ_DIR, os.path.basename(src) + '.o')
+    obj = _obj_of(src)
     hdrs = [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)]
     hdrs += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.h')]
     hdr_mtime = max(os.path.getmtime(h) for h in hdrs)

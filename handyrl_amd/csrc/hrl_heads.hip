@@ -36,6 +36,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/hrl_nn.h"
 #include "../../include/hrl_targets.h"
 
@@ -345,6 +347,264 @@ __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__
     }
 }
 
+// ------------------------------------------------------------------ backward, lane-per-channel form
+// heads_bwd_kernel keeps a row per lane, so its 3 x 32 conv weight-gradient and 32 x 2 BN-sum accumulators live in
+// LDS (52 KB per one-wave workgroup: 3 waves per CU, <= 27 KB of loads in flight per CU; 107 us in the step, 3 TB/s).
+// Here a lane owns (row half r = lane >> 5, channel c = lane & 31): per row pair it reads its channel's 9 cells (36
+// contiguous bytes; the wave's 64 lanes cover two whole rows), so its weight-gradient and BN-sum accumulators are 5
+// registers, W1[:, c] and the BN constants of c are 6 more, and nothing but the row block's small inputs and dz go
+// through LDS (~8 KB per 4-wave workgroup): ~100 VGPRs, 4 waves per SIMD, several row pairs in flight per wave.
+//  * stage (lanes 0..31, one row each): dz[m][q] = leaky'(a) * (dp . Wp | dv' . Wv) and db1's per-row sums, dz and
+//    the row's dp / dv' / a_p / a_v into LDS;
+//  * fc weight gradients: lane l owns weights l, l + 64, l + 128 of [dWp (9 x 18) | dWv (9)] and adds the block's
+//    rows in order (the products of fc_grad_kernel, dv' = the tanh backward's output);
+//  * main loop over the block's row pairs: x (BN + ReLU applied when fused), dW1[m][c] += sum_q dz[m][q] x[q],
+//    dh[q] = sum_m W1[m][c] dz[m][q] (the old kernel's operation order per element), the BN sums, dh stored;
+//  * the accumulators fold over the two row halves and the four waves in a fixed order into this workgroup's
+//    partial row (heads_reduce_kernel folds the workgroups) -- deterministic.
+constexpr int kBR = 32;                // rows per block (one wave)
+constexpr int kDZS = 28;               // LDS stride of a row's dz (27 + pad: 7 x ds_read_b128)
+constexpr int kSMS = 40;               // LDS stride of a row's small inputs: g[9] gv a_p[18] a_v[9] pad
+constexpr int kSmG = 0, kSmGV = 9, kSmAP = 10, kSmAV = 28;
+constexpr int kFcN = kOP * kZP + kHW;  // 171 fc weights
+constexpr int kWaves2 = 4;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t heads_rsrc(const void *base, uint32_t bytes) {
+    const uint64_t p = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, (int)n,
+                                             0x00020000);
+}
+
+typedef unsigned int hu32x3 __attribute__((ext_vector_type(3)));
+
+__device__ __forceinline__ void load9(__amdgpu_buffer_rsrc_t rs, uint32_t off, float (&d)[kHW]) {
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+        const hu32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, off + 12 * m, 0, 0);
+        d[3 * m] = __uint_as_float(v.x);
+        d[3 * m + 1] = __uint_as_float(v.y);
+        d[3 * m + 2] = __uint_as_float(v.z);
+    }
+}
+
+template <bool BN>
+__global__ __launch_bounds__(256, 4) void heads_bwd2_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
+                                                         const float *__restrict__ a_p, const float *__restrict__ a_v,
+                                                         const float *__restrict__ dp, const float *__restrict__ dv,
+                                                         const float *__restrict__ vt, float *__restrict__ dh,
+                                                         float *__restrict__ part) {
+    // the row blocks' dz and small inputs; after the loop the same bytes hold the folds
+    __shared__ __attribute__((aligned(16))) float sdz[kWaves2][kBR * kDZS];
+    __shared__ __attribute__((aligned(16))) float ssm[kWaves2][kBR * kSMS];
+    __shared__ float swp[kOP * kZP], swv[kHW];
+    static_assert(sizeof(float) * kWaves2 * 64 * 8 <= sizeof(float) * kWaves2 * kBR * kSMS, "fold");
+    static_assert(sizeof(double) * kWaves2 * 64 * 2 <= sizeof(float) * kWaves2 * kBR * kDZS, "foldd");
+    float(*fold)[64 * 8] = reinterpret_cast<float(*)[64 * 8]>(&ssm[0][0]);
+    double(*foldd)[64 * 2] = reinterpret_cast<double(*)[64 * 2]>(&sdz[0][0]);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int c = lane & 31, r = lane >> 5;
+    for (int i = threadIdx.x; i < kOP * kZP; i += 256) swp[i] = w.wp[i];
+    if (threadIdx.x < kHW) swv[threadIdx.x] = w.wv[threadIdx.x];
+    float w1[kM];
+#pragma unroll
+    for (int m = 0; m < kM; ++m) w1[m] = w1_at(w, m, c);
+    float al = 1.f, be = 0.f, mu = 0.f;
+    if constexpr (BN) {
+        al = bn.alpha[c];
+        be = bn.beta[c];
+        mu = bn.part ? bn.mean[c] : 0.f;
+    }
+    __syncthreads();
+    float *dzs = sdz[wave];
+    float *sm = ssm[wave];
+    // per-lane accumulators: dW1[:, c] over this lane's rows, db1 (lanes < 32, per staged row), the fc weights the
+    // lane owns, the BN sums of channel c
+    float gw[kM] = {0.f, 0.f, 0.f}, gb[kM] = {0.f, 0.f, 0.f}, fc[3] = {0.f, 0.f, 0.f};
+    double t1d = 0.0, t2d = 0.0;
+    // fc weight i = lane + 64 s: (k, j) of dWp or q of dWv, as LDS offsets into a staged row
+    int fo_g[3], fo_a[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        const int i = lane + 64 * s;
+        const bool pol = i < kOP * kZP;
+        fo_g[s] = pol ? kSmG + i / kZP : kSmGV;
+        fo_a[s] = pol ? kSmAP + i % kZP : kSmAV + (i - kOP * kZP < kHW ? i - kOP * kZP : 0);
+    }
+    const __amdgpu_buffer_rsrc_t rh = heads_rsrc(h, (uint32_t)(N * kRow * 4));
+    const __amdgpu_buffer_rsrc_t rd = heads_rsrc(dh, (uint32_t)(N * kRow * 4));
+    const int64_t nblocks = (N + kBR - 1) / kBR;
+    const int64_t wstep = (int64_t)gridDim.x * kWaves2;
+    for (int64_t blk = (int64_t)blockIdx.x * kWaves2 + wave; blk < nblocks; blk += wstep) {
+        const int64_t base = blk * kBR;
+        asm volatile("" ::: "memory");   // Wp / Wv are re-read from LDS per block, not held in 171 registers
+        // the first row pair's x is in flight while the block's dz is formed
+        float xn[kHW];
+        load9(rh, (uint32_t)(((base + r) * kRow + c * kHW) * 4), xn);
+        if (lane < kBR) {
+            const int64_t n = base + lane;
+            const bool valid = n < N;
+            const int64_t nn = valid ? n : 0;
+            float a[kZ], g[kOP], gv;
+#pragma unroll
+            for (int j = 0; j < kZP; ++j) a[j] = a_p[nn * kZP + j];
+#pragma unroll
+            for (int q = 0; q < kHW; ++q) a[kZP + q] = a_v[nn * kHW + q];
+#pragma unroll
+            for (int k = 0; k < kOP; ++k) g[k] = valid ? dp[nn * kOP + k] : 0.f;
+            gv = valid ? dv[nn] : 0.f;
+            if (vt) gv = gv * (1.f - vt[nn] * vt[nn]);   // tanh backward, torch's CPU operations
+            float dz[kZ];
+#pragma unroll
+            for (int j = 0; j < kZP; ++j) {
+                // one dz at a time: the compiler would otherwise issue all 162 products (packed) before any sum
+                asm volatile("" ::: "memory");
+                float t = 0.f;
+#pragma unroll
+                for (int k = 0; k < kOP; ++k) t += g[k] * swp[k * kZP + j];
+                dz[j] = a[j] > 0.f ? t : t * kSlope;
+            }
+#pragma unroll
+            for (int q = 0; q < kHW; ++q) {
+                const float t = gv * swv[q];
+                dz[kZP + q] = a[kZP + q] > 0.f ? t : t * kSlope;
+            }
+#pragma unroll
+            for (int m = 0; m < kM; ++m) {
+                float t = 0.f;
+#pragma unroll
+                for (int q = 0; q < kHW; ++q) t += dz[m * kHW + q];
+                gb[m] += t;
+            }
+            float4 *dzr = reinterpret_cast<float4 *>(dzs + lane * kDZS);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) dzr[j] = make_float4(dz[4 * j], dz[4 * j + 1], dz[4 * j + 2], dz[4 * j + 3]);
+            dzr[6] = make_float4(dz[24], dz[25], dz[26], 0.f);
+            float *smr = sm + lane * kSMS;
+#pragma unroll
+            for (int k = 0; k < kOP; ++k) smr[kSmG + k] = g[k];
+            smr[kSmGV] = gv;
+#pragma unroll
+            for (int j = 0; j < kZ; ++j) smr[kSmAP + j] = valid ? a[j] : 0.f;
+        }
+        lds_fence();
+        // fc weight gradients over the block's rows, in order
+#pragma unroll 4
+        for (int row = 0; row < kBR; ++row) {
+            const float *smr = sm + row * kSMS;
+#pragma unroll
+            for (int s = 0; s < 3; ++s) fc[s] += smr[fo_g[s]] * smr[fo_a[s]];
+        }
+        // the row pairs: lane (r, c) takes row base + 2 it + r, channel c
+#pragma unroll 1
+        for (int it = 0; it < kBR / 2; ++it) {
+            float x[kHW];
+#pragma unroll
+            for (int q = 0; q < kHW; ++q) x[q] = xn[q];
+            if (it + 1 < kBR / 2)
+                load9(rh, (uint32_t)(((base + 2 * (it + 1) + r) * kRow + c * kHW) * 4), xn);
+            float dz[kZ + 1];
+            const float4 *dzr = reinterpret_cast<const float4 *>(dzs + (2 * it + r) * kDZS);
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                const float4 v = dzr[j];
+                dz[4 * j] = v.x; dz[4 * j + 1] = v.y; dz[4 * j + 2] = v.z; dz[4 * j + 3] = v.w;
+            }
+            float hx[kHW];
+#pragma unroll
+            for (int q = 0; q < kHW; ++q) hx[q] = BN ? bn_relu(x[q], al, be) : x[q];
+            // conv weight gradient: dW1[m, c] += sum_q dz[m, q] * h[c, q]
+#pragma unroll
+            for (int m = 0; m < kM; ++m) {
+                float t = 0.f;
+#pragma unroll
+                for (int q = 0; q < kHW; ++q) t += dz[m * kHW + q] * hx[q];
+                gw[m] += t;
+            }
+            // input gradient dh[c, q] = sum_m W1[m, c] dz[m, q], the BN sums of channel c
+            float o[kHW];
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < kHW; ++q) {
+                float t = 0.f;
+#pragma unroll
+                for (int m = 0; m < kM; ++m) t += w1[m] * dz[m * kHW + q];
+                o[q] = t;
+                if constexpr (BN) {
+                    if (bn.part) {   // bn_bwd_reduce_kernel's mask and products
+                        const float gm = (x[q] * al + be > 0.f) ? t : 0.f;
+                        t1 += gm;
+                        t2 += gm * (x[q] - mu);
+                    }
+                }
+            }
+            t1d += (double)t1;
+            t2d += (double)t2;
+            const uint32_t off = (uint32_t)(((base + 2 * it + r) * kRow + c * kHW) * 4);
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                hu32x3 v;
+                v.x = __float_as_uint(o[3 * m]);
+                v.y = __float_as_uint(o[3 * m + 1]);
+                v.z = __float_as_uint(o[3 * m + 2]);
+                __builtin_amdgcn_raw_buffer_store_b96(v, rd, off + 12 * m, 0, 0);
+            }
+        }
+        lds_fence();   // the block's LDS rows are read before the next block overwrites them
+    }
+    // fixed-order folds: lanes (r, c) of the 4 waves -> channel c; the wave's lanes < 32 -> db1; fc per lane
+    __syncthreads();   // every wave is out of its loop: the staging LDS is free
+    float *fw = fold[wave];
+#pragma unroll
+    for (int m = 0; m < kM; ++m) fw[m * 64 + lane] = gw[m];
+#pragma unroll
+    for (int m = 0; m < kM; ++m) fw[(3 + m) * 64 + lane] = gb[m];
+    fw[6 * 64 + lane] = 0.f;
+    foldd[wave][lane * 2] = t1d;
+    foldd[wave][lane * 2 + 1] = t2d;
+    __syncthreads();
+    float *out = part + (int64_t)blockIdx.x * kGN;
+    if (wave == 0) {
+        // dW1[m][c]: lanes c and c + 32 of waves 0..3, in order
+        for (int i = lane; i < kM * kC; i += 64) {
+            const int m = i / kC, cc = i % kC;
+            float t = 0.f;
+            for (int wv = 0; wv < kWaves2; ++wv) t += fold[wv][m * 64 + cc] + fold[wv][m * 64 + cc + 32];
+            out[kGW1 + i] = t;
+        }
+        if (lane < kM) {
+            float t = 0.f;
+            for (int wv = 0; wv < kWaves2; ++wv)
+                for (int l = 0; l < kBR; ++l) t += fold[wv][(3 + lane) * 64 + l];
+            out[kGB1 + lane] = t;
+        }
+        if (BN && bn.part) {   // part[block][c][2], fp64: halves and waves in order
+            const int cc = lane >> 1, k = lane & 1;
+            double t = 0.0;
+            for (int wv = 0; wv < kWaves2; ++wv) t += foldd[wv][cc * 2 + k] + foldd[wv][(cc + 32) * 2 + k];
+            bn.part[((int64_t)blockIdx.x * kC + cc) * 2 + k] = t;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 3; ++s) fw[s * 64 + lane] = fc[s];
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            const int i = lane + 64 * s;
+            if (i < kFcN) {
+                float t = 0.f;
+                for (int wv = 0; wv < kWaves2; ++wv) t += fold[wv][s * 64 + lane];
+                out[kGWP + i] = t;
+            }
+        }
+    }
+}
+
 // fc weight gradients: dWp[k][j] = sum_n dp[n,k] a_p[n,j], dWv[q] = sum_n dv[n] a_v[n,q]; workgroup b sums
 // its row range (rows in order) into partial row b, columns kGWP.. (one thread per weight)
 __global__ __launch_bounds__(256) void fc_grad_kernel(const float *__restrict__ a_p, const float *__restrict__ a_v,
@@ -411,6 +671,8 @@ __global__ __launch_bounds__(256) void heads_reduce_kernel(const float *__restri
 // occupancy.  The forward (10.8 KB LDS, 230 VGPRs) keeps all 1024 resident.
 constexpr int kGridFwd = 1024;
 constexpr int kGridBwd = 768;
+constexpr int kGridBwd2 = 1024;   // heads_bwd2_kernel: 4 four-wave workgroups per CU
+int g_heads_bwd_form = 2;         // hrl_heads_set_bwd_form
 
 int status() {
     const hipError_t e = hipGetLastError();
@@ -424,14 +686,29 @@ int grid_for(int64_t N, int cap = kGridBwd) {
     return (int)(blocks < cap ? blocks : cap);
 }
 
+// the backward's workgroups (its partial rows): form 2 runs 4-wave workgroups over 32-row blocks
+int grid_bwd(int64_t N) {
+    if (g_heads_bwd_form != 2) return grid_for(N);
+    const int64_t wgs = ((N + kBR - 1) / kBR + kWaves2 - 1) / kWaves2;
+    return (int)(wgs < kGridBwd2 ? wgs : kGridBwd2);
+}
+
 }  // namespace
 
 extern "C" {
 
 // workspace: the per-workgroup partials, then dv through the folded tanh's backward (N floats)
-int64_t hrl_heads_workspace_bytes(int64_t N) { return N < 1 ? -1 : ((int64_t)grid_for(N) * kGN + N) * 4; }
+int64_t hrl_heads_workspace_bytes(int64_t N) {
+    return N < 1 ? -1 : ((int64_t)std::max(grid_for(N), grid_bwd(N)) * kGN + N) * 4;
+}
 
-int64_t hrl_heads_bn_parts(int64_t N) { return N < 1 ? -1 : grid_for(N); }
+int64_t hrl_heads_bn_parts(int64_t N) { return N < 1 ? -1 : grid_bwd(N); }
+
+int hrl_heads_set_bwd_form(int form) {
+    const int prev = g_heads_bwd_form;
+    g_heads_bwd_form = form == 1 ? 1 : 2;
+    return prev;
+}
 
 int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *b1p, const float *w1v,
                       const float *b1v, const float *wp, const float *wv, const float *bn_alpha, const float *bn_beta,
@@ -459,8 +736,23 @@ int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float 
     hipStream_t s = static_cast<hipStream_t>(stream);
     const Weights w{w1p, w1v, nullptr, nullptr, wp, wv};
     const BnIn bn{bn_alpha, bn_beta, bn_mean, bn_part};
-    const int grid = grid_for(N);
     float *part = static_cast<float *>(workspace);
+    if (g_heads_bwd_form == 2) {
+        if (N * kRow * 4 >= (int64_t)1 << 32) return HRL_EINVAL;   // 32-bit buffer offsets
+        const int grid = grid_bwd(N);
+        if (bn_alpha)
+            hipLaunchKernelGGL(heads_bwd2_kernel<true>, dim3(grid), dim3(256), 0, s, h, N, w, bn, a_p, a_v, dp, dv,
+                               v_tanh, dh, part);
+        else
+            hipLaunchKernelGGL(heads_bwd2_kernel<false>, dim3(grid), dim3(256), 0, s, h, N, w, bn, a_p, a_v, dp, dv,
+                               v_tanh, dh, part);
+        const int rc = status();
+        if (rc) return rc;
+        hipLaunchKernelGGL(heads_reduce_kernel, dim3(kGN), dim3(256), 0, s, part, grid, dw1p, dw1v, db1p, db1v, dwp,
+                           dwv);
+        return status();
+    }
+    const int grid = grid_for(N);
     float *dv_raw = part + (int64_t)grid * kGN;
     hipLaunchKernelGGL(heads_bwd_kernel, dim3(grid), dim3(64), 0, s, h, N, w, bn, a_p, a_v, dp, dv, v_tanh, dv_raw, dh,
                        part);

@@ -229,6 +229,119 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const float *__res
     }
 }
 
+// ------------------------------------------------------------------ weight gradient, lane-per-channel form
+// stem_wgrad_kernel holds a 16-sample dy tile per wave in registers (18 float4 per lane) and 144 accumulators of
+// the dense 28 x 288 dWb, one wave per SIMD: one tile of loads in flight per wave, 63 us in the step (2.6 TB/s).
+// Only 49 (p, q) pairs x Cin of dWb are weights, so here a lane owns (row half r = lane >> 5, output channel
+// co = lane & 31) and accumulates dW[co][ci][tap] (Cin x 9) and db[co] in 28 registers:
+//   dW[co][ci][tap] += sum_{q on the board} dy[n][co][q] * x[n][ci][p(q, tap)],  db[co] += sum_q dy[n][co][q]
+// per sample n (fmaf, taps in order, q ascending).  A wave's 64 lanes read two whole dy rows per step (36
+// contiguous bytes per lane); the block's 32 observation rows (Cin*9 floats each) are staged in LDS once and read
+// back as broadcasts.  ~90 VGPRs: 4 workgroups of 4 waves per CU, the next row pair's dy in flight.
+template <int CIN>
+__global__ __launch_bounds__(kThreads, 4) void stem_wgrad2_kernel(const float *__restrict__ x,
+                                                                  const float *__restrict__ dy, int64_t N, int bias,
+                                                                  float *__restrict__ partial) {
+    constexpr int kBR = 32;                       // rows per block (one wave)
+    constexpr int kXF = CIN * kCells;             // observation floats per row
+    constexpr int kXS = (kXF + 3) / 4 * 4;        // LDS row stride (float4 reads)
+    constexpr int kNW = kCo * CIN * 9;
+    __shared__ __attribute__((aligned(16))) float xs[kWaves][kBR * kXS];   // after the loop: the fold
+    static_assert(64 * (CIN * 9 + 1) <= kWaves * kBR * kXS, "fold");
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int co = lane & 31, r = lane >> 5;
+    float acc[CIN * 9], accb = 0.f;
+#pragma unroll
+    for (int i = 0; i < CIN * 9; ++i) acc[i] = 0.f;
+    const uint64_t pd = reinterpret_cast<uint64_t>(dy);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pd >> 32)) << 32) |
+                                 __builtin_amdgcn_readfirstlane((uint32_t)pd)),
+        (short)0, (int)__builtin_amdgcn_readfirstlane((uint32_t)(N * kCols * 4)), 0x00020000);
+    float *xw = xs[wave];
+    const int64_t nblocks = (N + kBR - 1) / kBR;
+    const int64_t wstep = (int64_t)gridDim.x * kWaves;
+    typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+    auto load_dy = [&](int64_t row, float (&d)[kCells]) __attribute__((always_inline)) {
+        const uint32_t off = (uint32_t)((row * kCols + co * kCells) * 4);
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rd, off + 12 * m, 0, 0);
+            d[3 * m] = __uint_as_float(v.x);
+            d[3 * m + 1] = __uint_as_float(v.y);
+            d[3 * m + 2] = __uint_as_float(v.z);
+        }
+    };
+    for (int64_t blk = (int64_t)blockIdx.x * kWaves + wave; blk < nblocks; blk += wstep) {
+        const int64_t base = blk * kBR;
+        float dn[kCells];
+        load_dy(base + r, dn);   // rows past N read 0 (the descriptor's range)
+        // the block's observation rows into LDS (rows past N: 0)
+        for (int i = lane; i < kBR * kXS; i += 64) {
+            const int rr = i / kXS, k = i - rr * kXS;
+            const int64_t n = base + rr;
+            xw[i] = (k < kXF && n < N) ? x[n * kXF + k] : 0.f;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+        for (int it = 0; it < kBR / 2; ++it) {
+            float d[kCells];
+#pragma unroll
+            for (int q = 0; q < kCells; ++q) d[q] = dn[q];
+            if (it + 1 < kBR / 2) load_dy(base + 2 * (it + 1) + r, dn);
+            float xv[kXS];
+            const float4 *xr = reinterpret_cast<const float4 *>(xw + (2 * it + r) * kXS);
+#pragma unroll
+            for (int j = 0; j < kXS / 4; ++j) {
+                const float4 v = xr[j];
+                xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
+            }
+            float tb = 0.f;
+#pragma unroll
+            for (int q = 0; q < kCells; ++q) tb += d[q];
+            accb += tb;
+#pragma unroll
+            for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) {
+                    const int ky = tap / 3, kx = tap % 3;
+                    float t = 0.f;
+#pragma unroll
+                    for (int q = 0; q < kCells; ++q) {
+                        const int py = q / 3 + ky - 1, px = q % 3 + kx - 1;
+                        if (py >= 0 && py < 3 && px >= 0 && px < 3) t = __builtin_fmaf(d[q], xv[ci * 9 + py * 3 + px], t);
+                    }
+                    acc[ci * 9 + tap] += t;
+                }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // the block's LDS rows are read before the next block's overwrite
+        __builtin_amdgcn_wave_barrier();
+    }
+    // fold: the 4 waves in order into red[i][lane], then lanes co and co + 32 -> partial [dW (co, ci, tap) | db (co)]
+    float *red = &xs[0][0];
+    __syncthreads();
+#pragma unroll 1
+    for (int wv = 0; wv < kWaves; ++wv) {
+        if (wave == wv) {
+#pragma unroll
+            for (int i = 0; i < CIN * 9; ++i) red[i * 64 + lane] = wv == 0 ? acc[i] : red[i * 64 + lane] + acc[i];
+            red[CIN * 9 * 64 + lane] = wv == 0 ? accb : red[CIN * 9 * 64 + lane] + accb;
+        }
+        __syncthreads();
+    }
+    float *out = partial + (int64_t)blockIdx.x * kNOut;
+    for (int o = threadIdx.x; o < kNW + kCo; o += kThreads) {
+        const int c = o < kNW ? o / (CIN * 9) : o - kNW;
+        const int i = o < kNW ? o % (CIN * 9) : CIN * 9;
+        const float t = red[i * 64 + c] + red[i * 64 + c + 32];
+        out[o] = (o < kNW || bias) ? t : 0.f;
+    }
+}
+
+int g_stem_wgrad_form = 2;   // hrl_stem_set_wgrad_form
+
 // fixed-order fold of the workgroup partials: one workgroup per output, strided fp64 sums, LDS tree
 __global__ __launch_bounds__(256) void stem_reduce_kernel(const float *__restrict__ partial, int nparts, int nw,
                                                           float *__restrict__ dw, float *__restrict__ db) {
@@ -260,11 +373,31 @@ int grid_for(int64_t N, int cap) {
     return (int)(blocks < cap ? blocks : cap);
 }
 
+constexpr int kGrid2 = 1024;   // stem_wgrad2_kernel: 4 workgroups per CU
+
+// workgroups of the weight gradient's form: form 2 runs 4-wave workgroups over 32-row blocks
+int grid_wgrad(int64_t N) {
+    if (g_stem_wgrad_form != 2) return grid_for(N, kGrid);
+    const int64_t wgs = ((N + 31) / 32 + kWaves - 1) / kWaves;
+    return (int)(wgs < kGrid2 ? wgs : kGrid2);
+}
+
+
 }  // namespace
 
 extern "C" {
 
-int64_t hrl_stem_workspace_bytes(int64_t N) { return N < 1 ? -1 : (int64_t)grid_for(N, kGrid) * kNOut * 4; }
+int64_t hrl_stem_workspace_bytes(int64_t N) {
+    if (N < 1) return -1;
+    const int g1 = grid_for(N, kGrid), g2 = grid_wgrad(N);
+    return (int64_t)(g1 > g2 ? g1 : g2) * kNOut * 4;
+}
+
+int hrl_stem_set_wgrad_form(int form) {
+    const int prev = g_stem_wgrad_form;
+    g_stem_wgrad_form = form == 1 ? 1 : 2;
+    return prev;
+}
 
 int hrl_stem_forward(const float *x, int64_t N, int64_t Cin, const float *weight, const float *bias, float *y,
                      void *stream) {
@@ -279,10 +412,20 @@ int hrl_stem_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, floa
     if (N < 1 || Cin < 1 || Cin > 3 || !x || !dy || !dweight || !workspace) return HRL_EINVAL;
     if (workspace_bytes < hrl_stem_workspace_bytes(N)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const int grid = grid_for(N, kGrid);
+    const int grid = grid_wgrad(N);
     float *partial = static_cast<float *>(workspace);
-    hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)Cin, dbias ? 1 : 0,
-                       partial);
+    if (g_stem_wgrad_form == 2) {
+        if (N * kCols * 4 >= (int64_t)1 << 32) return HRL_EINVAL;   // 32-bit buffer offsets
+        if (Cin == 3)
+            hipLaunchKernelGGL(stem_wgrad2_kernel<3>, dim3(grid), dim3(kThreads), 0, s, x, dy, N, dbias ? 1 : 0, partial);
+        else if (Cin == 2)
+            hipLaunchKernelGGL(stem_wgrad2_kernel<2>, dim3(grid), dim3(kThreads), 0, s, x, dy, N, dbias ? 1 : 0, partial);
+        else
+            hipLaunchKernelGGL(stem_wgrad2_kernel<1>, dim3(grid), dim3(kThreads), 0, s, x, dy, N, dbias ? 1 : 0, partial);
+    } else {
+        hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)Cin, dbias ? 1 : 0,
+                           partial);
+    }
     int rc = status();
     if (rc) return rc;
     const int nw = kCo * (int)Cin * 9;

@@ -431,6 +431,10 @@ int64_t hrl_heads_bn_parts(int64_t N);
 int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *b1p, const float *w1v,
                       const float *b1v, const float *wp, const float *wv, const float *bn_alpha, const float *bn_beta,
                       float *a_p, float *a_v, float *p_out, float *v_out, int tanh_v, void *stream);
+/* hrl_heads_set_bwd_form: 2 (default) = the lane-per-channel backward (4-wave workgroups, accumulators in registers,
+ * the fc weight gradients in the same pass), 1 = the row-per-lane kernel + separate fc-gradient launch (measurement).
+ * Process-wide; returns the previous setting.  hrl_heads_bn_parts / hrl_heads_workspace_bytes follow the form. */
+int hrl_heads_set_bwd_form(int form);
 int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float *w1v, const float *wp,
                        const float *wv, const float *bn_alpha, const float *bn_beta, const float *bn_mean,
                        double *bn_part, const float *a_p, const float *a_v, const float *dp, const float *dv,
@@ -447,6 +451,10 @@ int hrl_stem_forward(const float *x, int64_t N, int64_t Cin, const float *weight
                      void *stream);
 int hrl_stem_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, float *dweight, float *dbias,
                    void *workspace, int64_t workspace_bytes, void *stream);
+/* hrl_stem_set_wgrad_form: 2 (default) = the lane-per-channel weight gradient (a lane owns one output channel's
+ * Cin x 9 weights and its bias of a row; 4-wave workgroups, 4 per CU), 1 = the dense-board fp32 MFMA kernel
+ * (measurement).  Process-wide; returns the previous setting.  hrl_stem_workspace_bytes covers both forms. */
+int hrl_stem_set_wgrad_form(int form);
 
 /* clip_grad_norm_(params, max_norm) on the learner's flat gradient buffer (handyrl/train.py:384)
  * in one launch: total = ||grads||_2 (fp64 fold) -> *total_norm; grads *= min(max_norm / (total + 1e-6), 1).

@@ -534,3 +534,68 @@ def test_grouped_batch_norm_matches_sequential_calls(cuda, G, N, C, HW):
     for a, r in zip(*outs):
         scale = max(float(r.abs().max()), 1e-30)
         assert float((a - r).abs().max()) <= 1e-6 * scale
+
+
+@pytest.mark.parametrize('N', [1, 37, 4099, 20000])
+@pytest.mark.parametrize('bn', [False, True])
+def test_heads_backward_forms_agree(cuda, N, bn):
+    """hrl_heads_backward's lane-per-channel form (2, the default: accumulators in registers, the fc weight
+    gradients in the same pass) against the row-per-lane form (1) on the same inputs: dh bit-identical (the same
+    float operations per element), every parameter gradient and the fused BatchNorm's backward sums against the
+    fp64 formulas within fp32 reassociation (different fold orders), on ragged row counts with and without the
+    body's last BatchNorm + ReLU in front and the value head's tanh folded in."""
+    from handyrl_amd import _native
+    lib = _native.load()
+    P = _native.ptr
+    stream = _native.stream_of(cuda)
+    g0 = torch.Generator(device=cuda).manual_seed(N + 7 * bn)
+    rnd = lambda *s: torch.randn(*s, device=cuda, generator=g0)   # noqa: E731
+    y = rnd(N, 288)
+    w1p, w1v, wp, wv = rnd(2, 32), rnd(1, 32), rnd(9, 18), rnd(1, 9)
+    a_p, a_v = rnd(N, 18), rnd(N, 9)
+    dp, dv = rnd(N, 9), rnd(N, 1)
+    vt = torch.tanh(rnd(N, 1))
+    al, be, mu = (rnd(32).abs() + 0.5, rnd(32) * 0.3, rnd(32) * 0.1) if bn else (None, None, None)
+    res = []
+    prev = lib.hrl_heads_set_bwd_form(1)
+    try:
+        for form in (1, 2):
+            lib.hrl_heads_set_bwd_form(form)
+            ws_bytes = lib.hrl_heads_workspace_bytes(N)
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+            nparts = lib.hrl_heads_bn_parts(N)
+            part = torch.zeros(nparts * 64, dtype=torch.float64, device=cuda)
+            dh = torch.empty_like(y)
+            outs = [torch.empty(2, 32, device=cuda), torch.empty(2, device=cuda), torch.empty(1, 32, device=cuda),
+                    torch.empty(1, device=cuda), torch.empty(9, 18, device=cuda), torch.empty(1, 9, device=cuda)]
+            _native.check(lib.hrl_heads_backward(P(y), N, P(w1p), P(w1v), P(wp), P(wv), P(al), P(be), P(mu),
+                                                 P(part) if bn else None, P(a_p), P(a_v), P(dp), P(dv), P(vt), P(dh),
+                                                 *[P(o) for o in outs], P(ws), ws_bytes, stream), 'heads_backward')
+            torch.cuda.synchronize(cuda)
+            res.append((dh, outs, part.view(nparts, 32, 2).sum(0) if bn else None))
+    finally:
+        lib.hrl_heads_set_bwd_form(prev)
+    assert torch.equal(res[0][0], res[1][0])
+    # fp64 formulas (tictactoe.py:35-49 heads; the tanh backward; bn_bwd_reduce's mask and products)
+    d = lambda t: t.double().cpu()   # noqa: E731
+    x = d(y).view(N, 32, 9)
+    h = torch.relu(x * d(al).view(1, 32, 1) + d(be).view(1, 32, 1)) if bn else x
+    gv = d(dv) * (1 - d(vt) ** 2)
+    tp = d(dp) @ d(wp)
+    zp = torch.where(d(a_p) > 0, tp, tp * 0.1)
+    tv = gv * d(wv)
+    zv = torch.where(d(a_v) > 0, tv, tv * 0.1)
+    dz = torch.cat([zp.view(N, 2, 9), zv.view(N, 1, 9)], 1)              # (N, 3, 9)
+    w1 = torch.cat([d(w1p), d(w1v)], 0)                                  # (3, 32)
+    ref = [torch.einsum('nmq,ncq->mc', dz, h)[:2], dz[:, :2].sum((0, 2)), torch.einsum('nmq,ncq->mc', dz, h)[2:],
+           dz[:, 2].sum((0, 1)).view(1), d(dp).t() @ d(a_p), (gv.t() @ d(a_v))]
+    for form, (_, outs, part) in zip((1, 2), res):
+        for i, (o, r) in enumerate(zip(outs, ref)):
+            err = float((d(o) - r).abs().max()) / max(float(r.abs().max()), 1e-30)
+            assert err < 2e-5 * max(1.0, (N / 4096) ** 0.5), (form, i, err)
+        if bn:
+            dhx = d(res[0][0]).view(N, 32, 9)
+            m = (x * d(al).view(1, 32, 1) + d(be).view(1, 32, 1) > 0).double()
+            bref = torch.stack([(dhx * m).sum((0, 2)), (dhx * m * (x - d(mu).view(1, 32, 1))).sum((0, 2))], 1)
+            scale = float((dhx.abs() * (1 + x.abs())).sum((0, 2)).max())
+            assert float((d(part) - bref).abs().max()) / scale < 1e-6, form
