@@ -1188,11 +1188,12 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         unsigned char *xi = smem + kX0 + (it & 1) * kImgBytes;
         uint32_t dp[3][5], xp[3][5];
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const bool valid = rho0 + r < rows;
+        for (int i = 0; i < 5; ++i) {
+            float dv[2], xv2[2];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) {
+            for (int r = 0; r < 2; ++r) {
                 // dY = BN_i backward apply (bn_bwd_apply_kernel's float operations); rows past the batch are 0
+                const bool valid = rho0 + r < rows;
                 const float yv = Y[r][i];
                 float gv = G[r][i];
                 if (!(yv * al + be > 0.f)) gv = 0.f;
@@ -1205,22 +1206,16 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                     xv = u < 0.f ? 0.f : u;
                 }
                 if constexpr (kFwd) d = xv;   // the forward's A operand: x' in the input-gradient waves' image
-                uint32_t h, m, l, xh, xm, xl;
-                if constexpr (kVariant & 1) {
-                    h = __float_as_uint(G[r][i]) >> 16; m = h; l = h;
-                    xh = __float_as_uint(X[r][i]) >> 16; xm = xh; xl = __float_as_uint(Y[r][i]) >> 16;
-                } else {
-                    hrl_split::split3(d, h, m, l);
-                    hrl_split::split3(xv, xh, xm, xl);
-                }
-                const int sh = 16 * r;
-                if (r == 0) {
-                    dp[0][i] = h; dp[1][i] = m; dp[2][i] = l;
-                    xp[0][i] = xh; xp[1][i] = xm; xp[2][i] = xl;
-                } else {
-                    dp[0][i] |= h << sh; dp[1][i] |= m << sh; dp[2][i] |= l << sh;
-                    xp[0][i] |= xh << sh; xp[1][i] |= xm << sh; xp[2][i] |= xl << sh;
-                }
+                dv[r] = d;
+                xv2[r] = xv;
+            }
+            if constexpr (kVariant & 1) {
+                dp[0][i] = dp[1][i] = dp[2][i] = __builtin_amdgcn_perm(__float_as_uint(G[1][i]), __float_as_uint(G[0][i]), 0x07060302u);
+                xp[0][i] = xp[1][i] = __builtin_amdgcn_perm(__float_as_uint(X[1][i]), __float_as_uint(X[0][i]), 0x07060302u);
+                xp[2][i] = __builtin_amdgcn_perm(__float_as_uint(Y[1][i]), __float_as_uint(Y[0][i]), 0x07060302u);
+            } else {
+                hrl_split::split_pair(dv[0], dv[1], dp[0][i], dp[1][i], dp[2][i]);
+                if constexpr (!kFwd) hrl_split::split_pair(xv2[0], xv2[1], xp[0][i], xp[1][i], xp[2][i]);
             }
         }
         const int half = rho0 >> 3, sub = 2 * (rho0 & 7);
@@ -1555,9 +1550,12 @@ __device__ __forceinline__ void wait_tile_after(int it) {
     static_assert(kSlots == 5, "the early-iteration counts above are written for kSlots = 5");
 }
 
-template <bool PRO, int W>
+template <bool PRO, int W, bool STAG>
 __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, int lane) {
     constexpr int kCt = W & 1, G = W >> 1;
+    // STAG (fwd form 3): waves 4-7 compute tile it before staging tile it+1, so on each SIMD one wave's staging
+    // VALU runs beside its partner's MFMAs instead of both staging, then both computing
+    constexpr bool kLate = STAG && W >= 4;
     using C = Cells<G>;
     constexpr int kNq = C::kN;
     constexpr int NP = pieces_of<W>();
@@ -1617,25 +1615,22 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         const float *raw = reinterpret_cast<const float *>(smem + kRaw0 + slot * kRawBytes);
         unsigned char *xi = smem + kImg0 + (it & 1) * bb2::kImgBytes;
         uint32_t xp[3][5];
+        float xv[2][5];
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             const float *src = raw + (rho0 + r) * kRow + ch * kCells + c0;
 #pragma unroll
             for (int i = 0; i < 5; ++i) {
-                float xv = src[i];
+                float v = src[i];
                 if constexpr (PRO) {   // bn_apply_kernel's float operations
-                    const float u = xv * pa + pb;
-                    xv = u < 0.f ? 0.f : u;
+                    const float u = v * pa + pb;
+                    v = u < 0.f ? 0.f : u;
                 }
-                uint32_t xh, xm, xl;
-                hrl_split::split3(xv, xh, xm, xl);
-                if (r == 0) {
-                    xp[0][i] = xh; xp[1][i] = xm; xp[2][i] = xl;
-                } else {
-                    xp[0][i] |= xh << 16; xp[1][i] |= xm << 16; xp[2][i] |= xl << 16;
-                }
+                xv[r][i] = v;
             }
         }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) hrl_split::split_pair(xv[0][i], xv[1][i], xp[0][i], xp[1][i], xp[2][i]);
         const int half = rho0 >> 3, sub = 2 * (rho0 & 7);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
@@ -1663,7 +1658,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         // tile it's slot was read by stage(it) before the last barrier: tile it + kSlots goes there
         dma(it + kSlots, slot);
         const int next = slot + 1 == kSlots ? 0 : slot + 1;
-        stage(it + 1, next);                                 // runs past the last tile too (stale rows, unread)
+        if constexpr (!kLate) stage(it + 1, next);           // runs past the last tile too (stale rows, unread)
         BB2_STAMP(it, 1);
         // the MFMAs of tile it: acc[s] += sum_p x'_p (16 rows x 32 ci) . W[tap(p, q_s)][kCt], p ascending
         const unsigned char *img = smem + kImg0 + (it & 1) * bb2::kImgBytes;
@@ -1740,6 +1735,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                 __builtin_amdgcn_raw_buffer_store_b64(v, od, off, 0, 0);
             }
         }
+        if constexpr (kLate) stage(it + 1, next);
         wait_tile_after<NP, NS>(it);                         // tile it+2 landed (it+3 .. it+kSlots in flight)
         BB2_STAMP(it, 3);
         bb2::bar_lds();                                      // tile it+1's image staged, tile it's image free
@@ -1763,20 +1759,20 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
 
 }  // namespace fw3
 
-template <bool PRO>
+template <bool PRO, bool STAG>
 __global__ __launch_bounds__(bb2::kThreads) void conv3x3_fwd_dma_kernel(BlockBwdArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[fw3::kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     switch (wave) {
-    case 0: fw3::run<PRO, 0>(a, smem, lane); break;
-    case 1: fw3::run<PRO, 1>(a, smem, lane); break;
-    case 2: fw3::run<PRO, 2>(a, smem, lane); break;
-    case 3: fw3::run<PRO, 3>(a, smem, lane); break;
-    case 4: fw3::run<PRO, 4>(a, smem, lane); break;
-    case 5: fw3::run<PRO, 5>(a, smem, lane); break;
-    case 6: fw3::run<PRO, 6>(a, smem, lane); break;
-    default: fw3::run<PRO, 7>(a, smem, lane); break;
+    case 0: fw3::run<PRO, 0, STAG>(a, smem, lane); break;
+    case 1: fw3::run<PRO, 1, STAG>(a, smem, lane); break;
+    case 2: fw3::run<PRO, 2, STAG>(a, smem, lane); break;
+    case 3: fw3::run<PRO, 3, STAG>(a, smem, lane); break;
+    case 4: fw3::run<PRO, 4, STAG>(a, smem, lane); break;
+    case 5: fw3::run<PRO, 5, STAG>(a, smem, lane); break;
+    case 6: fw3::run<PRO, 6, STAG>(a, smem, lane); break;
+    default: fw3::run<PRO, 7, STAG>(a, smem, lane); break;
     }
 }
 
@@ -1902,7 +1898,7 @@ int hrl_conv3x3_set_block_form(int form) {
 
 int hrl_conv3x3_set_fwd_form(int form) {
     const int prev = g_fwd_form;
-    g_fwd_form = form < 0 ? 0 : (form > 2 ? 2 : form);
+    g_fwd_form = form < 0 ? 0 : (form > 3 ? 3 : form);
     return prev;
 }
 
@@ -1938,9 +1934,12 @@ int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, con
         BlockBwdArgs a{};
         a.x = x; a.in_alpha = in_alpha; a.in_beta = in_beta; a.wpk = wpk; a.gin = y; a.part = part; a.M = M;
         const dim3 grid(grid_for(M)), block(bb2::kThreads);
-        if (g_fwd_form == 2) {
-            if (in_alpha) hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<true>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<false>), grid, block, 0, s, a);
+        if (g_fwd_form == 3) {
+            if (in_alpha) hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<true, true>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<false, true>), grid, block, 0, s, a);
+        } else if (g_fwd_form == 2) {
+            if (in_alpha) hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<true, false>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<false, false>), grid, block, 0, s, a);
         } else if (in_alpha) {
             hipLaunchKernelGGL((conv3x3_block_bwd2_kernel<true, 1>), grid, block, 0, s, a);
         } else {
@@ -2024,7 +2023,7 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
                                const float *in_beta, const float *packed_flip, float *dweight, float *gin,
                                int epilogue, const float *ep_mean, const float *ep_alpha, const float *ep_beta,
                                double *part, void *workspace, int64_t workspace_bytes, void *stream) {
-    if (M < 1 || !g || !y || !save_mean || !save_invstd || !kcoef || !gmean || !x || !dweight || !workspace)
+    if (M < 1 || !g || !y || !save_mean || !save_invstd || !kcoef || !gmean || !x || !workspace)
         return HRL_EINVAL;
     if ((in_alpha == nullptr) != (in_beta == nullptr)) return HRL_EINVAL;
     if (workspace_bytes < hrl_conv3x3_workspace_bytes(M) || M * kRow * 4 > 0xffffffffLL) return HRL_EINVAL;
@@ -2060,10 +2059,16 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
 #undef HRL_BLOCK_LAUNCH
 #undef HRL_BLOCK2_LAUNCH
     int rc = status();
-    if (rc) return rc;
+    if (rc || !dweight) return rc;   // no dweight: the partials stay for a later fold (hrl_grad_fold_norm)
     hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, wpart, grid,
                        dweight);
     return status();
+}
+
+int64_t hrl_conv3x3_wgrad_partials(int64_t M, int64_t *offset_bytes) {
+    if (M < 1) return -1;
+    if (offset_bytes) *offset_bytes = (int64_t)kTaps * 2 * kC * 16 * 2 * 4;
+    return grid_for(M);
 }
 
 int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, int64_t C_out, float *dweight,

@@ -730,7 +730,9 @@ int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float 
                        void *workspace, int64_t workspace_bytes, void *stream) {
     if (N < 1 || !h || !w1p || !w1v || !wp || !wv || !a_p || !a_v || !dp || !dv || !dh || !workspace)
         return HRL_EINVAL;
-    if (!dw1p || !db1p || !dw1v || !db1v || !dwp || !dwv) return HRL_EINVAL;
+    const bool defer = !dw1p && !db1p && !dw1v && !db1v && !dwp && !dwv;   // partials left for a later fold
+    if (!defer && (!dw1p || !db1p || !dw1v || !db1v || !dwp || !dwv)) return HRL_EINVAL;
+    if (defer && g_heads_bwd_form != 2) return HRL_EINVAL;
     if ((bn_alpha == nullptr) != (bn_beta == nullptr) || (bn_part && (!bn_alpha || !bn_mean))) return HRL_EINVAL;
     if (!aligned16(h) || !aligned16(dh) || workspace_bytes < hrl_heads_workspace_bytes(N)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -747,7 +749,7 @@ int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float 
             hipLaunchKernelGGL(heads_bwd2_kernel<false>, dim3(grid), dim3(256), 0, s, h, N, w, bn, a_p, a_v, dp, dv,
                                v_tanh, dh, part);
         const int rc = status();
-        if (rc) return rc;
+        if (rc || defer) return rc;
         hipLaunchKernelGGL(heads_reduce_kernel, dim3(kGN), dim3(256), 0, s, part, grid, dw1p, dw1v, db1p, db1v, dwp,
                            dwv);
         return status();

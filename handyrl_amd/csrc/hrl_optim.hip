@@ -1,4 +1,5 @@
-// hrl_optim.hip — gradient clipping of the learner's flat gradient buffer in one launch (gfx950).
+// hrl_optim.hip — the learner step's tail on the flat gradient buffer (gfx950): gradient clipping, the deferred
+// weight-gradient folds and Adam.
 //
 // The reference clips with nn.utils.clip_grad_norm_(params, 4.0) before Adam
 // (handyrl/train.py:384): total = ||g||_2 over all parameters,
@@ -7,7 +8,20 @@
 // the buffer is small (29 k floats for the TicTacToe net, 234 k for
 // GeisterNet), so one workgroup reads it, folds the squares (fp64, fixed
 // order), forms the coefficient and scales it in place: one launch.
-
+//
+// The step tail (hrl_grad_fold_norm + hrl_adam_clip) replaces what followed the backward as separate launches:
+// the weight-gradient folds of the HIP Functions (per-workgroup partial rows -> the parameter gradients: the
+// chain blocks' conv3x3_wgrad_reduce, heads_reduce, stem_reduce), the clip, torch's capturable step-count
+// increment, the BatchNorm batch counters and torch's fused Adam -- two launches:
+//  * step_fold_norm_kernel: 64-element blocks of the flat buffer; a block's elements that a fold covers are the
+//    fixed-order fp64 sum of their partial column (4 waves over interleaved partial rows, combined in wave
+//    order), the rest are read; each block writes the fp64 sum of squares of its final values; block 0 also
+//    advances the step count and the batch counters;
+//  * adam_clip_kernel: every workgroup folds the block sums in one fixed order (so all agree on the norm bit for
+//    bit), forms clip_grad_norm_'s coefficient, scales its chunk of the gradient in place (p.grad is the clipped
+//    gradient afterwards, as in the reference) and applies torch's fused Adam arithmetic (ATen
+//    fused_adam_utils.cuh adam_math, ADAM_MODE::ORIGINAL, the same double / float promotions) to the parameters
+//    of the live tensors.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -56,6 +70,228 @@ __global__ __launch_bounds__(kThreads) void clip_kernel(float *__restrict__ g, i
     for (int64_t i = nv * 4 + t; i < n; i += kThreads) g[i] *= c;
 }
 
+// Large buffers (GeisterNet: 234 k floats, 47 us in one workgroup): two launches over kParts workgroups.
+// clip_partial_kernel: workgroup b folds the squares of its fixed chunk (fp64, fixed order) into part[b];
+// clip_apply_kernel: every workgroup folds part[0 .. kParts) in the same fixed order (so all agree on the norm
+// bit for bit), workgroup 0 writes it, and each scales its own chunk.  Deterministic; no inter-workgroup sync.
+constexpr int kParts = 64;
+constexpr int kThreads2 = 256;
+constexpr int64_t kSplitAbove = 65536;   // floats; below it the one-launch kernel is faster
+
+__device__ __forceinline__ void chunk_of(int64_t nv, int b, int64_t &lo, int64_t &hi) {
+    const int64_t per = (nv + kParts - 1) / kParts;
+    lo = min(nv, (int64_t)b * per);
+    hi = min(nv, lo + per);
+}
+
+__global__ __launch_bounds__(kThreads2) void clip_partial_kernel(const float *__restrict__ g, int64_t n,
+                                                                  double *__restrict__ part) {
+    __shared__ double red[kThreads2];
+    const int t = threadIdx.x, b = blockIdx.x;
+    const int64_t nv = n / 4;
+    int64_t lo, hi;
+    chunk_of(nv, b, lo, hi);
+    const float4 *g4 = reinterpret_cast<const float4 *>(g);
+    double s = 0.0;
+    for (int64_t i = lo + t; i < hi; i += kThreads2) {
+        const float4 v = g4[i];
+        s += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+    if (b == kParts - 1)   // the tail past the last float4
+        for (int64_t i = nv * 4 + t; i < n; i += kThreads2) s += (double)g[i] * g[i];
+    red[t] = s;
+    __syncthreads();
+    for (int w = kThreads2 / 2; w > 0; w >>= 1) {
+        if (t < w) red[t] += red[t + w];
+        __syncthreads();
+    }
+    if (t == 0) part[b] = red[0];
+}
+
+__global__ __launch_bounds__(kThreads2) void clip_apply_kernel(float *__restrict__ g, int64_t n, float max_norm,
+                                                                const double *__restrict__ part,
+                                                                float *__restrict__ total_out) {
+    __shared__ float coef_s;
+    const int t = threadIdx.x, b = blockIdx.x;
+    if (t == 0) {
+        double s = 0.0;
+        for (int i = 0; i < kParts; ++i) s += part[i];   // the same order in every workgroup
+        const float total = (float)sqrt(s);
+        if (b == 0) total_out[0] = total;
+        const float c = max_norm / (total + 1e-6f);
+        coef_s = (c < 1.0f || c != c) ? c : 1.0f;          // clip_kernel's clamp (NaN propagates)
+    }
+    __syncthreads();
+    const float c = coef_s;
+    const int64_t nv = n / 4;
+    int64_t lo, hi;
+    chunk_of(nv, b, lo, hi);
+    float4 *g4 = reinterpret_cast<float4 *>(g);
+    for (int64_t i = lo + t; i < hi; i += kThreads2) {
+        float4 v = g4[i];
+        v.x *= c; v.y *= c; v.z *= c; v.w *= c;
+        g4[i] = v;
+    }
+    if (b == kParts - 1)
+        for (int64_t i = nv * 4 + t; i < n; i += kThreads2) g[i] *= c;
+}
+
+int status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
+}
+
+// ------------------------------------------------------------------ the step tail
+constexpr int kMaxFolds = 16;
+constexpr int kMaxTensors = 64;
+constexpr int kMaxCounters = 8;
+constexpr int kBlk = 64;    // elements per fold/norm block
+
+struct FoldTable {
+    const float *part[kMaxFolds];
+    int64_t stride[kMaxFolds], col0[kMaxFolds], nparts[kMaxFolds], dst[kMaxFolds], count[kMaxFolds];
+    int mode[kMaxFolds];
+    int nfolds;
+};
+
+struct StepCounters {
+    float *step;                       // the optimizer's step count (float, as torch's capturable state)
+    int64_t *ctr[kMaxCounters];        // BatchNorm num_batches_tracked
+    int nctr;
+};
+
+// source column of element j of a fold: mode 0 identity; mode 1 a (Cout = 32, Cin = 32, 3, 3) conv weight from
+// the chain blocks' [tap][ci][co] partial layout (conv3x3_wgrad_reduce_kernel's transposition)
+__device__ __forceinline__ int64_t fold_col(int mode, int64_t j) {
+    if (mode == 1) {
+        const int co = (int)(j / 288), ci = (int)((j / 9) % 32), tap = (int)(j % 9);
+        return (tap * 32 + ci) * 32 + co;
+    }
+    return j;
+}
+
+__global__ __launch_bounds__(256) void step_fold_norm_kernel(float *__restrict__ g, int64_t n, FoldTable ft,
+                                                             StepCounters sc, double *__restrict__ norm_part) {
+    __shared__ double red[4][kBlk];
+    __shared__ double sq[kBlk];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * kBlk + lane;
+    int f = -1;
+    if (i < n)
+        for (int k = 0; k < ft.nfolds; ++k)
+            if (i >= ft.dst[k] && i < ft.dst[k] + ft.count[k]) f = k;
+    double s = 0.0;
+    if (f >= 0) {
+        const float *src = ft.part[f] + ft.col0[f] + fold_col(ft.mode[f], i - ft.dst[f]);
+        const int64_t np = ft.nparts[f], st = ft.stride[f];
+        // wave w takes rows w, w+4, w+8, ...: eight independent chains (rows w + 4k + 32r, k < 8) with all eight
+        // loads of a round issued before their adds, combined in chain order -- a fixed order
+        double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        int64_t b = w;
+        for (; b + 28 < np; b += 32) {
+            float t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t[k] = src[(b + 4 * k) * st];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += (double)t[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (b + 4 * k < np) acc[k] += (double)src[(b + 4 * k) * st];
+        s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    }
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0) {
+        double v;
+        if (f >= 0) {
+            v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+            const float fv = (float)v;
+            g[i] = fv;
+            v = (double)fv;
+        } else {
+            v = i < n ? (double)g[i] : 0.0;
+        }
+        sq[lane] = v * v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int k = 0; k < kBlk; ++k) t += sq[k];
+        norm_part[blockIdx.x] = t;
+        if (blockIdx.x == 0) {
+            if (sc.step) sc.step[0] += 1.0f;
+            for (int k = 0; k < sc.nctr; ++k) sc.ctr[k][0] += 1;
+        }
+    }
+}
+
+struct AdamTable {
+    float *p[kMaxTensors];
+    int64_t off[kMaxTensors + 1];      // flat offsets; off[nt] = n
+    uint64_t live;                     // bit t: tensor t is updated (a parameter with no gradient is skipped)
+    int nt;
+};
+
+struct AdamArgs {
+    float *g, *m, *v;
+    int64_t n;
+    const double *norm_part;
+    int64_t nblocks;
+    float max_norm;
+    float *total_out;
+    const float *lr, *step;
+    double beta1, beta2, eps, wd;
+};
+
+__global__ __launch_bounds__(256) void adam_clip_kernel(AdamArgs a, AdamTable tab) {
+    __shared__ double red[256];
+    __shared__ float coef_s;
+    const int t = threadIdx.x;
+    double s = 0.0;
+    for (int64_t k = t; k < a.nblocks; k += 256) s += a.norm_part[k];
+    red[t] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (t < w) red[t] += red[t + w];
+        __syncthreads();
+    }
+    if (t == 0) {
+        const float total = (float)sqrt(red[0]);
+        if (blockIdx.x == 0) a.total_out[0] = total;
+        const float c = a.max_norm / (total + 1e-6f);
+        coef_s = (c < 1.0f || c != c) ? c : 1.0f;      // clip_kernel's clamp (NaN propagates)
+    }
+    __syncthreads();
+    const float c = coef_s;
+    // fused_adam_utils.cuh: bias corrections in double, handed to adam_math as opmath_t (float)
+    const double stepd = (double)a.step[0];
+    const float bc1 = (float)(1.0 - pow(a.beta1, stepd));
+    const float bc2s = (float)sqrt(1.0 - pow(a.beta2, stepd));
+    const double lr = (double)a.lr[0];
+    const float step_size = (float)(lr / bc1);
+    const int64_t per = (a.n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = min(a.n, lo + per);
+    int tt = 0;
+    for (int64_t i = lo + t; i < hi; i += 256) {
+        float gr = a.g[i] * c;
+        a.g[i] = gr;
+        while (tt + 1 < tab.nt && i >= tab.off[tt + 1]) ++tt;   // i ascends per thread: the tensor only advances
+        if (!((tab.live >> tt) & 1)) continue;
+        float *pp = tab.p[tt] + (i - tab.off[tt]);
+        float param = *pp;
+        float exp_avg = a.m[i], exp_avg_sq = a.v[i];
+        if (a.wd != 0) gr = (float)((double)gr + (double)param * a.wd);
+        exp_avg = (float)(a.beta1 * (double)exp_avg + (1 - a.beta1) * (double)gr);
+        exp_avg_sq = (float)(a.beta2 * (double)exp_avg_sq + (1 - a.beta2) * (double)gr * (double)gr);
+        const float denom = (float)((double)(sqrtf(exp_avg_sq) / bc2s) + a.eps);
+        param -= step_size * exp_avg / denom;
+        *pp = param;
+        a.m[i] = exp_avg;
+        a.v[i] = exp_avg_sq;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -64,8 +300,82 @@ int hrl_clip_grad_norm(float *grads, int64_t n, double max_norm, float *total_no
     if (!grads || !total_norm || n < 0 || (reinterpret_cast<uintptr_t>(grads) & 15) != 0) return HRL_EINVAL;
     hipLaunchKernelGGL(clip_kernel, dim3(1), dim3(kThreads), 0, static_cast<hipStream_t>(stream), grads, n,
                        (float)max_norm, total_norm);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
+    return status();
+}
+
+int64_t hrl_grad_fold_norm_blocks(int64_t n) { return n < 1 ? -1 : (n + kBlk - 1) / kBlk; }
+
+int hrl_grad_fold_norm(float *grads, int64_t n, const float *const *parts, const int64_t *strides,
+                       const int64_t *col0, const int64_t *nparts, const int64_t *dst, const int64_t *count,
+                       const int *modes, int nfolds, float *step, int64_t *const *counters, int ncounters,
+                       double *norm_part, int64_t norm_part_bytes, void *stream) {
+    if (!grads || n < 1 || nfolds < 0 || nfolds > kMaxFolds || ncounters < 0 || ncounters > kMaxCounters ||
+        !norm_part || norm_part_bytes < hrl_grad_fold_norm_blocks(n) * 8)
+        return HRL_EINVAL;
+    FoldTable ft{};
+    for (int k = 0; k < nfolds; ++k) {
+        if (!parts[k] || nparts[k] < 1 || count[k] < 1 || dst[k] < 0 || dst[k] + count[k] > n || col0[k] < 0 ||
+            (modes[k] != 0 && modes[k] != 1) || (modes[k] == 1 && count[k] != 9216))
+            return HRL_EINVAL;
+        const int64_t span = modes[k] == 1 ? 9216 : count[k];
+        if (strides[k] < col0[k] + span) return HRL_EINVAL;
+        ft.part[k] = parts[k]; ft.stride[k] = strides[k]; ft.col0[k] = col0[k]; ft.nparts[k] = nparts[k];
+        ft.dst[k] = dst[k]; ft.count[k] = count[k]; ft.mode[k] = modes[k];
+    }
+    ft.nfolds = nfolds;
+    StepCounters sc{};
+    sc.step = step;
+    for (int k = 0; k < ncounters; ++k) {
+        if (!counters[k]) return HRL_EINVAL;
+        sc.ctr[k] = counters[k];
+    }
+    sc.nctr = ncounters;
+    hipLaunchKernelGGL(step_fold_norm_kernel, dim3((unsigned)hrl_grad_fold_norm_blocks(n)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), grads, n, ft, sc, norm_part);
+    return status();
+}
+
+int hrl_adam_clip(float *grads, int64_t n, const double *norm_part, double max_norm, float *total_norm,
+                  float *const *params, const int64_t *offsets, const int *live, int ntensors, float *exp_avg,
+                  float *exp_avg_sq, const float *lr, const float *step, double beta1, double beta2, double eps,
+                  double weight_decay, void *stream) {
+    if (!grads || n < 1 || !norm_part || !total_norm || !params || !offsets || !live || ntensors < 1 ||
+        ntensors > kMaxTensors || !exp_avg || !exp_avg_sq || !lr || !step)
+        return HRL_EINVAL;
+    AdamTable tab{};
+    for (int k = 0; k < ntensors; ++k) {
+        if (!params[k] || offsets[k] < 0 || offsets[k + 1] < offsets[k]) return HRL_EINVAL;
+        tab.p[k] = params[k];
+        tab.off[k] = offsets[k];
+        if (live[k]) tab.live |= (uint64_t)1 << k;
+    }
+    if (offsets[0] != 0 || offsets[ntensors] != n) return HRL_EINVAL;
+    tab.off[ntensors] = n;
+    tab.nt = ntensors;
+    AdamArgs a{grads, exp_avg, exp_avg_sq, n, norm_part, hrl_grad_fold_norm_blocks(n), (float)max_norm, total_norm,
+               lr, step, beta1, beta2, eps, weight_decay};
+    const int64_t grid = (n + 2047) / 2048 < 64 ? (n + 2047) / 2048 : 64;
+    hipLaunchKernelGGL(adam_clip_kernel, dim3((unsigned)grid), dim3(256), 0, static_cast<hipStream_t>(stream), a,
+                       tab);
+    return status();
+}
+
+int64_t hrl_clip_workspace_bytes(int64_t n) { return n < 0 ? -1 : (int64_t)kParts * 8; }
+
+int hrl_clip_grad_norm_ws(float *grads, int64_t n, double max_norm, float *total_norm, void *workspace,
+                          int64_t workspace_bytes, void *stream) {
+    if (!grads || !total_norm || n < 0 || (reinterpret_cast<uintptr_t>(grads) & 15) != 0) return HRL_EINVAL;
+    if (n <= kSplitAbove) return hrl_clip_grad_norm(grads, n, max_norm, total_norm, stream);
+    if (!workspace || workspace_bytes < hrl_clip_workspace_bytes(n) || (reinterpret_cast<uintptr_t>(workspace) & 7))
+        return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    double *part = static_cast<double *>(workspace);
+    hipLaunchKernelGGL(clip_partial_kernel, dim3(kParts), dim3(kThreads2), 0, s, grads, n, part);
+    const int rc = status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(clip_apply_kernel, dim3(kParts), dim3(kThreads2), 0, s, grads, n, (float)max_norm, part,
+                       total_norm);
+    return status();
 }
 
 }  // extern "C"

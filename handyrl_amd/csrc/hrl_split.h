@@ -26,6 +26,21 @@ __device__ __forceinline__ void split3(float x, uint32_t &h, uint32_t &m, uint32
     l = __float_as_uint(r - __uint_as_float(mb)) >> 16;
 }
 
+// the exact split of two values (rows 2k and 2k+1 of an MFMA operand) packed as bf16 pairs: H = {h0, h1},
+// M = {m0, m1}, L = {l0, l1} (x0 in the low half).  The same parts as split3, in 11 VALU instead of 20: the parts
+// are kept as fp32 bit patterns whose low 16 bits are zero, and v_perm_b32 takes both high halves at once.
+__device__ __forceinline__ void split_pair(float x0, float x1, uint32_t &H, uint32_t &M, uint32_t &L) {
+    const uint32_t hb0 = __float_as_uint(x0) & 0xffff0000u, hb1 = __float_as_uint(x1) & 0xffff0000u;
+    const float r0 = x0 - __uint_as_float(hb0), r1 = x1 - __uint_as_float(hb1);
+    const uint32_t mb0 = __float_as_uint(r0) & 0xffff0000u, mb1 = __float_as_uint(r1) & 0xffff0000u;
+    const uint32_t lb0 = __float_as_uint(r0 - __uint_as_float(mb0));
+    const uint32_t lb1 = __float_as_uint(r1 - __uint_as_float(mb1));
+    // perm(S0, S1, sel): selector bytes 0-3 pick S1's bytes, 4-7 S0's: {S1.b2, S1.b3, S0.b2, S0.b3}
+    H = __builtin_amdgcn_perm(hb1, hb0, 0x07060302u);
+    M = __builtin_amdgcn_perm(mb1, mb0, 0x07060302u);
+    L = __builtin_amdgcn_perm(lb1, lb0, 0x07060302u);
+}
+
 // part 0/1/2 (h/m/l) of x as the 16 bf16 bits
 __device__ __forceinline__ uint32_t split_part(float x, int part) {
     uint32_t h, m, l;

@@ -393,6 +393,12 @@ int64_t hrl_stem_workspace_bytes(int64_t N) {
     return (int64_t)(g1 > g2 ? g1 : g2) * kNOut * 4;
 }
 
+int64_t hrl_stem_wgrad_partials(int64_t N, int64_t *row_floats) {
+    if (N < 1) return -1;
+    if (row_floats) *row_floats = kNOut;
+    return grid_wgrad(N);
+}
+
 int hrl_stem_set_wgrad_form(int form) {
     const int prev = g_stem_wgrad_form;
     g_stem_wgrad_form = form == 1 ? 1 : 2;
@@ -409,25 +415,29 @@ int hrl_stem_forward(const float *x, int64_t N, int64_t Cin, const float *weight
 
 int hrl_stem_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, float *dweight, float *dbias,
                    void *workspace, int64_t workspace_bytes, void *stream) {
-    if (N < 1 || Cin < 1 || Cin > 3 || !x || !dy || !dweight || !workspace) return HRL_EINVAL;
+    if (N < 1 || Cin < 1 || Cin > 3 || !x || !dy || !workspace) return HRL_EINVAL;
     if (workspace_bytes < hrl_stem_workspace_bytes(N)) return HRL_EINVAL;
+    // no dweight (and no dbias): the partial rows [dW | db] stay in the workspace for a later fold
+    const bool defer = !dweight;
+    if (defer && (dbias || g_stem_wgrad_form != 2)) return HRL_EINVAL;
+    const int want_bias = (dbias || defer) ? 1 : 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int grid = grid_wgrad(N);
     float *partial = static_cast<float *>(workspace);
     if (g_stem_wgrad_form == 2) {
         if (N * kCols * 4 >= (int64_t)1 << 32) return HRL_EINVAL;   // 32-bit buffer offsets
         if (Cin == 3)
-            hipLaunchKernelGGL(stem_wgrad2_kernel<3>, dim3(grid), dim3(kThreads), 0, s, x, dy, N, dbias ? 1 : 0, partial);
+            hipLaunchKernelGGL(stem_wgrad2_kernel<3>, dim3(grid), dim3(kThreads), 0, s, x, dy, N, want_bias, partial);
         else if (Cin == 2)
-            hipLaunchKernelGGL(stem_wgrad2_kernel<2>, dim3(grid), dim3(kThreads), 0, s, x, dy, N, dbias ? 1 : 0, partial);
+            hipLaunchKernelGGL(stem_wgrad2_kernel<2>, dim3(grid), dim3(kThreads), 0, s, x, dy, N, want_bias, partial);
         else
-            hipLaunchKernelGGL(stem_wgrad2_kernel<1>, dim3(grid), dim3(kThreads), 0, s, x, dy, N, dbias ? 1 : 0, partial);
+            hipLaunchKernelGGL(stem_wgrad2_kernel<1>, dim3(grid), dim3(kThreads), 0, s, x, dy, N, want_bias, partial);
     } else {
         hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)Cin, dbias ? 1 : 0,
                            partial);
     }
     int rc = status();
-    if (rc) return rc;
+    if (rc || !dweight) return rc;   // no dweight: the partial rows stay for a later fold (hrl_grad_fold_norm)
     const int nw = kCo * (int)Cin * 9;
     hipLaunchKernelGGL(stem_reduce_kernel, dim3(nw + (dbias ? kCo : 0)), dim3(256), 0, s, partial, grid, nw, dweight,
                        dbias);

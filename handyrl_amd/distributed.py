@@ -81,11 +81,14 @@ class FlatGrads:
         on the GPU one csrc/hrl_optim.hip launch instead of six torch ops."""
         if self.flat.is_cuda:
             from . import _native
+            lib = _native.load()
             if self._total is None:
                 self._total = torch.empty((), dtype=torch.float32, device=self.flat.device)
-            _native.check(_native.load().hrl_clip_grad_norm(_native.ptr(self.flat), self.flat.numel(),
-                                                            float(max_norm), _native.ptr(self._total),
-                                                            _native.stream_of(self.flat.device)),
+                self._clip_ws = torch.empty(max(lib.hrl_clip_workspace_bytes(self.flat.numel()), 8),
+                                            dtype=torch.uint8, device=self.flat.device)
+            _native.check(lib.hrl_clip_grad_norm_ws(_native.ptr(self.flat), self.flat.numel(), float(max_norm),
+                                                    _native.ptr(self._total), _native.ptr(self._clip_ws),
+                                                    self._clip_ws.numel(), _native.stream_of(self.flat.device)),
                           'hrl_clip_grad_norm')
             return self._total
         total = self.norm()

@@ -25,6 +25,7 @@ The HIP path is taken whenever the input is a CUDA tensor in training mode;
 if libhrl.so is missing that raises (no silent fallback).
 """
 
+import ctypes
 import operator
 
 import os
@@ -259,6 +260,60 @@ class direct_grads:
         global _DIRECT
         _DIRECT = self.prev
         return False
+
+
+_FOLDS = None
+
+
+class deferred_folds:
+    """Context manager (LearnerStep on one GPU, with the step tail): a HIP backward Function whose parameter
+    gradients are written in place (direct_grads) leaves them as its per-workgroup partial rows instead of
+    launching its reduce kernel, and registers the fold here; LearnerStep folds every registered partial into the
+    flat gradient buffer in the step tail's first launch (hrl_grad_fold_norm, together with the clip's norm).  The
+    fused chains' BatchNorm batch counters are collected here too, for the same launch."""
+
+    def __init__(self, enabled=True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        global _FOLDS
+        self.prev = _FOLDS
+        self.folds = []      # (partial rows (float32 tensor), stride, col0, nparts, dst gradient view, count, mode)
+        self.counters = []   # int64 num_batches_tracked tensors
+        self.keep = []       # workspaces read by the folds: referenced until the fold launch is enqueued
+        if self.enabled:
+            _FOLDS = self
+        return self
+
+    def __exit__(self, *exc):
+        global _FOLDS
+        if self.enabled:
+            _FOLDS = self.prev
+        return False
+
+    def add(self, part, stride, col0, nparts, dst, count, mode=0):
+        self.folds.append((part, stride, col0, nparts, dst, count, mode))
+
+
+def _defer_folds(bufs):
+    """The deferred-folds context when the gradients in `bufs` (_grad_buffer results) may stay as partials:
+    one is active and every buffer is a direct (in-place) one; else None."""
+    if _FOLDS is None or not all(b[1] for b in bufs if b[0] is not None):
+        return None
+    return _FOLDS
+
+
+def _heads_backward_deferred(lib, df, bufs, N, ws, call):
+    """hrl_heads_backward with the six weight-gradient pointers NULL (partials left in ws), then the folds of its
+    270-float partial rows [dW1 policy (64) | dW1 value (32) | db1 (3) | dWp (162) | dWv (9)] registered."""
+    call(None, None, None, None, None, None)
+    dw1p, db1p, dw1v, db1v, dwp, dwv = (b[0] for b in bufs)
+    part = ws.view(torch.float32)
+    nparts = lib.hrl_heads_bn_parts(N)
+    for dst, col0, count in ((dw1p, 0, 64), (dw1v, 64, 32), (db1p, 96, 2), (db1v, 98, 1), (dwp, 99, 162),
+                             (dwv, 261, 9)):
+        df.add(part, 270, col0, nparts, dst, count)
+    df.keep.append(ws)
 
 
 def _grad_buffer(p):
@@ -1276,10 +1331,16 @@ class _BoardHeadsFn(torch.autograd.Function):
         ws_bytes = lib.hrl_heads_workspace_bytes(N)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         P = _native.ptr
-        dw1p, db1p, dw1v, db1v, dwp, dwv = (b[0] for b in bufs)
-        _native.check(lib.hrl_heads_backward(P(h), N, P(w1p), P(w1v), P(wp), P(wv), None, None, None, None, P(a_p),
-                                             P(a_v), P(dp), P(dv), None, P(dh), P(dw1p), P(db1p), P(dw1v), P(db1v), P(dwp),
-                                             P(dwv), P(ws), ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward')
+
+        def call(*dws):
+            _native.check(lib.hrl_heads_backward(P(h), N, P(w1p), P(w1v), P(wp), P(wv), None, None, None, None,
+                                                 P(a_p), P(a_v), P(dp), P(dv), None, P(dh), *(P(t) for t in dws),
+                                                 P(ws), ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward')
+        df = _defer_folds(bufs)
+        if df is not None:
+            _heads_backward_deferred(lib, df, bufs, N, ws, call)
+        else:
+            call(*(b[0] for b in bufs))
         return (dh, *(_ret(b) for b in bufs))
 
 
@@ -1367,9 +1428,20 @@ class _StemConv(torch.autograd.Function):
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
         bw = _grad_buffer(weight)
         bb = _grad_buffer(bias) if bias is not None else (None, False)
-        _native.check(lib.hrl_stem_wgrad(_native.ptr(x), _native.ptr(dy.contiguous()), N, Cin, _native.ptr(bw[0]),
-                                         _native.ptr(bb[0]), _native.ptr(ws), ws_bytes,
+        df = _defer_folds([bw, bb])
+        dwp, dbp = (None, None) if df is not None else (bw[0], bb[0])
+        _native.check(lib.hrl_stem_wgrad(_native.ptr(x), _native.ptr(dy.contiguous()), N, Cin, _native.ptr(dwp),
+                                         _native.ptr(dbp), _native.ptr(ws), ws_bytes,
                                          _native.stream_of(x.device)), 'hrl_stem_wgrad')
+        if df is not None:   # partial rows [dW (32, Cin, 3, 3) | db (32)] left in ws
+            row = ctypes.c_int64(0)
+            nparts = lib.hrl_stem_wgrad_partials(N, ctypes.byref(row))
+            part = ws.view(torch.float32)
+            nw = 32 * Cin * 9
+            df.add(part, row.value, 0, nparts, bw[0], nw)
+            if bb[0] is not None:
+                df.add(part, row.value, nw, nparts, bb[0], 32)
+            df.keep.append(ws)
         return None, _ret(bw), _ret(bb)
 
 
@@ -1790,12 +1862,19 @@ def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, pa
                 gin, epi, ep = torch.empty_like(h0), 2, (coefs[i - 1][0], coefs[i - 1][2], coefs[i - 1][3])
             elif need_input_grad:
                 gin, epi = torch.empty_like(h0), (3 if relu_in else 0)
+            df = _defer_folds([bw])
+            wsb = ws if df is None else torch.empty(ws_bytes, dtype=torch.uint8, device=dev)   # partials live on
             ev = _block_timing_start()
             _native.check(lib.hrl_conv3x3_block_backward(
                 P(g), P(ys[i]), M, P(gamma), P(beta), P(mean), P(invstd), P(kg[0]), P(kg[1]), P(x), P(a), P(b),
-                P(packed[i, 1]), P(dw), P(gin), epi, P(ep[0]), P(ep[1]), P(ep[2]), P(part) if i > 0 else None,
-                P(ws), ws_bytes, stream), 'hrl_conv3x3_block_backward')
+                P(packed[i, 1]), None if df is not None else P(dw), P(gin), epi, P(ep[0]), P(ep[1]), P(ep[2]),
+                P(part) if i > 0 else None, P(wsb), ws_bytes, stream), 'hrl_conv3x3_block_backward')
             _block_timing_end(ev)
+            if df is not None:   # [block][tap][ci][co] partial rows -> dW (co, ci, kh, kw): fold mode 1
+                off = ctypes.c_int64(0)
+                nparts = lib.hrl_conv3x3_wgrad_partials(M, ctypes.byref(off))
+                df.add(wsb[off.value:].view(torch.float32), 9216, 0, nparts, dw, 9216, mode=1)
+                df.keep.append(wsb)
             grads[3 * i:3 * i + 3] = [_ret(bw), _ret(bgam), _ret(bbet)]
             g = gin
             if i > 0:
@@ -1911,12 +1990,16 @@ class _ChainHeadsFn(torch.autograd.Function):
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         nparts = lib.hrl_heads_bn_parts(N)
         bn_part = torch.empty(nparts * 64, dtype=torch.float64, device=dev)
-        dw1p, db1p, dw1v, db1v, dwp, dwv = (b[0] for b in hbufs)
-        _native.check(lib.hrl_heads_backward(P(y), N, P(w1p), P(w1v), P(wp), P(wv), P(coef[2]), P(coef[3]),
-                                             P(coef[0]), P(bn_part), P(a_p), P(a_v), P(dp), P(dv),
-                                             P(v) if ctx.tanh_v else None, P(dh), P(dw1p),
-                                             P(db1p), P(dw1v), P(db1v), P(dwp), P(dwv), P(ws), ws_bytes,
-                                             _native.stream_of(dev)), 'hrl_heads_backward(bn)')
+        def call(*dws):
+            _native.check(lib.hrl_heads_backward(P(y), N, P(w1p), P(w1v), P(wp), P(wv), P(coef[2]), P(coef[3]),
+                                                 P(coef[0]), P(bn_part), P(a_p), P(a_v), P(dp), P(dv),
+                                                 P(v) if ctx.tanh_v else None, P(dh), *(P(t) for t in dws),
+                                                 P(ws), ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward(bn)')
+        df = _defer_folds(hbufs)
+        if df is not None:
+            _heads_backward_deferred(lib, df, hbufs, N, ws, call)
+        else:
+            call(*(b[0] for b in hbufs))
         unit = _unit_coefs(dev) if ctx.relu_in else None
         g_in, grads = _chain_backward(h0, ys, coefs, unit, params, ctx.relu_in, dh, ctx.needs_input_grad[0], packed,
                                       part_in=bn_part, nblk_in=nparts)
@@ -1962,7 +2045,11 @@ class _ConvBNChain(nn.Module):
 
     def meta_params(self):
         """Advance the BatchNorms' batch counters (as their forward would) and collect the chain's arguments."""
-        torch._foreach_add_([b.num_batches_tracked for b in self.bns], 1)   # one launch for all counters
+        counters = [b.num_batches_tracked for b in self.bns]
+        if _FOLDS is not None:
+            _FOLDS.counters += counters            # advanced by the step tail's first launch
+        else:
+            torch._foreach_add_(counters, 1)       # one launch for all counters
         meta, params = [], []
         for c, b in zip(self.convs, self.bns):
             meta.append((b.running_mean, b.running_var, b.momentum, b.eps))

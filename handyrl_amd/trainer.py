@@ -27,11 +27,88 @@ import torch
 import torch.nn as nn
 
 from . import distributed as hdist
-from .nn import accelerate, fuse_bn_relu, deferred_weight_grads, direct_grads
+from .nn import accelerate, fuse_bn_relu, deferred_weight_grads, deferred_folds, direct_grads
 from .train import backward_total, forward_prediction, loss_terms
 from .util import map_r, bimap_r
 
 DEFAULT_LR = 3e-8  # train.py:318
+
+
+class StepTail:
+    """clip_grad_norm_(4.0) + torch.optim.Adam(lr, weight_decay=1e-5) (train.py:322, 384-385) over the learner's
+    flat gradient buffer as two HIP launches (csrc/hrl_optim.hip): hrl_grad_fold_norm (the deferred weight-gradient
+    folds of the step's HIP Functions, the norm's per-block sums of squares, the step count and the BatchNorm
+    batch counters) and hrl_adam_clip (the clip coefficient from those sums, the in-place scaling -- p.grad holds
+    the clipped gradient afterwards, as in the reference -- and torch's fused Adam arithmetic on the parameters
+    that receive a gradient).  Replaces the clip launch, torch's step-count / counter increments, its fused Adam
+    and the Functions' reduce launches.  lr and the step count are device scalars, so a captured graph replays
+    with their current values."""
+
+    def __init__(self, grads, lr, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8, max_norm=4.0):
+        from . import _native
+        self.lib = _native.load()
+        self.grads = grads
+        flat = grads.flat
+        dev = flat.device
+        n = flat.numel()
+        self.n = n
+        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.step_t = torch.zeros((), dtype=torch.float32, device=dev)
+        self.lr_t = torch.tensor(float(lr), dtype=torch.float32, device=dev)
+        self.norm_part = torch.empty(self.lib.hrl_grad_fold_norm_blocks(n), dtype=torch.float64, device=dev)
+        self.total = torch.empty((), dtype=torch.float32, device=dev)
+        self.wd, self.betas, self.eps, self.max_norm = weight_decay, betas, eps, max_norm
+        params = grads.params
+        self.ptrs = _native.ptr_array(params)
+        self.offsets = _native.i64_array([off for off, _ in grads.slices] + [n])
+        self.set_live([True] * len(params))
+
+    @staticmethod
+    def supports(params):
+        return (0 < len(params) <= 64 and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
+                                             for p in params))
+
+    def set_live(self, live):
+        import ctypes
+        self.live = (ctypes.c_int * len(live))(*[int(x) for x in live])
+
+    def set_lr(self, lr):
+        self.lr_t.fill_(lr)
+
+    def state_tensors(self):
+        return [self.m, self.v, self.step_t]
+
+    def __call__(self, folds=None):
+        """Fold, clip and update; folds: a finished nn.deferred_folds (or None).  Returns the norm (device)."""
+        from . import _native
+        lib, P = self.lib, _native.ptr
+        flat = self.grads.flat
+        base = flat.data_ptr()
+        fl = folds.folds if folds is not None else []
+        counters = folds.counters if folds is not None else []
+        if len(fl) > 16 or len(counters) > 8:
+            raise ValueError('step tail: %d folds / %d counters (at most 16 / 8)' % (len(fl), len(counters)))
+        dst = []
+        for f in fl:
+            off = (f[4].data_ptr() - base) // 4
+            if f[4].data_ptr() % 4 or off < 0 or off + f[5] > self.n:
+                raise ValueError('step tail: a fold destination outside the flat gradient buffer')
+            dst.append(off)
+        i64 = _native.i64_array
+        import ctypes
+        stream = _native.stream_of(flat.device)
+        _native.check(lib.hrl_grad_fold_norm(
+            P(flat), self.n, _native.ptr_array([f[0] for f in fl]), i64([f[1] for f in fl]),
+            i64([f[2] for f in fl]), i64([f[3] for f in fl]), i64(dst), i64([f[5] for f in fl]),
+            (ctypes.c_int * max(len(fl), 1))(*[f[6] for f in fl]), len(fl), P(self.step_t),
+            _native.ptr_array(counters), len(counters), P(self.norm_part), self.norm_part.numel() * 8, stream),
+            'hrl_grad_fold_norm')
+        _native.check(lib.hrl_adam_clip(
+            P(flat), self.n, P(self.norm_part), float(self.max_norm), P(self.total), self.ptrs, self.offsets,
+            self.live, len(self.live), P(self.m), P(self.v), P(self.lr_t), P(self.step_t), float(self.betas[0]),
+            float(self.betas[1]), float(self.eps), float(self.wd), stream), 'hrl_adam_clip')
+        return self.total
 
 
 class LearnerStep:
@@ -64,7 +141,12 @@ class LearnerStep:
                                     fused=True)
         else:
             self._opt_kwargs = dict(lr=lr, weight_decay=1e-5, fused=fused, foreach=None if fused else True)
-        self.optimizer = torch.optim.Adam(self.params, **self._opt_kwargs)
+        # the step tail (clip + Adam, and on one GPU the Functions' deferred gradient folds) as two HIP launches;
+        # torch's Adam where it does not apply (CPU, more than 64 parameter tensors)
+        self.tail = StepTail(self.grads, lr) if (fused and StepTail.supports(self.params)) else None
+        self.optimizer = None if self.tail is not None else torch.optim.Adam(self.params, **self._opt_kwargs)
+        self.fold_deferral = self.tail is not None and world_size == 1
+        self._folds = None
         self.live = None        # params that receive a gradient (set on the first batch)
         self.defer = hip_layers and device.type == 'cuda'   # batched weight gradients for recurrent steps
         self._graph = None
@@ -80,6 +162,9 @@ class LearnerStep:
 
     # -- learning rate (train.py:396-398) ---------------------------------
     def set_lr(self, lr):
+        if self.tail is not None:
+            self.tail.set_lr(lr)
+            return
         for group in self.optimizer.param_groups:
             if isinstance(group['lr'], torch.Tensor):
                 group['lr'].fill_(lr)
@@ -125,7 +210,9 @@ class LearnerStep:
                 self.reducer.enabled = True
                 self.reducer.reset()
         self.live = live
-        if not all(live):
+        if self.tail is not None:
+            self.tail.set_live(live)   # a parameter with no gradient: no update, no weight decay
+        elif not all(live):
             kw = dict(self._opt_kwargs)
             kw['lr'] = self.optimizer.param_groups[0]['lr']   # keep a set_lr() made before the first step
             self.optimizer = torch.optim.Adam([p for p, l in zip(self.params, live) if l], **kw)
@@ -151,17 +238,23 @@ class LearnerStep:
                 self.reducer.mark_ready(touched)
         else:
             # the HIP Functions write single-use parameter gradients straight into the flat buffer
-            # (zeroed above) instead of autograd's per-parameter accumulate-adds (nn.direct_grads)
-            with direct_grads():
+            # (zeroed above) instead of autograd's per-parameter accumulate-adds (nn.direct_grads); on one GPU
+            # they leave them as partial rows that the step tail folds (nn.deferred_folds)
+            with direct_grads(), deferred_folds(enabled=self.fold_deferral) as df:
                 outputs = forward_prediction(self.net, hidden, batch, self.args)
                 losses, dcnt = self.loss_fn(outputs, batch, self.args)
                 backward_total(losses)
+            self._folds = df if self.fold_deferral else None
         return losses, dcnt
 
     def _update(self, losses, dcnt):
         """clip_grad_norm_(4.0) on the (all-reduced) gradients, then Adam (train.py:384-385)."""
-        gnorm = self.grads.clip_(4.0)
-        self.optimizer.step()
+        if self.tail is not None:
+            folds, self._folds = self._folds, None
+            gnorm = self.tail(folds)
+        else:
+            gnorm = self.grads.clip_(4.0)
+            self.optimizer.step()
         out = {k: v.detach() for k, v in losses.items()}
         out['dcnt'] = dcnt
         out['grad_norm'] = gnorm
@@ -173,8 +266,7 @@ class LearnerStep:
         with torch.no_grad():
             return ([p.detach().clone() for p in self.net.parameters()],
                     [b.detach().clone() for b in self.net.buffers()],
-                    [(v, v.detach().clone()) for st in self.optimizer.state.values() for v in st.values()
-                     if isinstance(v, torch.Tensor)])
+                    [(v, v.detach().clone()) for v in self._opt_state()])
 
     def restore(self, snap):
         params, buffers, opt = snap
@@ -185,6 +277,11 @@ class LearnerStep:
                 b.copy_(v)
             for t, v in opt:
                 t.copy_(v)
+
+    def _opt_state(self):
+        if self.tail is not None:
+            return self.tail.state_tensors()
+        return [v for st in self.optimizer.state.values() for v in st.values() if isinstance(v, torch.Tensor)]
 
     def _body(self, batch, hidden):
         losses, dcnt = self._grads(batch, hidden)
@@ -263,10 +360,8 @@ class LearnerStep:
                 p.copy_(v)
             for b, v in zip(self.net.buffers(), saved_b):
                 b.copy_(v)
-            for state in self.optimizer.state.values():
-                for v in state.values():
-                    if isinstance(v, torch.Tensor):
-                        v.zero_()
+            for v in self._opt_state():
+                v.zero_()
         if self.reducer is None:
             self._graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._graph):

@@ -174,8 +174,9 @@ int hrl_conv3x3_set_split(int on);
  * association.  Process-wide; returns the previous setting. */
 int hrl_conv3x3_set_block_form(int form);
 /* The chain's forward conv with BN statistics (hrl_conv3x3_forward_ex, epilogue 1, packed weights, no bias):
- * 2 (default) = the LDS-DMA ring form (every wave computes, x' staged from a raw ring), 1 = the block backward's
- * tile-shared form, 0 = the per-wave conv3x3_kernel (tools/fwd_form_bench.py).  Returns the previous. */
+ * 2 (default) = the LDS-DMA ring form (every wave computes, x' staged from a raw ring), 3 = the same with waves 4-7
+ * computing before they stage (a stagger of each SIMD's two waves), 1 = the block backward's tile-shared form,
+ * 0 = the per-wave conv3x3_kernel (tools/fwd_form_bench.py).  Returns the previous. */
 int hrl_conv3x3_set_fwd_form(int form);
 /* Both packed layouts of n <= 8 weights (32, 32, 3, 3) in one launch: packed[(l*2 + f) * 9216], f = 0 forward,
  * 1 input gradient (host array of device pointers).  hrl_conv3x3_forward_ex with flip | 2 takes `weight`
@@ -201,6 +202,10 @@ int hrl_conv3x3_wgrad_ex(const float *x, const float *in_alpha, const float *in_
  * part: hrl_conv3x3_stats_blocks(M) x 32 x 2 doubles.  Replaces, for the TicTacToe body
  * (tictactoe.py:57-65), the autograd backward of conv -> BatchNorm2d -> ReLU per block.
  */
+/* dweight NULL: the weight gradient is left as per-workgroup partial rows in the workspace (9216 floats each,
+ * [tap][ci][co]) for hrl_grad_fold_norm (fold mode 1); hrl_conv3x3_wgrad_partials(M, &offset_bytes) returns their
+ * row count and byte offset in the workspace. */
+int64_t hrl_conv3x3_wgrad_partials(int64_t M, int64_t *offset_bytes);
 int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const float *bn_weight,
                                const float *bn_bias, const float *save_mean, const float *save_invstd,
                                const float *kcoef, const float *gmean, const float *x, const float *in_alpha,
@@ -431,6 +436,9 @@ int64_t hrl_heads_bn_parts(int64_t N);
 int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *b1p, const float *w1v,
                       const float *b1v, const float *wp, const float *wv, const float *bn_alpha, const float *bn_beta,
                       float *a_p, float *a_v, float *p_out, float *v_out, int tanh_v, void *stream);
+/* hrl_heads_backward with all six weight-gradient pointers NULL (form 2): the parameter gradients are left as
+ * hrl_heads_bn_parts(N) partial rows of 270 floats at the start of the workspace -- [dW1 (3 x 32: policy rows then
+ * the value row) | db1 (3) | dWp (9 x 18) | dWv (9)] -- for hrl_grad_fold_norm. */
 /* hrl_heads_set_bwd_form: 2 (default) = the lane-per-channel backward (4-wave workgroups, accumulators in registers,
  * the fc weight gradients in the same pass), 1 = the row-per-lane kernel + separate fc-gradient launch (measurement).
  * Process-wide; returns the previous setting.  hrl_heads_bn_parts / hrl_heads_workspace_bytes follow the form. */
@@ -451,15 +459,48 @@ int hrl_stem_forward(const float *x, int64_t N, int64_t Cin, const float *weight
                      void *stream);
 int hrl_stem_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, float *dweight, float *dbias,
                    void *workspace, int64_t workspace_bytes, void *stream);
+/* hrl_stem_wgrad with dweight and dbias NULL (form 2): the gradients are left as hrl_stem_wgrad_partials(N, &row)
+ * partial rows of `row` floats at the start of the workspace, [dW (32, Cin, 3, 3) | db (32)], for
+ * hrl_grad_fold_norm. */
+int64_t hrl_stem_wgrad_partials(int64_t N, int64_t *row_floats);
 /* hrl_stem_set_wgrad_form: 2 (default) = the lane-per-channel weight gradient (a lane owns one output channel's
  * Cin x 9 weights and its bias of a row; 4-wave workgroups, 4 per CU), 1 = the dense-board fp32 MFMA kernel
  * (measurement).  Process-wide; returns the previous setting.  hrl_stem_workspace_bytes covers both forms. */
 int hrl_stem_set_wgrad_form(int form);
 
+/* The learner step's tail on the flat gradient buffer `grads` (n floats; parameter gradients are views of it):
+ * hrl_grad_fold_norm: for each of nfolds (<= 16) deferred weight-gradient folds, grads[dst + j] (j < count) =
+ *   the fixed-order fp64 sum over nparts partial rows of parts[row * stride + col0 + col(j)] (mode 0: col(j) = j;
+ *   mode 1: a 32x32x3x3 conv weight from the chain blocks' [tap][ci][co] rows, count 9216); then the fp64 sum of
+ *   squares of every 64-element block of grads into norm_part (hrl_grad_fold_norm_blocks(n) doubles); and,
+ *   once, *step += 1 (may be NULL) and *counters[k] += 1 (BatchNorm num_batches_tracked, ncounters <= 8).
+ * hrl_adam_clip: clip_grad_norm_(max_norm) from those block sums (every workgroup folds them in one fixed order;
+ *   *total_norm = the norm; grads scaled in place) and torch.optim.Adam's step (fused_adam_utils.cuh adam_math,
+ *   L2 weight decay, the same double / float promotions) on the tensors params[t] (elements offsets[t] ..
+ *   offsets[t+1] of grads, offsets[ntensors] = n, ntensors <= 64) whose live[t] != 0; exp_avg / exp_avg_sq are n
+ *   floats each; lr and step are device scalars (a graph replays with their current values).
+ * Deterministic.  Replaces the reduce launches of the HIP backward Functions, the clip, torch's step-count and
+ * batch-counter increments and torch's fused Adam (train.py:384-385). */
+int64_t hrl_grad_fold_norm_blocks(int64_t n);
+int hrl_grad_fold_norm(float *grads, int64_t n, const float *const *parts, const int64_t *strides,
+                       const int64_t *col0, const int64_t *nparts, const int64_t *dst, const int64_t *count,
+                       const int *modes, int nfolds, float *step, int64_t *const *counters, int ncounters,
+                       double *norm_part, int64_t norm_part_bytes, void *stream);
+int hrl_adam_clip(float *grads, int64_t n, const double *norm_part, double max_norm, float *total_norm,
+                  float *const *params, const int64_t *offsets, const int *live, int ntensors, float *exp_avg,
+                  float *exp_avg_sq, const float *lr, const float *step, double beta1, double beta2, double eps,
+                  double weight_decay, void *stream);
+
 /* clip_grad_norm_(params, max_norm) on the learner's flat gradient buffer (handyrl/train.py:384)
  * in one launch: total = ||grads||_2 (fp64 fold) -> *total_norm; grads *= min(max_norm / (total + 1e-6), 1).
  * grads 16-byte aligned, n floats (csrc/hrl_optim.hip). */
 int hrl_clip_grad_norm(float *grads, int64_t n, double max_norm, float *total_norm, void *stream);
+/* The same with a workspace of hrl_clip_workspace_bytes(n) bytes (8-byte aligned): above 64 k floats it runs as
+ * two launches over 64 workgroups (per-chunk fp64 partials, then every workgroup folds them in one fixed order and
+ * scales its chunk) instead of one workgroup walking the whole buffer; deterministic, the same norm. */
+int64_t hrl_clip_workspace_bytes(int64_t n);
+int hrl_clip_grad_norm_ws(float *grads, int64_t n, double max_norm, float *total_norm, void *workspace,
+                          int64_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

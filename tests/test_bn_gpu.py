@@ -467,8 +467,8 @@ def test_block_backward_weight_gradient_exact_on_integer_data(cuda, M, pro, form
 @pytest.mark.parametrize('pro', [False, True])
 def test_tile_shared_forward_matches_per_wave_conv(cuda, M, pro):
     """The chain's forward conv with BN statistics (hrl_conv3x3_forward_ex, epilogue 1) in the tile-shared form
-    (the block backward kernel with x' staged in place of dY) and the LDS-DMA ring form (2, conv3x3_fwd_dma_kernel)
-    vs the per-wave conv3x3_kernel: the output is bit-identical (the same split MFMA order on the same x'), the
+    (the block backward kernel with x' staged in place of dY) and the LDS-DMA ring form (2, conv3x3_fwd_dma_kernel;
+    3 the same with waves 4-7 computing before they stage) vs the per-wave conv3x3_kernel: the output is bit-identical (the same split MFMA order on the same x'), the
     per-channel sums sum(y) and sum(y^2) agree
     with the fp64 sums to fp32 rounding of a different per-tile grouping.  Ragged M = 37 (rows past the batch
     contribute nothing) and M = 20000 (several tiles per workgroup); with and without the BN + ReLU prologue."""
@@ -487,7 +487,7 @@ def test_tile_shared_forward_matches_per_wave_conv(cuda, M, pro):
     nblk = lib.hrl_conv3x3_stats_blocks(M)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
     outs = []
-    for form in (0, 1, 2):
+    for form in (0, 1, 2, 3):
         prev = lib.hrl_conv3x3_set_fwd_form(form)
         y, part = torch.empty_like(x), torch.full((nblk * 64,), float('nan'), dtype=torch.float64, device=cuda)
         try:
@@ -497,13 +497,14 @@ def test_tile_shared_forward_matches_per_wave_conv(cuda, M, pro):
         finally:
             lib.hrl_conv3x3_set_fwd_form(prev)
         outs.append((y, part))
-    (y0, p0), (y1, p1), (y2, p2) = outs
+    (y0, p0), (y1, p1), (y2, p2), (y3, p3) = outs
     assert torch.equal(y1, y0)
     assert torch.equal(y2, y0)
+    assert torch.equal(y3, y0)   # the staggered ring (waves 4-7 compute before staging): the same arithmetic
     yd = y0.double().view(M, 32, 9)
     ref = torch.stack([yd.sum((0, 2)), (yd * yd).sum((0, 2))], 1)
     scale = torch.stack([yd.abs().sum((0, 2)), (yd * yd).sum((0, 2))], 1)
-    for p in (p0, p1, p2):
+    for p in (p0, p1, p2, p3):
         s = p.view(nblk, 32, 2).sum(0)
         assert bool(torch.isfinite(s).all())
         assert float(((s - ref).abs() / scale).max()) < 1e-6
