@@ -254,11 +254,14 @@ __global__ __launch_bounds__(kThreads, 4) void stem_wgrad2_kernel(const float *_
     float acc[CIN * 9], accb = 0.f;
 #pragma unroll
     for (int i = 0; i < CIN * 9; ++i) acc[i] = 0.f;
+    // the buffer descriptor over dy (rows past N read 0).  readfirstlane returns an int: each half goes through a
+    // uint32_t first, or a low half with bit 31 set would sign-extend over the high half of the base address
     const uint64_t pd = reinterpret_cast<uint64_t>(dy);
+    const uint32_t pd_lo = __builtin_amdgcn_readfirstlane((uint32_t)pd);
+    const uint32_t pd_hi = __builtin_amdgcn_readfirstlane((uint32_t)(pd >> 32));
+    const uint32_t nrec = __builtin_amdgcn_readfirstlane((uint32_t)(N * kCols * 4));
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void *>(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pd >> 32)) << 32) |
-                                 __builtin_amdgcn_readfirstlane((uint32_t)pd)),
-        (short)0, (int)__builtin_amdgcn_readfirstlane((uint32_t)(N * kCols * 4)), 0x00020000);
+        reinterpret_cast<void *>(((uint64_t)pd_hi << 32) | pd_lo), (short)0, (int)nrec, 0x00020000);
     float *xw = xs[wave];
     const int64_t nblocks = (N + kBR - 1) / kBR;
     const int64_t wstep = (int64_t)gridDim.x * kWaves;

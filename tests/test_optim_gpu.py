@@ -129,8 +129,8 @@ def test_step_tail_matches_torch_clip_and_adam(cuda, graph):
         with torch.cuda.graph(tg):
             gr = tail(None)
     for k in range(4):
-        for p, t in zip(ref, grads[k]):
-            p.grad = t.to(cuda).clone() if live[ref.index(p)] else None
+        for i, (p, t) in enumerate(zip(ref, grads[k])):
+            p.grad = t.to(cuda).clone() if live[i] else None
         for group in opt.param_groups:
             group['lr'] = lrs[k]
         tr = float(nn.utils.clip_grad_norm_([p for p in ref if p.grad is not None], 4.0))
