@@ -125,6 +125,7 @@ SIGNATURES = {
     'hrl_stem_wgrad': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _f32p, _f32p, ctypes.c_void_p, _i64,
                                       ctypes.c_void_p]),
     'hrl_stem_set_wgrad_form': (ctypes.c_int, [ctypes.c_int]),
+    'hrl_stem_set_fwd_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_clip_grad_norm': (ctypes.c_int, [_f32p, _i64, _dbl, _f32p, ctypes.c_void_p]),
     'hrl_clip_workspace_bytes': (ctypes.c_int64, [_i64]),
     'hrl_grad_fold_norm_blocks': (ctypes.c_int64, [_i64]),
@@ -134,7 +135,7 @@ SIGNATURES = {
                                           ctypes.c_void_p]),
     'hrl_adam_clip': (ctypes.c_int, [_f32p, _i64, ctypes.c_void_p, _dbl, _f32p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _dbl, _dbl, _dbl,
-                                     _dbl, ctypes.c_void_p]),
+                                     _dbl, ctypes.c_void_p, ctypes.c_int, _f32p, ctypes.c_void_p]),
     'hrl_conv3x3_wgrad_partials': (ctypes.c_int64, [_i64, ctypes.c_void_p]),
     'hrl_stem_wgrad_partials': (ctypes.c_int64, [_i64, ctypes.c_void_p]),
     'hrl_clip_grad_norm_ws': (ctypes.c_int, [_f32p, _i64, _dbl, _f32p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
@@ -212,7 +213,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _lib = None
 

@@ -770,6 +770,7 @@ int hrl_gboard_forward_groups(const float *const *xs, const int64_t *x_strides, 
     a.wpk = static_cast<const uint4 *>(packed);
     a.nct = (int)((Cout + 15) / 16); a.cout = (int)Cout;
     a.y = y; a.ys = y_stride;
+    ++g_gboard_stats[kStFwdGroups];
     return gboard_launch(a, Cin_g, groups, static_cast<hipStream_t>(stream));
 }
 

@@ -706,7 +706,7 @@ int64_t hrl_heads_bn_parts(int64_t N) { return N < 1 ? -1 : grid_bwd(N); }
 
 int hrl_heads_set_bwd_form(int form) {
     const int prev = g_heads_bwd_form;
-    g_heads_bwd_form = form == 1 ? 1 : 2;
+    if (form == 1 || form == 2) g_heads_bwd_form = form;   // any other value only queries
     return prev;
 }
 

@@ -13,9 +13,10 @@
 // the weight-gradient folds of the HIP Functions (per-workgroup partial rows -> the parameter gradients: the
 // chain blocks' conv3x3_wgrad_reduce, heads_reduce, stem_reduce), the clip, torch's capturable step-count
 // increment, the BatchNorm batch counters and torch's fused Adam -- two launches:
-//  * step_fold_norm_kernel: 64-element blocks of the flat buffer; a block's elements that a fold covers are the
-//    fixed-order fp64 sum of their partial column (4 waves over interleaved partial rows, combined in wave
-//    order), the rest are read; each block writes the fp64 sum of squares of its final values; block 0 also
+//  * step_fold_norm_kernel: 64-position blocks of the flat buffer; a position that a fold covers takes the
+//    fixed-order fp64 sum of the partial column at that position (16 waves over interleaved partial rows,
+//    combined in wave order) and stores it to its element (for a transposed fold, another position of the same fold), the
+//    rest are read; each block writes the fp64 sum of squares of its final values; block 0 also
 //    advances the step count and the batch counters;
 //  * adam_clip_kernel: every workgroup folds the block sums in one fixed order (so all agree on the norm bit for
 //    bit), forms clip_grad_norm_'s coefficient, scales its chunk of the gradient in place (p.grad is the clipped
@@ -160,19 +161,24 @@ struct StepCounters {
     int nctr;
 };
 
-// source column of element j of a fold: mode 0 identity; mode 1 a (Cout = 32, Cin = 32, 3, 3) conv weight from
-// the chain blocks' [tap][ci][co] partial layout (conv3x3_wgrad_reduce_kernel's transposition)
-__device__ __forceinline__ int64_t fold_col(int mode, int64_t j) {
+// destination element of a fold's source column j: mode 0 identity; mode 1 a (Cout = 32, Cin = 32, 3, 3) conv
+// weight from the chain blocks' [tap][ci][co] partial layout (conv3x3_wgrad_reduce_kernel's transposition).  A
+// lane takes the source column at its own position, so a wave's 64 loads of a partial row are one contiguous
+// 256-byte run; the transposition moves to the (once per element) store
+__device__ __forceinline__ int64_t fold_dst(int mode, int64_t j) {
     if (mode == 1) {
-        const int co = (int)(j / 288), ci = (int)((j / 9) % 32), tap = (int)(j % 9);
-        return (tap * 32 + ci) * 32 + co;
+        const int tap = (int)(j >> 10), ci = (int)((j >> 5) & 31), co = (int)(j & 31);
+        return co * 288 + ci * 9 + tap;
     }
     return j;
 }
 
-__global__ __launch_bounds__(256) void step_fold_norm_kernel(float *__restrict__ g, int64_t n, FoldTable ft,
-                                                             StepCounters sc, double *__restrict__ norm_part) {
-    __shared__ double red[4][kBlk];
+constexpr int kFoldWaves = 16;   // waves per fold block: 16 x 8 row loads of 256 B in flight per workgroup
+
+__global__ __launch_bounds__(64 * kFoldWaves) void step_fold_norm_kernel(float *__restrict__ g, int64_t n,
+                                                                        FoldTable ft, StepCounters sc,
+                                                                        double *__restrict__ norm_part) {
+    __shared__ double red[kFoldWaves][kBlk];
     __shared__ double sq[kBlk];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t i = (int64_t)blockIdx.x * kBlk + lane;
@@ -182,22 +188,22 @@ __global__ __launch_bounds__(256) void step_fold_norm_kernel(float *__restrict__
             if (i >= ft.dst[k] && i < ft.dst[k] + ft.count[k]) f = k;
     double s = 0.0;
     if (f >= 0) {
-        const float *src = ft.part[f] + ft.col0[f] + fold_col(ft.mode[f], i - ft.dst[f]);
+        const float *src = ft.part[f] + ft.col0[f] + (i - ft.dst[f]);
         const int64_t np = ft.nparts[f], st = ft.stride[f];
-        // wave w takes rows w, w+4, w+8, ...: eight independent chains (rows w + 4k + 32r, k < 8) with all eight
-        // loads of a round issued before their adds, combined in chain order -- a fixed order
+        // wave w takes rows w, w+16, w+32, ...: eight independent chains (rows w + 16k + 128r, k < 8) with all
+        // eight loads of a round issued before their adds, combined in chain order -- a fixed order
         double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         int64_t b = w;
-        for (; b + 28 < np; b += 32) {
+        for (; b + 7 * kFoldWaves < np; b += 8 * kFoldWaves) {
             float t[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) t[k] = src[(b + 4 * k) * st];
+            for (int k = 0; k < 8; ++k) t[k] = src[(b + kFoldWaves * k) * st];
 #pragma unroll
             for (int k = 0; k < 8; ++k) acc[k] += (double)t[k];
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-            if (b + 4 * k < np) acc[k] += (double)src[(b + 4 * k) * st];
+            if (b + kFoldWaves * k < np) acc[k] += (double)src[(b + kFoldWaves * k) * st];
         s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     }
     red[w][lane] = s;
@@ -205,9 +211,10 @@ __global__ __launch_bounds__(256) void step_fold_norm_kernel(float *__restrict__
     if (w == 0) {
         double v;
         if (f >= 0) {
-            v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+            v = 0.0;
+            for (int k = 0; k < kFoldWaves; ++k) v += red[k][lane];   // wave order
             const float fv = (float)v;
-            g[i] = fv;
+            g[ft.dst[f] + fold_dst(ft.mode[f], i - ft.dst[f])] = fv;
             v = (double)fv;
         } else {
             v = i < n ? (double)g[i] : 0.0;
@@ -242,6 +249,10 @@ struct AdamArgs {
     float *total_out;
     const float *lr, *step;
     double beta1, beta2, eps, wd;
+    // the learner's running statistics: acc_dst[k] += *acc_src[k] (NULL: the norm), once per step
+    const float *acc_src[kMaxCounters];
+    float *acc_dst;
+    int nacc;
 };
 
 __global__ __launch_bounds__(256) void adam_clip_kernel(AdamArgs a, AdamTable tab) {
@@ -258,7 +269,10 @@ __global__ __launch_bounds__(256) void adam_clip_kernel(AdamArgs a, AdamTable ta
     }
     if (t == 0) {
         const float total = (float)sqrt(red[0]);
-        if (blockIdx.x == 0) a.total_out[0] = total;
+        if (blockIdx.x == 0) {
+            a.total_out[0] = total;
+            for (int k = 0; k < a.nacc; ++k) a.acc_dst[k] += a.acc_src[k] ? a.acc_src[k][0] : total;
+        }
         const float c = a.max_norm / (total + 1e-6f);
         coef_s = (c < 1.0f || c != c) ? c : 1.0f;      // clip_kernel's clamp (NaN propagates)
     }
@@ -273,6 +287,7 @@ __global__ __launch_bounds__(256) void adam_clip_kernel(AdamArgs a, AdamTable ta
     const int64_t per = (a.n + gridDim.x - 1) / gridDim.x;
     const int64_t lo = (int64_t)blockIdx.x * per, hi = min(a.n, lo + per);
     int tt = 0;
+    while (tt + 1 < tab.nt && lo >= tab.off[tt + 1]) ++tt;     // the chunk's first tensor (uniform)
     for (int64_t i = lo + t; i < hi; i += 256) {
         float gr = a.g[i] * c;
         a.g[i] = gr;
@@ -330,7 +345,7 @@ int hrl_grad_fold_norm(float *grads, int64_t n, const float *const *parts, const
         sc.ctr[k] = counters[k];
     }
     sc.nctr = ncounters;
-    hipLaunchKernelGGL(step_fold_norm_kernel, dim3((unsigned)hrl_grad_fold_norm_blocks(n)), dim3(256), 0,
+    hipLaunchKernelGGL(step_fold_norm_kernel, dim3((unsigned)hrl_grad_fold_norm_blocks(n)), dim3(64 * kFoldWaves), 0,
                        static_cast<hipStream_t>(stream), grads, n, ft, sc, norm_part);
     return status();
 }
@@ -338,9 +353,10 @@ int hrl_grad_fold_norm(float *grads, int64_t n, const float *const *parts, const
 int hrl_adam_clip(float *grads, int64_t n, const double *norm_part, double max_norm, float *total_norm,
                   float *const *params, const int64_t *offsets, const int *live, int ntensors, float *exp_avg,
                   float *exp_avg_sq, const float *lr, const float *step, double beta1, double beta2, double eps,
-                  double weight_decay, void *stream) {
+                  double weight_decay, const float *const *acc_src, int nacc, float *acc_dst, void *stream) {
     if (!grads || n < 1 || !norm_part || !total_norm || !params || !offsets || !live || ntensors < 1 ||
-        ntensors > kMaxTensors || !exp_avg || !exp_avg_sq || !lr || !step)
+        ntensors > kMaxTensors || !exp_avg || !exp_avg_sq || !lr || !step || nacc < 0 || nacc > kMaxCounters ||
+        (nacc > 0 && (!acc_src || !acc_dst)))
         return HRL_EINVAL;
     AdamTable tab{};
     for (int k = 0; k < ntensors; ++k) {
@@ -353,8 +369,10 @@ int hrl_adam_clip(float *grads, int64_t n, const double *norm_part, double max_n
     tab.off[ntensors] = n;
     tab.nt = ntensors;
     AdamArgs a{grads, exp_avg, exp_avg_sq, n, norm_part, hrl_grad_fold_norm_blocks(n), (float)max_norm, total_norm,
-               lr, step, beta1, beta2, eps, weight_decay};
-    const int64_t grid = (n + 2047) / 2048 < 64 ? (n + 2047) / 2048 : 64;
+               lr, step, beta1, beta2, eps, weight_decay, {}, acc_dst, nacc};
+    for (int k = 0; k < nacc; ++k) a.acc_src[k] = acc_src[k];
+    // one element per thread up to 256 workgroups (each folds the block sums itself: a few KB from L2)
+    const int64_t grid = (n + 255) / 256 < 256 ? (n + 255) / 256 : 256;
     hipLaunchKernelGGL(adam_clip_kernel, dim3((unsigned)grid), dim3(256), 0, static_cast<hipStream_t>(stream), a,
                        tab);
     return status();

@@ -122,6 +122,80 @@ __global__ __launch_bounds__(kThreads) void stem_fwd_kernel(const float *__restr
     }
 }
 
+// a buffer descriptor over [base, base + bytes) (loads past it read 0, stores past it are dropped).
+// readfirstlane returns an int: each half of the address goes through a uint32_t, or a low half with bit 31 set
+// would sign-extend over the high half
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base, int64_t bytes) {
+    const uint64_t p = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, (int)n,
+                                             0x00020000);
+}
+
+typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// ------------------------------------------------------------------ forward, lane per channel (form 2)
+// stem_fwd2_kernel<CIN>: lane (h, co) of a wave computes output channel co of rows 4t + 2h and 4t + 2h + 1 of its
+// 4-row quad t as one float2 (v_pk_fma_f32 on the two rows), with its Cin*9 weights and bias in registers:
+//   y[n][co][q] = b[co] + sum_ci sum_{p: tap(p, q) on the board} w[co][ci][tap(p, q)] * x[n][ci][p]
+// (fused multiply-adds, ci then p ascending).  The observation rows are read as 12-byte runs (one address across the
+// 32 lanes of a row); a lane's 9 outputs of a row are 36 contiguous bytes, the row's 32 lanes its 1152.  Bound: the
+// output write (151 MB at N = 131,072); ~110 VGPRs, 4 waves per SIMD.
+template <int CIN>
+__global__ __launch_bounds__(kThreads) void stem_fwd2_kernel(const float *__restrict__ x, int64_t N,
+                                                             const float *__restrict__ w,
+                                                             const float *__restrict__ b, float *__restrict__ y) {
+    constexpr int kXF = CIN * kCells;
+    const int lane = threadIdx.x & 63, co = lane & 31, h = lane >> 5;
+    float wr[kXF];
+#pragma unroll
+    for (int k = 0; k < kXF; ++k) wr[k] = w[co * kXF + k];
+    const float bias = b ? b[co] : 0.f;
+    const int64_t nquads = (N + 3) / 4;
+    const int64_t wstep = (int64_t)gridDim.x * kWaves;
+    for (int64_t t = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); t < nquads; t += wstep) {
+        const int64_t rows = min<int64_t>(4, N - 4 * t);
+        const __amdgpu_buffer_rsrc_t rx = rsrc_of(x + 4 * t * kXF, rows * kXF * 4);
+        const __amdgpu_buffer_rsrc_t ry = rsrc_of(y + 4 * t * kCols, rows * kCols * 4);
+        f32x2 xv[kXF];
+#pragma unroll
+        for (int j = 0; j < kXF / 3; ++j) {
+            const u32x3 a = __builtin_amdgcn_raw_buffer_load_b96(rx, ((2 * h) * kXF + 3 * j) * 4, 0, 0);
+            const u32x3 c = __builtin_amdgcn_raw_buffer_load_b96(rx, ((2 * h + 1) * kXF + 3 * j) * 4, 0, 0);
+            xv[3 * j] = (f32x2){__uint_as_float(a.x), __uint_as_float(c.x)};
+            xv[3 * j + 1] = (f32x2){__uint_as_float(a.y), __uint_as_float(c.y)};
+            xv[3 * j + 2] = (f32x2){__uint_as_float(a.z), __uint_as_float(c.z)};
+        }
+        f32x2 acc[kCells];
+#pragma unroll
+        for (int q = 0; q < kCells; ++q) {
+            acc[q] = (f32x2){bias, bias};
+#pragma unroll
+            for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+                for (int p = 0; p < kCells; ++p) {
+                    const int tap = tap_of(p, q);
+                    if (tap < 0) continue;
+                    const float wv = wr[ci * kCells + tap];
+                    acc[q] = __builtin_elementwise_fma((f32x2){wv, wv}, xv[ci * kCells + p], acc[q]);
+                }
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                u32x3 v;
+                v.x = __float_as_uint(acc[3 * m][r]);
+                v.y = __float_as_uint(acc[3 * m + 1][r]);
+                v.z = __float_as_uint(acc[3 * m + 2][r]);
+                __builtin_amdgcn_raw_buffer_store_b96(v, ry, ((2 * h + r) * kCols + co * kCells + 3 * m) * 4, 0, 0);
+            }
+    }
+}
+
 // ------------------------------------------------------------------ weight gradient
 constexpr int kDyStride = kCols + 4;   // LDS row stride of a staged dy tile (16 B aligned rows)
 constexpr int kNOut = kCo * 3 * 9 + kCo;   // folded outputs per partial (Cin <= 3): dW then db
@@ -254,18 +328,10 @@ __global__ __launch_bounds__(kThreads, 4) void stem_wgrad2_kernel(const float *_
     float acc[CIN * 9], accb = 0.f;
 #pragma unroll
     for (int i = 0; i < CIN * 9; ++i) acc[i] = 0.f;
-    // the buffer descriptor over dy (rows past N read 0).  readfirstlane returns an int: each half goes through a
-    // uint32_t first, or a low half with bit 31 set would sign-extend over the high half of the base address
-    const uint64_t pd = reinterpret_cast<uint64_t>(dy);
-    const uint32_t pd_lo = __builtin_amdgcn_readfirstlane((uint32_t)pd);
-    const uint32_t pd_hi = __builtin_amdgcn_readfirstlane((uint32_t)(pd >> 32));
-    const uint32_t nrec = __builtin_amdgcn_readfirstlane((uint32_t)(N * kCols * 4));
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void *>(((uint64_t)pd_hi << 32) | pd_lo), (short)0, (int)nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd = rsrc_of(dy, N * kCols * 4);   // rows past N read 0
     float *xw = xs[wave];
     const int64_t nblocks = (N + kBR - 1) / kBR;
     const int64_t wstep = (int64_t)gridDim.x * kWaves;
-    typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
     auto load_dy = [&](int64_t row, float (&d)[kCells]) __attribute__((always_inline)) {
         const uint32_t off = (uint32_t)((row * kCols + co * kCells) * 4);
 #pragma unroll
@@ -344,6 +410,7 @@ __global__ __launch_bounds__(kThreads, 4) void stem_wgrad2_kernel(const float *_
 }
 
 int g_stem_wgrad_form = 2;   // hrl_stem_set_wgrad_form
+int g_stem_fwd_form = 2;     // hrl_stem_set_fwd_form: 2 = stem_fwd2_kernel, 1 = the fp32 MFMA form
 
 // fixed-order fold of the workgroup partials: one workgroup per output, strided fp64 sums, LDS tree
 __global__ __launch_bounds__(256) void stem_reduce_kernel(const float *__restrict__ partial, int nparts, int nw,
@@ -377,6 +444,7 @@ int grid_for(int64_t N, int cap) {
 }
 
 constexpr int kGrid2 = 1024;   // stem_wgrad2_kernel: 4 workgroups per CU
+constexpr int kGridF2 = 4096;  // stem_fwd2_kernel: 16 workgroups of 4 waves per CU, grid-strided over 4-row quads
 
 // workgroups of the weight gradient's form: form 2 runs 4-wave workgroups over 32-row blocks
 int grid_wgrad(int64_t N) {
@@ -404,15 +472,33 @@ int64_t hrl_stem_wgrad_partials(int64_t N, int64_t *row_floats) {
 
 int hrl_stem_set_wgrad_form(int form) {
     const int prev = g_stem_wgrad_form;
-    g_stem_wgrad_form = form == 1 ? 1 : 2;
+    if (form == 1 || form == 2) g_stem_wgrad_form = form;   // any other value only queries
+    return prev;
+}
+
+int hrl_stem_set_fwd_form(int form) {
+    const int prev = g_stem_fwd_form;
+    if (form == 1 || form == 2) g_stem_fwd_form = form;   // any other value only queries
     return prev;
 }
 
 int hrl_stem_forward(const float *x, int64_t N, int64_t Cin, const float *weight, const float *bias, float *y,
                      void *stream) {
     if (N < 1 || Cin < 1 || Cin > 3 || !x || !weight || !y) return HRL_EINVAL;
-    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid_for(N, 2 * kGrid)), dim3(kThreads), 0,
-                       static_cast<hipStream_t>(stream), x, N, (int)Cin, weight, bias, y);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (g_stem_fwd_form == 2) {
+        const int64_t wgs = ((N + 3) / 4 + kWaves - 1) / kWaves;
+        const dim3 grid((unsigned)(wgs < kGridF2 ? wgs : kGridF2));
+        if (Cin == 3)
+            hipLaunchKernelGGL(stem_fwd2_kernel<3>, grid, dim3(kThreads), 0, s, x, N, weight, bias, y);
+        else if (Cin == 2)
+            hipLaunchKernelGGL(stem_fwd2_kernel<2>, grid, dim3(kThreads), 0, s, x, N, weight, bias, y);
+        else
+            hipLaunchKernelGGL(stem_fwd2_kernel<1>, grid, dim3(kThreads), 0, s, x, N, weight, bias, y);
+        return status();
+    }
+    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid_for(N, 2 * kGrid)), dim3(kThreads), 0, s, x, N, (int)Cin, weight,
+                       bias, y);
     return status();
 }
 

@@ -1336,7 +1336,7 @@ class _BoardHeadsFn(torch.autograd.Function):
             _native.check(lib.hrl_heads_backward(P(h), N, P(w1p), P(w1v), P(wp), P(wv), None, None, None, None,
                                                  P(a_p), P(a_v), P(dp), P(dv), None, P(dh), *(P(t) for t in dws),
                                                  P(ws), ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward')
-        df = _defer_folds(bufs)
+        df = _defer_folds(bufs) if lib.hrl_heads_set_bwd_form(0) == 2 else None   # deferral needs form 2
         if df is not None:
             _heads_backward_deferred(lib, df, bufs, N, ws, call)
         else:
@@ -1428,7 +1428,7 @@ class _StemConv(torch.autograd.Function):
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
         bw = _grad_buffer(weight)
         bb = _grad_buffer(bias) if bias is not None else (None, False)
-        df = _defer_folds([bw, bb])
+        df = _defer_folds([bw, bb]) if lib.hrl_stem_set_wgrad_form(0) == 2 else None   # deferral needs form 2
         dwp, dbp = (None, None) if df is not None else (bw[0], bb[0])
         _native.check(lib.hrl_stem_wgrad(_native.ptr(x), _native.ptr(dy.contiguous()), N, Cin, _native.ptr(dwp),
                                          _native.ptr(dbp), _native.ptr(ws), ws_bytes,
@@ -1995,7 +1995,7 @@ class _ChainHeadsFn(torch.autograd.Function):
                                                  P(coef[0]), P(bn_part), P(a_p), P(a_v), P(dp), P(dv),
                                                  P(v) if ctx.tanh_v else None, P(dh), *(P(t) for t in dws),
                                                  P(ws), ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward(bn)')
-        df = _defer_folds(hbufs)
+        df = _defer_folds(hbufs) if lib.hrl_heads_set_bwd_form(0) == 2 else None
         if df is not None:
             _heads_backward_deferred(lib, df, hbufs, N, ws, call)
         else:

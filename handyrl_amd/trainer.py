@@ -79,8 +79,10 @@ class StepTail:
     def state_tensors(self):
         return [self.m, self.v, self.step_t]
 
-    def __call__(self, folds=None):
-        """Fold, clip and update; folds: a finished nn.deferred_folds (or None).  Returns the norm (device)."""
+    def __call__(self, folds=None, acc=None):
+        """Fold, clip and update; folds: a finished nn.deferred_folds (or None); acc: (sources, dst) -- dst[k] +=
+        sources[k] (0-dim float32 device tensors, self.total for the norm) in the same launch.  Returns the norm
+        (device)."""
         from . import _native
         lib, P = self.lib, _native.ptr
         flat = self.grads.flat
@@ -104,10 +106,13 @@ class StepTail:
             (ctypes.c_int * max(len(fl), 1))(*[f[6] for f in fl]), len(fl), P(self.step_t),
             _native.ptr_array(counters), len(counters), P(self.norm_part), self.norm_part.numel() * 8, stream),
             'hrl_grad_fold_norm')
+        srcs, acc_dst = acc if acc is not None else ([], None)
+        acc_src = (ctypes.c_void_p * max(len(srcs), 1))(*[None if t is self.total else t.data_ptr() for t in srcs])
         _native.check(lib.hrl_adam_clip(
             P(flat), self.n, P(self.norm_part), float(self.max_norm), P(self.total), self.ptrs, self.offsets,
             self.live, len(self.live), P(self.m), P(self.v), P(self.lr_t), P(self.step_t), float(self.betas[0]),
-            float(self.betas[1]), float(self.eps), float(self.wd), stream), 'hrl_adam_clip')
+            float(self.betas[1]), float(self.eps), float(self.wd), acc_src, len(srcs), P(acc_dst), stream),
+            'hrl_adam_clip')
         return self.total
 
 
@@ -159,6 +164,7 @@ class LearnerStep:
         self._static = None
         self._static_out = None
         self.stats = None
+        self._tail_stats = False
 
     # -- learning rate (train.py:396-398) ---------------------------------
     def set_lr(self, lr):
@@ -249,16 +255,31 @@ class LearnerStep:
 
     def _update(self, losses, dcnt):
         """clip_grad_norm_(4.0) on the (all-reduced) gradients, then Adam (train.py:384-385)."""
-        if self.tail is not None:
-            folds, self._folds = self._folds, None
-            gnorm = self.tail(folds)
-        else:
-            gnorm = self.grads.clip_(4.0)
-            self.optimizer.step()
         out = {k: v.detach() for k, v in losses.items()}
         out['dcnt'] = dcnt
-        out['grad_norm'] = gnorm
+        if self.tail is not None:
+            folds, self._folds = self._folds, None
+            out['grad_norm'] = self.tail.total
+            self._tail_stats = self._tail_accumulable(out)
+            acc = None
+            if self._tail_stats:
+                # the running statistics are summed by the tail's second launch (no stack + add per step)
+                if self.stats is None:
+                    self.stats_keys = sorted(out)
+                    self.stats = torch.zeros(len(out), dtype=torch.float32, device=self.device)
+                    self.batches = 0
+                acc = ([out[k] for k in self.stats_keys], self.stats)
+            self.tail(folds, acc)
+        else:
+            out['grad_norm'] = self.grads.clip_(4.0)
+            self.optimizer.step()
         return out
+
+    def _tail_accumulable(self, out):
+        keys = sorted(out)
+        return (len(keys) <= 8 and (self.stats is None or self.stats_keys == keys) and
+                all(isinstance(v, torch.Tensor) and v.numel() == 1 and v.dtype == torch.float32 and v.is_cuda
+                    for v in out.values()))
 
     def snapshot(self):
         """A copy of the training state (parameters, buffers, Adam's state tensors) that restore() puts back in
@@ -280,7 +301,8 @@ class LearnerStep:
 
     def _opt_state(self):
         if self.tail is not None:
-            return self.tail.state_tensors()
+            # with the running statistics, which the tail accumulates (zeroed after a capture's warm-up too)
+            return self.tail.state_tensors() + ([self.stats] if self._tail_stats else [])
         return [v for st in self.optimizer.state.values() for v in st.values() if isinstance(v, torch.Tensor)]
 
     def _body(self, batch, hidden):
@@ -290,6 +312,9 @@ class LearnerStep:
         return self._update(losses, dcnt)
 
     def _accumulate(self, out):
+        if self._tail_stats:          # summed on the device by the step tail
+            self.batches += 1
+            return
         vec = torch.stack([out[k].reshape(()) for k in sorted(out)])
         if self.stats is None:
             self.stats_keys = sorted(out)
@@ -496,7 +521,7 @@ class LearnerStep:
 
     def pop_stats(self):
         """Sum of the per-step losses since the last call (one host sync), as a dict."""
-        if self.stats is None:
+        if self.stats is None or self.batches == 0:
             return {}, 0
         vals = self.stats
         if self.reducer is not None:
@@ -504,7 +529,11 @@ class LearnerStep:
         vals = vals.tolist()
         res = dict(zip(self.stats_keys, vals))
         n = self.batches
-        self.stats = None
+        if self._tail_stats:
+            self.stats.zero_()    # the tail (a captured graph) keeps accumulating into this tensor
+            self.batches = 0
+        else:
+            self.stats = None
         return res, n
 
 

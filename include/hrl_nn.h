@@ -441,7 +441,8 @@ int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *
  * the value row) | db1 (3) | dWp (9 x 18) | dWv (9)] -- for hrl_grad_fold_norm. */
 /* hrl_heads_set_bwd_form: 2 (default) = the lane-per-channel backward (4-wave workgroups, accumulators in registers,
  * the fc weight gradients in the same pass), 1 = the row-per-lane kernel + separate fc-gradient launch (measurement).
- * Process-wide; returns the previous setting.  hrl_heads_bn_parts / hrl_heads_workspace_bytes follow the form. */
+ * Process-wide; returns the previous setting (any other value only queries it).  hrl_heads_bn_parts /
+ * hrl_heads_workspace_bytes follow the form; the deferred (NULL-gradient) mode needs form 2. */
 int hrl_heads_set_bwd_form(int form);
 int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float *w1v, const float *wp,
                        const float *wv, const float *bn_alpha, const float *bn_beta, const float *bn_mean,
@@ -465,8 +466,13 @@ int hrl_stem_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, floa
 int64_t hrl_stem_wgrad_partials(int64_t N, int64_t *row_floats);
 /* hrl_stem_set_wgrad_form: 2 (default) = the lane-per-channel weight gradient (a lane owns one output channel's
  * Cin x 9 weights and its bias of a row; 4-wave workgroups, 4 per CU), 1 = the dense-board fp32 MFMA kernel
- * (measurement).  Process-wide; returns the previous setting.  hrl_stem_workspace_bytes covers both forms. */
+ * (measurement).  Process-wide; returns the previous setting (any other value only queries it).
+ * hrl_stem_workspace_bytes covers both forms; the deferred (NULL-gradient) mode needs form 2. */
 int hrl_stem_set_wgrad_form(int form);
+/* hrl_stem_set_fwd_form: 2 (default) = the lane-per-channel forward (a lane owns one output channel of two rows as a
+ * float2: packed fp32 FMAs, weights in registers, 36-byte output runs), 1 = the fp32 MFMA kernel on the dense board
+ * matrix (measurement).  Process-wide; returns the previous setting (any other value only queries it). */
+int hrl_stem_set_fwd_form(int form);
 
 /* The learner step's tail on the flat gradient buffer `grads` (n floats; parameter gradients are views of it):
  * hrl_grad_fold_norm: for each of nfolds (<= 16) deferred weight-gradient folds, grads[dst + j] (j < count) =
@@ -478,7 +484,9 @@ int hrl_stem_set_wgrad_form(int form);
  *   *total_norm = the norm; grads scaled in place) and torch.optim.Adam's step (fused_adam_utils.cuh adam_math,
  *   L2 weight decay, the same double / float promotions) on the tensors params[t] (elements offsets[t] ..
  *   offsets[t+1] of grads, offsets[ntensors] = n, ntensors <= 64) whose live[t] != 0; exp_avg / exp_avg_sq are n
- *   floats each; lr and step are device scalars (a graph replays with their current values).
+ *   floats each; lr and step are device scalars (a graph replays with their current values).  Once per call
+ *   acc_dst[k] += *acc_src[k] for k < nacc (<= 8; acc_src[k] NULL: the norm) -- the learner's running loss
+ *   statistics, so their accumulation is no launch of its own.
  * Deterministic.  Replaces the reduce launches of the HIP backward Functions, the clip, torch's step-count and
  * batch-counter increments and torch's fused Adam (train.py:384-385). */
 int64_t hrl_grad_fold_norm_blocks(int64_t n);
@@ -489,7 +497,7 @@ int hrl_grad_fold_norm(float *grads, int64_t n, const float *const *parts, const
 int hrl_adam_clip(float *grads, int64_t n, const double *norm_part, double max_norm, float *total_norm,
                   float *const *params, const int64_t *offsets, const int *live, int ntensors, float *exp_avg,
                   float *exp_avg_sq, const float *lr, const float *step, double beta1, double beta2, double eps,
-                  double weight_decay, void *stream);
+                  double weight_decay, const float *const *acc_src, int nacc, float *acc_dst, void *stream);
 
 /* clip_grad_norm_(params, max_norm) on the learner's flat gradient buffer (handyrl/train.py:384)
  * in one launch: total = ||grads||_2 (fp64 fold) -> *total_norm; grads *= min(max_norm / (total + 1e-6), 1).

@@ -330,19 +330,30 @@ def test_fused_heads_match_torch_cpu(cuda, N):
     assert torch.equal(p2, p.detach()) and torch.equal(v2, v.detach())
 
 
-@pytest.mark.parametrize('N,cin,bias', [(1, 3, True), (17, 3, True), (4099, 3, True), (50, 2, False), (33, 1, True)])
-def test_stem_conv_matches_torch_cpu(cuda, N, cin, bias):
-    """csrc/hrl_stem.hip (the observation stem, tictactoe.py:57): forward and the weight / bias gradients
-    vs torch-CPU conv2d on ragged sample counts (the input is the observation: no input gradient)."""
+@pytest.mark.parametrize('fwd_form', [2, 1])
+@pytest.mark.parametrize('N,cin,bias,binary', [(1, 3, True, True), (17, 3, True, True), (4099, 3, True, True),
+                                               (50, 2, False, True), (33, 1, True, True), (4102, 3, True, False),
+                                               (7, 2, True, False)])
+def test_stem_conv_matches_torch_cpu(cuda, N, cin, bias, binary, fwd_form):
+    """csrc/hrl_stem.hip (the observation stem, tictactoe.py:57): forward (both forms: 2 = lane per channel,
+    1 = fp32 MFMA) and the weight / bias gradients vs torch-CPU conv2d on ragged sample counts (rows past a
+    4-row quad), 0/1 observations and real-valued inputs (the input is the observation: no input gradient)."""
+    from handyrl_amd import _native
     from handyrl_amd.nn import BoardConv2d
     torch.manual_seed(N + cin)
     ref = nn.Conv2d(cin, 32, 3, padding=1, bias=bias)
     hip = BoardConv2d(cin, 32, 3, padding=1, bias=bias).to(cuda)
     hip.load_state_dict(ref.state_dict())
-    x = (torch.rand(N, cin, 3, 3) < 0.5).float()
+    x = (torch.rand(N, cin, 3, 3) < 0.5).float() if binary else torch.randn(N, cin, 3, 3)
     dy = torch.randn(N, 32, 3, 3)
     yr = ref(x)
-    yh = hip(x.to(cuda))
+    lib = _native.load()
+    prev = lib.hrl_stem_set_fwd_form(fwd_form)
+    try:
+        yh = hip(x.to(cuda))
+        torch.cuda.synchronize()
+    finally:
+        lib.hrl_stem_set_fwd_form(prev)
     np.testing.assert_allclose(yh.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-5, atol=1e-5)
     yr.backward(dy)
     yh.backward(dy.to(cuda))

@@ -96,6 +96,33 @@ def test_graph_step_equals_eager(cuda):
         np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-5, atol=5e-6, err_msg=k)
 
 
+@pytest.mark.parametrize('graph', [False, True])
+def test_running_stats_summed_by_step_tail(cuda, graph):
+    """pop_stats() after k steps = the host sum of the k steps' outputs; the tail's second launch does the adds
+    (no stack + add launches per step), the capture's warm-up steps are not counted, and pop_stats restarts the
+    sums."""
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.synthetic import tictactoe_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    B, T = 64, 9
+    args = default_args(T, B)
+    torch.manual_seed(1)
+    step = LearnerStep(SimpleConv2dModel(), args, cuda, graph=graph)
+    assert step.tail is not None
+    for rnd in range(2):
+        want = {}
+        for s in range(3):
+            out = step.step(tictactoe_batch(B, T, cuda, seed=10 * rnd + s))
+            for k, v in out.items():
+                want[k] = want.get(k, 0.0) + float(v)
+        assert step._tail_stats
+        got, n = step.pop_stats()
+        assert n == 3 and set(got) == set(want)
+        for k in want:
+            _close(got[k], want[k], rtol=1e-6, what=(rnd, k))
+    assert step.pop_stats() == ({}, 0)
+
+
 @pytest.mark.parametrize('B,T', [(4096, 32), (4096, 9)])
 def test_baseline_batch_losses_vs_oracle(cuda, B, T):
     from handyrl_amd.synthetic import tictactoe_batch, default_args
