@@ -30,8 +30,9 @@
 // kernels read that BN's raw input y and apply relu(y*alpha + beta) per slice,
 // and the backward also emits the BN's backward sums, so the body's output
 // never reaches HBM and its last BN needs no separate reduce pass.
-// Numerics: fp32 throughout (-ffp-contract=off); sums in a fixed order; the
-// LeakyReLU and its gradient follow torch (x > 0 ? x : x * 0.1f).
+// Numerics: fp32 throughout (-ffp-contract=off; the forward's conv and fc sums are explicit fused multiply-adds,
+// packed on cell pairs, and the fused BN apply keeps bn_apply_kernel's separate multiply and add); sums in a fixed
+// order; the LeakyReLU and its gradient follow torch (x > 0 ? x : x * 0.1f).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -57,6 +58,9 @@ constexpr int kSF = kSC * kHW;         // 36 floats per row slice
 constexpr int kSV = kSF / 4;           // 9 float4 per row slice
 constexpr int kTS = kSF + 1;           // LDS row stride (odd)
 constexpr float kSlope = 0.1f;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int hu32x3 __attribute__((ext_vector_type(3)));
+typedef unsigned int hu32x4 __attribute__((ext_vector_type(4)));
 
 // parameter-gradient partial layout (per workgroup): dW1 [3][32] | db1 [3] | dWp [9][18] | dWv [9]
 constexpr int kGW1 = 0;
@@ -103,6 +107,35 @@ __device__ __forceinline__ void load_slice(const float *__restrict__ h, int64_t 
     }
 }
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t heads_rsrc(const void *base, uint32_t bytes) {
+    const uint64_t p = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, (int)n,
+                                             0x00020000);
+}
+
+// load_slice through a buffer descriptor over the 64-row block (rows past N read 0): lane offsets vo[k] are
+// slice-invariant, the slice's 144-byte step is the scalar offset -- 9 VGPRs of addressing instead of 9 pointers
+__device__ __forceinline__ void slice_offsets(int lane, uint32_t (&vo)[kSV]) {
+#pragma unroll
+    for (int k = 0; k < kSV; ++k) {
+        const int i = k * 64 + lane;
+        const int r = i / kSV, c4 = i - r * kSV;
+        vo[k] = (uint32_t)((r * kRow + c4 * 4) * 4);
+    }
+}
+
+__device__ __forceinline__ void load_slice_buf(__amdgpu_buffer_rsrc_t rs, const uint32_t (&vo)[kSV], int s,
+                                               float4 (&st)[kSV]) {
+#pragma unroll
+    for (int k = 0; k < kSV; ++k) {
+        const hu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo[k], s * kSF * 4, 0);
+        st[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+    }
+}
+
 __device__ __forceinline__ void slice_to_lds(const float4 (&st)[kSV], float *tile, int lane) {
 #pragma unroll
     for (int k = 0; k < kSV; ++k) {
@@ -114,7 +147,7 @@ __device__ __forceinline__ void slice_to_lds(const float4 (&st)[kSV], float *til
 }
 
 // ------------------------------------------------------------------ forward
-__global__ __launch_bounds__(64) void heads_fwd_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
+__global__ __launch_bounds__(64, 2) void heads_fwd_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
                                                        float *__restrict__ a_p, float *__restrict__ a_v,
                                                        float *__restrict__ p_out, float *__restrict__ v_out,
                                                        bool tanh_v) {
@@ -130,54 +163,95 @@ __global__ __launch_bounds__(64) void heads_fwd_kernel(const float *__restrict__
     for (int i = lane; i < kOP * kZP; i += 64) swp[i] = w.wp[i];
     if (lane < kHW) swv[lane] = w.wv[lane];
     __syncthreads();
+    uint32_t vo[kSV];
+    slice_offsets(lane, vo);
 
     for (int64_t base = (int64_t)blockIdx.x * 64; base < N; base += (int64_t)gridDim.x * 64) {
+        // Wp / W1 / the BN constants are re-read from LDS per block: hoisted out of the loop they held ~170 VGPRs
+        // (2 waves per SIMD, one 2.3 KB slice in flight per wave)
+        asm volatile("" ::: "memory");
         const int nrows = (int)min<int64_t>(64, N - base);
-        float z[kZ];
+        // z[m][q] = b1[m] + sum_c W1[m][c] h[c][q] (fused multiply-adds, channels in order): cells 0..7 as 4 pairs
+        f32x2 zp[kM][4];
+        float z8[kM];
 #pragma unroll
-        for (int m = 0; m < kM; ++m)
+        for (int m = 0; m < kM; ++m) {
 #pragma unroll
-            for (int q = 0; q < kHW; ++q) z[m * kHW + q] = sb1[m];
-        float4 st[kSV];
-        load_slice(h, base, nrows, 0, lane, st);
-#pragma unroll 1
-        for (int s = 0; s < kNS; ++s) {
+            for (int k = 0; k < 4; ++k) zp[m][k] = (f32x2){sb1[m], sb1[m]};
+            z8[m] = sb1[m];
+        }
+        // two slices in flight: st0 holds the even slices, st1 the odd ones; slice s + 2 is issued into the
+        // registers slice s just left for LDS
+        float4 st0[kSV], st1[kSV];
+        const __amdgpu_buffer_rsrc_t rh = heads_rsrc(h + base * kRow, (uint32_t)(nrows * kRow * 4));
+        load_slice_buf(rh, vo, 0, st0);
+        load_slice_buf(rh, vo, 1, st1);
+        auto slice = [&](float4 (&st)[kSV], int s) __attribute__((always_inline)) {
             slice_to_lds(st, tile, lane);
             lds_fence();
-            if (s + 1 < kNS) load_slice(h, base, nrows, s + 1, lane, st);   // in flight during the FMAs
-            float x[kSF];
+            if (s + 2 < kNS) load_slice_buf(rh, vo, s + 2, st);   // in flight during the FMAs
 #pragma unroll
-            for (int j = 0; j < kSF; ++j) x[j] = tile[lane * kTS + j];
-            if (bn.alpha) {
+            for (int cc = 0; cc < kSC; ++cc) {
+                // channel c's 9 cells as 4 pairs + 1: packed fp32 (v_pk_mul / v_pk_add / v_pk_fma) on cell pairs;
+                // one channel's LDS reads at a time (hoisted, the slice's 36 + its weights crowd the registers)
+                asm volatile("" ::: "memory");
+                const int c = s * kSC + cc;
+                const float *tr = tile + lane * kTS + cc * kHW;
+                f32x2 xp[4];
 #pragma unroll
-                for (int j = 0; j < kSF; ++j) x[j] = bn_relu(x[j], sal[s * kSC + j / kHW], sbe[s * kSC + j / kHW]);
-            }
+                for (int k = 0; k < 4; ++k) xp[k] = (f32x2){tr[2 * k], tr[2 * k + 1]};
+                float x8 = tr[8];
+                if (bn.alpha) {   // bn_apply_kernel's float operations (a multiply, then an add), then the ReLU
+                    const float al = sal[c], be = sbe[c];
 #pragma unroll
-            for (int m = 0; m < kM; ++m)
-#pragma unroll
-                for (int cc = 0; cc < kSC; ++cc) {
-                    const float wv1 = sw1[m * kC + s * kSC + cc];
-#pragma unroll
-                    for (int q = 0; q < kHW; ++q) z[m * kHW + q] += wv1 * x[cc * kHW + q];
+                    for (int k = 0; k < 4; ++k) {
+                        const f32x2 t = xp[k] * (f32x2){al, al} + (f32x2){be, be};
+                        xp[k] = (f32x2){t.x < 0.f ? 0.f : t.x, t.y < 0.f ? 0.f : t.y};
+                    }
+                    x8 = bn_relu(x8, al, be);
                 }
+#pragma unroll
+                for (int m = 0; m < kM; ++m) {
+                    const float wv1 = sw1[m * kC + c];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        zp[m][k] = __builtin_elementwise_fma((f32x2){wv1, wv1}, xp[k], zp[m][k]);
+                    z8[m] = __builtin_fmaf(wv1, x8, z8[m]);
+                }
+            }
             lds_fence();   // every lane's reads done before the next slice overwrites the tile
+        };
+#pragma unroll 1
+        for (int s = 0; s < kNS; s += 2) {
+            slice(st0, s);
+            slice(st1, s + 1);
         }
         float a[kZ];
 #pragma unroll
-        for (int j = 0; j < kZ; ++j) a[j] = z[j] > 0.f ? z[j] : z[j] * kSlope;
+        for (int m = 0; m < kM; ++m) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                a[m * kHW + 2 * k] = zp[m][k].x;
+                a[m * kHW + 2 * k + 1] = zp[m][k].y;
+            }
+            a[m * kHW + 8] = z8[m];
+        }
+#pragma unroll
+        for (int j = 0; j < kZ; ++j) a[j] = a[j] > 0.f ? a[j] : a[j] * kSlope;
         if (lane < nrows) {
             const int64_t n = base + lane;
             float p[kOP];
 #pragma unroll
             for (int k = 0; k < kOP; ++k) {
+                asm volatile("" ::: "memory");   // one output's 18 weights in flight at a time, not all 162
                 float t = 0.f;
 #pragma unroll
-                for (int j = 0; j < kZP; ++j) t += swp[k * kZP + j] * a[j];
+                for (int j = 0; j < kZP; ++j) t = __builtin_fmaf(swp[k * kZP + j], a[j], t);
                 p[k] = t;
             }
             float v = 0.f;
 #pragma unroll
-            for (int q = 0; q < kHW; ++q) v += swv[q] * a[kZP + q];
+            for (int q = 0; q < kHW; ++q) v = __builtin_fmaf(swv[q], a[kZP + q], v);
 #pragma unroll
             for (int k = 0; k < kOP; ++k) p_out[n * kOP + k] = p[k];
             v_out[n] = tanh_v ? tanhf(v) : v;   // the model's torch.tanh on the value head, folded
@@ -350,16 +424,19 @@ __global__ __launch_bounds__(64) void heads_bwd_kernel(const float *__restrict__
 // ------------------------------------------------------------------ backward, lane-per-channel form
 // heads_bwd_kernel keeps a row per lane, so its 3 x 32 conv weight-gradient and 32 x 2 BN-sum accumulators live in
 // LDS (52 KB per one-wave workgroup: 3 waves per CU, <= 27 KB of loads in flight per CU; 107 us in the step, 3 TB/s).
-// Here a lane owns (row half r = lane >> 5, channel c = lane & 31): per row pair it reads its channel's 9 cells (36
-// contiguous bytes; the wave's 64 lanes cover two whole rows), so its weight-gradient and BN-sum accumulators are 5
-// registers, W1[:, c] and the BN constants of c are 6 more, and nothing but the row block's small inputs and dz go
-// through LDS (~8 KB per 4-wave workgroup): ~100 VGPRs, 4 waves per SIMD, several row pairs in flight per wave.
+// Here a lane owns (row half r = lane >> 5, channel c = lane & 31): per row pair it reads its channel's 9 cells, so
+// its weight-gradient and BN-sum accumulators are 5 registers, W1[:, c] and the BN constants of c are 6 more.  h
+// arrives in 8-row groups as contiguous float4s (9 per lane, one group ahead) through the wave's LDS tile, the lanes
+// read their cells there and write dh in their place, and the group leaves as contiguous float4 stores (36-byte
+// per-lane runs straight to and from HBM ran at half the rate); with the row block's small inputs and dz, 72 KB of
+// LDS per 4-wave workgroup, 2 per CU.
 //  * stage (lanes 0..31, one row each): dz[m][q] = leaky'(a) * (dp . Wp | dv' . Wv) and db1's per-row sums, dz and
 //    the row's dp / dv' / a_p / a_v into LDS;
 //  * fc weight gradients: lane l owns weights l, l + 64, l + 128 of [dWp (9 x 18) | dWv (9)] and adds the block's
 //    rows in order (the products of fc_grad_kernel, dv' = the tanh backward's output);
-//  * main loop over the block's row pairs: x (BN + ReLU applied when fused), dW1[m][c] += sum_q dz[m][q] x[q],
-//    dh[q] = sum_m W1[m][c] dz[m][q] (the old kernel's operation order per element), the BN sums, dh stored;
+//  * main loop over the block's groups and their row pairs: x (BN + ReLU applied when fused), dW1[m][c] +=
+//    sum_q dz[m][q] x[q], dh[q] = sum_m W1[m][c] dz[m][q] (the old kernel's operation order per element), the BN
+//    sums, dh through the tile;
 //  * the accumulators fold over the two row halves and the four waves in a fixed order into this workgroup's
 //    partial row (heads_reduce_kernel folds the workgroups) -- deterministic.
 constexpr int kBR = 32;                // rows per block (one wave)
@@ -368,17 +445,10 @@ constexpr int kSMS = 40;               // LDS stride of a row's small inputs: g[
 constexpr int kSmG = 0, kSmGV = 9, kSmAP = 10, kSmAV = 28;
 constexpr int kFcN = kOP * kZP + kHW;  // 171 fc weights
 constexpr int kWaves2 = 4;
+constexpr int kGR = 8;                 // rows per contiguous load / store group
+constexpr int kGV = kGR * kRow / 4 / 64;   // 9 float4 per lane per group
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t heads_rsrc(const void *base, uint32_t bytes) {
-    const uint64_t p = reinterpret_cast<uint64_t>(base);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-    const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, (int)n,
-                                             0x00020000);
-}
 
-typedef unsigned int hu32x3 __attribute__((ext_vector_type(3)));
 
 __device__ __forceinline__ void load9(__amdgpu_buffer_rsrc_t rs, uint32_t off, float (&d)[kHW]) {
 #pragma unroll
@@ -390,8 +460,15 @@ __device__ __forceinline__ void load9(__amdgpu_buffer_rsrc_t rs, uint32_t off, f
     }
 }
 
+// rows [row0, row0 + 8) of h as 9 contiguous float4 per lane (rows past N read 0)
+__device__ __forceinline__ void load_group(__amdgpu_buffer_rsrc_t rh, int64_t row0, int lane, hu32x4 (&st)[kGV]) {
+    const uint32_t ob = (uint32_t)(row0 * kRow * 4);
+#pragma unroll
+    for (int k = 0; k < kGV; ++k) st[k] = __builtin_amdgcn_raw_buffer_load_b128(rh, ob + (k * 64 + lane) * 16, 0, 0);
+}
+
 template <bool BN>
-__global__ __launch_bounds__(256, 4) void heads_bwd2_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
+__global__ __launch_bounds__(256, 2) void heads_bwd2_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
                                                          const float *__restrict__ a_p, const float *__restrict__ a_v,
                                                          const float *__restrict__ dp, const float *__restrict__ dv,
                                                          const float *__restrict__ vt, float *__restrict__ dh,
@@ -400,6 +477,7 @@ __global__ __launch_bounds__(256, 4) void heads_bwd2_kernel(const float *__restr
     __shared__ __attribute__((aligned(16))) float sdz[kWaves2][kBR * kDZS];
     __shared__ __attribute__((aligned(16))) float ssm[kWaves2][kBR * kSMS];
     __shared__ float swp[kOP * kZP], swv[kHW];
+    __shared__ __attribute__((aligned(16))) float sx[kWaves2][kGR * kRow];   // a wave's 8-row group: x, then dh
     static_assert(sizeof(float) * kWaves2 * 64 * 8 <= sizeof(float) * kWaves2 * kBR * kSMS, "fold");
     static_assert(sizeof(double) * kWaves2 * 64 * 2 <= sizeof(float) * kWaves2 * kBR * kDZS, "foldd");
     float(*fold)[64 * 8] = reinterpret_cast<float(*)[64 * 8]>(&ssm[0][0]);
@@ -438,12 +516,13 @@ __global__ __launch_bounds__(256, 4) void heads_bwd2_kernel(const float *__restr
     const __amdgpu_buffer_rsrc_t rd = heads_rsrc(dh, (uint32_t)(N * kRow * 4));
     const int64_t nblocks = (N + kBR - 1) / kBR;
     const int64_t wstep = (int64_t)gridDim.x * kWaves2;
+    float *sxw = sx[wave];
+    hu32x4 st[kGV];
+    if ((int64_t)blockIdx.x * kWaves2 + wave < nblocks)
+        load_group(rh, ((int64_t)blockIdx.x * kWaves2 + wave) * kBR, lane, st);
     for (int64_t blk = (int64_t)blockIdx.x * kWaves2 + wave; blk < nblocks; blk += wstep) {
         const int64_t base = blk * kBR;
         asm volatile("" ::: "memory");   // Wp / Wv are re-read from LDS per block, not held in 171 registers
-        // the first row pair's x is in flight while the block's dz is formed
-        float xn[kHW];
-        load9(rh, (uint32_t)(((base + r) * kRow + c * kHW) * 4), xn);
         if (lane < kBR) {
             const int64_t n = base + lane;
             const bool valid = n < N;
@@ -498,60 +577,74 @@ __global__ __launch_bounds__(256, 4) void heads_bwd2_kernel(const float *__restr
 #pragma unroll
             for (int s = 0; s < 3; ++s) fc[s] += smr[fo_g[s]] * smr[fo_a[s]];
         }
-        // the row pairs: lane (r, c) takes row base + 2 it + r, channel c
+        // the block's four 8-row groups: x arrives as contiguous float4s (st, one group ahead) through this wave's
+        // LDS tile; lane (r, c) reads its channel's 9 cells of rows 2j + r, writes dh in their place, and the group
+        // leaves as contiguous float4 stores (36-byte per-lane runs straight from registers ran at half the rate)
 #pragma unroll 1
-        for (int it = 0; it < kBR / 2; ++it) {
-            float x[kHW];
+        for (int g = 0; g < kBR / kGR; ++g) {
 #pragma unroll
-            for (int q = 0; q < kHW; ++q) x[q] = xn[q];
-            if (it + 1 < kBR / 2)
-                load9(rh, (uint32_t)(((base + 2 * (it + 1) + r) * kRow + c * kHW) * 4), xn);
-            float dz[kZ + 1];
-            const float4 *dzr = reinterpret_cast<const float4 *>(dzs + (2 * it + r) * kDZS);
+            for (int k = 0; k < kGV; ++k) *reinterpret_cast<hu32x4 *>(sxw + 4 * (k * 64 + lane)) = st[k];
+            lds_fence();
+            {   // the next group: this block's, or the wave's next block's first
+                const int64_t nb = g + 1 < kBR / kGR ? base + kGR * (g + 1) : base + wstep * kBR;
+                if (nb < N) {
+                    load_group(rh, nb, lane, st);
+                } else {   // past the batch: zeros (no stale rows, no offset past 32 bits)
 #pragma unroll
-            for (int j = 0; j < 7; ++j) {
-                const float4 v = dzr[j];
-                dz[4 * j] = v.x; dz[4 * j + 1] = v.y; dz[4 * j + 2] = v.z; dz[4 * j + 3] = v.w;
-            }
-            float hx[kHW];
-#pragma unroll
-            for (int q = 0; q < kHW; ++q) hx[q] = BN ? bn_relu(x[q], al, be) : x[q];
-            // conv weight gradient: dW1[m, c] += sum_q dz[m, q] * h[c, q]
-#pragma unroll
-            for (int m = 0; m < kM; ++m) {
-                float t = 0.f;
-#pragma unroll
-                for (int q = 0; q < kHW; ++q) t += dz[m * kHW + q] * hx[q];
-                gw[m] += t;
-            }
-            // input gradient dh[c, q] = sum_m W1[m, c] dz[m, q], the BN sums of channel c
-            float o[kHW];
-            float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-            for (int q = 0; q < kHW; ++q) {
-                float t = 0.f;
-#pragma unroll
-                for (int m = 0; m < kM; ++m) t += w1[m] * dz[m * kHW + q];
-                o[q] = t;
-                if constexpr (BN) {
-                    if (bn.part) {   // bn_bwd_reduce_kernel's mask and products
-                        const float gm = (x[q] * al + be > 0.f) ? t : 0.f;
-                        t1 += gm;
-                        t2 += gm * (x[q] - mu);
-                    }
+                    for (int k = 0; k < kGV; ++k) st[k] = (hu32x4){0u, 0u, 0u, 0u};
                 }
             }
-            t1d += (double)t1;
-            t2d += (double)t2;
-            const uint32_t off = (uint32_t)(((base + 2 * it + r) * kRow + c * kHW) * 4);
+#pragma unroll 1
+            for (int jj = 0; jj < kGR / 2; ++jj) {
+                const int lr = 2 * jj + r;             // row within the group
+                float *xr = sxw + lr * kRow + c * kHW;
+                float x[kHW];
 #pragma unroll
-            for (int m = 0; m < 3; ++m) {
-                hu32x3 v;
-                v.x = __float_as_uint(o[3 * m]);
-                v.y = __float_as_uint(o[3 * m + 1]);
-                v.z = __float_as_uint(o[3 * m + 2]);
-                __builtin_amdgcn_raw_buffer_store_b96(v, rd, off + 12 * m, 0, 0);
+                for (int q = 0; q < kHW; ++q) x[q] = xr[q];
+                float dz[kZ + 1];
+                const float4 *dzr = reinterpret_cast<const float4 *>(dzs + (kGR * g + lr) * kDZS);
+#pragma unroll
+                for (int t = 0; t < 7; ++t) {
+                    const float4 v = dzr[t];
+                    dz[4 * t] = v.x; dz[4 * t + 1] = v.y; dz[4 * t + 2] = v.z; dz[4 * t + 3] = v.w;
+                }
+                float hx[kHW];
+#pragma unroll
+                for (int q = 0; q < kHW; ++q) hx[q] = BN ? bn_relu(x[q], al, be) : x[q];
+                // conv weight gradient: dW1[m, c] += sum_q dz[m, q] * h[c, q]
+#pragma unroll
+                for (int m = 0; m < kM; ++m) {
+                    float t = 0.f;
+#pragma unroll
+                    for (int q = 0; q < kHW; ++q) t += dz[m * kHW + q] * hx[q];
+                    gw[m] += t;
+                }
+                // input gradient dh[c, q] = sum_m W1[m, c] dz[m, q], the BN sums of channel c
+                float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+                for (int q = 0; q < kHW; ++q) {
+                    float t = 0.f;
+#pragma unroll
+                    for (int m = 0; m < kM; ++m) t += w1[m] * dz[m * kHW + q];
+                    if constexpr (BN) {
+                        if (bn.part) {   // bn_bwd_reduce_kernel's mask and products
+                            const float gm = (x[q] * al + be > 0.f) ? t : 0.f;
+                            t1 += gm;
+                            t2 += gm * (x[q] - mu);
+                        }
+                    }
+                    xr[q] = t;
+                }
+                t1d += (double)t1;
+                t2d += (double)t2;
             }
+            lds_fence();
+            const uint32_t ob = (uint32_t)((base + kGR * g) * kRow * 4);
+#pragma unroll
+            for (int k = 0; k < kGV; ++k)   // rows past N: dropped (the descriptor's range)
+                __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const hu32x4 *>(sxw + 4 * (k * 64 + lane)),
+                                                       rd, ob + (k * 64 + lane) * 16, 0, 0);
+            lds_fence();   // the tile's reads are done before the next group overwrites it
         }
         lds_fence();   // the block's LDS rows are read before the next block overwrites them
     }
@@ -669,9 +762,9 @@ __global__ __launch_bounds__(256) void heads_reduce_kernel(const float *__restri
 // Workgroups (one wave each).  The backward's 51.9 KB of LDS lets 3 reside per CU, so 768 on the
 // 256 CUs run in one round: its former 1024 ran as 768 + a tail of 256 at a third of the
 // occupancy.  The forward (10.8 KB LDS, 230 VGPRs) keeps all 1024 resident.
-constexpr int kGridFwd = 1024;
+constexpr int kGridFwd = 4096;   // one-wave workgroups: 64-row blocks, up to 4 waves per SIMD
 constexpr int kGridBwd = 768;
-constexpr int kGridBwd2 = 1024;   // heads_bwd2_kernel: 4 four-wave workgroups per CU
+constexpr int kGridBwd2 = 512;    // heads_bwd2_kernel: 2 four-wave workgroups per CU (72 KB LDS each)
 int g_heads_bwd_form = 2;         // hrl_heads_set_bwd_form
 
 int status() {
@@ -740,7 +833,7 @@ int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float 
     const BnIn bn{bn_alpha, bn_beta, bn_mean, bn_part};
     float *part = static_cast<float *>(workspace);
     if (g_heads_bwd_form == 2) {
-        if (N * kRow * 4 >= (int64_t)1 << 32) return HRL_EINVAL;   // 32-bit buffer offsets
+        if ((N + kBR) * kRow * 4 >= (int64_t)1 << 32) return HRL_EINVAL;   // 32-bit buffer offsets (+ a block)
         const int grid = grid_bwd(N);
         if (bn_alpha)
             hipLaunchKernelGGL(heads_bwd2_kernel<true>, dim3(grid), dim3(256), 0, s, h, N, w, bn, a_p, a_v, dp, dv,

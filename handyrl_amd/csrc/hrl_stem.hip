@@ -135,64 +135,86 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base, int6
 }
 
 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+typedef unsigned int hu32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------------ forward, lane per channel (form 2)
-// stem_fwd2_kernel<CIN>: lane (h, co) of a wave computes output channel co of rows 4t + 2h and 4t + 2h + 1 of its
-// 4-row quad t as one float2 (v_pk_fma_f32 on the two rows), with its Cin*9 weights and bias in registers:
+// stem_fwd2_kernel<CIN>: a wave takes 8-row octets; lane (h, co) computes output channel co of rows 4j + 2h and
+// 4j + 2h + 1 (j = 0, 1) as one float2 each (v_pk_fma_f32 on the two rows), with its Cin*9 weights and bias in
+// registers:
 //   y[n][co][q] = b[co] + sum_ci sum_{p: tap(p, q) on the board} w[co][ci][tap(p, q)] * x[n][ci][p]
-// (fused multiply-adds, ci then p ascending).  The observation rows are read as 12-byte runs (one address across the
-// 32 lanes of a row); a lane's 9 outputs of a row are 36 contiguous bytes, the row's 32 lanes its 1152.  Bound: the
-// output write (151 MB at N = 131,072); ~110 VGPRs, 4 waves per SIMD.
+// (fused multiply-adds, ci then p ascending).  The octet's observation rows (8 x Cin*9 floats, contiguous) come in
+// as float4s through LDS and are read back as broadcasts; its outputs go through LDS too and leave as contiguous
+// float4 stores (1 KiB per wave instruction): the 36-byte per-lane runs written straight from registers ran at
+// 3.0 TB/s against 6.6 for a plain fill (tools/stem_bench.py).
+constexpr int kOct = 8;                       // rows per wave step
+constexpr int kYO = kOct * kCols;             // 2304 output floats per octet
+
 template <int CIN>
 __global__ __launch_bounds__(kThreads) void stem_fwd2_kernel(const float *__restrict__ x, int64_t N,
                                                              const float *__restrict__ w,
                                                              const float *__restrict__ b, float *__restrict__ y) {
     constexpr int kXF = CIN * kCells;
+    constexpr int kXO = kOct * kXF;           // observation floats per octet (multiple of 4: kXF * 8)
+    __shared__ __attribute__((aligned(16))) float ys[kWaves][kYO];
+    __shared__ __attribute__((aligned(16))) float xs[kWaves][kXO];
     const int lane = threadIdx.x & 63, co = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float *yw = ys[wave];
+    float *xw = xs[wave];
     float wr[kXF];
 #pragma unroll
     for (int k = 0; k < kXF; ++k) wr[k] = w[co * kXF + k];
     const float bias = b ? b[co] : 0.f;
-    const int64_t nquads = (N + 3) / 4;
+    const int64_t noct = (N + kOct - 1) / kOct;
     const int64_t wstep = (int64_t)gridDim.x * kWaves;
-    for (int64_t t = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); t < nquads; t += wstep) {
-        const int64_t rows = min<int64_t>(4, N - 4 * t);
-        const __amdgpu_buffer_rsrc_t rx = rsrc_of(x + 4 * t * kXF, rows * kXF * 4);
-        const __amdgpu_buffer_rsrc_t ry = rsrc_of(y + 4 * t * kCols, rows * kCols * 4);
-        f32x2 xv[kXF];
-#pragma unroll
-        for (int j = 0; j < kXF / 3; ++j) {
-            const u32x3 a = __builtin_amdgcn_raw_buffer_load_b96(rx, ((2 * h) * kXF + 3 * j) * 4, 0, 0);
-            const u32x3 c = __builtin_amdgcn_raw_buffer_load_b96(rx, ((2 * h + 1) * kXF + 3 * j) * 4, 0, 0);
-            xv[3 * j] = (f32x2){__uint_as_float(a.x), __uint_as_float(c.x)};
-            xv[3 * j + 1] = (f32x2){__uint_as_float(a.y), __uint_as_float(c.y)};
-            xv[3 * j + 2] = (f32x2){__uint_as_float(a.z), __uint_as_float(c.z)};
+    for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < noct; t += wstep) {
+        const int64_t rows = min<int64_t>(kOct, N - kOct * t);
+        const __amdgpu_buffer_rsrc_t rx = rsrc_of(x + kOct * t * kXF, rows * kXF * 4);
+        const __amdgpu_buffer_rsrc_t ry = rsrc_of(y + kOct * t * kCols, rows * kCols * 4);
+        // the octet's observations: kXO / 4 float4s (rows past N read 0)
+        if (lane < kXO / 4) {
+            const hu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16, 0, 0);
+            *reinterpret_cast<hu32x4 *>(xw + 4 * lane) = v;
         }
-        f32x2 acc[kCells];
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes done
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int q = 0; q < kCells; ++q) {
-            acc[q] = (f32x2){bias, bias};
+        for (int j = 0; j < 2; ++j) {
+            const int r0 = 4 * j + 2 * h;     // rows r0, r0 + 1 of the octet
+            f32x2 xv[kXF];
 #pragma unroll
-            for (int ci = 0; ci < CIN; ++ci)
+            for (int k = 0; k < kXF; ++k) xv[k] = (f32x2){xw[r0 * kXF + k], xw[(r0 + 1) * kXF + k]};
+            f32x2 acc[kCells];
 #pragma unroll
-                for (int p = 0; p < kCells; ++p) {
-                    const int tap = tap_of(p, q);
-                    if (tap < 0) continue;
-                    const float wv = wr[ci * kCells + tap];
-                    acc[q] = __builtin_elementwise_fma((f32x2){wv, wv}, xv[ci * kCells + p], acc[q]);
-                }
-        }
+            for (int q = 0; q < kCells; ++q) {
+                acc[q] = (f32x2){bias, bias};
 #pragma unroll
-        for (int r = 0; r < 2; ++r)
+                for (int ci = 0; ci < CIN; ++ci)
 #pragma unroll
-            for (int m = 0; m < 3; ++m) {
-                u32x3 v;
-                v.x = __float_as_uint(acc[3 * m][r]);
-                v.y = __float_as_uint(acc[3 * m + 1][r]);
-                v.z = __float_as_uint(acc[3 * m + 2][r]);
-                __builtin_amdgcn_raw_buffer_store_b96(v, ry, ((2 * h + r) * kCols + co * kCells + 3 * m) * 4, 0, 0);
+                    for (int p = 0; p < kCells; ++p) {
+                        const int tap = tap_of(p, q);
+                        if (tap < 0) continue;
+                        const float wv = wr[ci * kCells + tap];
+                        acc[q] = __builtin_elementwise_fma((f32x2){wv, wv}, xv[ci * kCells + p], acc[q]);
+                    }
             }
+#pragma unroll
+            for (int q = 0; q < kCells; ++q) {
+                yw[r0 * kCols + co * kCells + q] = acc[q].x;
+                yw[(r0 + 1) * kCols + co * kCells + q] = acc[q].y;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < kYO / 4 / 64; ++k) {   // 9 contiguous float4 per lane (rows past N: dropped)
+            const int i = k * 64 + lane;
+            const hu32x4 v = *reinterpret_cast<const hu32x4 *>(yw + 4 * i);
+            __builtin_amdgcn_raw_buffer_store_b128(v, ry, i * 16, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);        // the LDS reads done before the next octet overwrites
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -444,7 +466,7 @@ int grid_for(int64_t N, int cap) {
 }
 
 constexpr int kGrid2 = 1024;   // stem_wgrad2_kernel: 4 workgroups per CU
-constexpr int kGridF2 = 4096;  // stem_fwd2_kernel: 16 workgroups of 4 waves per CU, grid-strided over 4-row quads
+constexpr int kGridF2 = 1024;  // stem_fwd2_kernel: 4 workgroups of 4 waves per CU (40 KB LDS each), over 8-row octets
 
 // workgroups of the weight gradient's form: form 2 runs 4-wave workgroups over 32-row blocks
 int grid_wgrad(int64_t N) {
@@ -487,7 +509,7 @@ int hrl_stem_forward(const float *x, int64_t N, int64_t Cin, const float *weight
     if (N < 1 || Cin < 1 || Cin > 3 || !x || !weight || !y) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (g_stem_fwd_form == 2) {
-        const int64_t wgs = ((N + 3) / 4 + kWaves - 1) / kWaves;
+        const int64_t wgs = ((N + kOct - 1) / kOct + kWaves - 1) / kWaves;
         const dim3 grid((unsigned)(wgs < kGridF2 ? wgs : kGridF2));
         if (Cin == 3)
             hipLaunchKernelGGL(stem_fwd2_kernel<3>, grid, dim3(kThreads), 0, s, x, N, weight, bias, y);
@@ -514,7 +536,7 @@ int hrl_stem_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, floa
     const int grid = grid_wgrad(N);
     float *partial = static_cast<float *>(workspace);
     if (g_stem_wgrad_form == 2) {
-        if (N * kCols * 4 >= (int64_t)1 << 32) return HRL_EINVAL;   // 32-bit buffer offsets
+        if ((N + 32) * kCols * 4 >= (int64_t)1 << 32) return HRL_EINVAL;   // 32-bit buffer offsets (+ a block)
         if (Cin == 3)
             hipLaunchKernelGGL(stem_wgrad2_kernel<3>, dim3(grid), dim3(kThreads), 0, s, x, dy, N, want_bias, partial);
         else if (Cin == 2)

@@ -333,7 +333,7 @@ def test_fused_heads_match_torch_cpu(cuda, N):
 @pytest.mark.parametrize('fwd_form', [2, 1])
 @pytest.mark.parametrize('N,cin,bias,binary', [(1, 3, True, True), (17, 3, True, True), (4099, 3, True, True),
                                                (50, 2, False, True), (33, 1, True, True), (4102, 3, True, False),
-                                               (7, 2, True, False)])
+                                               (7, 2, True, False), (200003, 3, True, False)])
 def test_stem_conv_matches_torch_cpu(cuda, N, cin, bias, binary, fwd_form):
     """csrc/hrl_stem.hip (the observation stem, tictactoe.py:57): forward (both forms: 2 = lane per channel,
     1 = fp32 MFMA) and the weight / bias gradients vs torch-CPU conv2d on ragged sample counts (rows past a
@@ -548,14 +548,15 @@ def test_grouped_batch_norm_matches_sequential_calls(cuda, G, N, C, HW):
         assert float((a - r).abs().max()) <= 1e-6 * scale
 
 
-@pytest.mark.parametrize('N', [1, 37, 4099, 20000])
+@pytest.mark.parametrize('N', [1, 37, 4099, 20000, 140001])
 @pytest.mark.parametrize('bn', [False, True])
 def test_heads_backward_forms_agree(cuda, N, bn):
     """hrl_heads_backward's lane-per-channel form (2, the default: accumulators in registers, the fc weight
     gradients in the same pass) against the row-per-lane form (1) on the same inputs: dh bit-identical (the same
     float operations per element), every parameter gradient and the fused BatchNorm's backward sums against the
     fp64 formulas within fp32 reassociation (different fold orders), on ragged row counts with and without the
-    body's last BatchNorm + ReLU in front and the value head's tanh folded in."""
+    body's last BatchNorm + ReLU in front and the value head's tanh folded in.  N = 140001: several 32-row blocks
+    per wave (the next block's first 8-row group prefetched across the block boundary)."""
     from handyrl_amd import _native
     lib = _native.load()
     P = _native.ptr
