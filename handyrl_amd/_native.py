@@ -107,6 +107,12 @@ SIGNATURES = {
                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     'hrl_hidden_gather_backward': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, ctypes.c_int, ctypes.c_void_p,
                                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    'hrl_hidden_gather_backward_add': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, ctypes.c_int,
+                                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_void_p, ctypes.c_void_p]),
+    'hrl_hidden_update_backward_add': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, _i64, ctypes.c_int,
+                                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     'hrl_hidden_update': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, _i64, _f32p, _i64, _i64, ctypes.c_int,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     'hrl_hidden_update_backward': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, _i64, ctypes.c_int,
@@ -131,8 +137,8 @@ SIGNATURES = {
     'hrl_grad_fold_norm_blocks': (ctypes.c_int64, [_i64]),
     'hrl_grad_fold_norm': (ctypes.c_int, [_f32p, _i64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                          ctypes.c_int, _f32p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, _i64,
-                                          ctypes.c_void_p]),
+                                          ctypes.c_int, _f32p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                          ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_adam_clip': (ctypes.c_int, [_f32p, _i64, ctypes.c_void_p, _dbl, _f32p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _dbl, _dbl, _dbl,
                                      _dbl, ctypes.c_void_p, ctypes.c_int, _f32p, ctypes.c_void_p]),
@@ -213,7 +219,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 _lib = None
 

@@ -38,6 +38,8 @@ struct Leaves {
     const float *b[kMaxLeaves];   // update: nh
     float *c[kMaxLeaves];         // gather: out; gather bwd: dH; update: out; update bwd: dH
     float *d[kMaxLeaves];         // update bwd: dnh
+    const float *e[kMaxLeaves];   // gather bwd: addend of dH; update bwd: addend of dnh (NULL: none)
+    int64_t es[kMaxLeaves];       // the addend's row stride in floats (a channel slice of a wider tensor)
 };
 
 template <int VW>
@@ -96,11 +98,14 @@ __global__ __launch_bounds__(kThreads) void hidden_gather_bwd_kernel(const float
     using T = typename W::T;
     HRL_LEAF_LOOP
     const T *g = reinterpret_cast<const T *>(L.a[l]);
+    const T *e = reinterpret_cast<const T *>(L.e[l]);
     T *d = reinterpret_cast<T *>(L.c[l]);
     for (int b = blockIdx.y; b < B; b += gridDim.y) {
         for (int p = 0; p < P; ++p) {
             const int bp = b * P + p;
-            d[(int64_t)bp * nv + v] = W::mul(g[(int64_t)(summed ? b : bp) * nv + v], m[bp]);
+            const T t = W::mul(g[(int64_t)(summed ? b : bp) * nv + v], m[bp]);
+            // the state's other consumer's gradient (the update's keep path), summed here instead of by autograd
+            d[(int64_t)bp * nv + v] = e ? W::add(e[(int64_t)bp * (L.es[l] / VW) + v], t) : t;
         }
     }
 }
@@ -133,19 +138,24 @@ __global__ __launch_bounds__(kThreads) void hidden_update_bwd_kernel(const float
     using T = typename W::T;
     HRL_LEAF_LOOP
     const T *g = reinterpret_cast<const T *>(L.a[l]);
+    const T *e = reinterpret_cast<const T *>(L.e[l]);
     T *d = reinterpret_cast<T *>(L.c[l]);
     T *dn = reinterpret_cast<T *>(L.d[l]);
     for (int b = blockIdx.y; b < B; b += gridDim.y) {
         if (Pn == 1) {
             T acc = W::mul(g[(int64_t)(b * P) * nv + v], m[b * P]);
             for (int p = 1; p < P; ++p) acc = W::add(acc, W::mul(g[(int64_t)(b * P + p) * nv + v], m[b * P + p]));
-            dn[(int64_t)b * nv + v] = acc;
+            // the new state's other consumer's gradient (e.g. the step's output to the heads), summed here
+            dn[(int64_t)b * nv + v] = e ? W::add(e[(int64_t)b * (L.es[l] / VW) + v], acc) : acc;
         }
         for (int p = 0; p < P; ++p) {
             const int bp = b * P + p;
             const T gv = g[(int64_t)bp * nv + v];
             d[(int64_t)bp * nv + v] = W::mul(gv, 1.0f - m[bp]);
-            if (Pn != 1) dn[(int64_t)bp * nv + v] = W::mul(gv, m[bp]);
+            if (Pn != 1) {
+                const T t = W::mul(gv, m[bp]);
+                dn[(int64_t)bp * nv + v] = e ? W::add(e[(int64_t)bp * (L.es[l] / VW) + v], t) : t;
+            }
         }
     }
 }
@@ -171,6 +181,8 @@ bool build(int n, const int64_t *F, int64_t B, int64_t P, const float *const *a,
         L.b[l] = b ? b[l] : nullptr;
         L.c[l] = c[l];
         L.d[l] = d ? d[l] : nullptr;
+        L.e[l] = nullptr;
+        L.es[l] = F[l];
         if (F[l] % 4 || !aligned16(L.a[l]) || !aligned16(L.b[l]) || !aligned16(L.c[l]) || !aligned16(L.d[l])) vw = 1;
         if (F[l] > fmax) fmax = (int)F[l];
     }
@@ -182,6 +194,20 @@ dim3 grid_of(int fmax, int vw, int64_t rows, int n) {
     const int gx = (nv + kThreads - 1) / kThreads;
     const int64_t gy = rows < 1 ? 1 : (rows > 4096 ? 4096 : rows);
     return dim3((unsigned)gx, (unsigned)gy, (unsigned)n);
+}
+
+// the addend table (NULL, or per leaf NULL / rows of the output's row length F, `strides` floats apart (NULL:
+// F)): false on a stride shorter than the row
+bool set_addend(Leaves &L, const float *const *add, const int64_t *strides, int &vw) {
+    if (!add) return true;
+    for (int l = 0; l < L.n; ++l) {
+        L.e[l] = add[l];
+        const int64_t st = strides ? strides[l] : L.F[l];
+        if (add[l] && (st < L.F[l] || st > ((int64_t)1 << 31))) return false;
+        L.es[l] = st;
+        if (!aligned16(add[l]) || st % 4) vw = 1;
+    }
+    return true;
 }
 
 }  // namespace
@@ -208,9 +234,16 @@ int hrl_hidden_gather(const float *const *H, const float *mask, int64_t B, int64
 
 int hrl_hidden_gather_backward(const float *const *dout, const float *mask, int64_t B, int64_t P, int nleaves,
                                const int64_t *F, int sum, float *const *dH, void *stream) {
+    return hrl_hidden_gather_backward_add(dout, mask, B, P, nleaves, F, sum, nullptr, nullptr, dH, stream);
+}
+
+int hrl_hidden_gather_backward_add(const float *const *dout, const float *mask, int64_t B, int64_t P, int nleaves,
+                                   const int64_t *F, int sum, const float *const *addend,
+                                   const int64_t *addend_strides, float *const *dH, void *stream) {
     Leaves L;
     int vw, fmax;
-    if (!mask || !build(nleaves, F, B, P, dout, nullptr, dH, nullptr, L, vw, fmax)) return HRL_EINVAL;
+    if (!mask || !build(nleaves, F, B, P, dout, nullptr, dH, nullptr, L, vw, fmax) || !set_addend(L, addend, addend_strides, vw))
+        return HRL_EINVAL;
     if (B == 0) return HRL_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 grid = grid_of(fmax, vw, B, nleaves);
@@ -235,10 +268,18 @@ int hrl_hidden_update(const float *const *H, const float *const *nh, int64_t Pn,
 
 int hrl_hidden_update_backward(const float *const *dout, const float *mask, int64_t B, int64_t P, int64_t Pn,
                                int nleaves, const int64_t *F, float *const *dH, float *const *dnh, void *stream) {
+    return hrl_hidden_update_backward_add(dout, mask, B, P, Pn, nleaves, F, nullptr, nullptr, dH, dnh, stream);
+}
+
+int hrl_hidden_update_backward_add(const float *const *dout, const float *mask, int64_t B, int64_t P, int64_t Pn,
+                                   int nleaves, const int64_t *F, const float *const *addend,
+                                   const int64_t *addend_strides, float *const *dH, float *const *dnh,
+                                   void *stream) {
     Leaves L;
     int vw, fmax;
     if (!mask || !dnh || (Pn != 1 && Pn != P)) return HRL_EINVAL;
-    if (!build(nleaves, F, B, P, dout, nullptr, dH, dnh, L, vw, fmax)) return HRL_EINVAL;
+    if (!build(nleaves, F, B, P, dout, nullptr, dH, dnh, L, vw, fmax) || !set_addend(L, addend, addend_strides, vw))
+        return HRL_EINVAL;
     if (B == 0) return HRL_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 grid = grid_of(fmax, vw, B, nleaves);

@@ -158,6 +158,7 @@ struct FoldTable {
 struct StepCounters {
     float *step;                       // the optimizer's step count (float, as torch's capturable state)
     int64_t *ctr[kMaxCounters];        // BatchNorm num_batches_tracked
+    int64_t inc[kMaxCounters];         // their increments (a recurrent unroll's per-step BatchNorm: T)
     int nctr;
 };
 
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(64 * kFoldWaves) void step_fold_norm_kernel(float *
         norm_part[blockIdx.x] = t;
         if (blockIdx.x == 0) {
             if (sc.step) sc.step[0] += 1.0f;
-            for (int k = 0; k < sc.nctr; ++k) sc.ctr[k][0] += 1;
+            for (int k = 0; k < sc.nctr; ++k) sc.ctr[k][0] += sc.inc[k];
         }
     }
 }
@@ -322,8 +323,9 @@ int64_t hrl_grad_fold_norm_blocks(int64_t n) { return n < 1 ? -1 : (n + kBlk - 1
 
 int hrl_grad_fold_norm(float *grads, int64_t n, const float *const *parts, const int64_t *strides,
                        const int64_t *col0, const int64_t *nparts, const int64_t *dst, const int64_t *count,
-                       const int *modes, int nfolds, float *step, int64_t *const *counters, int ncounters,
-                       double *norm_part, int64_t norm_part_bytes, void *stream) {
+                       const int *modes, int nfolds, float *step, int64_t *const *counters,
+                       const int64_t *increments, int ncounters, double *norm_part, int64_t norm_part_bytes,
+                       void *stream) {
     if (!grads || n < 1 || nfolds < 0 || nfolds > kMaxFolds || ncounters < 0 || ncounters > kMaxCounters ||
         !norm_part || norm_part_bytes < hrl_grad_fold_norm_blocks(n) * 8)
         return HRL_EINVAL;
@@ -341,8 +343,9 @@ int hrl_grad_fold_norm(float *grads, int64_t n, const float *const *parts, const
     StepCounters sc{};
     sc.step = step;
     for (int k = 0; k < ncounters; ++k) {
-        if (!counters[k]) return HRL_EINVAL;
+        if (!counters[k] || (increments && increments[k] < 0)) return HRL_EINVAL;
         sc.ctr[k] = counters[k];
+        sc.inc[k] = increments ? increments[k] : 1;
     }
     sc.nctr = ncounters;
     hipLaunchKernelGGL(step_fold_norm_kernel, dim3((unsigned)hrl_grad_fold_norm_blocks(n)), dim3(64 * kFoldWaves), 0,

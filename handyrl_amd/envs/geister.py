@@ -499,8 +499,12 @@ class GeisterNet(nn.Module):
     @staticmethod
     def _bn_steps(bn, y, T):
         """relu(bn(y)) for T time steps' rows (time-major) with per-step statistics."""
+        from .. import nn as hnn
         from ..nn import batch_norm_train
-        bn.num_batches_tracked.add_(T)
+        if hnn._FOLDS is not None and bn.momentum is not None:
+            hnn._FOLDS.add_counter(bn.num_batches_tracked, T)   # advanced by the learner's step tail
+        else:
+            bn.num_batches_tracked.add_(T)
         return batch_norm_train(y, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
                                 relu=True, groups=T)
 

@@ -118,10 +118,10 @@ class DeferredGrads:
                 touched[id(b)] = b
         for (w, b), rec in self.affine.items():
             if w is not None:
-                _add_grad(w, torch.stack([r[0] for r in rec]).sum(0), None)
+                _add_grad(w, rec[0][0] if len(rec) == 1 else torch.stack([r[0] for r in rec]).sum(0), None)
                 touched[id(w)] = w
             if b is not None:
-                _add_grad(b, torch.stack([r[1] for r in rec]).sum(0), None)
+                _add_grad(b, rec[0][1] if len(rec) == 1 else torch.stack([r[1] for r in rec]).sum(0), None)
                 touched[id(b)] = b
         self.conv.clear()
         self.affine.clear()
@@ -280,6 +280,7 @@ class deferred_folds:
         self.prev = _FOLDS
         self.folds = []      # (partial rows (float32 tensor), stride, col0, nparts, dst gradient view, count, mode)
         self.counters = []   # int64 num_batches_tracked tensors
+        self.increments = []  # and what each advances by
         self.keep = []       # workspaces read by the folds: referenced until the fold launch is enqueued
         if self.enabled:
             _FOLDS = self
@@ -293,6 +294,10 @@ class deferred_folds:
 
     def add(self, part, stride, col0, nparts, dst, count, mode=0):
         self.folds.append((part, stride, col0, nparts, dst, count, mode))
+
+    def add_counter(self, counter, inc=1):
+        self.counters.append(counter)
+        self.increments.append(int(inc))
 
 
 def _defer_folds(bufs):
@@ -762,17 +767,26 @@ class _BatchNormTrain(torch.autograd.Function):
         ws_bytes = lib.hrl_bn_workspace_bytes_grouped(N, C, HW, ctx.groups)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
         dx = torch.empty_like(x)
-        dw = torch.empty(C, dtype=torch.float32, device=x.device) if weight is not None else None
-        db = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_bias else None
+        # the affine gradients straight into .grad when they may be written in place (direct_grads: the
+        # parameter's first use in the step), else into fresh tensors for the deferral / autograd
+        bw = _grad_buffer(weight) if (weight is not None and ctx.needs_input_grad[1]) else (None, False)
+        bb = _grad_buffer(bias) if (ctx.has_bias and ctx.needs_input_grad[2]) else (None, False)
+        dw = bw[0] if bw[0] is not None else (torch.empty(C, dtype=torch.float32, device=x.device)
+                                              if weight is not None else None)
+        db = bb[0] if bb[0] is not None else (torch.empty(C, dtype=torch.float32, device=x.device)
+                                              if ctx.has_bias else None)
         code = lib.hrl_bn_backward_grouped(
             _native.ptr(x), _native.ptr(dy), N, C, HW, ctx.groups, _native.ptr(weight), _native.ptr(bias),
             _native.ptr(mean), _native.ptr(invstd), int(ctx.relu), _native.ptr(dx), _native.ptr(dw), _native.ptr(db),
             _native.ptr(ws), ws_bytes, _native.stream_of(x.device))
         _native.check(code, 'hrl_bn_backward_grouped')
-        if ctx.defer is not None and (dw is not None or db is not None):
-            ctx.defer.add_affine((weight, bias if ctx.has_bias else None), dw, db)
+        dw_out = None if bw[1] else dw
+        db_out = None if bb[1] else db
+        if ctx.defer is not None and (dw_out is not None or db_out is not None):
+            ctx.defer.add_affine((weight if dw_out is not None else None,
+                                  bias if (ctx.has_bias and db_out is not None) else None), dw_out, db_out)
             return dx, None, None, None, None, None, None, None, None
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw_out, db_out, None, None, None, None, None, None
 
 
 def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps, relu=False, groups=1):
@@ -1561,11 +1575,26 @@ def _live(xs):
     return [k for k, x in enumerate(xs) if x is not None]
 
 
+def _rows_view(t, lead):
+    """t as (rows, features) with unit-stride features (rows may be any stride apart: a channel slice of a wider
+    gradient), flattening the first `lead` dims into rows; a contiguous copy only when that is not possible."""
+    rows = t.flatten(lead) if t.dim() > lead else t.unsqueeze(-1)
+    if rows.stride(-1) != 1:
+        rows = rows.contiguous()
+    rows = rows.reshape(-1, rows.shape[-1]) if lead > 1 else rows
+    if rows.stride(-1) != 1 or (rows.shape[0] > 1 and rows.stride(0) < rows.shape[-1]):
+        rows = rows.contiguous()
+    return rows
+
+
 class _HiddenGather(torch.autograd.Function):
     """Per-step recurrent input (csrc/hrl_hidden.hip, train.py:157-164), one launch for every state tensor.
 
     apply(m, summed, B, P, *H): H[l] is (B, P, *shape_l); returns sum_p H[l] * m (summed, (B, *shape_l))
-    or H[l] * m as (B*P, *shape_l).  Tensors whose output gradient is None get None back.
+    or H[l] * m as (B*P, *shape_l), then H itself again (views) for the step's _HiddenUpdate: the state then has
+    one autograd consumer, and the backward adds the update's keep-path gradient into its own launch
+    (hrl_hidden_gather_backward_add) instead of autograd adding the two.  Tensors whose gradients are None get
+    None back.
     """
 
     @staticmethod
@@ -1580,21 +1609,29 @@ class _HiddenGather(torch.autograd.Function):
             _native.ptr_array(outs), _native.stream_of(m.device)), 'hrl_hidden_gather')
         ctx.save_for_backward(m)
         ctx.meta = (summed, B, P, [tuple(h.shape) for h in H])
-        return tuple(outs)
+        return (*outs, *[h.view_as(h) for h in H])
 
     @staticmethod
     def backward(ctx, *grads):
         (m,) = ctx.saved_tensors
         summed, B, P, shapes = ctx.meta
-        live = _live(grads)
-        dH = [None] * len(grads)
+        n = len(shapes)
+        gout, galias = grads[:n], grads[n:]
+        dH = [None] * n
+        live = [k for k in range(n) if gout[k] is not None]
+        for k in range(n):   # only the update's gradient: it is the state's
+            if gout[k] is None and galias[k] is not None:
+                dH[k] = galias[k]
         if live:
-            g = [grads[k].contiguous() for k in live]
-            d = [torch.empty(shapes[k], dtype=m.dtype, device=m.device) for k in live]
+            g = [gout[k].contiguous() for k in live]
             F = [int(torch.Size(shapes[k][2:]).numel()) for k in live]
-            _native.check(_native.load().hrl_hidden_gather_backward(
+            add = [None if galias[k] is None else _rows_view(galias[k], 2) for k in live]
+            d = [torch.empty(shapes[k], dtype=m.dtype, device=m.device) for k in live]
+            _native.check(_native.load().hrl_hidden_gather_backward_add(
                 _native.ptr_array(g), _native.ptr(m), B, P, len(live), _native.i64_array(F), int(summed),
-                _native.ptr_array(d), _native.stream_of(m.device)), 'hrl_hidden_gather_backward')
+                _native.ptr_array(add) if any(a is not None for a in add) else None,
+                _native.i64_array([a.stride(-2) if a is not None else f for a, f in zip(add, F)]),
+                _native.ptr_array(d), _native.stream_of(m.device)), 'hrl_hidden_gather_backward_add')
             for k, t in zip(live, d):
                 dH[k] = t
         return (None, None, None, None, *dH)
@@ -1621,12 +1658,15 @@ def masked_rows_copy_(dst, src, mask):
 class _HiddenUpdate(torch.autograd.Function):
     """New state H[l] * (1 - m) + nh[l] * m (csrc/hrl_hidden.hip, train.py:167-174), one launch for all.
 
-    apply(m, B, P, Pn, n, *H, *nh): H[l] (B, P, *shape_l), nh[l] (B*Pn, *shape_l).  Tensors whose
-    output gradient is None get None back (their producers are pruned, as with the torch ops).
+    apply(m, B, P, Pn, n, out_k, *H, *nh): H[l] (B, P, *shape_l), nh[l] (B*Pn, *shape_l).  out_k >= 0: nh[out_k]
+    is also the step's output (a recurrent net's h_last): it is returned again (a view) after the new states, so
+    its consumers' gradient comes back here and is added into dnh[out_k] in the adjoint's launch
+    (hrl_hidden_update_backward_add) instead of by autograd.  Tensors whose output gradient is None get None back
+    (their producers are pruned, as with the torch ops).
     """
 
     @staticmethod
-    def forward(ctx, m, B, P, Pn, n, *tensors):
+    def forward(ctx, m, B, P, Pn, n, out_k, *tensors):
         ctx.set_materialize_grads(False)   # a state tensor without a gradient stays None (pruned)
         H = [h.contiguous() for h in tensors[:n]]
         nh = [x.contiguous() for x in tensors[n:]]
@@ -1636,27 +1676,37 @@ class _HiddenUpdate(torch.autograd.Function):
             _native.ptr_array(H), _native.ptr_array(nh), Pn, _native.ptr(m), B, P, n, _native.i64_array(F),
             _native.ptr_array(outs), _native.stream_of(m.device)), 'hrl_hidden_update')
         ctx.save_for_backward(m)
-        ctx.meta = (B, P, Pn, n, [tuple(h.shape) for h in H], [tuple(x.shape) for x in nh])
+        ctx.meta = (B, P, Pn, n, out_k, [tuple(h.shape) for h in H], [tuple(x.shape) for x in nh])
+        if out_k >= 0:
+            return (*outs, tensors[n + out_k].view_as(tensors[n + out_k]))
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *douts):
         (m,) = ctx.saved_tensors
-        B, P, Pn, n, h_shapes, nh_shapes = ctx.meta
-        live = _live(douts)
+        B, P, Pn, n, out_k, h_shapes, nh_shapes = ctx.meta
+        dout = douts[:n]
+        gk = douts[n] if out_k >= 0 else None
+        live = _live(dout)
         dH, dnh = [None] * n, [None] * n
+        if gk is not None and dout[out_k] is None:
+            dnh[out_k] = gk
         if live:
-            g = [douts[k].contiguous() for k in live]
+            g = [dout[k].contiguous() for k in live]
+            # the step output's gradient: typically a channel slice of the heads' input gradient, read in place
+            add = [_rows_view(gk, 1) if (k == out_k and gk is not None) else None for k in live]
             a = [torch.empty(h_shapes[k], dtype=m.dtype, device=m.device) for k in live]
             b = [torch.empty(nh_shapes[k], dtype=m.dtype, device=m.device) for k in live]
             F = [int(torch.Size(h_shapes[k][2:]).numel()) for k in live]
-            _native.check(_native.load().hrl_hidden_update_backward(
+            _native.check(_native.load().hrl_hidden_update_backward_add(
                 _native.ptr_array(g), _native.ptr(m), B, P, Pn, len(live), _native.i64_array(F),
+                _native.ptr_array(add) if any(x is not None for x in add) else None,
+                _native.i64_array([x.stride(-2) if x is not None else f for x, f in zip(add, F)]),
                 _native.ptr_array(a), _native.ptr_array(b), _native.stream_of(m.device)),
-                'hrl_hidden_update_backward')
+                'hrl_hidden_update_backward_add')
             for k, x, y in zip(live, a, b):
                 dH[k], dnh[k] = x, y
-        return (None, None, None, None, None, *dH, *dnh)
+        return (None, None, None, None, None, None, *dH, *dnh)
 
 
 def _board_conv_ok(m):
@@ -2047,7 +2097,8 @@ class _ConvBNChain(nn.Module):
         """Advance the BatchNorms' batch counters (as their forward would) and collect the chain's arguments."""
         counters = [b.num_batches_tracked for b in self.bns]
         if _FOLDS is not None:
-            _FOLDS.counters += counters            # advanced by the step tail's first launch
+            for c in counters:                     # advanced by the step tail's first launch
+                _FOLDS.add_counter(c)
         else:
             torch._foreach_add_(counters, 1)       # one launch for all counters
         meta, params = [], []

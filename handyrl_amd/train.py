@@ -200,12 +200,17 @@ def _unroll_flat_hidden(model, hidden, batch, args):
         h_lasts = []
         for t in range(T):
             m = masks[t]
-            h_in = _rebuild(hidden, iter(_HiddenGather.apply(m, summed, B, P, *leaves)))
+            g = _HiddenGather.apply(m, summed, B, P, *leaves)
+            h_in = _rebuild(hidden, iter(g[:n]))
             h_last, next_hidden = model.sequence_step(seq, t, h_in)
-            h_lasts.append(h_last)
             nh = _leaves(next_hidden)
             Pn = nh[0].shape[0] // B
-            leaves = list(_HiddenUpdate.apply(m, B, P, Pn, n, *leaves, *nh))
+            # the state continues through the gather's pass-through views, and the step output that is also a
+            # new state leaf comes back from the update: every tensor has one consumer, the adjoints add
+            k = next((i for i, x in enumerate(nh) if x is h_last), -1)
+            u = _HiddenUpdate.apply(m, B, P, Pn, n, k, *g[n:], *nh)
+            leaves = list(u[:n])
+            h_lasts.append(u[n] if k >= 0 else h_last)
         out = model.sequence_end(seq, h_lasts)
         # (T*N, ...) -> (N, T, ...), the per-step loop's torch.stack(dim=1) layout
         return {k: o.view(T, -1, *o.shape[1:]).transpose(0, 1).contiguous() for k, o in out.items()
@@ -214,7 +219,8 @@ def _unroll_flat_hidden(model, hidden, batch, args):
     for t in range(T):
         obs = map_r(observations, lambda o: o[:, t].reshape(-1, *o.shape[3:]))
         m = masks[t]
-        h_in = _rebuild(hidden, iter(_HiddenGather.apply(m, summed, B, P, *leaves)))
+        g = _HiddenGather.apply(m, summed, B, P, *leaves)
+        h_in = _rebuild(hidden, iter(g[:n]))
         out_t = model(obs, h_in)
         next_hidden = None
         for k, o in out_t.items():
@@ -224,7 +230,7 @@ def _unroll_flat_hidden(model, hidden, batch, args):
                 per_t.setdefault(k, []).append(o)
         nh = _leaves(next_hidden)
         Pn = nh[0].shape[0] // B
-        leaves = list(_HiddenUpdate.apply(m, B, P, Pn, n, *leaves, *nh))
+        leaves = list(_HiddenUpdate.apply(m, B, P, Pn, n, -1, *g[n:], *nh))
     return {k: torch.stack(o, dim=1) for k, o in per_t.items() if o[0] is not None}
 
 

@@ -21,6 +21,7 @@ copy of the model, lr schedule at epoch end, train.py:357-401) over any batch
 source with a ``batch()`` method.
 """
 
+import contextlib
 import copy
 
 import torch
@@ -89,6 +90,7 @@ class StepTail:
         base = flat.data_ptr()
         fl = folds.folds if folds is not None else []
         counters = folds.counters if folds is not None else []
+        incs = folds.increments if folds is not None else []
         if len(fl) > 16 or len(counters) > 8:
             raise ValueError('step tail: %d folds / %d counters (at most 16 / 8)' % (len(fl), len(counters)))
         dst = []
@@ -104,7 +106,8 @@ class StepTail:
             P(flat), self.n, _native.ptr_array([f[0] for f in fl]), i64([f[1] for f in fl]),
             i64([f[2] for f in fl]), i64([f[3] for f in fl]), i64(dst), i64([f[5] for f in fl]),
             (ctypes.c_int * max(len(fl), 1))(*[f[6] for f in fl]), len(fl), P(self.step_t),
-            _native.ptr_array(counters), len(counters), P(self.norm_part), self.norm_part.numel() * 8, stream),
+            _native.ptr_array(counters), i64(incs) if incs else None, len(counters), P(self.norm_part),
+            self.norm_part.numel() * 8, stream),
             'hrl_grad_fold_norm')
         srcs, acc_dst = acc if acc is not None else ([], None)
         acc_src = (ctypes.c_void_p * max(len(srcs), 1))(*[None if t is self.total else t.data_ptr() for t in srcs])
@@ -167,6 +170,11 @@ class LearnerStep:
         self._tail_stats = False
 
     # -- learning rate (train.py:396-398) ---------------------------------
+    def current_lr(self):
+        """The lr the next update uses (a float; the step tail's and a capturable Adam's live on the device)."""
+        lr = self.tail.lr_t if self.tail is not None else self.optimizer.param_groups[0]['lr']
+        return float(lr)
+
     def set_lr(self, lr):
         if self.tail is not None:
             self.tail.set_lr(lr)
@@ -234,12 +242,17 @@ class LearnerStep:
                 self.fused_pairs = fuse_bn_relu(self.net, obs[:2].reshape(-1, *obs.shape[3:]))
         self.grads.zero()
         if hidden is not None and self.defer:
-            # recurrent unroll: every weight is used T times; batch its weight gradients (nn.DeferredGrads)
-            with deferred_weight_grads() as deferred:
+            # recurrent unroll: every weight is used T times; batch its weight gradients (nn.DeferredGrads).  On
+            # one GPU the single-use parameters' gradients are written in place (direct_grads: the grouped
+            # BatchNorms) and the BatchNorm batch counters ride on the step tail (deferred_folds)
+            single = self.reducer is None
+            with deferred_weight_grads() as deferred, (direct_grads() if single else contextlib.nullcontext()), \
+                    deferred_folds(enabled=self.fold_deferral) as df:
                 outputs = forward_prediction(self.net, hidden, batch, self.args)
                 losses, dcnt = self.loss_fn(outputs, batch, self.args)
                 backward_total(losses)
             touched = deferred.flush()
+            self._folds = df if self.fold_deferral else None
             if self.reducer is not None:
                 self.reducer.mark_ready(touched)
         else:

@@ -265,6 +265,18 @@ int hrl_hidden_update(const float *const *H, const float *const *nh, int64_t Pn,
                       int64_t P, int nleaves, const int64_t *F, float *const *out, void *stream);
 int hrl_hidden_update_backward(const float *const *dout, const float *mask, int64_t B, int64_t P, int64_t Pn,
                                int nleaves, const int64_t *F, float *const *dH, float *const *dnh, void *stream);
+/* The adjoints with an addend per state tensor (addend NULL, or per tensor NULL / rows of F[l] floats that are
+ * addend_strides[l] floats apart, NULL: F[l]): gather: dH[l] = addend[l] + (the adjoint); update: dnh[l] =
+ * addend[l] + (the adjoint).  The sum a state tensor with two consumers needs (the gather and the update of the
+ * same step; the new state and the step's output) formed in the adjoint's launch instead of by autograd
+ * (train._unroll_flat_hidden); the stride takes a channel slice of a wider gradient without a copy. */
+int hrl_hidden_gather_backward_add(const float *const *dout, const float *mask, int64_t B, int64_t P, int nleaves,
+                                   const int64_t *F, int sum, const float *const *addend,
+                                   const int64_t *addend_strides, float *const *dH, void *stream);
+int hrl_hidden_update_backward_add(const float *const *dout, const float *mask, int64_t B, int64_t P, int64_t Pn,
+                                   int nleaves, const int64_t *F, const float *const *addend,
+                                   const int64_t *addend_strides, float *const *dH, float *const *dnh,
+                                   void *stream);
 
 /*
  * 3x3 convolution on a torus board, 17 or 32 -> 32 channels, H*W <= 80
@@ -479,7 +491,8 @@ int hrl_stem_set_fwd_form(int form);
  *   the fixed-order fp64 sum over nparts partial rows of parts[row * stride + col0 + col(j)] (mode 0: col(j) = j;
  *   mode 1: a 32x32x3x3 conv weight from the chain blocks' [tap][ci][co] rows, count 9216); then the fp64 sum of
  *   squares of every 64-element block of grads into norm_part (hrl_grad_fold_norm_blocks(n) doubles); and,
- *   once, *step += 1 (may be NULL) and *counters[k] += 1 (BatchNorm num_batches_tracked, ncounters <= 8).
+ *   once, *step += 1 (may be NULL) and *counters[k] += increments[k] (BatchNorm num_batches_tracked,
+ *   ncounters <= 8; increments NULL: all 1, e.g. T for a recurrent unroll's per-step BatchNorm).
  * hrl_adam_clip: clip_grad_norm_(max_norm) from those block sums (every workgroup folds them in one fixed order;
  *   *total_norm = the norm; grads scaled in place) and torch.optim.Adam's step (fused_adam_utils.cuh adam_math,
  *   L2 weight decay, the same double / float promotions) on the tensors params[t] (elements offsets[t] ..
@@ -492,8 +505,9 @@ int hrl_stem_set_fwd_form(int form);
 int64_t hrl_grad_fold_norm_blocks(int64_t n);
 int hrl_grad_fold_norm(float *grads, int64_t n, const float *const *parts, const int64_t *strides,
                        const int64_t *col0, const int64_t *nparts, const int64_t *dst, const int64_t *count,
-                       const int *modes, int nfolds, float *step, int64_t *const *counters, int ncounters,
-                       double *norm_part, int64_t norm_part_bytes, void *stream);
+                       const int *modes, int nfolds, float *step, int64_t *const *counters,
+                       const int64_t *increments, int ncounters, double *norm_part, int64_t norm_part_bytes,
+                       void *stream);
 int hrl_adam_clip(float *grads, int64_t n, const double *norm_part, double max_norm, float *total_norm,
                   float *const *params, const int64_t *offsets, const int *live, int ntensors, float *exp_avg,
                   float *exp_avg_sq, const float *lr, const float *step, double beta1, double beta2, double eps,

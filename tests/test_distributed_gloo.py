@@ -136,10 +136,10 @@ def test_data_parallel_lr_is_the_global_batch_lr():
     from handyrl_amd.trainer import LearnerStep, Trainer
     _, args = make_batch_and_args(B=8, T=9)
     step = LearnerStep(SmallNet(), args, torch.device('cpu'), world_size=4)
-    assert step.optimizer.param_groups[0]['lr'] == pytest.approx(3e-8 * 4 * 8 * 9, rel=1e-12)
+    assert step.current_lr() == pytest.approx(3e-8 * 4 * 8 * 9, rel=1e-12)
     tr = Trainer(args, SmallNet(), batcher=None, device=torch.device('cpu'), world_size=4)
     assert tr.data_cnt_ema == 4 * 8 * 9
-    assert tr.learner.optimizer.param_groups[0]['lr'] == pytest.approx(3e-8 * 4 * 8 * 9, rel=1e-12)
+    assert tr.learner.current_lr() == pytest.approx(3e-8 * 4 * 8 * 9, rel=1e-12)
 
 
 def test_bucket_layout_covers_flat_buffer():
@@ -491,7 +491,9 @@ def _simulated_dp(name, dev, steps=2, world=2):
     for r in range(world):
         torch.manual_seed(0)
         net = cls()
-        reps.append((net, LearnerStep(net, args, dev, lr=lr)))
+        st = LearnerStep(net, args, dev, lr=lr)
+        st.fold_deferral = False    # the shard's gradient complete in the flat buffer after _grads
+        reps.append((net, st))
     for _ in range(steps):
         grads = []
         for (net, st), sh in zip(reps, shards):
@@ -501,8 +503,11 @@ def _simulated_dp(name, dev, steps=2, world=2):
         total = sum(grads[1:], grads[0].clone())
         for net, st in reps:
             st.grads.flat.copy_(total)
-            st.grads.clip_(4.0)
-            st.optimizer.step()
+            if st.tail is not None:      # clip + Adam as the step tail's two launches
+                st.tail(None)
+            else:
+                st.grads.clip_(4.0)
+                st.optimizer.step()
     torch.cuda.synchronize()
     params = torch.cat([p.detach().reshape(-1) for p in reps[0][0].parameters()]).cpu()
     bufs = [torch.cat([b.detach().double().reshape(-1) for b in net.buffers()]).cpu() for net, _ in reps]

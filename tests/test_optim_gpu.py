@@ -156,7 +156,8 @@ def test_step_tail_matches_torch_clip_and_adam(cuda, graph):
 def test_grad_fold_norm_folds_partials(cuda):
     """hrl_grad_fold_norm's deferred folds: mode 0 columns of partial rows and mode 1 (a 32x32x3x3 conv weight from
     [tap][ci][co] rows) summed over the rows into their destinations of the flat buffer, the rest untouched; the
-    per-block sums of squares add up to the squared norm; the step count and the counters advance once."""
+    per-block sums of squares add up to the squared norm; the step count advances once and each counter by its
+    increment (a recurrent unroll's per-step BatchNorm counts T)."""
     import ctypes
     from handyrl_amd import _native
     lib = _native.load()
@@ -177,8 +178,8 @@ def test_grad_fold_norm_folds_partials(cuda):
     _native.check(lib.hrl_grad_fold_norm(
         P(flat), n, _native.ptr_array([f[0] for f in folds]), i64([f[1] for f in folds]), i64([f[2] for f in folds]),
         i64([f[3] for f in folds]), i64([f[4] for f in folds]), i64([f[5] for f in folds]),
-        (ctypes.c_int * 3)(*[f[6] for f in folds]), 3, P(step), _native.ptr_array(ctr), 3, P(norm_part), nb * 8,
-        _native.stream_of(cuda)), 'fold')
+        (ctypes.c_int * 3)(*[f[6] for f in folds]), 3, P(step), _native.ptr_array(ctr), i64([1, 16, 3]), 3,
+        P(norm_part), nb * 8, _native.stream_of(cuda)), 'fold')
     torch.cuda.synchronize(cuda)
     ref = before.double().cpu()
     conv = p1.double().sum(0).view(9, 32, 32).permute(2, 1, 0).reshape(-1)   # (tap, ci, co) -> (co, ci, tap)
@@ -190,4 +191,4 @@ def test_grad_fold_norm_folds_partials(cuda):
     assert torch.equal(got[9216:9226], before[9216:9226].double().cpu())
     tot = float(norm_part.sum())
     assert abs(tot - float((got ** 2).sum())) <= 1e-9 * tot
-    assert float(step) == 1.0 and all(int(c) == 1 for c in ctr)
+    assert float(step) == 1.0 and [int(c) for c in ctr] == [1, 16, 3]   # each counter by its increment

@@ -60,8 +60,7 @@ def _run(golden, device, loss_fn=None, graph=False):
         assert tr.steps == ep['steps']
         assert tr.data_cnt_ema == pytest.approx(ep['data_cnt_ema'], rel=1e-12)
         assert tr.lr == pytest.approx(ep['lr'], rel=1e-12)
-        lr = tr.learner.optimizer.param_groups[0]['lr']
-        assert float(lr) == pytest.approx(ep['lr'], rel=1e-6)
+        assert tr.learner.current_lr() == pytest.approx(ep['lr'], rel=1e-6)
     state = tr.model.state_dict()
     for k in arrays.files:
         if k.startswith('final.'):

@@ -1,6 +1,6 @@
 """Per-wave phase timeline of the tile-shared chain block backward (conv3x3_block_bwd2_kernel).
 
-    python tools/bb2_stamps.py --build     # here (CPU): tools/micro/libhrl_stamps.so with -DHRL_STAMPS
+    python tools/bb2_stamps.py --build     # here (CPU): tools/diag/libhrl_stamps.so with -DHRL_STAMPS
     python tools/bb2_stamps.py             # on the GPU box
 
 Lane 0 of every wave writes s_memtime, without draining its memory operations, at the phase boundaries of
@@ -12,7 +12,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, 'tools', 'micro', 'libhrl_stamps.so')
+LIB = os.path.join(ROOT, 'tools', 'diag', 'libhrl_stamps.so')
 
 
 def main():

@@ -1,6 +1,6 @@
 """Per-phase wave timelines of the scan and fused-loss kernels from in-kernel clock stamps.
 
-    python tools/stamps.py --build     # here (CPU): tools/micro/libhrl_stamps.so with -DHRL_STAMPS
+    python tools/stamps.py --build     # here (CPU): tools/diag/libhrl_stamps.so with -DHRL_STAMPS
     python tools/stamps.py             # on the GPU box
 
 The diagnostic library is the product sources built with -DHRL_STAMPS (hrl_scan.h): lane 0 of each
@@ -14,7 +14,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, 'tools', 'micro', 'libhrl_stamps.so')
+LIB = os.path.join(ROOT, 'tools', 'diag', 'libhrl_stamps.so')   # not gpurun-ignored: it travels to the box
 SRCS = sorted(f for f in os.listdir(os.path.join(ROOT, 'handyrl_amd', 'csrc')) if f.endswith('.hip'))   # all: _native binds every symbol
 
 
