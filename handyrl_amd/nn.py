@@ -1107,10 +1107,14 @@ class _TorusTower(torch.autograd.Function):
     Per unit only h_i and y_i reach HBM (as with the per-unit Functions); the residual-apply and masked
     reduce passes of nn.torus_block are gone.  ``units`` carries each BatchNorm's running statistics,
     momentum and eps; ``params`` is (conv weight, conv bias, bn weight, bn bias) per unit.
+
+    residual_in: the chain starts at a residual unit whose input x is also its residual (the upper part of a
+    tower split in two, torus_tower's `split`): h_1 = relu(x + bn_0(conv_0(x))), and the input gradient adds
+    the residual branch (g_1 [h_1 > 0]) to the first conv's adjoint.
     """
 
     @staticmethod
-    def forward(ctx, x, units, *params):
+    def forward(ctx, x, units, residual_in, *params):
         x = x.contiguous()
         N, Cin, H, W = x.shape
         HW = H * W
@@ -1135,7 +1139,8 @@ class _TorusTower(torch.autograd.Function):
                                                          None, *ws_), 'hrl_torus_conv_forward(stats)')
             else:
                 h = torch.empty(N, 32, H, W, device=dev, dtype=x.dtype)
-                _native.check(lib.hrl_torus_unit_forward(P(ys[-1]), P(hs[-1]) if i >= 2 else None, P(coef[i - 1, 2]),
+                res = hs[-1] if (i >= 2 or residual_in) else None
+                _native.check(lib.hrl_torus_unit_forward(P(ys[-1]), P(res), P(coef[i - 1, 2]),
                                                          P(coef[i - 1, 3]), P(h), N, H, W, P(w), P(b), P(y), P(part),
                                                          *ws_), 'hrl_torus_unit_forward')
                 hs.append(h)
@@ -1145,12 +1150,13 @@ class _TorusTower(torch.autograd.Function):
                                                     P(coef[i, 3]), stream), 'hrl_bn_finalize_stats')
             ys.append(y)
         out = torch.empty_like(ys[-1])
-        _native.check(lib.hrl_bn_apply_residual(P(ys[-1]), P(hs[-1]) if n >= 2 else None, N, 32, HW,
+        _native.check(lib.hrl_bn_apply_residual(P(ys[-1]), P(hs[-1]) if (n >= 2 or residual_in) else None, N, 32, HW,
                                                 P(coef[n - 1, 2]), P(coef[n - 1, 3]), P(out), stream),
                       'hrl_bn_apply_residual')
         gammas = [params[4 * i + 2] for i in range(n)]
         ctx.save_for_backward(out, coef, *weights, *gammas, *ys, *hs)
         ctx.n = n
+        ctx.residual_in = bool(residual_in)
         ctx.has_bias = [params[4 * i + 1] is not None for i in range(n)]
         return out
 
@@ -1196,8 +1202,10 @@ class _TorusTower(torch.autograd.Function):
             if i == 0:
                 if ctx.needs_input_grad[0]:
                     dx = torch.empty_like(x)
+                    # residual_in: + the residual branch g_1 [h_1 > 0] (h_1: the next unit's input, or the output)
+                    add, mask = (g_cur, hs[1] if n > 1 else out) if ctx.residual_in else (None, None)
                     _native.check(lib.hrl_torus_conv_forward(P(dy), N, Cin, 32, H, W, P(weights[0]), None, 1, P(dx),
-                                                             None, None, None, P(ws), ws_bytes, stream),
+                                                             None, P(add), P(mask), P(ws), ws_bytes, stream),
                                   'hrl_torus_conv_forward(flip)')
                 break
             out_i = hs[i + 1] if i + 1 < n else out
@@ -1214,13 +1222,32 @@ class _TorusTower(torch.autograd.Function):
                                                            P(kg[0]), P(kg[1]), P(dy), stream),
                           'hrl_bn_backward_apply_masked')
             g_cur = g_prev
-        return (dx, None, *grads)
+        return (dx, None, None, *grads)
+
+
+# A data-parallel learner's segmented capture (trainer.LearnerStep._grab_cut_tensor): called with the tensor
+# between the two parts of a split tower, it returns the view that is the backward's cut
+_CUT_FN = None
 
 
 def torus_tower(x, units):
     """The chain relu(bn(conv(x))) -> relu(h + bn(conv(h))) ... over training-mode TorusConv2d ``units``
     (GeeseNet's conv0 and blocks, hungry_geese.py:48-51) as one HIP Function (_TorusTower); each
-    BatchNorm module's batch counter and running statistics advance as in its forward."""
+    BatchNorm module's batch counter and running statistics advance as in its forward.
+
+    ``units[0].tower_split = k`` (set by a data-parallel LearnerStep) runs it as two Functions, units [0, k) and
+    [k, n) (the second with residual_in), so the backward can be cut between them and the upper part's gradient
+    all-reduce overlaps the lower part's backward; the value between them passes through _CUT_FN when set."""
+    k = getattr(units[0], 'tower_split', None)
+    if k is not None and 0 < k < len(units):
+        h = _tower_part(x, units[:k], False)
+        if _CUT_FN is not None:
+            h = _CUT_FN(h)
+        return _tower_part(h, units[k:], True)
+    return _tower_part(x, units, False)
+
+
+def _tower_part(x, units, residual_in):
     meta, params = [], []
     for unit in units:
         bn = unit.bn
@@ -1232,7 +1259,7 @@ def torus_tower(x, units):
         meta.append((bn.running_mean if bn.track_running_stats else None,
                      bn.running_var if bn.track_running_stats else None, momentum, bn.eps))
         params += [unit.conv.weight, unit.conv.bias, bn.weight, bn.bias]
-    return _TorusTower.apply(x, meta, *params)
+    return _TorusTower.apply(x, meta, residual_in, *params)
 
 
 class _GeesePool(torch.autograd.Function):

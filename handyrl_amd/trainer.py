@@ -119,6 +119,17 @@ class StepTail:
         return self.total
 
 
+def split_torus_tower(net):
+    """Run a torus-conv tower (GeeseNet) as two Functions split after its middle unit (nn.torus_tower), so a
+    data-parallel segmented capture can all-reduce the upper half's gradients while the lower half's backward
+    replays (hungry_geese.py:48-51: conv0 and 12 blocks -> units [0, 7) and [7, 13)).  Same values as the one
+    Function up to the order of the BatchNorm sums at the split."""
+    from .envs.hungry_geese import TorusConv2d
+    torus = [m for m in net.modules() if isinstance(m, TorusConv2d)]
+    if len(torus) >= 2:
+        torus[0].tower_split = (len(torus) + 1) // 2
+
+
 class LearnerStep:
     def __init__(self, net, args, device, lr=None, graph=False, reduce_group=None, world_size=1,
                  bucket_bytes=256 * 1024, hip_layers=True, loss_fn=None, segment_backward=True):
@@ -137,6 +148,7 @@ class LearnerStep:
         self.reducer = None
         if world_size > 1:
             self.reducer = hdist.GradAllReduce(self.grads, group=reduce_group, bucket_bytes=bucket_bytes)
+            split_torus_tower(self.net)
         if lr is None:
             # train.py:318-321: lr = 3e-8 * batch_size * forward_steps for the batch ONE update sees.
             # Here args['batch_size'] is the per-rank shard and the gradients are SUMmed over the ranks,
@@ -413,8 +425,7 @@ class LearnerStep:
             # thread-local capture: the process group's watchdog thread may query its events meanwhile
             if self.segments is not None:
                 seg2 = torch.cuda.CUDAGraph()
-                handle = self._cut_module().register_forward_pre_hook(self._grab_cut)
-                try:
+                with self._cut_hook():
                     with direct_grads():
                         with torch.cuda.graph(grads_graph, capture_error_mode='thread_local'):
                             self.grads.zero()
@@ -424,9 +435,6 @@ class LearnerStep:
                             backward_total(losses, inputs=[cut] + upper, retain_graph=True)
                         with torch.cuda.graph(seg2, capture_error_mode='thread_local'):
                             torch.autograd.backward(cut, grad_tensors=cut.grad, inputs=lower)
-                finally:
-                    handle.remove()
-                    self._cut = None
             else:
                 with torch.cuda.graph(grads_graph, capture_error_mode='thread_local'):
                     losses, dcnt = self._grads(batch, hidden)
@@ -438,6 +446,34 @@ class LearnerStep:
         self._graph, self._graph_update, self._graph_seg2 = grads_graph, update_graph, seg2
 
     # -- data parallel: two backward segments ------------------------------------------------------
+    @contextlib.contextmanager
+    def _cut_hook(self):
+        """Inside: the step's forward records the segment cut in self._cut -- the fused conv chain's input (a
+        forward pre-hook on it) or the tensor between a split torus tower's two parts (nn._CUT_FN)."""
+        from . import nn as hnn
+        mod = self._cut_module()
+        handle = mod.register_forward_pre_hook(self._grab_cut) if mod is not None else None
+        prev = hnn._CUT_FN
+        if mod is None:
+            hnn._CUT_FN = self._grab_cut_tensor
+        try:
+            yield
+        finally:
+            if handle is not None:
+                handle.remove()
+            hnn._CUT_FN = prev
+            self._cut = None
+
+    def _has_cut_site(self):
+        if self._cut_module() is not None:
+            return True
+        return any(getattr(m, 'tower_split', None) for m in self.net.modules())
+
+    def _grab_cut_tensor(self, t):
+        cut = t.view_as(t)
+        self._cut = cut
+        return cut
+
     def _cut_module(self):
         """The fused conv chain (nn._ChainHeads / nn._ConvBNChain): the backward is cut at its input,
         the upper segment (loss, heads, chain) holds nearly all of the step's backward, the lower one
@@ -465,22 +501,17 @@ class LearnerStep:
     def _try_plan_segments(self, batch):
         """Eager dry run (forward + loss) that finds the segment cut and splits the parameters; leaves
         self.segments None when the net has no fused chain or its parameters do not split cleanly."""
-        mod = self._cut_module()
-        if mod is None:
-            self.segment_error = 'no fused conv chain in the net'
+        if not self._has_cut_site():
+            self.segment_error = 'no fused conv chain or split torus tower in the net'
             return
-        handle = mod.register_forward_pre_hook(self._grab_cut)
         try:
-            with direct_grads():
+            with self._cut_hook(), direct_grads():
                 outputs = forward_prediction(self.net, None, batch, self.args)
                 losses, _ = self.loss_fn(outputs, batch, self.args)
                 self._plan_segments(losses['total'])
         except RuntimeError as e:
             self.segments = None
             self.segment_error = str(e)
-        finally:
-            handle.remove()
-            self._cut = None
 
     def _plan_segments(self, loss):
         """Split the live parameters at the cut tensor by walking the autograd graph: `upper` are reached

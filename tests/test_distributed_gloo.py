@@ -343,21 +343,19 @@ def test_rccl_graph_step_matches_single_gpu_step(cuda):
         assert abs(res['sums'][k] - ref_sums[k]) <= 1e-4 * max(1.0, abs(ref_sums[k])), k
 
 
-def _segmented_rank_main(rank, world, port, out_path, steps, segment=True):
+def _segmented_rank_main(rank, world, port, out_path, steps, segment=True, name='TicTacToe'):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK='0')
-    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
-    from handyrl_amd.synthetic import tictactoe_batch, default_args
     from handyrl_amd.trainer import LearnerStep
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    B, T = 64, 9
-    batch = tictactoe_batch(B, T, dev, seed=4)
+    cls, batch, args, _ = _net_case(name, dev)
+    B = batch['value'].size(0)
     shard = {k: v[rank * B // world:(rank + 1) * B // world].contiguous() for k, v in batch.items()}
-    args = default_args(T, B // world)   # per-rank shard; LearnerStep's lr is the global batch's
+    args = dict(args, batch_size=B // world)   # per-rank shard; LearnerStep's lr is the global batch's
     torch.manual_seed(0)
-    step = LearnerStep(SimpleConv2dModel(), args, dev, graph=True, world_size=world, segment_backward=segment)
+    step = LearnerStep(cls(), args, dev, graph=True, world_size=world, segment_backward=segment)
     for _ in range(steps):
         step.step(shard)
     sums, _ = step.pop_stats()
@@ -397,6 +395,10 @@ def test_segmented_graph_step_matches_one_segment_step(cuda):
     (up_ranges, up_names), (low_ranges, low_names) = r['sched']
     assert sorted(low_names) == ['conv.bias', 'conv.weight'], low_names      # the stem (tictactoe.py:55)
     assert any(n.startswith('blocks.') for n in up_names) and any(n.startswith('head') for n in up_names)
+    _check_same_step(r, ref, up_ranges, low_ranges)
+
+
+def _check_same_step(r, ref, up_ranges, low_ranges):
     covered = sorted(up_ranges + low_ranges)
     assert covered[0][0] == 0 and covered[-1][1] == r['numel']
     assert all(a[1] <= b[0] for a, b in zip(covered, covered[1:]))           # disjoint
@@ -411,6 +413,34 @@ def test_segmented_graph_step_matches_one_segment_step(cuda):
     assert not diff, diff
     for k in ('p', 'v', 'ent', 'total', 'dcnt'):
         assert r['sums'][k] == ref['sums'][k], k
+
+
+@pytest.mark.gpu
+def test_segmented_geese_tower_step_matches_one_segment_step(cuda):
+    """GeeseNet's data-parallel graph step in two backward segments: the torus tower runs as two Functions
+    (units [0, 7) and [7, 13), hungry_geese.py:48-51), the cut is the tensor between them, and the upper segment's
+    gradients (blocks 6-11 and the heads) are all-reduced while the lower segment (conv0 and blocks 0-5) replays.
+    The schedule: two segments with exactly that parameter split, the buckets' ranges disjoint and covering the
+    flat buffer.  Two ranks (gloo, one GPU) give exactly the parameters and loss sums of the same two-rank step
+    captured as one backward graph (the same split tower) with one flat all-reduce."""
+    steps = 2
+    res = {}
+    with tempfile.TemporaryDirectory() as d:
+        for seg in (True, False):
+            out = os.path.join(d, 'g_%d.pt' % seg)
+            mp.spawn(_segmented_rank_main, args=(2, _free_port(), out, steps, seg, 'Geese'), nprocs=2, join=True)
+            res[seg] = torch.load(out, weights_only=True)
+    r, ref = res[True], res[False]
+    assert r['seg2'] and len(r['sched']) == 2, r['why']
+    assert not ref['seg2']
+    (up_ranges, up_names), (low_ranges, low_names) = r['sched']
+    lower_units = {'conv0'} | {'blocks.%d' % i for i in range(6)}
+    assert {n.rsplit('.', 2)[0] if n.startswith('blocks.') else n.split('.')[0] for n in low_names} == lower_units, \
+        low_names
+    assert all(n.startswith(('blocks.', 'head_')) for n in up_names)
+    assert {'blocks.%d' % i for i in range(6, 12)} <= {'.'.join(n.split('.')[:2]) for n in up_names}
+    assert any(n.startswith('head_') for n in up_names)
+    _check_same_step(r, ref, up_ranges, low_ranges)
 
 
 def _net_case(name, dev):
@@ -479,7 +509,7 @@ def _simulated_dp(name, dev, steps=2, world=2):
     as under the reference's nn.DataParallel), each computing its shard's gradients with LearnerStep's own
     backward; the SUM of the replicas' gradients is clipped and applied by Adam with the global batch's lr
     (3e-8 * world * B_shard * T, train.py:318) on every replica."""
-    from handyrl_amd.trainer import LearnerStep
+    from handyrl_amd.trainer import LearnerStep, split_torus_tower
     cls, batch, args, rec = _net_case(name, dev)
     B = batch['value'].size(0)
     args = dict(args, batch_size=B // world)
@@ -491,6 +521,7 @@ def _simulated_dp(name, dev, steps=2, world=2):
     for r in range(world):
         torch.manual_seed(0)
         net = cls()
+        split_torus_tower(net)      # as a data-parallel LearnerStep runs GeeseNet's tower
         st = LearnerStep(net, args, dev, lr=lr)
         st.fold_deferral = False    # the shard's gradient complete in the flat buffer after _grads
         reps.append((net, st))

@@ -229,13 +229,15 @@ def test_fused_torus_block_matches_torch(cuda, residual, cin, N):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('split', [None, 1, 2, 3])
 @pytest.mark.parametrize('N', [41, 1500])
-def test_torus_tower_matches_unit_chain(cuda, N):
+def test_torus_tower_matches_unit_chain(cuda, N, split):
     """nn.torus_tower (BN apply folded into the next conv's prologue, the previous unit's masked BN
     reduce folded into the input gradient's epilogue) vs the per-unit Functions (nn.torus_block):
     the forward, the hidden states and the running statistics are bit-identical (same arithmetic,
     one pass less); the backward's BN sums are folded in another order, so gradients agree to
-    fp32 rounding."""
+    fp32 rounding.  split k: the tower as two Functions, units [0, k) and [k, 4) (the second starting at a
+    residual unit: a data-parallel learner's segmented capture), the same values."""
     from handyrl_amd.nn import torus_block, torus_tower
     torch.manual_seed(N)
     ref_units = [TorusConv2d(17, 32, (3, 3), True)] + [TorusConv2d(32, 32, (3, 3), True) for _ in range(3)]
@@ -249,6 +251,8 @@ def test_torus_tower_matches_unit_chain(cuda, N):
         b.load_state_dict(a.state_dict())
     for u in units_a + units_b:
         u.use_hip = True
+    if split is not None:
+        units_b[0].tower_split = split
     x = torch.randn(N, 17, 7, 11, device=cuda)
     g = torch.randn(N, 32, 7, 11, device=cuda)
     xa = x.clone().requires_grad_(True)
