@@ -1550,12 +1550,9 @@ __device__ __forceinline__ void wait_tile_after(int it) {
     static_assert(kSlots == 5, "the early-iteration counts above are written for kSlots = 5");
 }
 
-template <bool PRO, int W, bool STAG>
+template <bool PRO, int W>
 __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, int lane) {
     constexpr int kCt = W & 1, G = W >> 1;
-    // STAG (fwd form 3): waves 4-7 compute tile it before staging tile it+1, so on each SIMD one wave's staging
-    // VALU runs beside its partner's MFMAs instead of both staging, then both computing
-    constexpr bool kLate = STAG && W >= 4;
     using C = Cells<G>;
     constexpr int kNq = C::kN;
     constexpr int NP = pieces_of<W>();
@@ -1658,7 +1655,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         // tile it's slot was read by stage(it) before the last barrier: tile it + kSlots goes there
         dma(it + kSlots, slot);
         const int next = slot + 1 == kSlots ? 0 : slot + 1;
-        if constexpr (!kLate) stage(it + 1, next);           // runs past the last tile too (stale rows, unread)
+        stage(it + 1, next);                                 // runs past the last tile too (stale rows, unread)
         BB2_STAMP(it, 1);
         // the MFMAs of tile it: acc[s] += sum_p x'_p (16 rows x 32 ci) . W[tap(p, q_s)][kCt], p ascending
         const unsigned char *img = smem + kImg0 + (it & 1) * bb2::kImgBytes;
@@ -1735,7 +1732,6 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
                 __builtin_amdgcn_raw_buffer_store_b64(v, od, off, 0, 0);
             }
         }
-        if constexpr (kLate) stage(it + 1, next);
         wait_tile_after<NP, NS>(it);                         // tile it+2 landed (it+3 .. it+kSlots in flight)
         BB2_STAMP(it, 3);
         bb2::bar_lds();                                      // tile it+1's image staged, tile it's image free
@@ -1759,20 +1755,20 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
 
 }  // namespace fw3
 
-template <bool PRO, bool STAG>
+template <bool PRO>
 __global__ __launch_bounds__(bb2::kThreads) void conv3x3_fwd_dma_kernel(BlockBwdArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[fw3::kLdsBytes];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     switch (wave) {
-    case 0: fw3::run<PRO, 0, STAG>(a, smem, lane); break;
-    case 1: fw3::run<PRO, 1, STAG>(a, smem, lane); break;
-    case 2: fw3::run<PRO, 2, STAG>(a, smem, lane); break;
-    case 3: fw3::run<PRO, 3, STAG>(a, smem, lane); break;
-    case 4: fw3::run<PRO, 4, STAG>(a, smem, lane); break;
-    case 5: fw3::run<PRO, 5, STAG>(a, smem, lane); break;
-    case 6: fw3::run<PRO, 6, STAG>(a, smem, lane); break;
-    default: fw3::run<PRO, 7, STAG>(a, smem, lane); break;
+    case 0: fw3::run<PRO, 0>(a, smem, lane); break;
+    case 1: fw3::run<PRO, 1>(a, smem, lane); break;
+    case 2: fw3::run<PRO, 2>(a, smem, lane); break;
+    case 3: fw3::run<PRO, 3>(a, smem, lane); break;
+    case 4: fw3::run<PRO, 4>(a, smem, lane); break;
+    case 5: fw3::run<PRO, 5>(a, smem, lane); break;
+    case 6: fw3::run<PRO, 6>(a, smem, lane); break;
+    default: fw3::run<PRO, 7>(a, smem, lane); break;
     }
 }
 
@@ -1898,7 +1894,7 @@ int hrl_conv3x3_set_block_form(int form) {
 
 int hrl_conv3x3_set_fwd_form(int form) {
     const int prev = g_fwd_form;
-    g_fwd_form = form < 0 ? 0 : (form > 3 ? 3 : form);
+    g_fwd_form = form < 0 ? 0 : (form > 2 ? 2 : form);
     return prev;
 }
 
@@ -1934,12 +1930,9 @@ int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, con
         BlockBwdArgs a{};
         a.x = x; a.in_alpha = in_alpha; a.in_beta = in_beta; a.wpk = wpk; a.gin = y; a.part = part; a.M = M;
         const dim3 grid(grid_for(M)), block(bb2::kThreads);
-        if (g_fwd_form == 3) {
-            if (in_alpha) hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<true, true>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<false, true>), grid, block, 0, s, a);
-        } else if (g_fwd_form == 2) {
-            if (in_alpha) hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<true, false>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<false, false>), grid, block, 0, s, a);
+        if (g_fwd_form == 2) {
+            if (in_alpha) hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<true>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<false>), grid, block, 0, s, a);
         } else if (in_alpha) {
             hipLaunchKernelGGL((conv3x3_block_bwd2_kernel<true, 1>), grid, block, 0, s, a);
         } else {

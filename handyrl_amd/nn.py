@@ -58,6 +58,7 @@ class DeferredGrads:
 
     def __init__(self):
         self.conv = {}     # (param, bias param, in slice, padding) -> [(x, dy)]
+        self.late_params = set()   # ids of the weights with a late record (flushed in phase 2)
         self.affine = {}   # (weight, bias) -> [(dweight, dbias)]
         self.adjoint = {}  # (param, in slice) -> the input-gradient conv's packed weights, packed once per step
 
@@ -71,18 +72,31 @@ class DeferredGrads:
             pk = self.adjoint[key] = fn(w.detach(), ci0, cin)
         return pk
 
-    def add_conv(self, key, x, dy):
+    def add_conv(self, key, x, dy, late=False):
+        """late: the record belongs to the unroll's innermost cells (GeisterNet's DRC), whose weight gradients a
+        data-parallel step flushes last (flush(phase=2)) so the other buckets' all-reduce runs meanwhile."""
         self.conv.setdefault(key, []).append((x, dy))
+        if late:
+            self.late_params.add(id(key[0]))
 
     def add_affine(self, key, dw, db):
         self.affine.setdefault(key, []).append((dw, db))
 
+    def late_ids(self):
+        """ids of the parameters flush(phase=2) completes: the weights with a late record and the biases recorded
+        with them."""
+        return set(self.late_params) | {id(k[1]) for k in self.conv if id(k[0]) in self.late_params and
+                                        k[1] is not None}
+
     @torch.no_grad()
-    def flush(self):
+    def flush(self, phase=None):
         """Accumulate the deferred gradients into .grad; returns the parameters that got one, each once
-        (a ConvLSTM h-conv weight is recorded once per input slice)."""
+        (a ConvLSTM h-conv weight is recorded once per input slice).  phase 1: every weight without a late record
+        (and the affine records); phase 2: the rest; None: both."""
         touched = {}
-        for (w, b, sl, pad), rec in self.conv.items():
+        keys = [k for k in self.conv if phase is None or ((id(k[0]) in self.late_params) == (phase == 2))]
+        for key in keys:
+            (w, b, sl, pad), rec = key, self.conv.pop(key)
             wv = w if sl is None else w[:, sl[0]:sl[1]]
             if GBOARD_WGRAD and _gboard_wgrad_ok(rec, wv, pad):
                 # the 6x6 board: games as the MFMA K over every recorded use, no concatenation (hrl_gboard_wgrad)
@@ -116,16 +130,18 @@ class DeferredGrads:
             if b is not None:
                 _add_grad(b, db, None)
                 touched[id(b)] = b
-        for (w, b), rec in self.affine.items():
-            if w is not None:
-                _add_grad(w, rec[0][0] if len(rec) == 1 else torch.stack([r[0] for r in rec]).sum(0), None)
-                touched[id(w)] = w
-            if b is not None:
-                _add_grad(b, rec[0][1] if len(rec) == 1 else torch.stack([r[1] for r in rec]).sum(0), None)
-                touched[id(b)] = b
-        self.conv.clear()
-        self.affine.clear()
-        self.adjoint.clear()
+        if phase != 2:
+            for (w, b), rec in self.affine.items():
+                if w is not None:
+                    _add_grad(w, rec[0][0] if len(rec) == 1 else torch.stack([r[0] for r in rec]).sum(0), None)
+                    touched[id(w)] = w
+                if b is not None:
+                    _add_grad(b, rec[0][1] if len(rec) == 1 else torch.stack([r[1] for r in rec]).sum(0), None)
+                    touched[id(b)] = b
+            self.affine.clear()
+        if phase != 1:
+            self.conv.clear()
+            self.adjoint.clear()
         return list(touched.values())
 
 
@@ -682,7 +698,7 @@ class _DRCStep(torch.autograd.Function):
                     _native.ptr(g_r), _native.ptr(c_r), _native.ptr(co_r), _native.ptr(dh_t), dh_stride, dh_parts,
                     H * 36, _native.ptr(gc), N, H, 36, _native.ptr(dz), _native.ptr(dcr), _native.ptr(acc),
                     int(r == R - 1), _native.stream_of(dz.device)), 'hrl_lstm_gates_backward_ex')
-                rec.add_conv((w, None, sl, tuple(pad)), h_r, dz)
+                rec.add_conv((w, None, sl, tuple(pad)), h_r, dz, late=True)
                 gc = dcr
                 if r == 0 and not ctx.needs_input_grad[1 + L + i]:
                     break

@@ -174,6 +174,7 @@ class LearnerStep:
         self._graph_update = None
         self.segments = None        # data parallel: [(flat-buffer ranges, params)] per backward segment
         self.segment_error = None   # why the step stayed one backward graph
+        self._late_ids = set()      # recurrent nets: the weights whose deferred gradients are flushed last
         self.segment_backward = segment_backward
         self._cut = None            # forward pre-hook state: the fused chain's input (the segment cut)
         self._static = None
@@ -263,10 +264,15 @@ class LearnerStep:
                 outputs = forward_prediction(self.net, hidden, batch, self.args)
                 losses, dcnt = self.loss_fn(outputs, batch, self.args)
                 backward_total(losses)
-            touched = deferred.flush()
             self._folds = df if self.fold_deferral else None
-            if self.reducer is not None:
-                self.reducer.mark_ready(touched)
+            self._late_ids = deferred.late_ids()
+            if self.reducer is None:
+                deferred.flush()
+            else:
+                # data parallel: the weights outside the recurrent cells first, so their buckets can launch
+                # while the cells' (late) weight gradients are formed
+                self.reducer.mark_ready(deferred.flush(phase=1))
+                self.reducer.mark_ready(deferred.flush(phase=2))
         else:
             # the HIP Functions write single-use parameter gradients straight into the flat buffer
             # (zeroed above) instead of autograd's per-parameter accumulate-adds (nn.direct_grads); on one GPU
@@ -404,6 +410,8 @@ class LearnerStep:
                 self._body(batch, hidden)
             if self.reducer is not None and hidden is None and self.segment_backward:
                 self._try_plan_segments(batch)   # its forward's BatchNorm updates are undone below
+            elif self.reducer is not None and hidden is not None and self.defer and self.segment_backward:
+                self._plan_flush_segments()
         torch.cuda.current_stream(self.device).wait_stream(side)
         with torch.no_grad():
             for p, v in zip(params, saved_p):
@@ -423,7 +431,19 @@ class LearnerStep:
         try:
             grads_graph, update_graph = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             # thread-local capture: the process group's watchdog thread may query its events meanwhile
-            if self.segments is not None:
+            if self.segments is not None and hidden is not None:
+                # recurrent net: the backward and the first flush phase, then the cells' flush
+                seg2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(grads_graph, capture_error_mode='thread_local'):
+                    self.grads.zero()
+                    with deferred_weight_grads() as deferred:
+                        outputs = forward_prediction(self.net, hidden, batch, self.args)
+                        losses, dcnt = self.loss_fn(outputs, batch, self.args)
+                        backward_total(losses)
+                    deferred.flush(phase=1)
+                with torch.cuda.graph(seg2, capture_error_mode='thread_local'):
+                    deferred.flush(phase=2)
+            elif self.segments is not None:
                 seg2 = torch.cuda.CUDAGraph()
                 with self._cut_hook():
                     with direct_grads():
@@ -513,6 +533,28 @@ class LearnerStep:
             self.segments = None
             self.segment_error = str(e)
 
+    def _plan_flush_segments(self):
+        """Recurrent net, data parallel: segment 1 = the live parameters completed by the backward and the first
+        flush phase, segment 2 = the recurrent cells' weights (late records, nn.DeferredGrads.flush(phase=2)), as
+        flat-buffer ranges.  None when the unroll records nothing late."""
+        late = [p for p, l in zip(self.params, self.live) if l and id(p) in self._late_ids]
+        early = [p for p, l in zip(self.params, self.live) if l and id(p) not in self._late_ids]
+        if not late or not early:
+            self.segments = None
+            self.segment_error = 'no late (recurrent-cell) weight records in the unroll'
+            return
+        self.segments = [(self._ranges(early), early), (self._ranges(late), late)]
+
+    def _ranges(self, ps):
+        index = {id(p): i for i, p in enumerate(self.params)}
+        out = []
+        for off, n in sorted(self.grads.slices[index[id(p)]] for p in ps):
+            if out and out[-1][1] == off:
+                out[-1][1] = off + n
+            else:
+                out.append([off, off + n])
+        return [tuple(r) for r in out]
+
     def _plan_segments(self, loss):
         """Split the live parameters at the cut tensor by walking the autograd graph: `upper` are reached
         from the loss without passing the cut's node, `lower` from the cut.  Both sets disjoint and each a
@@ -540,17 +582,7 @@ class LearnerStep:
         lower = [p for p, l in zip(self.params, live) if l and id(p) in low]
         if set(map(id, upper)) & set(map(id, lower)) or len(upper) + len(lower) != sum(live):
             raise RuntimeError('segmented capture: parameters shared across the cut')
-        index = {id(p): i for i, p in enumerate(self.params)}
-
-        def ranges(ps):
-            out = []
-            for off, n in sorted(self.grads.slices[index[id(p)]] for p in ps):
-                if out and out[-1][1] == off:
-                    out[-1][1] = off + n
-                else:
-                    out.append([off, off + n])
-            return [tuple(r) for r in out]
-        self.segments = [(ranges(upper), upper), (ranges(lower), lower)]
+        self.segments = [(self._ranges(upper), upper), (self._ranges(lower), lower)]
         return cut, upper, lower
 
     def load_batch(self, batch):

@@ -174,9 +174,8 @@ int hrl_conv3x3_set_split(int on);
  * association.  Process-wide; returns the previous setting. */
 int hrl_conv3x3_set_block_form(int form);
 /* The chain's forward conv with BN statistics (hrl_conv3x3_forward_ex, epilogue 1, packed weights, no bias):
- * 2 (default) = the LDS-DMA ring form (every wave computes, x' staged from a raw ring), 3 = the same with waves 4-7
- * computing before they stage (a stagger of each SIMD's two waves), 1 = the block backward's tile-shared form,
- * 0 = the per-wave conv3x3_kernel (tools/fwd_form_bench.py).  Returns the previous. */
+ * 2 (default) = the LDS-DMA ring form (every wave computes, x' staged from a raw ring), 1 = the block backward's
+ * tile-shared form, 0 = the per-wave conv3x3_kernel (tools/fwd_form_bench.py).  Returns the previous. */
 int hrl_conv3x3_set_fwd_form(int form);
 /* Both packed layouts of n <= 8 weights (32, 32, 3, 3) in one launch: packed[(l*2 + f) * 9216], f = 0 forward,
  * 1 input gradient (host array of device pointers).  hrl_conv3x3_forward_ex with flip | 2 takes `weight`

@@ -350,14 +350,18 @@ def _segmented_rank_main(rank, world, port, out_path, steps, segment=True, name=
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    cls, batch, args, _ = _net_case(name, dev)
+    cls, batch, args, rec = _net_case(name, dev)
     B = batch['value'].size(0)
-    shard = {k: v[rank * B // world:(rank + 1) * B // world].contiguous() for k, v in batch.items()}
+    shard = {k: (v[rank * B // world:(rank + 1) * B // world].contiguous() if isinstance(v, torch.Tensor) else
+                 {kk: vv[rank * B // world:(rank + 1) * B // world].contiguous() for kk, vv in v.items()})
+             for k, v in batch.items()}
     args = dict(args, batch_size=B // world)   # per-rank shard; LearnerStep's lr is the global batch's
     torch.manual_seed(0)
-    step = LearnerStep(cls(), args, dev, graph=True, world_size=world, segment_backward=segment)
+    net = cls()
+    step = LearnerStep(net, args, dev, graph=True, world_size=world, segment_backward=segment)
+    hidden = _hidden(net, B // world, batch['value'].size(2), dev) if rec else None
     for _ in range(steps):
-        step.step(shard)
+        step.step(shard, hidden)
     sums, _ = step.pop_stats()
     names = {id(p): n for n, p in step.net.named_parameters()}
     sched = [([tuple(r) for r in ranges], [names[id(p)] for p in ps]) for ranges, ps in (step.segments or [])]
@@ -441,6 +445,32 @@ def test_segmented_geese_tower_step_matches_one_segment_step(cuda):
     assert {'blocks.%d' % i for i in range(6, 12)} <= {'.'.join(n.split('.')[:2]) for n in up_names}
     assert any(n.startswith('head_') for n in up_names)
     _check_same_step(r, ref, up_ranges, low_ranges)
+
+
+@pytest.mark.gpu
+def test_segmented_geister_flush_step_matches_one_segment_step(cuda):
+    """GeisterNet's data-parallel graph step in two segments: the backward and the first flush phase (every
+    weight outside the DRC cells: stem, heads, the grouped BatchNorms) in the first graph, whose bucket is
+    all-reduced while the second graph flushes the cells' deferred weight gradients (nn.DeferredGrads late
+    records, the DRC step's h-half convolutions).  The schedule: the cells' conv weights alone in the second
+    segment, the ranges disjoint and covering the flat buffer.  Two ranks (gloo, one GPU) give exactly the
+    parameters and loss sums of the same step captured as one backward graph with one flat all-reduce."""
+    steps = 2
+    res = {}
+    with tempfile.TemporaryDirectory() as d:
+        for seg in (True, False):
+            out = os.path.join(d, 'q_%d.pt' % seg)
+            mp.spawn(_segmented_rank_main, args=(2, _free_port(), out, steps, seg, 'Geister'), nprocs=2, join=True)
+            res[seg] = torch.load(out, weights_only=True)
+    r, ref = res[True], res[False]
+    assert r['seg2'] and len(r['sched']) == 2, r['why']
+    assert not ref['seg2']
+    (early_ranges, early_names), (late_ranges, late_names) = r['sched']
+    assert late_names and all(n.startswith('body.blocks.') for n in late_names), late_names   # weights + biases
+    assert any(n.endswith('conv.weight') for n in late_names), late_names
+    assert any(n.startswith('head') for n in early_names) and not any(n.startswith('body.blocks.')
+                                                                     for n in early_names), early_names
+    _check_same_step(r, ref, early_ranges, late_ranges)
 
 
 def _net_case(name, dev):
