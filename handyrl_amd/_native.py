@@ -89,6 +89,7 @@ SIGNATURES = {
     'hrl_conv3x3_set_block_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_conv3x3_set_fwd_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_torus_set_split': (ctypes.c_int, [ctypes.c_int]),
+    'hrl_torus_set_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_conv3x3_pack_n': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _f32p, ctypes.c_void_p]),
     'hrl_conv3x3_forward_ex': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _f32p, _f32p, ctypes.c_int, _f32p,
                                               ctypes.c_int, _f32p, _f32p, _f32p, _f32p, ctypes.c_void_p,
@@ -219,7 +220,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 _lib = None
 

@@ -147,11 +147,27 @@ __device__ __forceinline__ void slice_to_lds(const float4 (&st)[kSV], float *til
 }
 
 // ------------------------------------------------------------------ forward
+// nf contiguous floats from LDS to global: float4 per lane where whole (dst 16-byte aligned: a 64-row block's
+// run), the tail one float at a time
+__device__ __forceinline__ void store_rows(const float *src, float *dst, int nf, int lane) {
+    if (reinterpret_cast<uintptr_t>(dst) & 15) {   // an unaligned caller buffer: one float per lane
+        for (int e = lane; e < nf; e += 64) dst[e] = src[e];
+        return;
+    }
+    for (int i = lane; 4 * i < nf; i += 64) {
+        if (4 * i + 4 <= nf) {
+            reinterpret_cast<float4 *>(dst)[i] = *reinterpret_cast<const float4 *>(src + 4 * i);
+        } else {
+            for (int e = 4 * i; e < nf; ++e) dst[e] = src[e];
+        }
+    }
+}
+
 __global__ __launch_bounds__(64, 2) void heads_fwd_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
                                                        float *__restrict__ a_p, float *__restrict__ a_v,
                                                        float *__restrict__ p_out, float *__restrict__ v_out,
                                                        bool tanh_v) {
-    __shared__ float tile[64 * kTS];
+    __shared__ __attribute__((aligned(16))) float tile[64 * kTS];
     __shared__ float sw1[kM * kC], sb1[kM], swp[kOP * kZP], swv[kHW], sal[kC], sbe[kC];
     const int lane = threadIdx.x;
     if (bn.alpha && lane < kC) {
@@ -238,30 +254,38 @@ __global__ __launch_bounds__(64, 2) void heads_fwd_kernel(const float *__restric
         }
 #pragma unroll
         for (int j = 0; j < kZ; ++j) a[j] = a[j] > 0.f ? a[j] : a[j] * kSlope;
-        if (lane < nrows) {
-            const int64_t n = base + lane;
-            float p[kOP];
+        float p[kOP];
 #pragma unroll
-            for (int k = 0; k < kOP; ++k) {
-                asm volatile("" ::: "memory");   // one output's 18 weights in flight at a time, not all 162
-                float t = 0.f;
+        for (int k = 0; k < kOP; ++k) {
+            asm volatile("" ::: "memory");   // one output's 18 weights in flight at a time, not all 162
+            float t = 0.f;
 #pragma unroll
-                for (int j = 0; j < kZP; ++j) t = __builtin_fmaf(swp[k * kZP + j], a[j], t);
-                p[k] = t;
-            }
-            float v = 0.f;
-#pragma unroll
-            for (int q = 0; q < kHW; ++q) v = __builtin_fmaf(swv[q], a[kZP + q], v);
-#pragma unroll
-            for (int k = 0; k < kOP; ++k) p_out[n * kOP + k] = p[k];
-            v_out[n] = tanh_v ? tanhf(v) : v;   // the model's torch.tanh on the value head, folded
-            if (a_p) {
-#pragma unroll
-                for (int j = 0; j < kZP; ++j) a_p[n * kZP + j] = a[j];
-#pragma unroll
-                for (int q = 0; q < kHW; ++q) a_v[n * kHW + q] = a[kZP + q];
-            }
+            for (int j = 0; j < kZP; ++j) t = __builtin_fmaf(swp[k * kZP + j], a[j], t);
+            p[k] = t;
         }
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < kHW; ++q) v = __builtin_fmaf(swv[q], a[kZP + q], v);
+        v = tanh_v ? tanhf(v) : v;   // the model's torch.tanh on the value head, folded
+        // the block's outputs leave through the (dead) tile as contiguous runs: one row per lane straight from
+        // registers is a 36- or 72-byte stride across the wave's 64 rows, many partial lines per store
+        // (tile = [a_p 64 x 18 | a_v 64 x 9 | p 64 x 9 | v 64] = 64 x 37 floats)
+        float *to_ap = tile, *to_av = tile + 64 * kZP, *to_p = to_av + 64 * kHW, *to_v = to_p + 64 * kOP;
+#pragma unroll
+        for (int j = 0; j < kZP; ++j) to_ap[lane * kZP + j] = a[j];
+#pragma unroll
+        for (int q = 0; q < kHW; ++q) to_av[lane * kHW + q] = a[kZP + q];
+#pragma unroll
+        for (int k = 0; k < kOP; ++k) to_p[lane * kOP + k] = p[k];
+        to_v[lane] = v;
+        lds_fence();
+        store_rows(to_p, p_out + base * kOP, nrows * kOP, lane);
+        store_rows(to_v, v_out + base, nrows, lane);
+        if (a_p) {
+            store_rows(to_ap, a_p + base * kZP, nrows * kZP, lane);
+            store_rows(to_av, a_v + base * kHW, nrows * kHW, lane);
+        }
+        lds_fence();   // the stores' LDS reads are done before the next block's slices land in the tile
     }
 }
 

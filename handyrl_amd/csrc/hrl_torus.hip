@@ -509,6 +509,237 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
 }
 
+// ------------------------------------------------------------------ pre-split forward / input gradient (round 5)
+// torus_conv_ps_kernel<PRO, STATS, SUMS>: the split torus_conv_kernel for 32 input channels with each input value
+// split ONCE per sample instead of once per tap that gathers it (9x).  The kernel above spends ≈27k SIMD cycles
+// per sample, ≈60% of them in the A splits' vector instructions, against 8.6k of MFMA.
+//   * the sample's image is kept in LDS already split: a cell row of 192 bytes = [part h/m/l][channels 0-31] as
+//     bf16, so an A fragment (8 consecutive channels at one cell) is one ds_read_b128 per part.  The 16-byte
+//     channel chunk g of cell c sits at chunk g ^ ((c >> 2) & 3) of its part: 16 lanes reading 16 consecutive
+//     cells hit 16 distinct bank quads (the row stride is 48 dwords);
+//   * staging: lane unit u = (channel group g, cell c) loads its 8 channels at cell c with dword loads (lanes of
+//     a load instruction read consecutive cells: coalesced), optionally applies the BatchNorm prologue, splits the
+//     8 values and writes the three 16-byte fragments;
+//   * 8 waves per workgroup, one workgroup per CU (8 x 15 KB images + the 37 KB packed weights = 156 KB of LDS):
+//     the same two waves per SIMD as the 4-wave kernel at two workgroups per CU.  A wave walks the samples
+//     n = 8 b + w (mod 2048) that wave w & 3 of the 4-wave kernel's block 2b + (w >> 2) walks, and its
+//     statistics / sums fold into that block's partial row in the same order: results are bit-identical to
+//     torus_conv_kernel<8, *, *, true, PRO, SUMS> (tests/test_geese.py::test_presplit_form_is_bit_identical).
+// The B fragments are split per tap from the fp32 packed weights as before (pre-split weights would not fit).
+constexpr int kPW = 8;
+constexpr int kPThreads = 64 * kPW;
+constexpr int kRowDw = 48;                    // dwords per cell row of the split image
+constexpr int kImgDw = kMaxCells * kRowDw;    // dwords per wave image (15 KB)
+constexpr int kPU = 4 * kMaxCells / 64;       // staging units per lane (4 channel groups x 80 cells / 64 lanes)
+static_assert(kImgDw >= kTile, "the fp32 output tile lives in the image region");
+
+__device__ __forceinline__ int ps_row(int cell, int g) { return cell * kRowDw + 4 * (g ^ ((cell >> 2) & 3)); }
+
+template <int PRO, bool STATS, bool SUMS>
+__global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void torus_conv_ps_kernel(
+    ConvArgs a, int nvb) {
+    const int64_t N = a.N;
+    const int H = a.H, W = a.W, out_c = a.out_c;
+    constexpr int kNW = kTaps * 8 * 2 * 64;
+    __shared__ float w_lds[kNW];
+    __shared__ __attribute__((aligned(16))) uint32_t imgs[kPW * kImgDw];
+    __shared__ __attribute__((aligned(16))) float coef_s[2 * kCo + 2];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int HW = H * W;
+    const float inv_hw = 1.0f / (float)HW;
+    const int in_elem = kCo * HW;
+    uint32_t *img = imgs + wave * kImgDw;
+    float *tile = reinterpret_cast<float *>(img);
+
+    for (int i = threadIdx.x; i < kNW; i += kPThreads) w_lds[i] = a.wpk[i];
+    if constexpr (PRO != 0) {
+        if (threadIdx.x < 2 * kCo) coef_s[threadIdx.x] = threadIdx.x < kCo ? a.alpha[threadIdx.x] : a.beta[threadIdx.x - kCo];
+    }
+    if constexpr (SUMS) {
+        if (threadIdx.x < kCo) coef_s[threadIdx.x] = a.mean[threadIdx.x];
+    }
+
+    uint32_t nbp[kMT][3];   // (row (r + d - 1) * W) | (column (c + d - 1)) << 16 of the lane's A cells
+#pragma unroll
+    for (int mt = 0; mt < kMT; ++mt) {
+        int q = mt * 16 + (lane & 15);
+        while (q >= HW) q -= HW;
+        const int r = q / W, c = q - r * W;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            int rr = r + d - 1, cc = c + d - 1;
+            rr = rr < 0 ? rr + H : (rr >= H ? rr - H : rr);
+            cc = cc < 0 ? cc + W : (cc >= W ? cc - W : cc);
+            nbp[mt][d] = (uint32_t)(rr * W) | ((uint32_t)cc << 16);
+        }
+    }
+    const int g = lane >> 4;
+    float bias_v[2] = {0.f, 0.f};
+    if (a.bias) {
+        bias_v[0] = a.bias[lane & 15];
+        bias_v[1] = a.bias[16 + (lane & 15)];
+    }
+    double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
+
+    // staging unit u = k * 64 + lane (valid below 4 HW): channels 8 gu .. 8 gu + 7 at cell cu
+    float sv[kPU][8], sr[PRO == 2 ? kPU : 1][8];
+    auto unit = [&](int k, int &gu, int &cu) {
+        const int u = opaque(k * 64 + lane);
+        gu = fdiv(u, inv_hw);
+        cu = u - gu * HW;
+        return u < 4 * HW;
+    };
+    auto load = [&](float (&v)[kPU][8], const float *src) {
+#pragma unroll
+        for (int k = 0; k < kPU; ++k) {
+            int gu, cu;
+            const bool ok = unit(k, gu, cu);
+            const float *p = src + (ok ? 8 * gu * HW + cu : 0);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[k][e] = p[e * HW];
+        }
+    };
+
+    const int64_t stride = (int64_t)gridDim.x * kPW;
+    int64_t n = (int64_t)blockIdx.x * kPW + wave;
+    if (n < N) {
+        load(sv, a.x + n * in_elem);
+        if constexpr (PRO == 2) load(sr, a.res + n * in_elem);
+    }
+    __syncthreads();   // weights (and coefficients) in LDS
+
+    for (; n < N; n += stride) {
+        // the staged sample -> (prologue) -> split image
+#pragma unroll
+        for (int k = 0; k < kPU; ++k) {
+            int gu, cu;
+            if (unit(k, gu, cu)) {
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = sv[k][e];
+                if constexpr (PRO != 0) {
+                    const float4 *al = reinterpret_cast<const float4 *>(coef_s + 8 * gu);
+                    const float4 *be = reinterpret_cast<const float4 *>(coef_s + kCo + 8 * gu);
+                    const float4 a0 = al[0], a1 = al[1], b0 = be[0], b1 = be[1];
+                    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                    float *ho = a.hout + n * in_elem + 8 * gu * HW + cu;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        float t = v[e] * av[e] + bv[e];
+                        if constexpr (PRO == 2) t = sr[k][e] + t;
+                        v[e] = relu(t);
+                        ho[e * HW] = v[e];
+                    }
+                }
+                uint4 Ah, Am, Al;
+                split8(v, Ah, Am, Al);
+                uint4 *row = reinterpret_cast<uint4 *>(img + ps_row(cu, gu));
+                row[0] = Ah;
+                row[4] = Am;
+                row[8] = Al;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        lds_fence();
+        const int64_t next = n + stride;
+        if (next < N) {
+            load(sv, a.x + next * in_elem);   // in flight during the MFMAs
+            if constexpr (PRO == 2) load(sr, a.res + next * in_elem);
+        }
+
+        f32x4 acc[kMT][2];
+#pragma unroll
+        for (int mt = 0; mt < kMT; ++mt) acc[mt][0] = acc[mt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) {
+            uint4 Bh[2], Bm[2], Bl[2];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                float bv[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int ci = 8 * g + e;
+                    bv[e] = w_lds[((t * 8 + (ci >> 2)) * 2 + ct) * 64 + (ci & 3) * 16 + (lane & 15)];
+                }
+                split8(bv, Bh[ct], Bm[ct], Bl[ct]);
+            }
+#pragma unroll
+            for (int mt = 0; mt < kMT; ++mt) {
+                const int cell = (int)(nbp[mt][t / 3] & 0xffffu) + (int)(nbp[mt][t % 3] >> 16);
+                const uint4 *row = reinterpret_cast<const uint4 *>(img + ps_row(cell, g));
+                const uint4 Ah = row[0], Am = row[4], Al = row[8];
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct)
+                    acc[mt][ct] = mfma_split(Ah, Am, Al, Bh[ct], Bm[ct], Bl[ct], acc[mt][ct]);
+            }
+        }
+        lds_fence();   // every lane's A reads done before the image becomes the output tile
+
+        float t1[2] = {0.f, 0.f}, t2[2] = {0.f, 0.f};
+#pragma unroll
+        for (int mt = 0; mt < kMT; ++mt)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int cell = mt * 16 + (lane >> 4) * 4 + r;
+                    const int co = ct * 16 + (lane & 15);
+                    if (cell < HW) {
+                        const float v = acc[mt][ct][r] + bias_v[ct];
+                        tile[co * kS + cell] = v;
+                        if constexpr (STATS) {
+                            t1[ct] += v;
+                            t2[ct] += v * v;
+                        }
+                    }
+                }
+        if constexpr (STATS) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                s1[ct] += (double)t1[ct];
+                s2[ct] += (double)t2[ct];
+            }
+        }
+        lds_fence();
+        const int64_t ob = n * ((int64_t)out_c * HW);
+        if constexpr (SUMS)
+            store_sample_sums(tile, a.y + ob, out_c * HW, HW, inv_hw, lane, a.add + ob, a.add_mask + ob, a.hmask + ob,
+                              a.yprev + ob, coef_s, s1[0], s2[0]);
+        else
+            store_sample(tile, a.y + ob, out_c * HW, a.vec_out, HW, inv_hw, lane, a.add ? a.add + ob : nullptr,
+                         a.add ? a.add_mask + ob : nullptr);
+        lds_fence();   // the tile's reads done before the next image is written
+    }
+    if constexpr (STATS || SUMS) {
+        // the 4-wave kernel's fold per virtual block vb = 2 b + (w >> 2): its waves w & 3 (and their lane
+        // groups / halves) in the same fixed order
+        constexpr int kG = STATS ? 4 : 2;   // lane groups (STATS: l >> 4 of a column tile) or halves (SUMS)
+        __syncthreads();
+        double *red = reinterpret_cast<double *>(imgs);   // [wave][group][32][2]
+        if constexpr (STATS) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const int co = ct * 16 + (lane & 15);
+                red[((wave * kG + g) * kCo + co) * 2 + 0] = s1[ct];
+                red[((wave * kG + g) * kCo + co) * 2 + 1] = s2[ct];
+            }
+        } else {
+            red[((wave * kG + (lane >> 5)) * kCo + (lane & 31)) * 2 + 0] = s1[0];
+            red[((wave * kG + (lane >> 5)) * kCo + (lane & 31)) * 2 + 1] = s2[0];
+        }
+        __syncthreads();
+        if (threadIdx.x < 4 * kCo) {
+            const int hb = threadIdx.x >> 6, co = (threadIdx.x & 63) >> 1, k = threadIdx.x & 1;
+            const int vb = 2 * (int)blockIdx.x + hb;
+            double t = 0.0;
+            for (int i = 0; i < 4 * kG; ++i) t += red[((hb * 4 * kG + i) * kCo + co) * 2 + k];
+            if (vb < nvb) a.part[((int64_t)vb * kCo + co) * 2 + k] = t;
+        }
+    }
+}
+
 // W (32, Cin, 3, 3) -> packed [tap][KS][ct][64]: lane l of k-step s holds W^T[ci = 4s + (l>>4)][co = 16ct + (l&15)].
 // flip = 1 (KS = 8): the input gradient's weights, W'[co' = ci][ci' = co][tap] = W[co][ci][8 - tap],
 // output channels ci >= Cin zero.
@@ -937,6 +1168,16 @@ constexpr int64_t kPartFloats = kTaps * kCo * kCo + kCo;
 
 // Forward / input-gradient arithmetic: exact-split bf16 MFMA (1, default) or fp32 MFMA (0).
 int g_split = 1;
+// The split 32-channel torus forward / input gradient: 2 = pre-split images (torus_conv_ps_kernel, default),
+// 1 = per-tap splits (torus_conv_kernel).  Bit-identical results.
+int g_form = 2;
+
+// torus_conv_ps_kernel launch: the 4-wave kernel's blocks pairwise (its partial rows: grid_for(N, kGridConv))
+template <int PRO, bool STATS, bool SUMS>
+void launch_ps(const ConvArgs &a, hipStream_t s) {
+    const int nvb = grid_for(a.N, kGridConv);
+    hipLaunchKernelGGL((torus_conv_ps_kernel<PRO, STATS, SUMS>), dim3((nvb + 1) / 2), dim3(kPThreads), 0, s, a, nvb);
+}
 
 }  // namespace
 
@@ -945,6 +1186,12 @@ extern "C" {
 int hrl_torus_set_split(int on) {
     const int prev = g_split;
     g_split = on ? 1 : 0;
+    return prev;
+}
+
+int hrl_torus_set_form(int form) {
+    const int prev = g_form;
+    if (form == 1 || form == 2) g_form = form;
     return prev;
 }
 
@@ -988,6 +1235,10 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
         else hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_, false>), grid, block, 0, s, a);               \
     } while (0)
     const bool st = part != nullptr;
+    if (KS == 8 && g_split && g_form == 2) {
+        if (st) launch_ps<0, true, false>(a, s); else launch_ps<0, false, false>(a, s);
+        return status();
+    }
     if (KS == 8) {
         if (vec) { if (st) HRL_TORUS_LAUNCH(8, true, true); else HRL_TORUS_LAUNCH(8, true, false); }
         else { if (st) HRL_TORUS_LAUNCH(8, false, true); else HRL_TORUS_LAUNCH(8, false, false); }
@@ -1068,6 +1319,10 @@ int hrl_torus_unit_forward(const float *y_prev, const float *res, const float *a
     a.x = y_prev; a.N = N; a.Cin = kCo; a.H = (int)H; a.W = (int)W; a.wpk = wpk; a.bias = bias; a.out_c = kCo;
     a.vec_out = true; a.y = y; a.part = part; a.res = res; a.alpha = alpha; a.beta = beta; a.hout = h;
     a.co_total = kCo;
+    if (g_split && g_form == 2) {
+        if (res) launch_ps<2, true, false>(a, s); else launch_ps<1, true, false>(a, s);
+        return status();
+    }
     const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
     if (res) {
         if (g_split) hipLaunchKernelGGL((torus_conv_kernel<8, true, true, true, 2>), grid, block, 0, s, a);
@@ -1101,6 +1356,10 @@ int hrl_torus_unit_input_grad(const float *dy, int64_t N, int64_t H, int64_t W, 
     a.x = dy; a.N = N; a.Cin = kCo; a.H = (int)H; a.W = (int)W; a.wpk = wpk; a.out_c = kCo; a.vec_out = true;
     a.y = dh; a.part = part; a.add = g; a.add_mask = out; a.hmask = h_mask; a.yprev = y_prev; a.mean = mean_prev;
     a.co_total = kCo;
+    if (g_split && g_form == 2) {
+        launch_ps<0, false, true>(a, s);
+        return status();
+    }
     const dim3 grid(grid_for(N, kGridConv)), block(kThreads);
     if (g_split) hipLaunchKernelGGL((torus_conv_kernel<8, true, false, true, 0, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((torus_conv_kernel<8, true, false, false, 0, true>), grid, block, 0, s, a);

@@ -298,6 +298,11 @@ int64_t hrl_torus_workspace_bytes(int64_t N);
 /* Arithmetic of the torus forward / input-gradient kernel, as hrl_conv3x3_set_split: on != 0 (default) the exact
  * three-way bf16 split on v_mfma_f32_16x16x32_bf16, 0 fp32 MFMA.  Process-wide; returns the previous setting. */
 int hrl_torus_set_split(int on);
+/* Kernel form of the split 32-input-channel launches (hrl_torus_conv_forward with 32 input channels,
+ * hrl_torus_unit_forward, hrl_torus_unit_input_grad): 2 (default) splits each input value once per sample into an
+ * LDS image of bf16 parts, 1 splits the gathered values per tap.  The results are bit-identical.  1 or 2 sets the
+ * form; any other value only queries.  Process-wide; returns the previous setting. */
+int hrl_torus_set_form(int form);
 int64_t hrl_torus_stats_blocks(int64_t N);
 int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
                            const float *weight, const float *bias, int flip, float *y, double *part,

@@ -277,6 +277,59 @@ def test_torus_tower_matches_unit_chain(cuda, N, split):
             assert (q.grad - p.grad).abs().max().item() <= 1e-4 * scale + 1e-6, (name, scale)
 
 
+def _with_torus_form(lib, form, fn):
+    prev = lib.hrl_torus_set_form(form)
+    try:
+        return fn()
+    finally:
+        lib.hrl_torus_set_form(prev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,H,W', [(37, 7, 11), (2043, 7, 11), (4301, 7, 11), (29, 8, 10), (11, 3, 3),
+                                   (9, 4, 5)])
+def test_presplit_form_is_bit_identical(cuda, N, H, W):
+    """The pre-split torus kernel (hrl_torus_set_form(2), csrc/hrl_torus.hip torus_conv_ps_kernel) against the
+    per-tap-split kernel (form 1): torus_conv2d's forward and input gradient (32 and 17 channels) and a 3-unit
+    torus_tower step (BatchNorm prologue, statistics and masked-sum epilogues), bit for bit, on ragged sample
+    counts around the 2048-wave stride and on boards of 9 to 80 cells."""
+    from handyrl_amd import _native
+    from handyrl_amd.nn import torus_conv2d, torus_tower
+    lib = _native.load()
+    assert lib.hrl_torus_set_form(0) == 2   # the default form; 0 only queries
+
+    def conv_run(cin):
+        g = torch.Generator(device=cuda).manual_seed(N + cin)
+        x = torch.randn(N, cin, H, W, device=cuda, generator=g).requires_grad_(True)
+        w = (torch.randn(32, cin, 3, 3, device=cuda, generator=g) * 0.1).requires_grad_(True)
+        b = torch.randn(32, device=cuda, generator=g).requires_grad_(True)
+        y = torus_conv2d(x, w, b)
+        y.backward(torch.randn(N, 32, H, W, device=cuda, generator=g))
+        return [y.detach(), x.grad, w.grad, b.grad]
+
+    def tower_run():
+        torch.manual_seed(N)
+        units = [TorusConv2d(17, 32, (3, 3), True)] + [TorusConv2d(32, 32, (3, 3), True) for _ in range(2)]
+        for u in units:
+            with torch.no_grad():
+                u.bn.weight.uniform_(0.5, 1.5)
+                u.bn.bias.uniform_(-0.2, 0.2)
+            u.to(cuda).use_hip = True
+        x = torch.randn(N, 17, H, W, device=cuda).requires_grad_(True)
+        h = torus_tower(x, units)
+        h.backward(torch.randn(N, 32, H, W, device=cuda))
+        outs = [h.detach(), x.grad]
+        for u in units:
+            outs += [p.grad for p in u.parameters()] + [u.bn.running_mean, u.bn.running_var]
+        return outs
+
+    for run in (lambda: conv_run(32), lambda: conv_run(17), tower_run):
+        a = _with_torus_form(lib, 1, run)
+        b = _with_torus_form(lib, 2, run)
+        for i, (u, v) in enumerate(zip(a, b)):
+            assert torch.equal(u, v), i
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('N', [1, 37, 3000])
 def test_geese_pool_matches_torch(cuda, N):
