@@ -159,6 +159,12 @@ SIGNATURES = {
                                               _f32p, _f32p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_torus_conv_wgrad': (ctypes.c_int, [_f32p, _f32p, _i64, _i64, _i64, _i64, _i64, _f32p, _f32p,
                                             ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_torus_conv_wgrad_bn': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p,
+                                               ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
+                                               ctypes.c_void_p, _i64, ctypes.c_void_p]),
+    'hrl_bn_backward_masked_coefs': (ctypes.c_int, [_f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p,
+                                                    _f32p, _f32p, _f32p, _f32p, ctypes.c_void_p, _i64,
+                                                    ctypes.c_void_p]),
     'hrl_torus_unit_forward': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _f32p, _i64, _i64, _i64, _f32p, _f32p,
                                               _f32p, ctypes.c_void_p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_torus_unit_input_grad': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _f32p, _f32p, _f32p, _f32p, _f32p,
@@ -220,7 +226,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 _lib = None
 

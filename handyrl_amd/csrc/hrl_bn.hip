@@ -762,6 +762,33 @@ int hrl_bn_backward_apply_masked(const float *x, const float *dy, const float *o
     return launch_status();
 }
 
+int hrl_bn_backward_masked_coefs(const float *x, const float *dy, const float *out, int64_t N, int64_t C,
+                                 int64_t HW, const float *weight, const float *save_mean, const float *save_invstd,
+                                 float *kcoef, float *gmean, float *dweight, float *dbias, void *workspace,
+                                 int64_t workspace_bytes, void *stream) {
+    if (!x || !dy || !out || !save_mean || !save_invstd || !kcoef || !gmean || !workspace) return HRL_EINVAL;
+    const bool vec = (C * HW) % 4 == 0 && aligned16(x) && aligned16(dy) && aligned16(out);
+    Geo g;
+    if (!make_geo(N, C, HW, vec ? 4 : 1, g)) return HRL_EINVAL;
+    if (workspace_bytes < ws_bytes(g)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    double *part = static_cast<double *>(workspace);
+    const size_t lds = sizeof(double) * 2 * g.S;
+    const dim3 grid(g.nblocks), block(kThreads);
+    const float *nul = nullptr;
+    if (vec) hipLaunchKernelGGL((bn_bwd_reduce_kernel<4, false, 2>), grid, block, lds, s, x, dy, g, save_mean,
+                                save_invstd, weight, nul, part, out);
+    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, false, 2>), grid, block, lds, s, x, dy, g, save_mean,
+                            save_invstd, weight, nul, part, out);
+    int rc = launch_status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(g.C), dim3(kThreads), 0, s, 1, part, g.nblocks, g.C,
+                       (double)N * (double)HW, weight, (const float *)nullptr, (float *)nullptr, (float *)nullptr,
+                       0.0f, 0.0, (float *)nullptr, const_cast<float *>(save_invstd), kcoef, gmean, dweight, dbias,
+                       1);
+    return launch_status();
+}
+
 int hrl_bn_backward_masked(const float *x, const float *dy, const float *out, int64_t N, int64_t C, int64_t HW,
                            const float *weight, const float *save_mean, const float *save_invstd, float *dx,
                            float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream) {

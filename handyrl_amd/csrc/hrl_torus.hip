@@ -539,7 +539,7 @@ template <int PRO, bool STATS, bool SUMS>
 __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void torus_conv_ps_kernel(
     ConvArgs a, int nvb) {
     const int64_t N = a.N;
-    const int H = a.H, W = a.W, out_c = a.out_c;
+    const int H = a.H, W = a.W, out_c = a.out_c, Cin = a.Cin;
     constexpr int kNW = kTaps * 8 * 2 * 64;
     __shared__ float w_lds[kNW];
     __shared__ __attribute__((aligned(16))) uint32_t imgs[kPW * kImgDw];
@@ -548,7 +548,7 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
     const int wave = threadIdx.x >> 6;
     const int HW = H * W;
     const float inv_hw = 1.0f / (float)HW;
-    const int in_elem = kCo * HW;
+    const int in_elem = Cin * HW;
     uint32_t *img = imgs + wave * kImgDw;
     float *tile = reinterpret_cast<float *>(img);
 
@@ -597,7 +597,7 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             const bool ok = unit(k, gu, cu);
             const float *p = src + (ok ? 8 * gu * HW + cu : 0);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[k][e] = p[e * HW];
+            for (int e = 0; e < 8; ++e) v[k][e] = (!ok || 8 * gu + e < Cin) ? p[e * HW] : 0.f;   // rows >= Cin: 0
         }
     };
 
@@ -903,23 +903,59 @@ __device__ __forceinline__ f32x16 mfma32(const uint4 &a, const uint4 &b, f32x16 
                                                    c, 0, 0, 0);
 }
 
-__global__ __launch_bounds__(kThreads) void torus_wgrad_split_kernel(const float *__restrict__ x,
-                                                                     const float *__restrict__ dy, int64_t N, int H,
-                                                                     int W, float *__restrict__ partial) {
+// APPLY (round 5): dY is not read but formed in the staging from the BatchNorm that follows the conv,
+// dY = (((g [out > 0] - gmean) - (y - mean) k) invstd) gamma per channel (bn_bwd_apply_kernel<4, false, 2>'s
+// operations, hrl_bn_backward_apply_masked), and written to dy_out for the input gradient: the separate masked
+// apply pass (3 reads + 1 write of the activation) becomes 2 extra reads here.  The block output's mask
+// [out > 0] is recomputed as [([x +] (y alpha + beta)) > 0] (residual: the block's input x is its residual),
+// the forward's own operations (bn_res_apply_kernel, torus_conv_ps_kernel's prologue), so out is not read.
+// X32 = false: x has Cin < 32 channels (GeeseNet's 17-channel stem, dword loads); rows Cin..31 stay zero.
+struct WgArgs {
+    const float *x, *dy;
+    int64_t N;
+    int Cin, H, W;
+    float *partial;
+    const float *yb, *gb, *mean, *invstd, *gamma, *kcoef, *gmean, *alpha, *beta;   // APPLY
+    float *dy_out;
+    bool residual;
+};
+
+template <bool APPLY, bool X32>
+__global__ __launch_bounds__(kThreads) void torus_wgrad_split_kernel(WgArgs args) {
+    const float *__restrict__ x = args.x;
+    const float *__restrict__ dy = args.dy;
+    const int64_t N = args.N;
+    const int H = args.H, W = args.W, Cin = X32 ? kCo : args.Cin;
+    float *__restrict__ partial = args.partial;
     constexpr int kNLd = (kCo * kMaxCells / 4 + 63) / 64;   // float4 per lane per sample tensor
+    constexpr int kNLdS = (kCo * kMaxCells + 63) / 64;      // !X32: x floats per lane
     constexpr int kPart = kTaps * kCo * kCo + kCo;
     constexpr int kHalf = kMaxCells / 2;
     __shared__ __attribute__((aligned(16))) float gs_all[kWaves][kCo * kSG];   // dY [co][cell]
     __shared__ uint2 xs_all[kWaves][kCo * kS];                                  // X (hi | mid << 16, lo) [ci][cell]
     __shared__ uint32_t nbp_tab[kMaxCells * 3];   // per cell and d: (row (r + d - 1) * W) | (column (c + d - 1)) << 16
+    __shared__ float bnc[APPLY ? 7 * kCo + 1 : 1];   // APPLY: mean, k, gmean, invstd, gamma, alpha, beta (+1 pad)
     static_assert(sizeof(gs_all) + sizeof(xs_all) >= (kPart + kWaves * 2 * kCo) * sizeof(float), "fold buffer");
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int HW = H * W;
     const float inv_hw = 1.0f / (float)HW;
-    const int n_elem = kCo * HW, nv = n_elem / 4;
+    const int n_elem = kCo * HW, nv = n_elem / 4, x_elem = Cin * HW;
     float *gs = gs_all[wave];
     uint2 *xs = xs_all[wave];
+    if constexpr (APPLY) {
+        if (threadIdx.x < kCo) {
+            const int c = threadIdx.x;
+            bnc[c] = args.mean[c];
+            bnc[kCo + c] = args.kcoef[c];
+            bnc[2 * kCo + c] = args.gmean[c];
+            bnc[3 * kCo + c] = args.invstd[c];
+            bnc[4 * kCo + c] = args.gamma ? args.gamma[c] : 1.0f;
+            bnc[5 * kCo + c] = args.alpha[c];
+            bnc[6 * kCo + c] = args.beta[c];
+        }
+        if (threadIdx.x == kCo) bnc[7 * kCo] = 0.f;
+    }
     for (int i = threadIdx.x; i < kMaxCells * 3; i += kThreads) {
         const int q = i / 3, d = i - q * 3;
         uint32_t v = 0u;   // cells past the board: dY is zero there, any cell will do
@@ -946,36 +982,74 @@ __global__ __launch_bounds__(kThreads) void torus_wgrad_split_kernel(const float
 
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int64_t n = (int64_t)blockIdx.x * kWaves + wave;
-    float4 sx[kNLd], sg[kNLd];
+    float4 sx[X32 ? kNLd : 1], sg[kNLd], sy[APPLY ? kNLd : 1];
+    float sxs[X32 ? 1 : kNLdS];
     auto load = [&](int64_t m) {
-        const float4 *xp = reinterpret_cast<const float4 *>(x + m * n_elem);
-        const float4 *gp = reinterpret_cast<const float4 *>(dy + m * n_elem);
+        if constexpr (X32) {
+            const float4 *xp = reinterpret_cast<const float4 *>(x + m * n_elem);
 #pragma unroll
-        for (int k = 0; k < kNLd; ++k) {
-            const int i = min(k * 64 + lane, nv - 1);
-            sx[k] = xp[i];
-            sg[k] = gp[i];
+            for (int k = 0; k < kNLd; ++k) sx[k] = xp[min(k * 64 + lane, nv - 1)];
+        } else {
+            const float *xp = x + m * x_elem;
+#pragma unroll
+            for (int k = 0; k < kNLdS; ++k) sxs[k] = xp[min(k * 64 + lane, x_elem - 1)];
+        }
+        const float4 *gp = reinterpret_cast<const float4 *>((APPLY ? args.gb : dy) + m * n_elem);
+#pragma unroll
+        for (int k = 0; k < kNLd; ++k) sg[k] = gp[min(k * 64 + lane, nv - 1)];
+        if constexpr (APPLY) {
+            const float4 *yp = reinterpret_cast<const float4 *>(args.yb + m * n_elem);
+#pragma unroll
+            for (int k = 0; k < kNLd; ++k) sy[k] = yp[min(k * 64 + lane, nv - 1)];
         }
     };
     if (n < N) load(n);
     for (; n < N; n += stride) {
+        if constexpr (!X32) {
+#pragma unroll
+            for (int k = 0; k < kNLdS; ++k) {
+                const int e = opaque(k * 64 + lane);
+                if (e < x_elem) {
+                    const int c = fdiv(e, inv_hw);
+                    uint32_t hb, mb, lb;
+                    hrl_split::split3(sxs[k], hb, mb, lb);
+                    xs[c * kS + (e - c * HW)] = make_uint2(hb | (mb << 16), lb);
+                }
+            }
+        }
 #pragma unroll
         for (int k = 0; k < kNLd; ++k) {
             const int i = k * 64 + lane;
             if (i < nv) {
                 const Quad q(i, HW, inv_hw);
-                const float x4[4] = {sx[k].x, sx[k].y, sx[k].z, sx[k].w};
-                const float g4[4] = {sg[k].x, sg[k].y, sg[k].z, sg[k].w};
+                float g4[4] = {sg[k].x, sg[k].y, sg[k].z, sg[k].w};
+                const float x4[4] = {sx[X32 ? k : 0].x, sx[X32 ? k : 0].y, sx[X32 ? k : 0].z, sx[X32 ? k : 0].w};
+                if constexpr (APPLY) {
+                    const float y4[4] = {sy[k].x, sy[k].y, sy[k].z, sy[k].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int c = q.c0 + (q.wrap(j, HW) ? 1 : 0);
+                        const float z = y4[j] * bnc[5 * kCo + c] + bnc[6 * kCo + c];
+                        const float o = (X32 && args.residual) ? x4[j] + z : z;   // relu(o) > 0 <=> o > 0
+                        const float gv = o > 0.f ? g4[j] : 0.f;
+                        const float t = (y4[j] - bnc[c]) * bnc[kCo + c];
+                        g4[j] = (((gv - bnc[2 * kCo + c]) - t) * bnc[3 * kCo + c]) * bnc[4 * kCo + c];
+                    }
+                    reinterpret_cast<float4 *>(args.dy_out + n * n_elem)[i] = make_float4(g4[0], g4[1], g4[2], g4[3]);
+                }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const bool w = q.wrap(j, HW);
                     const int c = q.c0 + (w ? 1 : 0), cell = q.r0 + j - (w ? HW : 0);
-                    uint32_t hb, mb, lb;
-                    hrl_split::split3(x4[j], hb, mb, lb);
-                    xs[c * kS + cell] = make_uint2(hb | (mb << 16), lb);
+                    if constexpr (X32) {
+                        uint32_t hb, mb, lb;
+                        hrl_split::split3(x4[j], hb, mb, lb);
+                        xs[c * kS + cell] = make_uint2(hb | (mb << 16), lb);
+                    }
                     gs[c * kSG + cell] = g4[j];
                 }
             }
+            if constexpr (APPLY) __builtin_amdgcn_sched_barrier(0);
         }
         lds_fence();
         if (n + stride < N) load(n + stride);   // in flight during the MFMAs
@@ -1214,7 +1288,8 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
     // the conv this launch computes: forward Cin -> 32; flip: 32 -> Cin (the forward's adjoint)
     const int in_c = flip ? (int)kCo : (int)Cin;
     const int out_c = flip ? (int)Cin : (int)kCo;
-    const int KS = in_c == 17 ? 5 : 8;
+    const bool ps = g_split && g_form == 2;   // the pre-split kernel (32 or 17 input channels, KS = 8 packing)
+    const int KS = in_c == 17 && !ps ? 5 : 8;
     float *wpk = static_cast<float *>(workspace);
     hipLaunchKernelGGL(torus_pack_kernel, dim3((kTaps * KS * 128 + 255) / 256), dim3(256), 0, s, weight, (int)Cin, KS,
                        flip, wpk);
@@ -1235,7 +1310,7 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
         else hipLaunchKernelGGL((torus_conv_kernel<KS_, VEC_, ST_, false>), grid, block, 0, s, a);               \
     } while (0)
     const bool st = part != nullptr;
-    if (KS == 8 && g_split && g_form == 2) {
+    if (ps) {
         if (st) launch_ps<0, true, false>(a, s); else launch_ps<0, false, false>(a, s);
         return status();
     }
@@ -1375,8 +1450,13 @@ int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin
     const bool vec = HW >= 4 && (Cin * HW) % 4 == 0 && (kCo * HW) % 4 == 0 && aligned16(x) && aligned16(dy);
     const int grid = grid_for(N, kGridWgrad);
     float *partial = static_cast<float *>(workspace) + kPackFloats;
+    const bool dy_vec = HW >= 4 && aligned16(dy);   // 32 * HW is a multiple of 4
+    WgArgs wa{};
+    wa.x = x; wa.dy = dy; wa.N = N; wa.Cin = (int)Cin; wa.H = (int)H; wa.W = (int)W; wa.partial = partial;
     if (Cin == kCo && vec && g_split) {
-        hipLaunchKernelGGL(torus_wgrad_split_kernel, dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)H, (int)W, partial);
+        hipLaunchKernelGGL((torus_wgrad_split_kernel<false, true>), dim3(grid), dim3(kThreads), 0, s, wa);
+    } else if (Cin != kCo && dy_vec && g_split) {
+        hipLaunchKernelGGL((torus_wgrad_split_kernel<false, false>), dim3(grid), dim3(kThreads), 0, s, wa);
     } else if (Cin == kCo) {
         if (vec)
             hipLaunchKernelGGL((torus_wgrad_kernel<8, true>), dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)Cin,
@@ -1388,6 +1468,38 @@ int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin
         hipLaunchKernelGGL((torus_wgrad_kernel<5, false>), dim3(grid), dim3(kThreads), 0, s, x, dy, N, (int)Cin,
                            (int)H, (int)W, partial);
     }
+    int rc = status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(torus_wgrad_reduce_kernel, dim3((int)((kPartFloats + 255) / 256)), dim3(256), 0, s, partial,
+                       grid, (int)Cin, dweight, dbias);
+    return status();
+}
+
+int hrl_torus_conv_wgrad_bn(const float *x, int64_t N, int64_t Cin, int64_t H, int64_t W, const float *y,
+                            const float *g, const float *alpha, const float *beta, int residual, const float *gamma,
+                            const float *save_mean, const float *save_invstd, const float *kcoef, const float *gmean,
+                            float *dy, float *dweight, float *dbias, void *workspace, int64_t workspace_bytes,
+                            void *stream) {
+    if (!shape_ok(N, Cin, kCo, H, W) || !x || !y || !g || !alpha || !beta || !save_mean || !save_invstd || !kcoef ||
+        !gmean || !dy || !dweight || !workspace)
+        return HRL_EINVAL;
+    if (residual && Cin != kCo) return HRL_EINVAL;
+    if (workspace_bytes < hrl_torus_workspace_bytes(N) || !g_split) return HRL_EINVAL;
+    const int64_t HW = H * W;
+    if (HW < 4) return HRL_EINVAL;
+    for (const void *p : {(const void *)y, (const void *)g, (const void *)dy})
+        if (!aligned16(p)) return HRL_EINVAL;
+    const bool x32 = Cin == kCo;
+    if (x32 && !aligned16(x)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int grid = grid_for(N, kGridWgrad);
+    float *partial = static_cast<float *>(workspace) + kPackFloats;
+    WgArgs wa{};
+    wa.x = x; wa.N = N; wa.Cin = (int)Cin; wa.H = (int)H; wa.W = (int)W; wa.partial = partial;
+    wa.yb = y; wa.gb = g; wa.mean = save_mean; wa.invstd = save_invstd; wa.gamma = gamma;
+    wa.kcoef = kcoef; wa.gmean = gmean; wa.alpha = alpha; wa.beta = beta; wa.dy_out = dy; wa.residual = residual != 0;
+    if (x32) hipLaunchKernelGGL((torus_wgrad_split_kernel<true, true>), dim3(grid), dim3(kThreads), 0, s, wa);
+    else hipLaunchKernelGGL((torus_wgrad_split_kernel<true, false>), dim3(grid), dim3(kThreads), 0, s, wa);
     int rc = status();
     if (rc) return rc;
     hipLaunchKernelGGL(torus_wgrad_reduce_kernel, dim3((int)((kPartFloats + 255) / 256)), dim3(256), 0, s, partial,

@@ -1201,19 +1201,35 @@ class _TorusTower(torch.autograd.Function):
         for i in range(n):
             grads[4 * i + 2] = torch.empty(32, device=dev, dtype=g.dtype)
             grads[4 * i + 3] = torch.empty(32, device=dev, dtype=g.dtype)
+        # TOWER_BN_FOLD: every unit's masked BN backward apply is formed in its weight gradient's staging
+        # (hrl_torus_conv_wgrad_bn, which writes dy for the input gradient) instead of a pass of its own
+        fold = TOWER_BN_FOLD
         dy = torch.empty_like(ys[-1])
-        _native.check(lib.hrl_bn_backward_masked(P(ys[-1]), P(g), P(out), N, 32, HW, P(gammas[-1]),
-                                                 P(coef[n - 1, 0]), P(coef[n - 1, 1]), P(dy), P(grads[4 * n - 2]),
-                                                 P(grads[4 * n - 1]), P(ws), bn_ws_bytes, stream),
-                      'hrl_bn_backward_masked')
+        if fold:
+            _native.check(lib.hrl_bn_backward_masked_coefs(P(ys[-1]), P(g), P(out), N, 32, HW, P(gammas[-1]),
+                                                           P(coef[n - 1, 0]), P(coef[n - 1, 1]), P(kg[0]), P(kg[1]),
+                                                           P(grads[4 * n - 2]), P(grads[4 * n - 1]), P(ws),
+                                                           bn_ws_bytes, stream), 'hrl_bn_backward_masked_coefs')
+        else:
+            _native.check(lib.hrl_bn_backward_masked(P(ys[-1]), P(g), P(out), N, 32, HW, P(gammas[-1]),
+                                                     P(coef[n - 1, 0]), P(coef[n - 1, 1]), P(dy), P(grads[4 * n - 2]),
+                                                     P(grads[4 * n - 1]), P(ws), bn_ws_bytes, stream),
+                          'hrl_bn_backward_masked')
         g_cur = g
         dx = None
         for i in range(n - 1, -1, -1):
             dw = torch.empty_like(weights[i])
             db = torch.empty(32, device=dev, dtype=g.dtype) if ctx.has_bias[i] else None
             cin = Cin if i == 0 else 32
-            _native.check(lib.hrl_torus_conv_wgrad(P(hs[i]), P(dy), N, cin, 32, H, W, P(dw), P(db), P(ws), ws_bytes,
-                                                   stream), 'hrl_torus_conv_wgrad')
+            if fold:
+                residual = 1 if (i >= 1 or ctx.residual_in) else 0   # unit i's block output relu([h_i +] bn(y_i))
+                _native.check(lib.hrl_torus_conv_wgrad_bn(P(hs[i]), N, cin, H, W, P(ys[i]), P(g_cur), P(coef[i, 2]),
+                                                          P(coef[i, 3]), residual, P(gammas[i]), P(coef[i, 0]),
+                                                          P(coef[i, 1]), P(kg[0]), P(kg[1]), P(dy), P(dw), P(db),
+                                                          P(ws), ws_bytes, stream), 'hrl_torus_conv_wgrad_bn')
+            else:
+                _native.check(lib.hrl_torus_conv_wgrad(P(hs[i]), P(dy), N, cin, 32, H, W, P(dw), P(db), P(ws),
+                                                       ws_bytes, stream), 'hrl_torus_conv_wgrad')
             grads[4 * i], grads[4 * i + 1] = dw, db
             if i == 0:
                 if ctx.needs_input_grad[0]:
@@ -1232,14 +1248,19 @@ class _TorusTower(torch.autograd.Function):
             _native.check(lib.hrl_bn_finalize_backward(P(part), nparts, 32, N * HW, P(gammas[i - 1]),
                                                        P(coef[i - 1, 1]), P(grads[4 * i - 2]), P(grads[4 * i - 1]),
                                                        P(kg[0]), P(kg[1]), stream), 'hrl_bn_finalize_backward')
-            dy = torch.empty_like(dy)
-            _native.check(lib.hrl_bn_backward_apply_masked(P(ys[i - 1]), P(g_prev), P(hs[i]), N, 32, HW,
-                                                           P(gammas[i - 1]), P(coef[i - 1, 0]), P(coef[i - 1, 1]),
-                                                           P(kg[0]), P(kg[1]), P(dy), stream),
-                          'hrl_bn_backward_apply_masked')
+            if not fold:
+                dy = torch.empty_like(dy)
+                _native.check(lib.hrl_bn_backward_apply_masked(P(ys[i - 1]), P(g_prev), P(hs[i]), N, 32, HW,
+                                                               P(gammas[i - 1]), P(coef[i - 1, 0]), P(coef[i - 1, 1]),
+                                                               P(kg[0]), P(kg[1]), P(dy), stream),
+                              'hrl_bn_backward_apply_masked')
             g_cur = g_prev
         return (dx, None, None, *grads)
 
+
+# _TorusTower's backward forms each unit's masked BatchNorm backward apply inside its weight gradient (True) or
+# runs it as a pass of its own (False; bit-identical, tests/test_geese.py::test_tower_bn_fold_is_bit_identical)
+TOWER_BN_FOLD = True
 
 # A data-parallel learner's segmented capture (trainer.LearnerStep._grab_cut_tensor): called with the tensor
 # between the two parts of a split tower, it returns the view that is the backward's cut

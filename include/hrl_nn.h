@@ -104,6 +104,13 @@ int hrl_bn_apply_residual(const float *x, const float *res, int64_t N, int64_t C
 int hrl_bn_backward_masked(const float *x, const float *dy, const float *out, int64_t N, int64_t C, int64_t HW,
                            const float *weight, const float *save_mean, const float *save_invstd, float *dx,
                            float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream);
+/* hrl_bn_backward_masked without its apply pass (round 5): the reduce and finalize only, the apply's per-channel
+ * coefficients k and mean(dy [out > 0]) into kcoef / gmean (C floats each) for a consumer that applies them itself
+ * (hrl_torus_conv_wgrad_bn).  workspace: hrl_bn_workspace_bytes(N, C, HW). */
+int hrl_bn_backward_masked_coefs(const float *x, const float *dy, const float *out, int64_t N, int64_t C,
+                                 int64_t HW, const float *weight, const float *save_mean, const float *save_invstd,
+                                 float *kcoef, float *gmean, float *dweight, float *dbias, void *workspace,
+                                 int64_t workspace_bytes, void *stream);
 /* The apply half of hrl_bn_backward_masked with the coefficients of hrl_bn_finalize_backward
  * (sums from hrl_torus_unit_input_grad). */
 int hrl_bn_backward_apply_masked(const float *x, const float *dy, const float *out, int64_t N, int64_t C, int64_t HW,
@@ -310,6 +317,22 @@ int hrl_torus_conv_forward(const float *x, int64_t N, int64_t Cin, int64_t Cout,
                            void *stream);
 int hrl_torus_conv_wgrad(const float *x, const float *dy, int64_t N, int64_t Cin, int64_t Cout, int64_t H, int64_t W,
                          float *dweight, float *dbias, void *workspace, int64_t workspace_bytes, void *stream);
+/* The weight gradient of a torus conv followed by a training-mode BatchNorm and a ReLU (round 5), with the
+ * BatchNorm's masked backward apply formed in the kernel's staging instead of a pass of its own:
+ *   dy = (((g [o > 0] - gmean) - (y - save_mean) kcoef) save_invstd) gamma   per channel,
+ *   o = [x +] (y alpha + beta)   (the block output relu(o) recomputed as the forward formed it; residual != 0:
+ *                                 the block's input x is its residual, Cin 32)
+ * (hrl_bn_backward_apply_masked's arithmetic, bit for bit; gamma NULL = 1) is written to dy (N, 32, H, W) for the
+ * input gradient, and dweight (32, Cin, 3, 3) / dbias (32, may be NULL) are hrl_torus_conv_wgrad(x, dy).
+ * y, g: (N, 32, H, W) float4-aligned (the conv output, the gradient w.r.t. the block output); alpha / beta the
+ * forward's hrl_bn_finalize_stats coefficients; kcoef / gmean from hrl_bn_finalize_backward or
+ * hrl_bn_backward_masked_coefs.  Cin 17 or 32 (32: x float4-aligned); split arithmetic only
+ * (hrl_torus_set_split(1), else HRL_EINVAL).  workspace: hrl_torus_workspace_bytes(N). */
+int hrl_torus_conv_wgrad_bn(const float *x, int64_t N, int64_t Cin, int64_t H, int64_t W, const float *y,
+                            const float *g, const float *alpha, const float *beta, int residual, const float *gamma,
+                            const float *save_mean, const float *save_invstd, const float *kcoef, const float *gmean,
+                            float *dy, float *dweight, float *dbias, void *workspace, int64_t workspace_bytes,
+                            void *stream);
 
 /*
  * The GeeseNet unit chain (hungry_geese.py:48-51, h_{i+1} = relu(h_i + bn_i(conv_i(h_i)))) with the

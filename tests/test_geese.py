@@ -331,6 +331,42 @@ def test_presplit_form_is_bit_identical(cuda, N, H, W):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('N,split', [(41, None), (3001, None), (1500, 2)])
+def test_tower_bn_fold_is_bit_identical(cuda, N, split):
+    """_TorusTower's backward with each unit's masked BatchNorm backward apply formed in its weight gradient's
+    staging (nn.TOWER_BN_FOLD, hrl_torus_conv_wgrad_bn + hrl_bn_backward_masked_coefs) against the separate
+    apply passes (hrl_bn_backward_masked / hrl_bn_backward_apply_masked + hrl_torus_conv_wgrad): every gradient
+    bit for bit, the tower whole and split in two."""
+    from handyrl_amd import nn as hnn
+
+    def run():
+        torch.manual_seed(N)
+        units = [TorusConv2d(17, 32, (3, 3), True)] + [TorusConv2d(32, 32, (3, 3), True) for _ in range(3)]
+        for u in units:
+            with torch.no_grad():
+                u.bn.weight.uniform_(0.5, 1.5)
+                u.bn.bias.uniform_(-0.2, 0.2)
+            u.to(cuda).use_hip = True
+        if split is not None:
+            units[0].tower_split = split
+        x = torch.randn(N, 17, 7, 11, device=cuda).requires_grad_(True)
+        h = hnn.torus_tower(x, units)
+        h.backward(torch.randn(N, 32, 7, 11, device=cuda))
+        return [x.grad] + [p.grad for u in units for p in u.parameters()]
+
+    prev = hnn.TOWER_BN_FOLD
+    try:
+        hnn.TOWER_BN_FOLD = False
+        a = run()
+        hnn.TOWER_BN_FOLD = True
+        b = run()
+    finally:
+        hnn.TOWER_BN_FOLD = prev
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), i
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('N', [1, 37, 3000])
 def test_geese_pool_matches_torch(cuda, N):
     """nn.geese_pool (HIP head pooling) vs the reference's torch expressions (hungry_geese.py:52-53) on the
