@@ -391,7 +391,7 @@ def cpu_baseline(B=4096, T=32, steps=3, threads_secondary=8):
             'host': {'cpu_model': cpu_model(), 'os_cpu_count': os.cpu_count()}}
 
 
-def secondary_t9(device, steps=10, warmup=3, B=4096, T=9):
+def secondary_t9(device, steps=40, warmup=20, B=4096, T=9):
     """BASELINE.json configs[1]: TicTacToe B=4096 T=9, the north star's >=50x point."""
     args = default_args(T, B)
     torch.manual_seed(0)
@@ -440,7 +440,7 @@ def secondary_rollout(device, E=16384, reps=5):
             'reference_cpu_source': 'SURVEY §6: generation.py per worker process, measured in the survey container'}
 
 
-def secondary_geister_learner(device, B=256, T=16, steps=10, warmup=3):
+def secondary_geister_learner(device, B=256, T=16, steps=20, warmup=10):
     """recurrent learner step (GeisterNet unrolled over T, config.yaml batch 256)."""
     from handyrl_amd.envs.geister import GeisterNet
     from handyrl_amd.synthetic import geister_batch
@@ -467,7 +467,7 @@ def secondary_geister_learner(device, B=256, T=16, steps=10, warmup=3):
                                     'B=64 T=16, 1 thread, 929 env-steps/s (build container)'}
 
 
-def secondary_geese_learner(device, B=2048, T=64, steps=3, warmup=1):
+def secondary_geese_learner(device, B=2048, T=64, steps=5, warmup=3):
     """BASELINE.json configs[3]: Hungry Geese GeeseNet learner, B=2048 T=64, solo training (P = Pp = 1),
     UPGO policy / VTRACE value targets; 13 torus 3x3 convs (csrc/hrl_torus.hip) over B*T boards."""
     from handyrl_amd.envs.hungry_geese import GeeseNet
@@ -578,8 +578,10 @@ def secondary_geister_rollout(device, E=2048, reps=2):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=5)
+    # the warm-up covers the eager steps, the capture and the first graph replays, which run ~10% slow while
+    # the clocks settle after the capture's idle GPU (profiles/r05_replay_gaps.txt: replays 0-9)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=30)
     ap.add_argument('--batch', type=int, default=4096, help='trajectories per GPU (B)')
     ap.add_argument('--seq', type=int, default=32, help='forward_steps (T)')
     ap.add_argument('--graph', type=int, default=1, help='capture the step in HIP graphs (N>1: backward and update graphs around the all-reduce)')

@@ -13,7 +13,7 @@ timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method threa
 tail -2 $out/tests.log
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $out/trace -o run -- python3 bench.py --cpu-baseline 0 --secondary 0 > $out/bench_trace.log 2>&1 || { tail -20 $out/bench_trace.log; exit 1; }
 tr=$(ls $out/trace/*kernel_trace.csv)
-python3 tools/replay_gaps.py $tr --marker adam_clip_kernel --skip 4 --count 20 > $out/replay_gaps.txt
+python3 tools/replay_gaps.py $tr --marker adam_clip_kernel --skip 30 --count 40 > $out/replay_gaps.txt
 rm -f $tr
 sed -n '21,60p' $out/replay_gaps.txt
 timeout -k 10 300 python3 bench.py > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
