@@ -290,7 +290,7 @@ def time_block_backward(device, M, iters=20):
 
 def time_block_in_step(learner, batch, device, steps=4):
     """The dominant kernel as the step runs it: HIP events on the launch stream around every chain block backward
-    launch (conv3x3_block_bwd2_kernel + its weight-gradient fold) of a few EAGER learner steps (the same
+    launch (conv3x3_block_bwd2_kernel; its partials are folded by the step tail) of a few EAGER learner steps (the same
     kernels the graph replays, on the step's own data), after the timed region."""
     from handyrl_amd import nn as hnn
     hnn.BLOCK_TIMING = []
@@ -668,8 +668,9 @@ def main():
         blk_gbs = blk_bytes / (us_blk * 1e-6) / 1e9
         blk_tf = block_roof['flops_per_launch'] / (us_blk * 1e-6) / 1e12
         roof = {
-            'kernel': 'conv3x3_block_bwd2_kernel (+ its weight-gradient fold): one chain block backward of the step '
-                      '(BN backward apply + weight gradient + input gradient, csrc/hrl_conv.hip)',
+            'kernel': 'conv3x3_block_bwd2_kernel: one chain block backward of the step (BN backward apply + weight '
+                      'gradient + input gradient, csrc/hrl_conv.hip; its weight-gradient partials are folded by the '
+                      'step tail)',
             'bound': 'hbm',
             'achieved': round(blk_gbs, 1),
             'peak': HBM_PEAK_GBS,
@@ -682,7 +683,8 @@ def main():
             'us_per_launch': round(us_blk, 2),
             'launches_timed': n_blk,
             'timing': 'HIP events on the launch stream around each of the step\'s block backward launches in eager '
-                      'steps after the timed region (the graph replays the same launches)',
+                      'steps after the timed region (the graph replays the same launches), each start event queued '
+                      'behind a ~50 us GPU spin so the host\'s launch latency is not inside the interval',
             'mfma_achieved_TFLOPs': round(blk_tf, 1),
             'mfma_frac_split': round(blk_tf / (MFMA_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS), 4),
         }

@@ -397,6 +397,10 @@ BLOCK_TIMING = None
 def _block_timing_start():
     if BLOCK_TIMING is None or torch.cuda.is_current_stream_capturing():
         return None
+    # an eager step is host-bound: without work queued ahead, the start event fires while the host is still
+    # marshalling the launch and the interval measures that wait too.  A ~50 us spin keeps the stream busy until
+    # the launch is queued behind the event, so the interval is the kernel's own duration (as rocprofv3 sees it).
+    torch.cuda._sleep(100000)
     ev = torch.cuda.Event(enable_timing=True)
     ev.record()
     return ev
