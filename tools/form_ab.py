@@ -23,7 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--setter', required=True)
     ap.add_argument('--forms', default='1,2,1,2')
-    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=30)
     ap.add_argument('--seq', type=int, default=32)
     opts = ap.parse_args()
     dev = torch.device('cuda', 0)
@@ -36,7 +37,7 @@ def main():
         net = SimpleConv2dModel().to(dev)
         batch = tictactoe_batch(B, T, dev, seed=1000)
         learner = LearnerStep(net, default_args(T, B), dev, graph=True)
-        for _ in range(5):
+        for _ in range(opts.warmup):   # past the first graph replays, which run slow while the clocks settle
             learner.step(batch)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
