@@ -148,7 +148,6 @@ SIGNATURES = {
     'hrl_clip_grad_norm_ws': (ctypes.c_int, [_f32p, _i64, _dbl, _f32p, ctypes.c_void_p, _i64, ctypes.c_void_p]),
     'hrl_heads_workspace_bytes': (ctypes.c_int64, [_i64]),
     'hrl_heads_bn_parts': (ctypes.c_int64, [_i64]),
-    'hrl_heads_set_fwd_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_heads_set_bwd_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_heads_forward': (ctypes.c_int, [_f32p, _i64, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
                                          _f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_void_p]),
@@ -227,7 +226,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 24
+ABI_VERSION = 23
 
 _lib = None
 

@@ -163,8 +163,7 @@ __device__ __forceinline__ void store_rows(const float *src, float *dst, int nf,
     }
 }
 
-// Form 1 (hrl_heads_set_fwd_form(1), for measurement): the 4-channel slices of 144 bytes
-__global__ __launch_bounds__(64, 2) void heads_fwd1_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
+__global__ __launch_bounds__(64, 2) void heads_fwd_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
                                                        float *__restrict__ a_p, float *__restrict__ a_v,
                                                        float *__restrict__ p_out, float *__restrict__ v_out,
                                                        bool tanh_v) {
@@ -243,162 +242,6 @@ __global__ __launch_bounds__(64, 2) void heads_fwd1_kernel(const float *__restri
             slice(st0, s);
             slice(st1, s + 1);
         }
-        float a[kZ];
-#pragma unroll
-        for (int m = 0; m < kM; ++m) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                a[m * kHW + 2 * k] = zp[m][k].x;
-                a[m * kHW + 2 * k + 1] = zp[m][k].y;
-            }
-            a[m * kHW + 8] = z8[m];
-        }
-#pragma unroll
-        for (int j = 0; j < kZ; ++j) a[j] = a[j] > 0.f ? a[j] : a[j] * kSlope;
-        float p[kOP];
-#pragma unroll
-        for (int k = 0; k < kOP; ++k) {
-            asm volatile("" ::: "memory");   // one output's 18 weights in flight at a time, not all 162
-            float t = 0.f;
-#pragma unroll
-            for (int j = 0; j < kZP; ++j) t = __builtin_fmaf(swp[k * kZP + j], a[j], t);
-            p[k] = t;
-        }
-        float v = 0.f;
-#pragma unroll
-        for (int q = 0; q < kHW; ++q) v = __builtin_fmaf(swv[q], a[kZP + q], v);
-        v = tanh_v ? tanhf(v) : v;   // the model's torch.tanh on the value head, folded
-        // the block's outputs leave through the (dead) tile as contiguous runs: one row per lane straight from
-        // registers is a 36- or 72-byte stride across the wave's 64 rows, many partial lines per store
-        // (tile = [a_p 64 x 18 | a_v 64 x 9 | p 64 x 9 | v 64] = 64 x 37 floats)
-        float *to_ap = tile, *to_av = tile + 64 * kZP, *to_p = to_av + 64 * kHW, *to_v = to_p + 64 * kOP;
-#pragma unroll
-        for (int j = 0; j < kZP; ++j) to_ap[lane * kZP + j] = a[j];
-#pragma unroll
-        for (int q = 0; q < kHW; ++q) to_av[lane * kHW + q] = a[kZP + q];
-#pragma unroll
-        for (int k = 0; k < kOP; ++k) to_p[lane * kOP + k] = p[k];
-        to_v[lane] = v;
-        lds_fence();
-        store_rows(to_p, p_out + base * kOP, nrows * kOP, lane);
-        store_rows(to_v, v_out + base, nrows, lane);
-        if (a_p) {
-            store_rows(to_ap, a_p + base * kZP, nrows * kZP, lane);
-            store_rows(to_av, a_v + base * kHW, nrows * kHW, lane);
-        }
-        lds_fence();   // the stores' LDS reads are done before the next block's slices land in the tile
-    }
-}
-
-// The forward streams h in LINE-ALIGNED slices: 32 floats = one 128-byte line of every row, 9 per row (channel
-// c's 9 cells, floats 9c .. 9c+8, may straddle two slices).  The 4-channel slices of 144 bytes straddle lines and
-// every line is touched by two slices: that pattern reads at 5.0 TB/s against 6.4 for line slices
-// (tools/micro/slice_patterns.hip, profiles/r05_slice_patterns.txt).  Two slices in flight in registers, two slice
-// buffers in LDS: a channel is consumed once the slice holding its last cell has landed, reading its first cells
-// from the previous slice's buffer.
-constexpr int kLF = 32;                  // floats per line slice
-constexpr int kNL = kRow / kLF;          // 9 line slices per row
-constexpr int kLV = kLF / 4 * 64 / 64;   // float4 per lane per slice (8)
-constexpr int kLS = kLF + 1;             // LDS row stride of a slice buffer (odd)
-static_assert(2 * 64 * kLS >= 64 * (kZP + kHW + kOP + 1), "the output staging reuses the slice buffers");
-
-__global__ __launch_bounds__(64, 2) void heads_fwd_kernel(const float *__restrict__ h, int64_t N, Weights w, BnIn bn,
-                                                       float *__restrict__ a_p, float *__restrict__ a_v,
-                                                       float *__restrict__ p_out, float *__restrict__ v_out,
-                                                       bool tanh_v) {
-    __shared__ __attribute__((aligned(16))) float tile[2 * 64 * kLS];
-    __shared__ float sw1[kM * kC], sb1[kM], swp[kOP * kZP], swv[kHW], sal[kC], sbe[kC];
-    const int lane = threadIdx.x;
-    if (bn.alpha && lane < kC) {
-        sal[lane] = bn.alpha[lane];
-        sbe[lane] = bn.beta[lane];
-    }
-    for (int i = lane; i < kM * kC; i += 64) sw1[i] = w1_at(w, i / kC, i % kC);
-    if (lane < kM) sb1[lane] = lane < kMP ? w.b1p[lane] : w.b1v[lane - kMP];
-    for (int i = lane; i < kOP * kZP; i += 64) swp[i] = w.wp[i];
-    if (lane < kHW) swv[lane] = w.wv[lane];
-    __syncthreads();
-    // lane's loads of a slice: float4 c4 = lane & 7 of rows 8k + (lane >> 3): every load instruction reads 8 whole
-    // lines; the slice's 128-byte step is the scalar offset
-    uint32_t vo[kLV];
-#pragma unroll
-    for (int k = 0; k < kLV; ++k) vo[k] = (uint32_t)(((8 * k + (lane >> 3)) * kRow + (lane & 7) * 4) * 4);
-
-    for (int64_t base = (int64_t)blockIdx.x * 64; base < N; base += (int64_t)gridDim.x * 64) {
-        // Wp / W1 / the BN constants are re-read from LDS per block: hoisted out of the loop they held ~170 VGPRs
-        asm volatile("" ::: "memory");
-        const int nrows = (int)min<int64_t>(64, N - base);
-        // z[m][q] = b1[m] + sum_c W1[m][c] h[c][q] (fused multiply-adds, channels in order): cells 0..7 as 4 pairs
-        f32x2 zp[kM][4];
-        float z8[kM];
-#pragma unroll
-        for (int m = 0; m < kM; ++m) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) zp[m][k] = (f32x2){sb1[m], sb1[m]};
-            z8[m] = sb1[m];
-        }
-        const __amdgpu_buffer_rsrc_t rh = heads_rsrc(h + base * kRow, (uint32_t)(nrows * kRow * 4));
-        float4 st[2][kLV];
-        auto load = [&](float4 (&v)[kLV], int sl) __attribute__((always_inline)) {
-#pragma unroll
-            for (int k = 0; k < kLV; ++k) {
-                const hu32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rh, vo[k], sl * kLF * 4, 0);
-                v[k] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
-                                   __uint_as_float(u.w));
-            }
-        };
-        auto slice = [&](float4 (&v)[kLV], int sl) __attribute__((always_inline)) {
-            float *buf = tile + (sl & 1) * 64 * kLS;
-#pragma unroll
-            for (int k = 0; k < kLV; ++k) {
-                float *d = buf + (8 * k + (lane >> 3)) * kLS + (lane & 7) * 4;
-                d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
-            }
-            lds_fence();
-            if (sl + 2 < kNL) load(v, sl + 2);   // in flight during the FMAs
-            // channel c ends at float 9c + 8: c_lo .. c_hi - 1 end in [32 sl, 32 sl + 31]
-            const int c_lo = (kLF * sl) / kHW, c_hi = (kLF * (sl + 1)) / kHW;
-#pragma unroll 1
-            for (int c = c_lo; c < c_hi; ++c) {
-                float x9[kHW];
-#pragma unroll
-                for (int q = 0; q < kHW; ++q) {
-                    const int f = c * kHW + q;   // float of the row: slice f / 32 sits in buffer (f / 32) & 1
-                    x9[q] = tile[((f >> 5) & 1) * 64 * kLS + lane * kLS + (f & (kLF - 1))];
-                }
-                f32x2 xp[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) xp[k] = (f32x2){x9[2 * k], x9[2 * k + 1]};
-                float x8 = x9[8];
-                if (bn.alpha) {   // bn_apply_kernel's float operations (a multiply, then an add), then the ReLU
-                    const float al = sal[c], be = sbe[c];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const f32x2 t = xp[k] * (f32x2){al, al} + (f32x2){be, be};
-                        xp[k] = (f32x2){t.x < 0.f ? 0.f : t.x, t.y < 0.f ? 0.f : t.y};
-                    }
-                    x8 = bn_relu(x8, al, be);
-                }
-#pragma unroll
-                for (int m = 0; m < kM; ++m) {
-                    const float wv1 = sw1[m * kC + c];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        zp[m][k] = __builtin_elementwise_fma((f32x2){wv1, wv1}, xp[k], zp[m][k]);
-                    z8[m] = __builtin_fmaf(wv1, x8, z8[m]);
-                }
-            }
-            // the next slice overwrites the buffer before this one: its channels are all consumed
-            lds_fence();
-        };
-        load(st[0], 0);
-        load(st[1], 1);
-#pragma unroll 1
-        for (int sl = 0; sl + 1 < kNL; sl += 2) {
-            slice(st[0], sl);
-            slice(st[1], sl + 1);
-        }
-        slice(st[0], kNL - 1);   // 9 slices: the last one is even
         float a[kZ];
 #pragma unroll
         for (int m = 0; m < kM; ++m) {
@@ -947,7 +790,6 @@ constexpr int kGridFwd = 4096;   // one-wave workgroups: 64-row blocks, up to 4 
 constexpr int kGridBwd = 768;
 constexpr int kGridBwd2 = 512;    // heads_bwd2_kernel: 2 four-wave workgroups per CU (72 KB LDS each)
 int g_heads_bwd_form = 2;         // hrl_heads_set_bwd_form
-int g_heads_fwd_form = 2;         // hrl_heads_set_fwd_form: 2 = line slices (heads_fwd_kernel), 1 = 144-byte slices
 
 int status() {
     const hipError_t e = hipGetLastError();
@@ -985,12 +827,6 @@ int hrl_heads_set_bwd_form(int form) {
     return prev;
 }
 
-int hrl_heads_set_fwd_form(int form) {
-    const int prev = g_heads_fwd_form;
-    if (form == 1 || form == 2) g_heads_fwd_form = form;   // any other value only queries
-    return prev;
-}
-
 int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *b1p, const float *w1v,
                       const float *b1v, const float *wp, const float *wv, const float *bn_alpha, const float *bn_beta,
                       float *a_p, float *a_v, float *p_out, float *v_out, int tanh_v, void *stream) {
@@ -999,12 +835,8 @@ int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *
         return HRL_EINVAL;
     const Weights w{w1p, w1v, b1p, b1v, wp, wv};
     const BnIn bn{bn_alpha, bn_beta, nullptr, nullptr};
-    if (g_heads_fwd_form == 1)
-        hipLaunchKernelGGL(heads_fwd1_kernel, dim3(grid_for(N, kGridFwd)), dim3(64), 0, static_cast<hipStream_t>(stream),
-                           h, N, w, bn, a_p, a_v, p_out, v_out, tanh_v != 0);
-    else
-        hipLaunchKernelGGL(heads_fwd_kernel, dim3(grid_for(N, kGridFwd)), dim3(64), 0, static_cast<hipStream_t>(stream),
-                           h, N, w, bn, a_p, a_v, p_out, v_out, tanh_v != 0);
+    hipLaunchKernelGGL(heads_fwd_kernel, dim3(grid_for(N, kGridFwd)), dim3(64), 0, static_cast<hipStream_t>(stream), h, N, w,
+                       bn, a_p, a_v, p_out, v_out, tanh_v != 0);
     return status();
 }
 

@@ -483,9 +483,6 @@ int hrl_heads_forward(const float *h, int64_t N, const float *w1p, const float *
  * Process-wide; returns the previous setting (any other value only queries it).  hrl_heads_bn_parts /
  * hrl_heads_workspace_bytes follow the form; the deferred (NULL-gradient) mode needs form 2. */
 int hrl_heads_set_bwd_form(int form);
-/* hrl_heads_set_fwd_form: 2 (default) = the forward reading h in 128-byte line slices, 1 = in 144-byte 4-channel
- * slices (for measurement); identical results.  1 or 2 sets, any other value only queries; returns the previous. */
-int hrl_heads_set_fwd_form(int form);
 int hrl_heads_backward(const float *h, int64_t N, const float *w1p, const float *w1v, const float *wp,
                        const float *wv, const float *bn_alpha, const float *bn_beta, const float *bn_mean,
                        double *bn_part, const float *a_p, const float *a_v, const float *dp, const float *dv,

@@ -53,18 +53,9 @@ def main():
         return a.elapsed_time(b) / o.iters * 1e3
 
     rd, wr = h.numel() * 4, (a_p.numel() + a_v.numel() + p_out.numel() + v_out.numel()) * 4
-    res = {'N': N, 'read_bytes': rd, 'write_bytes': wr}
-    outs = {}
-    for rnd in range(2):   # forms alternated twice on the same box
-        for form in (1, 2):
-            prev = lib.hrl_heads_set_fwd_form(form)
-            us = timed()
-            lib.hrl_heads_set_fwd_form(prev)
-            res['form%d_us_%d' % (form, rnd)] = round(us, 2)
-            res['form%d_TBps_%d' % (form, rnd)] = round((rd + wr) / us / 1e6, 2)
-            outs[form] = [t.clone() for t in (a_p, a_v, p_out, v_out)]
-    res['forms_identical'] = all(torch.equal(x, y) for x, y in zip(outs[1], outs[2]))
-    print(json.dumps(res))
+    us = timed()
+    print(json.dumps({'N': N, 'us': round(us, 2), 'read_bytes': rd, 'write_bytes': wr,
+                      'TBps': round((rd + wr) / us / 1e6, 2)}))
 
 
 if __name__ == '__main__':
