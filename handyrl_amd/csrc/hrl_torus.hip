@@ -232,52 +232,72 @@ __device__ __forceinline__ void pro_to_lds(const Stage<true, NLD, true> &sx, con
 
 // SUMS epilogue, after the output tile is complete (vec layout only): store out = tile + add*[mask > 0],
 // then the per-channel sums of out*[hmask > 0] (s1) and out*[hmask > 0]*(yprev - mean) (s2) in fp64.
-// Lane l owns channel l & 31 and half (l >> 5) of the cells; its masked values wait in registers while
-// the tile is refilled with yprev - mean.
+// Lane l owns channel l & 31 and half (l >> 5) of the cells: it reads its 40 yprev values straight from the
+// channel row (issued first, in flight during the store pass) and the masked values from the tile twice.
+// Every global load of a pass is issued before its first use: the per-float4 loop this replaces waited for each
+// iteration's loads in turn, ten round trips per sample.
 __device__ __forceinline__ void store_sample_sums(float *tile, float *dst, int n_elem, int HW, float inv_hw,
-                                                  int lane, const float *add, const float *mask,
-                                                  const float *hmask, const float *yprev, const float *mean_s,
+                                                  int lane, const float *__restrict__ add,
+                                                  const float *__restrict__ mask, const float *__restrict__ hmask,
+                                                  const float *__restrict__ yprev, const float *mean_s,
                                                   double &s1, double &s2) {
+    constexpr int kNV = kCo * kMaxCells / 4 / 64;   // float4 per lane of an 80-cell sample
+    constexpr int kH = kNV / 2;                     // the store pass in two halves: 15 float4 in flight
+    constexpr int kHalf = kMaxCells / 2;
     const int nv = n_elem >> 2;
-    for (int i = lane; i < nv; i += 64) {
-        const float4 a = reinterpret_cast<const float4 *>(add)[i];
-        const float4 m = reinterpret_cast<const float4 *>(mask)[i];
-        const float4 hm = reinterpret_cast<const float4 *>(hmask)[i];
-        const float a4[4] = {a.x, a.y, a.z, a.w}, m4[4] = {m.x, m.y, m.z, m.w}, h4[4] = {hm.x, hm.y, hm.z, hm.w};
-        float x4[4];
-        const Quad q(i, HW, inv_hw);
+    const int c = lane & 31, c0 = (lane >> 5) * kHalf;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float *slot = tile + q.slot(j, HW);
-            x4[j] = *slot + (m4[j] > 0.f ? a4[j] : 0.f);
-            *slot = h4[j] > 0.f ? x4[j] : 0.f;
+    for (int h = 0; h < 2; ++h) {
+        asm volatile("" ::: "memory");
+        float4 a[kH], m[kH], hm[kH];
+#pragma unroll
+        for (int k = 0; k < kH; ++k) {
+            const int i = min((h * kH + k) * 64 + lane, nv - 1);
+            a[k] = reinterpret_cast<const float4 *>(add)[i];
+            m[k] = reinterpret_cast<const float4 *>(mask)[i];
+            hm[k] = reinterpret_cast<const float4 *>(hmask)[i];
         }
-        reinterpret_cast<float4 *>(dst)[i] = make_float4(x4[0], x4[1], x4[2], x4[3]);
+#pragma unroll
+        for (int k = 0; k < kH; ++k) {
+            const int i = (h * kH + k) * 64 + lane;
+            if (i < nv) {
+                const float a4[4] = {a[k].x, a[k].y, a[k].z, a[k].w}, m4[4] = {m[k].x, m[k].y, m[k].z, m[k].w};
+                const float h4[4] = {hm[k].x, hm[k].y, hm[k].z, hm[k].w};
+                float x4[4];
+                const Quad q(i, HW, inv_hw);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float *slot = tile + q.slot(j, HW);
+                    x4[j] = *slot + (m4[j] > 0.f ? a4[j] : 0.f);
+                    *slot = h4[j] > 0.f ? x4[j] : 0.f;
+                }
+                reinterpret_cast<float4 *>(dst)[i] = make_float4(x4[0], x4[1], x4[2], x4[3]);
+            }
+        }
+    }
+    // the lane's channel row segment through a buffer descriptor over the sample: one address register, the cell as
+    // the immediate offset; cells past the row read the next channel's (unused), past the sample 0
+    float yv[kHalf];
+    {
+        const uint64_t p = reinterpret_cast<uint64_t>(yprev);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+        const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), (short)0, n_elem * 4, 0x00020000);
+        const int vo = (c * HW + c0) * 4;
+#pragma unroll
+        for (int j = 0; j < kHalf; ++j)
+            yv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, vo, j * 4, 0));
     }
     lds_fence();
-    constexpr int kHalf = kMaxCells / 2;
-    const int c = lane & 31, c0 = (lane >> 5) * kHalf;
-    float gm[kHalf];
     float t1 = 0.f, t2 = 0.f;   // fp32 within the sample, fp64 across samples (as the STATS epilogue)
 #pragma unroll
-    for (int j = 0; j < kHalf; ++j) {
-        gm[j] = c0 + j < HW ? tile[c * kS + c0 + j] : 0.f;
-        t1 += gm[j];
-    }
+    for (int j = 0; j < kHalf; ++j) t1 += c0 + j < HW ? tile[c * kS + c0 + j] : 0.f;
     s1 += (double)t1;
-    lds_fence();
-    for (int i = lane; i < nv; i += 64) {
-        const float4 yv = reinterpret_cast<const float4 *>(yprev)[i];
-        const float y4[4] = {yv.x, yv.y, yv.z, yv.w};
-        const Quad q(i, HW, inv_hw);
-        const float mu0 = mean_s[q.c0], mu1 = mean_s[q.c0 + 1];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) tile[q.slot(j, HW)] = y4[j] - (q.wrap(j, HW) ? mu1 : mu0);
-    }
-    lds_fence();
+    const float mu = mean_s[c];
 #pragma unroll
     for (int j = 0; j < kHalf; ++j)
-        if (c0 + j < HW) t2 += gm[j] * tile[c * kS + c0 + j];
+        if (c0 + j < HW) t2 += tile[c * kS + c0 + j] * (yv[j] - mu);
     s2 += (double)t2;
 }
 
