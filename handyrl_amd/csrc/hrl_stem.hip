@@ -168,15 +168,20 @@ __global__ __launch_bounds__(kThreads) void stem_fwd2_kernel(const float *__rest
     const float bias = b ? b[co] : 0.f;
     const int64_t noct = (N + kOct - 1) / kOct;
     const int64_t wstep = (int64_t)gridDim.x * kWaves;
-    for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < noct; t += wstep) {
+    // the octet's observations: kXO / 4 float4s (rows past N read 0); the next octet's are in flight during this
+    // one's FMAs and stores
+    auto load_x = [&](int64_t t) __attribute__((always_inline)) {
         const int64_t rows = min<int64_t>(kOct, N - kOct * t);
         const __amdgpu_buffer_rsrc_t rx = rsrc_of(x + kOct * t * kXF, rows * kXF * 4);
+        return lane < kXO / 4 ? __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16, 0, 0) : (hu32x4){0u, 0u, 0u, 0u};
+    };
+    int64_t t = (int64_t)blockIdx.x * kWaves + wave;
+    hu32x4 xn = t < noct ? load_x(t) : (hu32x4){0u, 0u, 0u, 0u};
+    for (; t < noct; t += wstep) {
+        const int64_t rows = min<int64_t>(kOct, N - kOct * t);
         const __amdgpu_buffer_rsrc_t ry = rsrc_of(y + kOct * t * kCols, rows * kCols * 4);
-        // the octet's observations: kXO / 4 float4s (rows past N read 0)
-        if (lane < kXO / 4) {
-            const hu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16, 0, 0);
-            *reinterpret_cast<hu32x4 *>(xw + 4 * lane) = v;
-        }
+        if (lane < kXO / 4) *reinterpret_cast<hu32x4 *>(xw + 4 * lane) = xn;
+        if (t + wstep < noct) xn = load_x(t + wstep);
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes done
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -364,15 +369,29 @@ __global__ __launch_bounds__(kThreads, 4) void stem_wgrad2_kernel(const float *_
             d[3 * m + 2] = __uint_as_float(v.z);
         }
     };
+    // the block's observation rows are one contiguous run of kBR * kXF floats: all of a lane's loads issue together
+    // (a load-then-store loop over the padded LDS layout waited for each load in turn); the pad columns stay 0
+    const __amdgpu_buffer_rsrc_t rx = rsrc_of(x, N * kXF * 4);   // rows past N read 0
+    constexpr int kXL = (kBR * kXF + 63) / 64;
+    for (int i = lane; i < kBR * (kXS - kXF); i += 64) xw[(i / (kXS - kXF)) * kXS + kXF + i % (kXS - kXF)] = 0.f;
     for (int64_t blk = (int64_t)blockIdx.x * kWaves + wave; blk < nblocks; blk += wstep) {
         const int64_t base = blk * kBR;
         float dn[kCells];
         load_dy(base + r, dn);   // rows past N read 0 (the descriptor's range)
-        // the block's observation rows into LDS (rows past N: 0)
-        for (int i = lane; i < kBR * kXS; i += 64) {
-            const int rr = i / kXS, k = i - rr * kXS;
-            const int64_t n = base + rr;
-            xw[i] = (k < kXF && n < N) ? x[n * kXF + k] : 0.f;
+        float xr[kXL];
+        const uint32_t xb = (uint32_t)(base * kXF * 4);
+#pragma unroll
+        for (int k = 0; k < kXL; ++k) {
+            const int e = k * 64 + lane;
+            xr[k] = e < kBR * kXF ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, xb + e * 4, 0, 0)) : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < kXL; ++k) {
+            const int e = k * 64 + lane;
+            if (e < kBR * kXF) {
+                const int rr = e / kXF;
+                xw[rr * kXS + e - rr * kXF] = xr[k];
+            }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();

@@ -1173,10 +1173,14 @@ __global__ __launch_bounds__(256) void torus_wgrad_reduce_kernel(const float *__
 // One wave per sample: the sample is staged [c][cell] in LDS (coalesced float4 loads), then lane l sums
 // channel l & 31 over the cells, lanes 0-31 the x-weighted sum and 32-63 the mean (sum / HW, as the
 // reference's CPU mean: sum then divide).
+// (round 5: each sample's loads are issued together and the next sample's are in flight during this one's sums;
+// the per-float4 loops waited for every iteration's loads in turn)
 __global__ __launch_bounds__(kThreads) void torus_head_pool_kernel(const float *__restrict__ h,
                                                                    const float *__restrict__ x, int64_t N, int HW,
                                                                    int64_t x_stride, float *__restrict__ head,
                                                                    float *__restrict__ avg) {
+    constexpr int kNV = kCo * kMaxCells / 4 / 64;   // float4 per lane of an 80-cell sample
+    constexpr int kNX = kMaxCells / 64 + 1;         // x0 cells per lane
     __shared__ float tiles[kWaves * kTile];
     __shared__ float x0s[kWaves][kMaxCells];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1185,17 +1189,34 @@ __global__ __launch_bounds__(kThreads) void torus_head_pool_kernel(const float *
     const float inv_hw = 1.0f / (float)HW;
     const int nv = kCo * HW / 4;
     const int c = lane & 31;
-    for (int64_t n = (int64_t)blockIdx.x * kWaves + wave; n < N; n += (int64_t)gridDim.x * kWaves) {
-        const float4 *src = reinterpret_cast<const float4 *>(h + n * (kCo * HW));
-        for (int i = lane; i < nv; i += 64) {
-            const float4 v = src[i];
-            const float v4[4] = {v.x, v.y, v.z, v.w};
-            const Quad q(i, HW, inv_hw);
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    float4 v[kNV];
+    float xv[kNX];
+    auto load = [&](int64_t m) __attribute__((always_inline)) {
+        const float4 *src = reinterpret_cast<const float4 *>(h + m * (kCo * HW));
 #pragma unroll
-            for (int j = 0; j < 4; ++j) tile[q.slot(j, HW)] = v4[j];
+        for (int k = 0; k < kNV; ++k) v[k] = src[min(k * 64 + lane, nv - 1)];
+#pragma unroll
+        for (int k = 0; k < kNX; ++k) xv[k] = x[m * x_stride + min(k * 64 + lane, HW - 1)];
+    };
+    int64_t n = (int64_t)blockIdx.x * kWaves + wave;
+    if (n < N) load(n);
+    for (; n < N; n += stride) {
+#pragma unroll
+        for (int k = 0; k < kNV; ++k) {
+            const int i = k * 64 + lane;
+            if (i < nv) {
+                const float v4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+                const Quad q(i, HW, inv_hw);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) tile[q.slot(j, HW)] = v4[j];
+            }
         }
-        for (int q = lane; q < HW; q += 64) x0[q] = x[n * x_stride + q];
+#pragma unroll
+        for (int k = 0; k < kNX; ++k)
+            if (k * 64 + lane < HW) x0[k * 64 + lane] = xv[k];
         lds_fence();
+        if (n + stride < N) load(n + stride);   // in flight during the sums
         float acc = 0.f;
         if (lane < 32) {
             for (int q = 0; q < HW; ++q) acc += tile[c * kS + q] * x0[q];
@@ -1210,17 +1231,35 @@ __global__ __launch_bounds__(kThreads) void torus_head_pool_kernel(const float *
 
 // the backward of both poolings as CPU autograd computes it (mul backward dhead*x0, mean backward davg / HW,
 // summed):
-// g[n, c, q] = dhead[n, c] * x[n, 0, q] + davg[n, c] / HW; one wave per sample, float4 stores
+// g[n, c, q] = dhead[n, c] * x[n, 0, q] + davg[n, c] / HW; one wave per sample, float4 stores.  The sample's
+// dhead / davg / x0 go through LDS, the next sample's loads in flight during this one's stores.
 __global__ __launch_bounds__(kThreads) void torus_head_unpool_kernel(const float *__restrict__ dhead,
                                                                      const float *__restrict__ davg,
                                                                      const float *__restrict__ x, int64_t N, int HW,
                                                                      int64_t x_stride, float *__restrict__ g) {
+    constexpr int kNX = kMaxCells / 64 + 1;
+    __shared__ float sds[kWaves][2 * kCo + kMaxCells];   // dhead [32] | davg [32] | x0 [80]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float *sd = sds[wave];
     const float inv_hw = 1.0f / (float)HW;
     const float fhw = (float)HW;
     const int nv = kCo * HW / 4;
-    for (int64_t n = (int64_t)blockIdx.x * kWaves + wave; n < N; n += (int64_t)gridDim.x * kWaves) {
-        const float *x0 = x + n * x_stride;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    float dv, xv[kNX];
+    auto load = [&](int64_t m) __attribute__((always_inline)) {
+        dv = lane < kCo ? dhead[m * kCo + lane] : davg[m * kCo + lane - kCo];
+#pragma unroll
+        for (int k = 0; k < kNX; ++k) xv[k] = x[m * x_stride + min(k * 64 + lane, HW - 1)];
+    };
+    int64_t n = (int64_t)blockIdx.x * kWaves + wave;
+    if (n < N) load(n);
+    for (; n < N; n += stride) {
+        sd[lane] = dv;
+#pragma unroll
+        for (int k = 0; k < kNX; ++k)
+            if (k * 64 + lane < HW) sd[2 * kCo + k * 64 + lane] = xv[k];
+        lds_fence();
+        if (n + stride < N) load(n + stride);
         float4 *dst = reinterpret_cast<float4 *>(g + n * (kCo * HW));
         for (int i = lane; i < nv; i += 64) {
             const Quad q(i, HW, inv_hw);
@@ -1230,10 +1269,11 @@ __global__ __launch_bounds__(kThreads) void torus_head_unpool_kernel(const float
                 const bool w = q.wrap(j, HW);
                 const int c = q.c0 + (w ? 1 : 0);
                 const int cell = q.r0 + j - (w ? HW : 0);
-                o[j] = dhead[n * kCo + c] * x0[cell] + davg[n * kCo + c] / fhw;
+                o[j] = sd[c] * sd[2 * kCo + cell] + sd[kCo + c] / fhw;
             }
             dst[i] = make_float4(o[0], o[1], o[2], o[3]);
         }
+        lds_fence();
     }
 }
 
