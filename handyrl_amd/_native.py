@@ -111,6 +111,13 @@ SIGNATURES = {
     'hrl_hidden_gather_backward_add': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, ctypes.c_int,
                                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                                       ctypes.c_void_p, ctypes.c_void_p]),
+    'hrl_hidden_update_gather': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, _i64, _f32p, _f32p, _i64, _i64,
+                                                ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p]),
+    'hrl_hidden_update_gather_backward': (ctypes.c_int, [ctypes.c_void_p, _f32p, _f32p, _i64, _i64, _i64,
+                                                         ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     'hrl_hidden_update_backward_add': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, _i64, ctypes.c_int,
                                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -226,7 +233,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 _lib = None
 

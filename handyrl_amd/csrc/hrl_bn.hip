@@ -246,8 +246,46 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
             }
             __syncthreads();
         }
+        // each group's outputs by a thread of its own (the fp64 divisions and square roots in parallel), then the
+        // order-dependent parts -- the running statistics' G updates, the weight / bias gradient sums -- by one
+        // thread in group order, as fin would run them (bit-identical)
+        __shared__ float gv[2][kThreads / 2];
+        if ((int)threadIdx.x < G) {
+            const int grp = threadIdx.x, gc = grp * C + c;
+            const double S0 = red[0][grp * tpg], S1 = red[1][grp * tpg];
+            if (mode == 0) {
+                const double mean = S0 / M;
+                double var = S1 / M - mean * mean;
+                if (var < 0.0) var = 0.0;
+                const float meanf = (float)mean;
+                const float invstd = (float)(1.0 / sqrt(var + eps));
+                save_mean[gc] = meanf;
+                save_invstd[gc] = invstd;
+                const float alpha = invstd * w;
+                coef_a[gc] = alpha;
+                coef_b[gc] = (bias ? bias[c] : 0.0f) - meanf * alpha;
+                gv[0][grp] = meanf;
+                gv[1][grp] = (float)(M > 1.0 ? var * M / (M - 1.0) : var);
+            } else {
+                const float invstd = save_invstd[gc];
+                const float sum_dy = (float)S0, dot = (float)S1;
+                coef_a[gc] = dot * invstd * invstd / (float)M;   // k
+                coef_b[gc] = sum_dy / (float)M;                   // mean(dy)
+                gv[0][grp] = dot * invstd;
+                gv[1][grp] = sum_dy;
+            }
+        }
+        __syncthreads();
         if (threadIdx.x == 0) {
-            for (int g2 = 0; g2 < G; ++g2) fin(g2, red[0][g2 * tpg], red[1][g2 * tpg]);
+            for (int g2 = 0; g2 < G; ++g2) {
+                if (mode == 0) {
+                    if (running_mean) running_mean[c] = momentum * gv[0][g2] + (1.0f - momentum) * running_mean[c];
+                    if (running_var) running_var[c] = momentum * gv[1][g2] + (1.0f - momentum) * running_var[c];
+                } else {
+                    dw = g2 == 0 ? gv[0][g2] : dw + gv[0][g2];
+                    db = g2 == 0 ? gv[1][g2] : db + gv[1][g2];
+                }
+            }
             if (mode == 1) {
                 if (dweight) dweight[c] = dw;
                 if (dbias) dbias[c] = db;

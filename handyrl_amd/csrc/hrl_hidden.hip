@@ -40,6 +40,8 @@ struct Leaves {
     float *d[kMaxLeaves];         // update bwd: dnh
     const float *e[kMaxLeaves];   // gather bwd: addend of dH; update bwd: addend of dnh (NULL: none)
     int64_t es[kMaxLeaves];       // the addend's row stride in floats (a channel slice of a wider tensor)
+    const float *f[kMaxLeaves];   // update-gather bwd: addend of dnh (e: of the new state's gradient)
+    int64_t fs[kMaxLeaves];
 };
 
 template <int VW>
@@ -160,6 +162,74 @@ __global__ __launch_bounds__(kThreads) void hidden_update_bwd_kernel(const float
     }
 }
 
+// step t's update fused with step t+1's gather (round 5): out = H (1 - m) + nh m as hidden_update_kernel, then
+// the next step's input from out with mask mn as hidden_gather_sum/keep_kernel (the same float operations in the
+// same order: the two launches' results bit for bit).  a = H, b = nh, c = out, d = the gathered input.
+template <int VW>
+__global__ __launch_bounds__(kThreads) void hidden_update_gather_kernel(const float *__restrict__ m,
+                                                                        const float *__restrict__ mn, int B, int P,
+                                                                        int Pn, int summed, Leaves L) {
+    using W = V<VW>;
+    using T = typename W::T;
+    HRL_LEAF_LOOP
+    const T *h = reinterpret_cast<const T *>(L.a[l]);
+    const T *nh = reinterpret_cast<const T *>(L.b[l]);
+    T *o = reinterpret_cast<T *>(L.c[l]);
+    T *go = reinterpret_cast<T *>(L.d[l]);
+    for (int b = blockIdx.y; b < B; b += gridDim.y) {
+        T acc;
+        for (int p = 0; p < P; ++p) {
+            const int bp = b * P + p;
+            const float mv = m[bp];
+            const T ov = W::add(W::mul(h[(int64_t)bp * nv + v], 1.0f - mv),
+                                W::mul(nh[(int64_t)(b * Pn + (Pn == 1 ? 0 : p)) * nv + v], mv));
+            o[(int64_t)bp * nv + v] = ov;
+            const T t = W::mul(ov, mn[bp]);
+            if (summed) acc = p == 0 ? t : W::add(acc, t);
+            else go[(int64_t)bp * nv + v] = t;
+        }
+        if (summed) go[(int64_t)b * nv + v] = acc;
+    }
+}
+
+// its adjoint: the gather's (dout = g m_next [+ e, the new state's other gradient]) then the update's (dH = dout
+// (1 - m); dnh = sum_p dout m (Pn = 1) or dout m [+ f, the step output's gradient]) -- the two adjoint launches'
+// operations in their order.  a = the gathered input's gradient (NULL: zero), c = dH, d = dnh.
+template <int VW>
+__global__ __launch_bounds__(kThreads) void hidden_update_gather_bwd_kernel(const float *__restrict__ m,
+                                                                            const float *__restrict__ mn, int B,
+                                                                            int P, int Pn, int summed, Leaves L) {
+    using W = V<VW>;
+    using T = typename W::T;
+    HRL_LEAF_LOOP
+    const T *g = reinterpret_cast<const T *>(L.a[l]);
+    const T *e = reinterpret_cast<const T *>(L.e[l]);
+    const T *fa = reinterpret_cast<const T *>(L.f[l]);
+    T *d = reinterpret_cast<T *>(L.c[l]);
+    T *dn = reinterpret_cast<T *>(L.d[l]);
+    for (int b = blockIdx.y; b < B; b += gridDim.y) {
+        T acc;
+        for (int p = 0; p < P; ++p) {
+            const int bp = b * P + p;
+            T go;
+            if (g) {
+                const T t = W::mul(g[(int64_t)(summed ? b : bp) * nv + v], mn[bp]);
+                go = e ? W::add(e[(int64_t)bp * (L.es[l] / VW) + v], t) : t;
+            } else {
+                go = e[(int64_t)bp * (L.es[l] / VW) + v];
+            }
+            d[(int64_t)bp * nv + v] = W::mul(go, 1.0f - m[bp]);
+            const T t = W::mul(go, m[bp]);
+            if (Pn == 1) {
+                acc = p == 0 ? t : W::add(acc, t);
+            } else {
+                dn[(int64_t)bp * nv + v] = fa ? W::add(fa[(int64_t)bp * (L.fs[l] / VW) + v], t) : t;
+            }
+        }
+        if (Pn == 1) dn[(int64_t)b * nv + v] = fa ? W::add(fa[(int64_t)b * (L.fs[l] / VW) + v], acc) : acc;
+    }
+}
+
 int status() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
@@ -183,6 +253,8 @@ bool build(int n, const int64_t *F, int64_t B, int64_t P, const float *const *a,
         L.d[l] = d ? d[l] : nullptr;
         L.e[l] = nullptr;
         L.es[l] = F[l];
+        L.f[l] = nullptr;
+        L.fs[l] = F[l];
         if (F[l] % 4 || !aligned16(L.a[l]) || !aligned16(L.b[l]) || !aligned16(L.c[l]) || !aligned16(L.d[l])) vw = 1;
         if (F[l] > fmax) fmax = (int)F[l];
     }
@@ -285,6 +357,64 @@ int hrl_hidden_update_backward_add(const float *const *dout, const float *mask, 
     const dim3 grid = grid_of(fmax, vw, B, nleaves);
     if (vw == 4) hipLaunchKernelGGL(hidden_update_bwd_kernel<4>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, (int)Pn, L);
     else hipLaunchKernelGGL(hidden_update_bwd_kernel<1>, grid, dim3(kThreads), 0, s, mask, (int)B, (int)P, (int)Pn, L);
+    return status();
+}
+
+int hrl_hidden_update_gather(const float *const *H, const float *const *nh, int64_t Pn, const float *mask,
+                             const float *mask_next, int64_t B, int64_t P, int nleaves, const int64_t *F, int sum,
+                             float *const *out, float *const *gathered, void *stream) {
+    Leaves L;
+    int vw, fmax;
+    if (!mask || !mask_next || !nh || !gathered || (Pn != 1 && Pn != P)) return HRL_EINVAL;
+    if (!build(nleaves, F, B, P, H, nh, out, gathered, L, vw, fmax)) return HRL_EINVAL;
+    if (B == 0) return HRL_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 grid = grid_of(fmax, vw, B, nleaves);
+    if (vw == 4)
+        hipLaunchKernelGGL(hidden_update_gather_kernel<4>, grid, dim3(kThreads), 0, s, mask, mask_next, (int)B, (int)P,
+                           (int)Pn, sum, L);
+    else
+        hipLaunchKernelGGL(hidden_update_gather_kernel<1>, grid, dim3(kThreads), 0, s, mask, mask_next, (int)B, (int)P,
+                           (int)Pn, sum, L);
+    return status();
+}
+
+int hrl_hidden_update_gather_backward(const float *const *dgathered, const float *mask, const float *mask_next,
+                                      int64_t B, int64_t P, int64_t Pn, int nleaves, const int64_t *F, int sum,
+                                      const float *const *dstate, const int64_t *dstate_strides,
+                                      const float *const *dout_add, const int64_t *dout_add_strides,
+                                      float *const *dH, float *const *dnh, void *stream) {
+    if (!mask || !mask_next || !dgathered || !dnh || (Pn != 1 && Pn != P) || nleaves < 1 || nleaves > kMaxLeaves)
+        return HRL_EINVAL;
+    // a leaf's gathered-input gradient may be NULL (zero) when its new-state gradient is given
+    const float *a[kMaxLeaves];
+    for (int l = 0; l < nleaves; ++l) {
+        if (!dgathered[l] && !(dstate && dstate[l])) return HRL_EINVAL;
+        a[l] = dgathered[l] ? dgathered[l] : dnh[l];   // placeholder for build's check; reset below
+    }
+    Leaves L;
+    int vw, fmax;
+    if (!build(nleaves, F, B, P, a, nullptr, dH, dnh, L, vw, fmax) || !set_addend(L, dstate, dstate_strides, vw))
+        return HRL_EINVAL;
+    for (int l = 0; l < nleaves; ++l) {
+        L.a[l] = dgathered[l];
+        if (dout_add) {
+            const int64_t st = dout_add_strides ? dout_add_strides[l] : L.F[l];
+            if (dout_add[l] && (st < L.F[l] || st > ((int64_t)1 << 31))) return HRL_EINVAL;
+            L.f[l] = dout_add[l];
+            L.fs[l] = st;
+            if (!aligned16(dout_add[l]) || st % 4) vw = 1;
+        }
+    }
+    if (B == 0) return HRL_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 grid = grid_of(fmax, vw, B, nleaves);
+    if (vw == 4)
+        hipLaunchKernelGGL(hidden_update_gather_bwd_kernel<4>, grid, dim3(kThreads), 0, s, mask, mask_next, (int)B,
+                           (int)P, (int)Pn, sum, L);
+    else
+        hipLaunchKernelGGL(hidden_update_gather_bwd_kernel<1>, grid, dim3(kThreads), 0, s, mask, mask_next, (int)B,
+                           (int)P, (int)Pn, sum, L);
     return status();
 }
 

@@ -1777,6 +1777,63 @@ class _HiddenUpdate(torch.autograd.Function):
         return (None, None, None, None, None, None, *dH, *dnh)
 
 
+class _HiddenUpdateGather(torch.autograd.Function):
+    """Step t's _HiddenUpdate fused with step t+1's _HiddenGather (round 5): one launch each way
+    (hrl_hidden_update_gather[_backward]) where the unroll ran two, bit for bit the same values.
+
+    apply(m, m_next, summed, B, P, Pn, n, out_k, *H, *nh) -> (*gathered (step t+1's input), *state (views of the
+    new state, for step t+1's update), [nh[out_k] again if out_k >= 0: the step's output])."""
+
+    @staticmethod
+    def forward(ctx, m, m_next, summed, B, P, Pn, n, out_k, *tensors):
+        ctx.set_materialize_grads(False)
+        H = [h.contiguous() for h in tensors[:n]]
+        nh = [x.contiguous() for x in tensors[n:]]
+        outs = [torch.empty_like(h) for h in H]
+        rows = B if summed else B * P
+        gath = [torch.empty(rows, *h.shape[2:], dtype=h.dtype, device=h.device) for h in H]
+        F = [h[0, 0].numel() for h in H]
+        _native.check(_native.load().hrl_hidden_update_gather(
+            _native.ptr_array(H), _native.ptr_array(nh), Pn, _native.ptr(m), _native.ptr(m_next), B, P, n,
+            _native.i64_array(F), int(summed), _native.ptr_array(outs), _native.ptr_array(gath),
+            _native.stream_of(m.device)), 'hrl_hidden_update_gather')
+        ctx.save_for_backward(m, m_next)
+        ctx.meta = (summed, B, P, Pn, n, out_k, [tuple(h.shape) for h in H], [tuple(x.shape) for x in nh])
+        res = (*gath, *[o.view_as(o) for o in outs])
+        if out_k >= 0:
+            res = res + (tensors[n + out_k].view_as(tensors[n + out_k]),)
+        return res
+
+    @staticmethod
+    def backward(ctx, *grads):
+        m, m_next = ctx.saved_tensors
+        summed, B, P, Pn, n, out_k, h_shapes, nh_shapes = ctx.meta
+        ggath, gstate = grads[:n], grads[n:2 * n]
+        gk = grads[2 * n] if out_k >= 0 else None
+        dH, dnh = [None] * n, [None] * n
+        live = [k for k in range(n) if ggath[k] is not None or gstate[k] is not None]
+        if gk is not None and out_k not in live:
+            dnh[out_k] = gk
+        if live:
+            g = [None if ggath[k] is None else ggath[k].contiguous() for k in live]
+            st = [None if gstate[k] is None else _rows_view(gstate[k], 2) for k in live]
+            add = [_rows_view(gk, 1) if (k == out_k and gk is not None) else None for k in live]
+            F = [int(torch.Size(h_shapes[k][2:]).numel()) for k in live]
+            a = [torch.empty(h_shapes[k], dtype=m.dtype, device=m.device) for k in live]
+            b = [torch.empty(nh_shapes[k], dtype=m.dtype, device=m.device) for k in live]
+            _native.check(_native.load().hrl_hidden_update_gather_backward(
+                _native.ptr_array(g), _native.ptr(m), _native.ptr(m_next), B, P, Pn, len(live), _native.i64_array(F),
+                int(summed), _native.ptr_array(st) if any(x is not None for x in st) else None,
+                _native.i64_array([x.stride(-2) if x is not None else f for x, f in zip(st, F)]),
+                _native.ptr_array(add) if any(x is not None for x in add) else None,
+                _native.i64_array([x.stride(-2) if x is not None else f for x, f in zip(add, F)]),
+                _native.ptr_array(a), _native.ptr_array(b), _native.stream_of(m.device)),
+                'hrl_hidden_update_gather_backward')
+            for k, x, y in zip(live, a, b):
+                dH[k], dnh[k] = x, y
+        return (None, None, None, None, None, None, None, None, *dH, *dnh)
+
+
 def _board_conv_ok(m):
     k = m.kernel_size
     return (m.stride == (1, 1) and m.dilation == (1, 1) and m.groups == 1 and m.padding_mode == 'zeros'

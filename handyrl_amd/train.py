@@ -178,6 +178,11 @@ def _flat_hidden_ok(hidden, tmask):
             and tmask.shape[0] == B and tmask.shape[2] == P)
 
 
+# _unroll_flat_hidden's sequence path runs step t's state update and step t+1's gather as one fused Function
+# (nn._HiddenUpdateGather); False: the two Functions (bit-identical; tests/test_geister.py)
+FUSE_UPDATE_GATHER = True
+
+
 def _unroll_flat_hidden(model, hidden, batch, args):
     """The recurrent branch on the GPU: the masking/summing and the mixing of every hidden tensor
     run as one HIP launch each per step (nn._HiddenGather / _HiddenUpdate), with the arithmetic of
@@ -195,12 +200,13 @@ def _unroll_flat_hidden(model, hidden, batch, args):
     if SEQUENCE_UNROLL and seq_ok is not None and seq_ok(map_r(observations, lambda o: o[:, 0])):
         # the net runs its state-free parts once over all T steps (e.g. GeisterNet.sequence_begin/end):
         # observations time-major, (T*N, ...) with N = B*P' in the per-step order
+        from .nn import _HiddenUpdateGather
         obs = map_r(observations, lambda o: o.transpose(0, 1).reshape(-1, *o.shape[3:]))
         seq = model.sequence_begin(obs, T)
         h_lasts = []
+        g = _HiddenGather.apply(masks[0], summed, B, P, *leaves)
         for t in range(T):
             m = masks[t]
-            g = _HiddenGather.apply(m, summed, B, P, *leaves)
             h_in = _rebuild(hidden, iter(g[:n]))
             h_last, next_hidden = model.sequence_step(seq, t, h_in)
             nh = _leaves(next_hidden)
@@ -208,9 +214,17 @@ def _unroll_flat_hidden(model, hidden, batch, args):
             # the state continues through the gather's pass-through views, and the step output that is also a
             # new state leaf comes back from the update: every tensor has one consumer, the adjoints add
             k = next((i for i, x in enumerate(nh) if x is h_last), -1)
+            if FUSE_UPDATE_GATHER and t + 1 < T:
+                # this step's update and the next step's gather in one launch each way
+                u = _HiddenUpdateGather.apply(m, masks[t + 1], summed, B, P, Pn, n, k, *g[n:], *nh)
+                g = u[:2 * n]
+                h_lasts.append(u[2 * n] if k >= 0 else h_last)
+                continue
             u = _HiddenUpdate.apply(m, B, P, Pn, n, k, *g[n:], *nh)
             leaves = list(u[:n])
             h_lasts.append(u[n] if k >= 0 else h_last)
+            if t + 1 < T:
+                g = _HiddenGather.apply(masks[t + 1], summed, B, P, *leaves)
         out = model.sequence_end(seq, h_lasts)
         # (T*N, ...) -> (N, T, ...), the per-step loop's torch.stack(dim=1) layout
         return {k: o.view(T, -1, *o.shape[1:]).transpose(0, 1).contiguous() for k, o in out.items()

@@ -283,6 +283,20 @@ int hrl_hidden_update_backward_add(const float *const *dout, const float *mask, 
                                    int nleaves, const int64_t *F, const float *const *addend,
                                    const int64_t *addend_strides, float *const *dH, float *const *dnh,
                                    void *stream);
+/* Step t's state update fused with step t+1's gather (round 5; the learner's recurrent unroll): out = H (1 - mask)
+ * + nh mask (hrl_hidden_update) and gathered = the next step's input from out with mask_next (hrl_hidden_gather, sum
+ * as there), one launch; bit for bit the two launches.  The adjoint: the gather's (dout = dgathered mask_next +
+ * dstate, dstate the new state's other gradient, rows dstate_strides floats apart, NULL: none; a leaf's dgathered
+ * may be NULL when its dstate is given) then the update's (dH, dnh = ... + dout_add, the step output's gradient,
+ * rows dout_add_strides apart), one launch. */
+int hrl_hidden_update_gather(const float *const *H, const float *const *nh, int64_t Pn, const float *mask,
+                             const float *mask_next, int64_t B, int64_t P, int nleaves, const int64_t *F, int sum,
+                             float *const *out, float *const *gathered, void *stream);
+int hrl_hidden_update_gather_backward(const float *const *dgathered, const float *mask, const float *mask_next,
+                                      int64_t B, int64_t P, int64_t Pn, int nleaves, const int64_t *F, int sum,
+                                      const float *const *dstate, const int64_t *dstate_strides,
+                                      const float *const *dout_add, const int64_t *dout_add_strides,
+                                      float *const *dH, float *const *dnh, void *stream);
 
 /*
  * 3x3 convolution on a torus board, 17 or 32 -> 32 channels, H*W <= 80

@@ -461,3 +461,39 @@ def test_recurrent_learner_step_at_bench_size_vs_oracle(cuda, graph):
     assert st[6] > 0, st                   # each repeat's h halves as one grouped launch over the layers' states
     assert st[7] > 0 and st[8] >= 3 * T, st    # weight gradients over the unroll's recorded uses (3T for the cell)
     assert st[9] > 256 and st[10] > 0, st  # > 256 tiles: workgroups carry accumulators over several tiles
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('graph', [False, True])
+def test_fused_update_gather_is_bit_identical(cuda, graph):
+    """The recurrent unroll with step t's state update and step t+1's gather fused (train.FUSE_UPDATE_GATHER,
+    nn._HiddenUpdateGather, hrl_hidden_update_gather[_backward]) against the two separate Functions: one GeisterNet
+    LearnerStep (B=32, T=6) from the same weights and batch, losses and every parameter gradient bit for bit."""
+    from handyrl_amd import train as htrain
+    from handyrl_amd.synthetic import geister_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    B, T = 32, 6
+    args = default_args(T, B)
+    batch = geister_batch(B, T, cuda, seed=23)
+    state = seeded_net().state_dict()
+
+    def run(fuse):
+        prev = htrain.FUSE_UPDATE_GATHER
+        htrain.FUSE_UPDATE_GATHER = fuse
+        try:
+            net = seeded_net()
+            net.load_state_dict(state)
+            step = LearnerStep(net, args, cuda, graph=graph)
+            hidden = tuple([h.to(cuda) for h in hs] for hs in net.init_hidden([B, 2]))
+            out = step.step(batch, hidden)
+            torch.cuda.synchronize()
+            return ({k: float(v) for k, v in out.items()},
+                    {n: p.grad.detach().clone() for n, p in step.net.named_parameters() if p.grad is not None})
+        finally:
+            htrain.FUSE_UPDATE_GATHER = prev
+
+    (o0, g0), (o1, g1) = run(False), run(True)
+    assert o0 == o1
+    assert g0.keys() == g1.keys()
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
