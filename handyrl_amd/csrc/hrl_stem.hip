@@ -374,10 +374,18 @@ __global__ __launch_bounds__(kThreads, 4) void stem_wgrad2_kernel(const float *_
     const __amdgpu_buffer_rsrc_t rx = rsrc_of(x, N * kXF * 4);   // rows past N read 0
     constexpr int kXL = (kBR * kXF + 63) / 64;
     for (int i = lane; i < kBR * (kXS - kXF); i += 64) xw[(i / (kXS - kXF)) * kXS + kXF + i % (kXS - kXF)] = 0.f;
+    // a lane takes two rows per step (4 it + 2 r and the next) as one packed f32x2 pair: v_pk_fma_f32 does both rows'
+    // multiply-adds in one instruction (the kernel was VALU-bound at one FMA per MAC); per lane the rows still add
+    // into its accumulators one after the other
+    auto load_pair = [&](int64_t row, f32x2 (&d)[kCells]) __attribute__((always_inline)) {
+        float a[kCells], b[kCells];
+        load_dy(row, a);
+        load_dy(row + 1, b);
+#pragma unroll
+        for (int q = 0; q < kCells; ++q) d[q] = (f32x2){a[q], b[q]};
+    };
     for (int64_t blk = (int64_t)blockIdx.x * kWaves + wave; blk < nblocks; blk += wstep) {
         const int64_t base = blk * kBR;
-        float dn[kCells];
-        load_dy(base + r, dn);   // rows past N read 0 (the descriptor's range)
         float xr[kXL];
         const uint32_t xb = (uint32_t)(base * kXF * 4);
 #pragma unroll
@@ -393,38 +401,42 @@ __global__ __launch_bounds__(kThreads, 4) void stem_wgrad2_kernel(const float *_
                 xw[rr * kXS + e - rr * kXF] = xr[k];
             }
         }
+        f32x2 dn[kCells];
+        load_pair(base + 2 * r, dn);   // rows past N read 0 (the descriptor's range)
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
-        for (int it = 0; it < kBR / 2; ++it) {
-            float d[kCells];
+        for (int it = 0; it < kBR / 4; ++it) {
+            f32x2 d[kCells];
 #pragma unroll
             for (int q = 0; q < kCells; ++q) d[q] = dn[q];
-            if (it + 1 < kBR / 2) load_dy(base + 2 * (it + 1) + r, dn);
-            float xv[kXS];
-            const float4 *xr = reinterpret_cast<const float4 *>(xw + (2 * it + r) * kXS);
-#pragma unroll
-            for (int j = 0; j < kXS / 4; ++j) {
-                const float4 v = xr[j];
-                xv[4 * j] = v.x; xv[4 * j + 1] = v.y; xv[4 * j + 2] = v.z; xv[4 * j + 3] = v.w;
-            }
-            float tb = 0.f;
+            if (it + 1 < kBR / 4) load_pair(base + 4 * (it + 1) + 2 * r, dn);
+            f32x2 tb = (f32x2){0.f, 0.f};
 #pragma unroll
             for (int q = 0; q < kCells; ++q) tb += d[q];
-            accb += tb;
+            accb += tb.x;
+            accb += tb.y;
+            const float *xr0 = xw + (4 * it + 2 * r) * kXS;
 #pragma unroll
-            for (int ci = 0; ci < CIN; ++ci)
+            for (int ci = 0; ci < CIN; ++ci) {
+                asm volatile("" ::: "memory");   // one input channel's observations at a time
+                f32x2 xv[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) xv[k] = (f32x2){xr0[ci * 9 + k], xr0[kXS + ci * 9 + k]};
 #pragma unroll
                 for (int tap = 0; tap < 9; ++tap) {
                     const int ky = tap / 3, kx = tap % 3;
-                    float t = 0.f;
+                    f32x2 t = (f32x2){0.f, 0.f};
 #pragma unroll
                     for (int q = 0; q < kCells; ++q) {
                         const int py = q / 3 + ky - 1, px = q % 3 + kx - 1;
-                        if (py >= 0 && py < 3 && px >= 0 && px < 3) t = __builtin_fmaf(d[q], xv[ci * 9 + py * 3 + px], t);
+                        if (py >= 0 && py < 3 && px >= 0 && px < 3)
+                            t = __builtin_elementwise_fma(d[q], xv[py * 3 + px], t);
                     }
-                    acc[ci * 9 + tap] += t;
+                    acc[ci * 9 + tap] += t.x;
+                    acc[ci * 9 + tap] += t.y;
                 }
+            }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);   // the block's LDS rows are read before the next block's overwrite
         __builtin_amdgcn_wave_barrier();
