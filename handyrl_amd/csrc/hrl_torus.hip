@@ -233,7 +233,8 @@ __device__ __forceinline__ void pro_to_lds(const Stage<true, NLD, true> &sx, con
 // SUMS epilogue, after the output tile is complete (vec layout only): store out = tile + add*[mask > 0],
 // then the per-channel sums of out*[hmask > 0] (s1) and out*[hmask > 0]*(yprev - mean) (s2) in fp64.
 // Lane l owns channel l & 31 and half (l >> 5) of the cells: it reads its 40 yprev values straight from the
-// channel row (issued first, in flight during the store pass) and the masked values from the tile twice.
+// channel row (issued after the store pass, in flight during the first sums: issued earlier they spill) and the
+// masked values from the tile twice.
 // Every global load of a pass is issued before its first use: the per-float4 loop this replaces waited for each
 // iteration's loads in turn, ten round trips per sample.
 __device__ __forceinline__ void store_sample_sums(float *tile, float *dst, int n_elem, int HW, float inv_hw,
