@@ -303,14 +303,24 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_kernel(
         red[0][threadIdx.x] = s0;
         red[1][threadIdx.x] = s1;
         __syncthreads();
-        for (int wd = kThreads / 2; wd > 0; wd >>= 1) {
+        // the fixed tree t += t + wd: the levels above one wave through LDS, the last six in wave 0's registers
+        // (the same pairs and order, without a barrier per level)
+        for (int wd = kThreads / 2; wd >= 64; wd >>= 1) {
             if ((int)threadIdx.x < wd) {
                 red[0][threadIdx.x] += red[0][threadIdx.x + wd];
                 red[1][threadIdx.x] += red[1][threadIdx.x + wd];
             }
             __syncthreads();
         }
-        if (threadIdx.x == 0) fin(grp, red[0][0], red[1][0]);
+        if (threadIdx.x < 64) {
+            double v0 = red[0][threadIdx.x], v1 = red[1][threadIdx.x];
+#pragma unroll
+            for (int wd = 32; wd > 0; wd >>= 1) {
+                v0 += __shfl_down(v0, wd, 64);
+                v1 += __shfl_down(v1, wd, 64);
+            }
+            if (threadIdx.x == 0) fin(grp, v0, v1);
+        }
         __syncthreads();   // red is reused by the next group
     }
     if (mode == 1 && threadIdx.x == 0) {
