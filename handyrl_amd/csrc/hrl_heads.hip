@@ -472,18 +472,6 @@ constexpr int kWaves2 = 4;
 constexpr int kGR = 8;                 // rows per contiguous load / store group
 constexpr int kGV = kGR * kRow / 4 / 64;   // 9 float4 per lane per group
 
-
-
-__device__ __forceinline__ void load9(__amdgpu_buffer_rsrc_t rs, uint32_t off, float (&d)[kHW]) {
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-        const hu32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, off + 12 * m, 0, 0);
-        d[3 * m] = __uint_as_float(v.x);
-        d[3 * m + 1] = __uint_as_float(v.y);
-        d[3 * m + 2] = __uint_as_float(v.z);
-    }
-}
-
 // rows [row0, row0 + 8) of h as 9 contiguous float4 per lane (rows past N read 0)
 __device__ __forceinline__ void load_group(__amdgpu_buffer_rsrc_t rh, int64_t row0, int lane, hu32x4 (&st)[kGV]) {
     const uint32_t ob = (uint32_t)(row0 * kRow * 4);
