@@ -949,7 +949,8 @@ __global__ __launch_bounds__(kThreads) void torus_wgrad_split_kernel(WgArgs args
     const int H = args.H, W = args.W, Cin = X32 ? kCo : args.Cin;
     float *__restrict__ partial = args.partial;
     constexpr int kNLd = (kCo * kMaxCells / 4 + 63) / 64;   // float4 per lane per sample tensor
-    constexpr int kNLdS = (kCo * kMaxCells + 63) / 64;      // !X32: x floats per lane
+    constexpr int kStemCin = 17;                             // !X32: the only narrower input (shape_ok)
+    constexpr int kNLdS = (kStemCin * kMaxCells + 63) / 64; // !X32: x floats per lane
     constexpr int kPart = kTaps * kCo * kCo + kCo;
     constexpr int kHalf = kMaxCells / 2;
     __shared__ __attribute__((aligned(16))) float gs_all[kWaves][kCo * kSG];   // dY [co][cell]
