@@ -535,51 +535,63 @@ __global__ __launch_bounds__(256, 2) void heads_bwd2_kernel(const float *__restr
     for (int64_t blk = (int64_t)blockIdx.x * kWaves2 + wave; blk < nblocks; blk += wstep) {
         const int64_t base = blk * kBR;
         asm volatile("" ::: "memory");   // Wp / Wv are re-read from LDS per block, not held in 171 registers
-        if (lane < kBR) {
-            const int64_t n = base + lane;
+        {
+            // row lane & 31; the half-waves split its dz: r = 0 the policy cells j = 0..8 and the value head,
+            // r = 1 the policy cells j = 9..17 (each dz the same 9-term sum in the same order as one lane alone)
+            const int row = lane & (kBR - 1);
+            const int64_t n = base + row;
             const bool valid = n < N;
             const int64_t nn = valid ? n : 0;
-            float a[kZ], g[kOP], gv;
+            const int j0 = r * kHW;          // this half's policy cells
+            float ap[kHW], g[kOP];
 #pragma unroll
-            for (int j = 0; j < kZP; ++j) a[j] = a_p[nn * kZP + j];
-#pragma unroll
-            for (int q = 0; q < kHW; ++q) a[kZP + q] = a_v[nn * kHW + q];
+            for (int j = 0; j < kHW; ++j) ap[j] = a_p[nn * kZP + j0 + j];
 #pragma unroll
             for (int k = 0; k < kOP; ++k) g[k] = valid ? dp[nn * kOP + k] : 0.f;
-            gv = valid ? dv[nn] : 0.f;
-            if (vt) gv = gv * (1.f - vt[nn] * vt[nn]);   // tanh backward, torch's CPU operations
-            float dz[kZ];
+            float dzp[kHW];
 #pragma unroll
-            for (int j = 0; j < kZP; ++j) {
-                // one dz at a time: the compiler would otherwise issue all 162 products (packed) before any sum
+            for (int j = 0; j < kHW; ++j) {
+                // one dz at a time: the compiler would otherwise issue all the products (packed) before any sum
                 asm volatile("" ::: "memory");
                 float t = 0.f;
 #pragma unroll
-                for (int k = 0; k < kOP; ++k) t += g[k] * swp[k * kZP + j];
-                dz[j] = a[j] > 0.f ? t : t * kSlope;
+                for (int k = 0; k < kOP; ++k) t += g[k] * swp[k * kZP + j0 + j];
+                dzp[j] = ap[j] > 0.f ? t : t * kSlope;
             }
-#pragma unroll
-            for (int q = 0; q < kHW; ++q) {
-                const float t = gv * swv[q];
-                dz[kZP + q] = a[kZP + q] > 0.f ? t : t * kSlope;
-            }
-#pragma unroll
-            for (int m = 0; m < kM; ++m) {
+            {
                 float t = 0.f;
 #pragma unroll
-                for (int q = 0; q < kHW; ++q) t += dz[m * kHW + q];
-                gb[m] += t;
+                for (int q = 0; q < kHW; ++q) t += dzp[q];
+                gb[r] += t;                  // db1[m = r]: lanes < 32 hold m = 0, lanes >= 32 m = 1
             }
-            float4 *dzr = reinterpret_cast<float4 *>(dzs + lane * kDZS);
+            float *dzr = dzs + row * kDZS;
+            float *smr = sm + row * kSMS;
 #pragma unroll
-            for (int j = 0; j < 6; ++j) dzr[j] = make_float4(dz[4 * j], dz[4 * j + 1], dz[4 * j + 2], dz[4 * j + 3]);
-            dzr[6] = make_float4(dz[24], dz[25], dz[26], 0.f);
-            float *smr = sm + lane * kSMS;
+            for (int j = 0; j < kHW; ++j) {
+                dzr[j0 + j] = dzp[j];
+                smr[kSmAP + j0 + j] = valid ? ap[j] : 0.f;
+            }
+            if (r == 0) {
+                float av[kHW];
 #pragma unroll
-            for (int k = 0; k < kOP; ++k) smr[kSmG + k] = g[k];
-            smr[kSmGV] = gv;
+                for (int q = 0; q < kHW; ++q) av[q] = a_v[nn * kHW + q];
+                float gv = valid ? dv[nn] : 0.f;
+                if (vt) gv = gv * (1.f - vt[nn] * vt[nn]);   // tanh backward, torch's CPU operations
+                float t2 = 0.f;
 #pragma unroll
-            for (int j = 0; j < kZ; ++j) smr[kSmAP + j] = valid ? a[j] : 0.f;
+                for (int q = 0; q < kHW; ++q) {
+                    const float t = gv * swv[q];
+                    const float d = av[q] > 0.f ? t : t * kSlope;
+                    dzr[kZP + q] = d;
+                    t2 += d;
+                    smr[kSmAV + q] = valid ? av[q] : 0.f;
+                }
+                gb[2] += t2;
+                dzr[kZ] = 0.f;
+#pragma unroll
+                for (int k = 0; k < kOP; ++k) smr[kSmG + k] = g[k];
+                smr[kSmGV] = gv;
+            }
         }
         lds_fence();
         // fc weight gradients over the block's rows, in order
@@ -681,9 +693,11 @@ __global__ __launch_bounds__(256, 2) void heads_bwd2_kernel(const float *__restr
             out[kGW1 + i] = t;
         }
         if (lane < kM) {
+            // db1[m]: the rows' lanes in order -- m = 0, 2 on lanes 0..31, m = 1 on lanes 32..63
+            const int l0 = lane == 1 ? kBR : 0;
             float t = 0.f;
             for (int wv = 0; wv < kWaves2; ++wv)
-                for (int l = 0; l < kBR; ++l) t += fold[wv][(3 + lane) * 64 + l];
+                for (int l = 0; l < kBR; ++l) t += fold[wv][(3 + lane) * 64 + l0 + l];
             out[kGB1 + lane] = t;
         }
         if (BN && bn.part) {   // part[block][c][2], fp64: halves and waves in order
