@@ -85,6 +85,7 @@ SIGNATURES = {
                                            ctypes.c_int, _f32p, _f32p, ctypes.c_void_p]),
     'hrl_bn_apply': (ctypes.c_int, [_f32p, _i64, _i64, _i64, _f32p, _f32p, ctypes.c_int, _f32p, ctypes.c_void_p]),
     'hrl_conv3x3_stats_blocks': (ctypes.c_int64, [_i64]),
+    'hrl_conv3x3_block_sum_blocks': (ctypes.c_int64, [_i64]),
     'hrl_conv3x3_set_split': (ctypes.c_int, [ctypes.c_int]),
     'hrl_conv3x3_set_block_form': (ctypes.c_int, [ctypes.c_int]),
     'hrl_conv3x3_set_fwd_form': (ctypes.c_int, [ctypes.c_int]),
@@ -233,7 +234,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 _lib = None
 

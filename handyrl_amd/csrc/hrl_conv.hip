@@ -34,6 +34,9 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <type_traits>
 
 #include "../../include/hrl_nn.h"
 #include "../../include/hrl_targets.h"
@@ -678,6 +681,8 @@ struct BlockBwdArgs {
     double *part;                                                // epilogue 2 sums [block][32][2]
     float *wpart;                                                // weight-gradient partials [block][tap][ci][co]
     int64_t M;
+    unsigned *tickets;                                           // block form 2: per-CU arrival tickets
+    int stagger;                                                 // block form 2: s_sleep(32)s of the later arrival
 };
 
 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
@@ -1458,6 +1463,398 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
 
 }  // namespace bb2
 
+// ------------------------------------------------------------------ one chain block's backward, two workgroups per CU
+// conv3x3_block_bwd4_kernel<PRO, EPI, DG> (block form 2): bb2's arithmetic with the CU shared by TWO independent
+// 4-wave workgroups instead of one 8-wave workgroup.  bb2 double-buffered its images in 148 KB of LDS, so one
+// workgroup filled the CU and all 8 waves met at every tile's barrier: a wave whose loads came late held the other
+// seven (18-28 % of every tile at the barrier, MFMA busy 0.39 of the SIMD cycles: profiles/r05_bb2_stamps.txt).
+// Here a workgroup's images are single-buffered (dY and x' part images 2 x 27 KB + the epilogue's raw x 18.3 KB =
+// 72.3 KB), so two workgroups reside on every CU, one wave of each on every SIMD, and each runs
+//     MFMAs of tile k + epilogue | barrier | stage tile k+1 (registers -> images) | issue the loads of tile k+2 | barrier
+// -- while one workgroup waits at a barrier or stages, the other's MFMAs run on the same SIMDs: the tile skew is
+// absorbed by the other workgroup instead of costing all eight waves.  Per workgroup:
+//  * waves 0, 1: the input gradient of column tile ct = wave for ALL nine output cells (49 (p, q) pairs, 294
+//    v_mfma_f32_16x16x32_bf16), the three split parts of their weights in registers; a row's nine cells leave in
+//    one 36-byte run per lane (two dwordx4 + one dword);
+//  * waves 2, 3: the weight gradient of taps {0, 2, 4, 6, 8} (25 pairs) and {1, 3, 5, 7} (24 pairs), 32x32x16;
+//  * the waves stage the tile as bb2's eight (row pair, channel) diagonals: one each for the input-gradient waves
+//    (30 registers of loads in flight per lane beside their 144 of weights and accumulators), three each for the
+//    weight-gradient waves (90).
+// Same operands, same images and the same per-accumulator MFMA order as bb2: the input gradient is bit-identical;
+// the weight gradient sums 16 instead of 32 tiles per partial row (512 rows per launch: a different association
+// across tiles); the epilogue-2 sums are per workgroup (hrl_conv3x3_block_sum_blocks rows).
+namespace bb4 {
+
+// diagnostic variants (tools/bb4_variants.sh; the product is 0): bit 1 = loads of the first tile only, bit 2 = no
+// MFMA phase, bit 4 = no epilogue / gin store
+#ifndef BB4_VARIANT
+#define BB4_VARIANT 0
+#endif
+constexpr int kVariant = BB4_VARIANT;
+
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kPartBytes = bb2::kPartBytes;
+constexpr int kImgBytes = bb2::kImgBytes;
+constexpr int kDy0 = 0;
+constexpr int kX0 = kImgBytes;
+constexpr int kXrStride = bb2::kXrStride;                  // 292
+constexpr int kXrBytes = bb2::kXrBytes;
+constexpr int kXr0 = 2 * kImgBytes;
+constexpr int kLdsBytes = kXr0 + kXrBytes;                 // 73,984 B
+static_assert(2 * kLdsBytes <= 160 * 1024, "two workgroups per CU");
+constexpr int kPerCu = 2;                                  // resident workgroups per CU
+constexpr int kGrid = 256 * kPerCu;
+
+// the weight-gradient waves' taps: corners + centre (4 x 4 + 9 = 25 pairs) and edges (4 x 6 = 24)
+template <int W> struct Taps;
+template <> struct Taps<2> { static constexpr int kN = 5; static constexpr int kT[5] = {0, 2, 4, 6, 8}; };
+template <> struct Taps<3> { static constexpr int kN = 4; static constexpr int kT[4] = {1, 3, 5, 7}; };
+template <> struct Taps<0> { static constexpr int kN = 1; static constexpr int kT[1] = {0}; };
+template <> struct Taps<1> { static constexpr int kN = 1; static constexpr int kT[1] = {0}; };
+
+// the (row pair, channel) diagonals a wave stages (bb2's diagonal of wave D: rows 2 ((D + ch/4) & 7) + {0, 1}), 30
+// registers of loads each: one for each input-gradient wave (108 registers of weights, 20 of accumulators, the
+// epilogue), three for each weight-gradient wave (80 / 64 accumulators) -- no wave spills (a spill reload is a
+// vector-memory operation: its wait would also wait for the next tile's loads)
+template <int W> struct Diags;
+template <> struct Diags<0> { static constexpr int kN = 1; static constexpr int kD[1] = {0}; };
+template <> struct Diags<1> { static constexpr int kN = 1; static constexpr int kD[1] = {1}; };
+template <> struct Diags<2> { static constexpr int kN = 3; static constexpr int kD[3] = {2, 4, 6}; };
+template <> struct Diags<3> { static constexpr int kN = 3; static constexpr int kD[3] = {3, 5, 7}; };
+
+// the lane id from an instruction the compiler may not hoist: the staging addresses derived from it are recomputed
+// where they are used (a few VALU) instead of held across the loop in registers the input-gradient waves lack
+__device__ __forceinline__ int fresh_lane() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+template <bool PRO, int EPI, bool DG, int W>
+__device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, int lane, int delay) {
+    constexpr bool kIg = W < 2;
+    constexpr int kCt = W & 1;
+    constexpr int kNt = Taps<W>::kN;
+    const int ch = lane & 31, hh = lane >> 5;
+    // BN_i's backward apply for channel ch (bn_bwd_apply_kernel's per-channel values), the prologue's BN_{i-1}
+    const float mu = a.bn_mean[ch], kk = a.bn_k[ch], gmn = a.bn_gm[ch], is = a.bn_invstd[ch];
+    const float ww = a.bn_w ? a.bn_w[ch] : 1.0f;
+    const float al = is * ww;
+    const float be = (a.bn_b ? a.bn_b[ch] : 0.0f) - mu * al;
+    float pa = 1.f, pb = 0.f;
+    if constexpr (PRO) {
+        pa = a.in_alpha[ch];
+        pb = a.in_beta[ch];
+    }
+    // the input gradient's weights, all three parts of all nine taps in registers (bb2's fragment layout)
+    uint4 wh[kTaps], wm[kTaps], wl[kTaps];
+    if constexpr (kIg && DG) {
+        const int ci0 = 8 * (lane >> 4), j = lane & 15;
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) {
+            uint32_t hv[4], mv[4], lv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int tc = t * 2 + kCt;
+                const float w0 = a.wpk[(tc * kC + ci0 + 2 * d) * 16 + j];
+                const float w1 = a.wpk[(tc * kC + ci0 + 2 * d + 1) * 16 + j];
+                uint32_t h0, m0, l0, h1, m1, l1;
+                hrl_split::split3(w0, h0, m0, l0);
+                hrl_split::split3(w1, h1, m1, l1);
+                hv[d] = h0 | (h1 << 16);
+                mv[d] = m0 | (m1 << 16);
+                lv[d] = l0 | (l1 << 16);
+            }
+            wh[t] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+            wm[t] = make_uint4(mv[0], mv[1], mv[2], mv[3]);
+            wl[t] = make_uint4(lv[0], lv[1], lv[2], lv[3]);
+        }
+    }
+    float em = 0.f, ea = 1.f, eb = 0.f;     // epilogue 2: BN_{i-1} of this lane's output channel
+    if constexpr (EPI == 2 && kIg && DG) {
+        em = a.ep_mean[kCt * 16 + (lane & 15)];
+        ea = a.ep_alpha[kCt * 16 + (lane & 15)];
+        eb = a.ep_beta[kCt * 16 + (lane & 15)];
+    }
+    double s1 = 0.0, s2 = 0.0;
+    f32x16 wacc[kNt];
+#pragma unroll
+    for (int t = 0; t < kNt; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wacc[t][i] = 0.f;
+
+    const int64_t ntiles = (a.M + kTile - 1) / kTile;
+    const int64_t t0 = blockIdx.x;
+    const int64_t step = gridDim.x;
+    const int n_iter = t0 < ntiles ? (int)((ntiles - 1 - t0) / step + 1) : 0;
+    // this lane stages rows rho_of(j), rho_of(j) + 1 (bb2's diagonals Diags<W>::kD) and cells c0 .. c0+4 of channel
+    // ch (lanes hh = 1 take cells 4..8)
+    constexpr int kNd = Diags<W>::kN;
+    auto rho_of = [](int j, int c) __attribute__((always_inline)) { return 2 * ((Diags<W>::kD[j] + (c >> 2)) & 7); };
+    float G[kNd][2][5], Y[kNd][2][5], X[kNd][2][5];
+    auto rsrc_of = [&](const float *base, int it, int &rows) __attribute__((always_inline)) {
+        const int64_t t = t0 + (int64_t)it * step;
+        const bool ok = it < n_iter;
+        rows = ok ? (int)min<int64_t>(kTile, a.M - t * kTile) : 0;
+        return wave_rsrc(base + (ok ? t * kTile * kRow : 0), (uint32_t)rows * kRow * 4);
+    };
+    auto issue = [&](int it) __attribute__((always_inline)) {   // loads of iteration it's tile (zeros past the end)
+        if constexpr (kVariant & 1) {
+            if (it > 0) return;
+        }
+        int rows;
+        const __amdgpu_buffer_rsrc_t rg = rsrc_of(a.g, it, rows), ry = rsrc_of(a.y, it, rows),
+                                     rx = rsrc_of(a.x, it, rows);
+        const int ln = fresh_lane(), cl = ln & 31, c0 = (ln >> 5) ? 4 : 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+#pragma unroll
+            for (int j = 0; j < kNd; ++j) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const int off = ((rho_of(j, cl) + r) * kRow + cl * kCells + c0) * 4;
+                    const __amdgpu_buffer_rsrc_t rs = k == 0 ? rg : (k == 1 ? ry : rx);
+                    float(&d)[5] = k == 0 ? G[j][r] : (k == 1 ? Y[j][r] : X[j][r]);
+                    const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+                    const u32x2 u = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 12, 0, 0);
+                    d[0] = __uint_as_float(v.x);
+                    d[1] = __uint_as_float(v.y);
+                    d[2] = __uint_as_float(v.z);
+                    d[3] = __uint_as_float(u.x);
+                    d[4] = __uint_as_float(u.y);
+                }
+            }
+        }
+    };
+    unsigned char *dyi = smem + kDy0;
+    unsigned char *xi = smem + kX0;
+    float *xr = reinterpret_cast<float *>(smem + kXr0);
+    auto stage = [&](int it) __attribute__((always_inline)) {   // registers -> the images
+        const int64_t t = t0 + (int64_t)it * step;
+        const int rows = (int)max<int64_t>(0, min<int64_t>(kTile, a.M - t * kTile));
+        const int ln = fresh_lane(), cl = ln & 31, c0 = (ln >> 5) ? 4 : 0;
+#pragma unroll
+        for (int j = 0; j < kNd; ++j) {
+            const int rj = rho_of(j, cl);
+            uint32_t dp[3][5], xp[3][5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                float dv[2], xv2[2];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    // dY = BN_i backward apply (bn_bwd_apply_kernel's float operations); rows past the batch are 0
+                    const bool valid = rj + r < rows;
+                    const float yv = Y[j][r][i];
+                    float gv = G[j][r][i];
+                    if (!(yv * al + be > 0.f)) gv = 0.f;
+                    const float tt = (yv - mu) * kk;
+                    float d = (((gv - gmn) - tt) * is) * ww;
+                    dv[r] = valid ? d : 0.f;
+                    float xv = X[j][r][i];
+                    if constexpr (PRO) {   // bn_apply_kernel's float operations
+                        const float u = xv * pa + pb;
+                        xv = u < 0.f ? 0.f : u;
+                    }
+                    xv2[r] = xv;
+                }
+                hrl_split::split_pair(dv[0], dv[1], dp[0][i], dp[1][i], dp[2][i]);
+                hrl_split::split_pair(xv2[0], xv2[1], xp[0][i], xp[1][i], xp[2][i]);
+            }
+            const int half = rj >> 3, sub = 2 * (rj & 7);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const int o = bb2::img_off(c0 + i, cl, half) + sub;
+#pragma unroll
+                for (int part = 0; part < 3; ++part) {
+                    *reinterpret_cast<uint32_t *>(dyi + part * kPartBytes + o) = dp[part][i];
+                    *reinterpret_cast<uint32_t *>(xi + part * kPartBytes + o) = xp[part][i];
+                }
+            }
+            if constexpr (DG && (EPI == 2 || EPI == 3)) {   // the epilogue's raw x (rows past the batch: 0)
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) xr[(rj + r) * kXrStride + cl * kCells + c0 + i] = X[j][r][i];
+            }
+        }
+    };
+    auto wgrad = [&]() __attribute__((always_inline)) {
+        // weight gradient: dW[tap] += x'_p^T (32 ci x 16 rows) . dY_q (16 rows x 32 co), p ascending
+        const int kg = lane >> 5;
+#pragma unroll
+        for (int p = 0; p < kCells; ++p) {
+            // one input cell's operands at a time: hoisting the next cells' LDS reads spilled (see Diags)
+            __builtin_amdgcn_sched_barrier(0);
+            const int o = bb2::img_off(p, ch, kg);
+            const uint4 Ah = *reinterpret_cast<const uint4 *>(xi + o);
+            const uint4 Am = *reinterpret_cast<const uint4 *>(xi + kPartBytes + o);
+            const uint4 Al = *reinterpret_cast<const uint4 *>(xi + 2 * kPartBytes + o);
+#pragma unroll
+            for (int s = 0; s < kNt; ++s) {
+                const int dy = Taps<W>::kT[s] / 3, dx = Taps<W>::kT[s] % 3;
+                const int qy = p / 3 - dy + 1, qx = p % 3 - dx + 1;
+                if (qy < 0 || qy > 2 || qx < 0 || qx > 2) continue;
+                const int ob = bb2::img_off(qy * 3 + qx, ch, kg);
+                const uint4 Bh = *reinterpret_cast<const uint4 *>(dyi + ob);
+                const uint4 Bm = *reinterpret_cast<const uint4 *>(dyi + kPartBytes + ob);
+                const uint4 Bl = *reinterpret_cast<const uint4 *>(dyi + 2 * kPartBytes + ob);
+                f32x16 c = wacc[s];
+                c = mfma32(Al, Bh, c);   // smallest terms first
+                c = mfma32(Am, Bm, c);
+                c = mfma32(Ah, Bl, c);
+                c = mfma32(Am, Bh, c);
+                c = mfma32(Ah, Bm, c);
+                c = mfma32(Ah, Bh, c);
+                wacc[s] = c;
+            }
+        }
+    };
+    // input gradient blocks (q, kCt) of output cells Q0 .. Q0+NQ-1: acc[s] += sum_p dY_p (16 rows x 32 co) .
+    // W'[tap(p, Q0+s)][kCt], p ascending, then their epilogue; the input-gradient waves run two such passes (cells
+    // 0-4 and 5-8), so their accumulators take 20 registers instead of 36 (the spill reloads a 36-accumulator form
+    // needed were vector-memory operations: each one's wait also waited for the next tile's loads)
+    float t1 = 0.f, t2 = 0.f;
+    auto ig_pass = [&](int it, auto q0c, auto nqc) __attribute__((always_inline)) {
+        constexpr int Q0 = decltype(q0c)::value, NQ = decltype(nqc)::value;
+        f32x4 acc[NQ];
+#pragma unroll
+        for (int s = 0; s < NQ; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if constexpr (!(kVariant & 2)) {
+            const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+            const int tr_sub = 8 * (pp & 1);
+#pragma unroll
+            for (int p = 0; p < kCells; ++p) {
+                uint32_t A[3][4];
+#pragma unroll
+                for (int part = 0; part < 3; ++part) {
+#pragma unroll
+                    for (int hlf = 0; hlf < 2; ++hlf) {
+                        const int o = part * kPartBytes + bb2::img_off(p, 8 * g + 4 * hlf + qq, pp >> 1) + tr_sub;
+                        const bb2::v4s r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (bb2::lds_v4s *)((__attribute__((address_space(3))) unsigned char *)(dyi + o)));
+                        const uint2 u = __builtin_bit_cast(uint2, r);
+                        A[part][2 * hlf] = u.x;
+                        A[part][2 * hlf + 1] = u.y;
+                    }
+                }
+                const uint4 Ah = make_uint4(A[0][0], A[0][1], A[0][2], A[0][3]);
+                const uint4 Am = make_uint4(A[1][0], A[1][1], A[1][2], A[1][3]);
+                const uint4 Al = make_uint4(A[2][0], A[2][1], A[2][2], A[2][3]);
+#pragma unroll
+                for (int s = 0; s < NQ; ++s) {
+                    const int tap = tap_of(p, Q0 + s);
+                    if (tap < 0) continue;
+                    f32x4 c = acc[s];
+                    c = mfma_bf16(Al, wh[tap], c);   // smallest terms first
+                    c = mfma_bf16(Am, wm[tap], c);
+                    c = mfma_bf16(Ah, wl[tap], c);
+                    c = mfma_bf16(Am, wh[tap], c);
+                    c = mfma_bf16(Ah, wm[tap], c);
+                    c = mfma_bf16(Ah, wh[tap], c);
+                    acc[s] = c;
+                }
+            }
+        }
+        if constexpr (kVariant & 4) return;
+        __builtin_amdgcn_sched_barrier(0);
+        // epilogue: accumulators -> gin straight from registers, per row one run of the pass's NQ cells
+        int rows;
+        const __amdgpu_buffer_rsrc_t ro = rsrc_of(a.gin, it, rows);
+        const int co = kCt * 16 + (lane & 15);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int row = (lane >> 4) * 4 + rr;     // C/D: row = (lane>>4)*4 + reg, col = lane & 15
+            float v[NQ];
+#pragma unroll
+            for (int s = 0; s < NQ; ++s) {
+                v[s] = acc[s][rr];
+                if constexpr (EPI == 2 || EPI == 3) {
+                    const float x0 = xr[row * kXrStride + co * kCells + Q0 + s];
+                    if constexpr (EPI == 2) {   // bn_bwd_reduce_kernel's mask and sums
+                        const float gm = (x0 * ea + eb > 0.f && row < rows) ? v[s] : 0.f;
+                        t1 += gm;
+                        t2 += gm * (x0 - em);
+                    } else {
+                        if (!(x0 > 0.f)) v[s] = 0.f;
+                    }
+                }
+            }
+            const int off = (row * kRow + co * kCells + Q0) * 4;
+            u32x4 w0;
+            w0.x = __float_as_uint(v[0]);
+            w0.y = __float_as_uint(v[1]);
+            w0.z = __float_as_uint(v[2]);
+            w0.w = __float_as_uint(v[3]);
+            __builtin_amdgcn_raw_buffer_store_b128(w0, ro, off, 0, 0);
+            if constexpr (NQ > 4) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[4 % NQ]), ro, off + 16, 0, 0);
+        }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I4 = std::integral_constant<int, 4>;
+    using I5 = std::integral_constant<int, 5>;
+
+    // stage(it + 1) follows the tile-it gin stores in every iteration, the first included (its loads were issued
+    // before them, in the prologue or the previous iteration), so the compiler's wait for the staged registers counts
+    // the stores as younger and never waits for them; stage / issue also run past the last tile (zeros nothing
+    // reads): a branch around them would make that wait a vmcnt(0)
+    if (n_iter > 0) {
+        issue(0);
+        stage(0);
+        issue(1);
+    }
+    for (int k = 0; k < delay; ++k) __builtin_amdgcn_s_sleep(32);
+    bb2::bar_lds();                                  // tile 0 staged
+    for (int it = 0; it < n_iter; ++it) {
+        if constexpr (!kIg) {
+            if constexpr (!(kVariant & 2)) wgrad();
+        } else if constexpr (DG) {
+            t1 = 0.f;
+            t2 = 0.f;
+            ig_pass(it, I0{}, I5{});                 // output cells 0-4
+            ig_pass(it, I5{}, I4{});                 // output cells 5-8
+            if constexpr (EPI == 2) {
+                s1 += (double)t1;
+                s2 += (double)t2;
+            }
+        }
+        bb2::bar_lds();                              // tile it's images read: the next stage may overwrite them
+        stage(it + 1);
+        issue(it + 2);
+        bb2::bar_lds();                              // tile it+1 staged
+    }
+    // weight-gradient partials partial[block][tap][ci][co] (C/D layout of 32x32x16: col = co = lane & 31,
+    // row = ci = (i&3) + 8(i>>2) + 4h); each tap has one owner wave
+    if constexpr (!kIg) {
+        constexpr int kW = kTaps * kC * kC;
+        float *outp = a.wpart + (int64_t)blockIdx.x * kW;
+        const int h = lane >> 5;
+#pragma unroll
+        for (int s = 0; s < kNt; ++s)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int ci = (i & 3) + 8 * (i >> 2) + 4 * h;
+                outp[(Taps<W>::kT[s] * kC + ci) * kC + ch] = wacc[s][i];
+            }
+    }
+    if constexpr (DG && EPI == 2) {   // the sums: waves 0-1 [wave][lane] -> channel wave*16 + (lane&15)
+        double *dred = reinterpret_cast<double *>(smem);     // the loop's last barrier freed the images
+        if (kIg) {
+            dred[(W * 64 + lane) * 2 + 0] = s1;
+            dred[(W * 64 + lane) * 2 + 1] = s2;
+        }
+        __syncthreads();
+        if (W == 0) {
+            const int c = lane >> 1, k = lane & 1, ct = c >> 4, l16 = c & 15;
+            double tot = 0.0;
+            for (int lg = 0; lg < 4; ++lg) tot += dred[(ct * 64 + lg * 16 + l16) * 2 + k];
+            a.part[((int64_t)blockIdx.x * kC + c) * 2 + k] = tot;
+        }
+    }
+}
+
+}  // namespace bb4
+
 // ------------------------------------------------------------------ the chain's forward conv, LDS-DMA ring
 // conv3x3_fwd_dma_kernel<PRO>: y = conv(x') with x' = relu(x*in_alpha + in_beta) (PRO) or x, and the output's BN
 // statistics (sum y, sum y^2 per channel): every output block is the same split MFMA sequence as bb2's forward (EPI 1)
@@ -1789,6 +2186,41 @@ __global__ __launch_bounds__(bb2::kThreads) void conv3x3_block_bwd2_kernel(Block
     }
 }
 
+// two 4-wave workgroups per CU: at most 256 registers per lane (two waves per SIMD), 72.3 KB of LDS each
+template <bool PRO, int EPI, bool DG>
+__global__ __launch_bounds__(bb4::kThreads, 2) void conv3x3_block_bwd4_kernel(BlockBwdArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[bb4::kLdsBytes];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the two workgroups of a CU run the same program with a barrier per phase and fall into lockstep (both
+    // staging, then both issuing MFMAs; MI355X_MICROARCH.md "Two waves per SIMD" item 9): the later arrival on its
+    // CU (a per-CU ticket: HW_ID's CU/SH/SE fields and XCC_ID) starts `stagger` s_sleep(32)s behind
+    int delay = 0;
+    if (a.stagger > 0) {
+        if (threadIdx.x == 0) {      // one lane: a vector atomic
+            unsigned hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            const unsigned key = ((xcc & 7u) << 8) | ((hw >> 8) & 0xffu);
+            *reinterpret_cast<volatile unsigned *>(smem) = atomicAdd(a.tickets + key, 1u) & 1u;
+        }
+        __syncthreads();
+        delay = *reinterpret_cast<volatile unsigned *>(smem) ? a.stagger : 0;
+        delay = __builtin_amdgcn_readfirstlane(delay);
+        __syncthreads();
+    }
+#ifdef BB4_ONLY_W
+    bb4::run<PRO, EPI, DG, BB4_ONLY_W>(a, smem, lane, delay);
+#else
+    switch (wave) {
+    case 0: bb4::run<PRO, EPI, DG, 0>(a, smem, lane, delay); break;
+    case 1: bb4::run<PRO, EPI, DG, 1>(a, smem, lane, delay); break;
+    case 2: bb4::run<PRO, EPI, DG, 2>(a, smem, lane, delay); break;
+    default: bb4::run<PRO, EPI, DG, 3>(a, smem, lane, delay); break;
+    }
+#endif
+}
+
 // fold per-workgroup partials into dW[co][ci][3][3]: a workgroup owns 64 consecutive
 // outputs; its 4 waves take every 4th partial (4 independent sums in flight per
 // thread) and combine in a fixed order -> deterministic.
@@ -1847,9 +2279,17 @@ __global__ void conv3x3_pack_n_kernel(WeightList wl, int n, float *__restrict__ 
 
 // Forward / input-gradient arithmetic: exact-split bf16 MFMA (1, default) or fp32 MFMA (0).
 int g_split = 1;
-// Chain block backward with an input gradient: 1 = tile-shared conv3x3_block_bwd2_kernel (default), 0 = the
-// per-wave conv3x3_block_bwd_kernel (the tests' reference form).
+// Chain block backward: 1 = the 8-wave tile-shared conv3x3_block_bwd2_kernel (default); 2 = two 4-wave workgroups
+// per CU, conv3x3_block_bwd4_kernel (round 6: bit-identical, slower -- DESIGN §4.3); 0 = the per-wave
+// conv3x3_block_bwd_kernel (the tests' reference form).  Forms 0 and 1 run the per-wave kernel when there is no
+// input gradient.
 int g_block_form = 1;
+// block form 2: the later-arriving workgroup of each CU starts this many s_sleep(32) behind (0: no stagger);
+// HRL_BB4_STAGGER overrides (tools)
+int g_bb4_stagger = [] {
+    const char *e = getenv("HRL_BB4_STAGGER");
+    return e ? atoi(e) : 0;
+}();
 // The chain's forward conv (epilogue 1, packed weights, no bias): 2 = the LDS-DMA ring form (fw3, default),
 // 1 = the tile-shared form (bb2, EPI 1), 0 = conv3x3_kernel<PRO, 1>.
 int g_fwd_form = 2;
@@ -1871,6 +2311,15 @@ int grid_for(int64_t M) {
     return (int)(blocks < kGrid ? blocks : kGrid);
 }
 
+// block form 2: one 16-row tile per workgroup and iteration, two workgroups per CU
+int grid4_for(int64_t M) {
+    const int64_t tiles = (M + kTile - 1) / kTile;
+    return (int)(tiles < bb4::kGrid ? tiles : bb4::kGrid);
+}
+
+// workgroups (= weight-gradient partial rows and epilogue-2 sum rows) of hrl_conv3x3_block_backward
+int block_grid_for(int64_t M) { return g_block_form == 2 ? grid4_for(M) : grid_for(M); }
+
 }  // namespace
 
 extern "C" {
@@ -1879,16 +2328,21 @@ extern "C" {
 int hrl_debug_set_stamps_conv(void *buf) { return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_hrl_stamps), &buf, sizeof(buf)); }
 #endif
 
+constexpr int64_t kTicketBytes = 2048 * 4;   // block form 2's per-CU tickets (any contents: only parity is used)
+
 int64_t hrl_conv3x3_workspace_bytes(int64_t M) {
     if (M < 1) return -1;
-    return (int64_t)grid_for(M) * kTaps * kC * kC * 4 + (int64_t)kTaps * 2 * kC * 16 * 4 * 2;
+    const int64_t rows = grid4_for(M) > grid_for(M) ? grid4_for(M) : grid_for(M);   // every block form's partials
+    return rows * kTaps * kC * kC * 4 + (int64_t)kTaps * 2 * kC * 16 * 4 * 2 + kTicketBytes;
 }
 
 int64_t hrl_conv3x3_stats_blocks(int64_t M) { return M < 1 ? -1 : grid_for(M); }
 
+int64_t hrl_conv3x3_block_sum_blocks(int64_t M) { return M < 1 ? -1 : block_grid_for(M); }
+
 int hrl_conv3x3_set_block_form(int form) {
     const int prev = g_block_form;
-    g_block_form = form < 0 ? 0 : (form > 1 ? 1 : form);
+    g_block_form = form < 0 ? 0 : (form > 2 ? 2 : form);
     return prev;
 }
 
@@ -2023,16 +2477,30 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
     if (gin && (!packed_flip || epilogue < 0 || epilogue == 1 || epilogue > 3)) return HRL_EINVAL;
     if (gin && epilogue == 2 && (!ep_mean || !ep_alpha || !ep_beta || !part)) return HRL_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const int grid = grid_for(M);
+    const int grid = block_grid_for(M);
     float *wpart = static_cast<float *>(workspace) + kTaps * 2 * kC * 16 * 2;
     BlockBwdArgs a{g, y, bn_weight, bn_bias, save_mean, save_invstd, kcoef, gmean, x, in_alpha, in_beta, packed_flip,
                    ep_mean, ep_alpha, ep_beta, gin, part, wpart, M};
+    a.tickets = reinterpret_cast<unsigned *>(static_cast<char *>(workspace) + workspace_bytes - kTicketBytes);
+    a.stagger = g_bb4_stagger;
     const bool pro = in_alpha != nullptr;
 #define HRL_BLOCK_LAUNCH(PRO, EPI, DG) \
     hipLaunchKernelGGL((conv3x3_block_bwd_kernel<PRO, EPI, DG>), dim3(grid), dim3(kThreads), 0, s, a)
 #define HRL_BLOCK2_LAUNCH(PRO, EPI) \
     hipLaunchKernelGGL((conv3x3_block_bwd2_kernel<PRO, EPI>), dim3(grid), dim3(bb2::kThreads), 0, s, a)
-    if (!gin) {
+#define HRL_BLOCK4_LAUNCH(PRO, EPI, DG) \
+    hipLaunchKernelGGL((conv3x3_block_bwd4_kernel<PRO, EPI, DG>), dim3(grid), dim3(bb4::kThreads), 0, s, a)
+    if (g_block_form == 2) {
+        if (!gin) {
+            if (pro) HRL_BLOCK4_LAUNCH(true, 0, false); else HRL_BLOCK4_LAUNCH(false, 0, false);
+        } else if (epilogue == 2) {
+            if (pro) HRL_BLOCK4_LAUNCH(true, 2, true); else HRL_BLOCK4_LAUNCH(false, 2, true);
+        } else if (epilogue == 3) {
+            if (pro) HRL_BLOCK4_LAUNCH(true, 3, true); else HRL_BLOCK4_LAUNCH(false, 3, true);
+        } else {
+            if (pro) HRL_BLOCK4_LAUNCH(true, 0, true); else HRL_BLOCK4_LAUNCH(false, 0, true);
+        }
+    } else if (!gin) {
         if (pro) HRL_BLOCK_LAUNCH(true, 0, false); else HRL_BLOCK_LAUNCH(false, 0, false);
     } else if (g_block_form == 0) {   // the per-wave form (kept for comparison)
         if (epilogue == 2) {
@@ -2051,6 +2519,7 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
     }
 #undef HRL_BLOCK_LAUNCH
 #undef HRL_BLOCK2_LAUNCH
+#undef HRL_BLOCK4_LAUNCH
     int rc = status();
     if (rc || !dweight) return rc;   // no dweight: the partials stay for a later fold (hrl_grad_fold_norm)
     hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, wpart, grid,
@@ -2061,7 +2530,7 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
 int64_t hrl_conv3x3_wgrad_partials(int64_t M, int64_t *offset_bytes) {
     if (M < 1) return -1;
     if (offset_bytes) *offset_bytes = (int64_t)kTaps * 2 * kC * 16 * 2 * 4;
-    return grid_for(M);
+    return block_grid_for(M);
 }
 
 int hrl_conv3x3_wgrad(const float *x, const float *dy, int64_t M, int64_t C_in, int64_t C_out, float *dweight,

@@ -15,7 +15,7 @@
 // increment, the BatchNorm batch counters and torch's fused Adam -- two launches:
 //  * step_fold_norm_kernel: 64-position blocks of the flat buffer; a position that a fold covers takes the
 //    fixed-order fp64 sum of the partial column at that position (16 waves over interleaved partial rows,
-//    combined in wave order) and stores it to its element (for a transposed fold, another position of the same fold), the
+//    combined in wave order) and adds it into its element (for a transposed fold, another position of the same fold), the
 //    rest are read; each block writes the fp64 sum of squares of its final values; block 0 also
 //    advances the step count and the batch counters;
 //  * adam_clip_kernel: every workgroup folds the block sums in one fixed order (so all agree on the norm bit for
@@ -214,8 +214,12 @@ __global__ __launch_bounds__(64 * kFoldWaves) void step_fold_norm_kernel(float *
         if (f >= 0) {
             v = 0.0;
             for (int k = 0; k < kFoldWaves; ++k) v += red[k][lane];   // wave order
-            const float fv = (float)v;
-            g[ft.dst[f] + fold_dst(ft.mode[f], i - ft.dst[f])] = fv;
+            // accumulated, not assigned: a parameter reached again later in the backward has had that use's
+            // gradient added into its p.grad by autograd already (the buffer is zeroed at step start, so a
+            // single-use parameter gets 0 + fold = the fold exactly)
+            const int64_t d = ft.dst[f] + fold_dst(ft.mode[f], i - ft.dst[f]);
+            const float fv = g[d] + (float)v;
+            g[d] = fv;
             v = (double)fv;
         } else {
             v = i < n ? (double)g[i] : 0.0;

@@ -501,10 +501,8 @@ class GeisterNet(nn.Module):
         """relu(bn(y)) for T time steps' rows (time-major) with per-step statistics."""
         from .. import nn as hnn
         from ..nn import batch_norm_train
-        if hnn._FOLDS is not None and bn.momentum is not None:
-            hnn._FOLDS.add_counter(bn.num_batches_tracked, T)   # advanced by the learner's step tail
-        else:
-            bn.num_batches_tracked.add_(T)
+        if bn.momentum is None or not hnn._defer_counters([bn.num_batches_tracked], T):
+            bn.num_batches_tracked.add_(T)      # else advanced by the learner's step tail
         return batch_norm_train(y, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
                                 relu=True, groups=T)
 

@@ -308,20 +308,42 @@ class deferred_folds:
             _FOLDS = self.prev
         return False
 
+    # the step tail's launch tables (csrc/hrl_optim.hip kMaxFolds / kMaxCounters): a Function that finds no room
+    # left runs its own reduce launch and a counter its own add, so a deep net degrades to launches, never fails
+    MAX_FOLDS = 16
+    MAX_COUNTERS = 8
+
+    def has_room(self, folds=0, counters=0):
+        return (len(self.folds) + folds <= self.MAX_FOLDS and len(self.counters) + counters <= self.MAX_COUNTERS)
+
     def add(self, part, stride, col0, nparts, dst, count, mode=0):
+        assert len(self.folds) < self.MAX_FOLDS, 'deferred folds: table full (check has_room first)'
         self.folds.append((part, stride, col0, nparts, dst, count, mode))
 
     def add_counter(self, counter, inc=1):
+        assert len(self.counters) < self.MAX_COUNTERS, 'deferred folds: counter table full (check has_room first)'
         self.counters.append(counter)
         self.increments.append(int(inc))
 
 
-def _defer_folds(bufs):
+def _defer_folds(bufs, nfolds=None):
     """The deferred-folds context when the gradients in `bufs` (_grad_buffer results) may stay as partials:
-    one is active and every buffer is a direct (in-place) one; else None."""
+    one is active, every buffer is a direct (in-place) one and its table has room for the `nfolds` folds the
+    caller registers (default: one per buffer); else None (the caller folds with its own launch)."""
     if _FOLDS is None or not all(b[1] for b in bufs if b[0] is not None):
         return None
-    return _FOLDS
+    n = sum(1 for b in bufs if b[0] is not None) if nfolds is None else nfolds
+    return _FOLDS if _FOLDS.has_room(folds=n) else None
+
+
+def _defer_counters(counters, inc=1):
+    """Hand BatchNorm batch counters to the active deferred-folds context (the step tail advances them); False
+    when there is none or its counter table is full (the caller advances them itself)."""
+    if _FOLDS is None or not _FOLDS.has_room(counters=len(counters)):
+        return False
+    for c in counters:
+        _FOLDS.add_counter(c, inc)
+    return True
 
 
 def _heads_backward_deferred(lib, df, bufs, N, ws, call):
@@ -1418,7 +1440,7 @@ class _BoardHeadsFn(torch.autograd.Function):
             _native.check(lib.hrl_heads_backward(P(h), N, P(w1p), P(w1v), P(wp), P(wv), None, None, None, None,
                                                  P(a_p), P(a_v), P(dp), P(dv), None, P(dh), *(P(t) for t in dws),
                                                  P(ws), ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward')
-        df = _defer_folds(bufs) if lib.hrl_heads_set_bwd_form(0) == 2 else None   # deferral needs form 2
+        df = _defer_folds(bufs, 6) if lib.hrl_heads_set_bwd_form(0) == 2 else None   # deferral needs form 2
         if df is not None:
             _heads_backward_deferred(lib, df, bufs, N, ws, call)
         else:
@@ -1975,8 +1997,9 @@ def _chain_forward(h0, meta, relu_in, params, apply_out=True):
     # every conv's forward and input-gradient weight layouts in one launch (the backward reuses them)
     weights = [params[3 * i].contiguous() for i in range(len(meta))]
     packed = torch.empty(len(weights), 2, 9216, dtype=torch.float32, device=dev)
-    _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array(weights), len(weights), P(packed), stream),
-                  'hrl_conv3x3_pack_n')
+    for k in range(0, len(weights), 8):       # hrl_conv3x3_pack_n takes up to 8 weights per launch
+        _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array(weights[k:k + 8]), len(weights[k:k + 8]),
+                                             P(packed[k]), stream), 'hrl_conv3x3_pack_n')
     for i, (rm, rv, momentum, eps) in enumerate(meta):
         w, gamma, beta = params[3 * i:3 * i + 3]
         y = torch.empty_like(h0)
@@ -2010,7 +2033,8 @@ def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, pa
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     bn_ws_bytes = lib.hrl_bn_workspace_bytes(M, 32, 9)
     bn_ws = torch.empty(bn_ws_bytes, dtype=torch.uint8, device=dev)
-    nblk = lib.hrl_conv3x3_stats_blocks(M)
+    # the block backward's epilogue-2 sum rows (its workgroups) or the input-gradient conv's
+    nblk = max(lib.hrl_conv3x3_block_sum_blocks(M), lib.hrl_conv3x3_stats_blocks(M))
     part = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
     g = g.contiguous()
     grads = [None] * (3 * n)
@@ -2052,8 +2076,8 @@ def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, pa
                 df.keep.append(wsb)
             grads[3 * i:3 * i + 3] = [_ret(bw), _ret(bgam), _ret(bbet)]
             g = gin
-            if i > 0:
-                sums, sums_n = part, nblk   # read by the next block's finalize before its launch rewrites part
+            if i > 0:   # read by the next block's finalize before its launch rewrites part
+                sums, sums_n = part, lib.hrl_conv3x3_block_sum_blocks(M)
             continue
         dy = torch.empty_like(h0)
         _native.check(lib.hrl_bn_backward(P(ys[i]), P(g), M, 32, 9, P(gamma), P(beta), P(mean), P(invstd),
@@ -2069,7 +2093,7 @@ def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, pa
                                                      P(coefs[i - 1][0]), P(coefs[i - 1][2]),
                                                      P(coefs[i - 1][3]), P(part), P(ws), ws_bytes, stream),
                           'hrl_conv3x3_forward_ex(flip, bn sums)')
-            sums, sums_n = part, nblk
+            sums, sums_n = part, lib.hrl_conv3x3_stats_blocks(M)
         elif need_input_grad:
             g = torch.empty_like(h0)
             _native.check(lib.hrl_conv3x3_forward_ex(P(dy), M, None, None, P(packed[i, 1]), None, 3, P(g),
@@ -2170,7 +2194,7 @@ class _ChainHeadsFn(torch.autograd.Function):
                                                  P(coef[0]), P(bn_part), P(a_p), P(a_v), P(dp), P(dv),
                                                  P(v) if ctx.tanh_v else None, P(dh), *(P(t) for t in dws),
                                                  P(ws), ws_bytes, _native.stream_of(dev)), 'hrl_heads_backward(bn)')
-        df = _defer_folds(hbufs) if lib.hrl_heads_set_bwd_form(0) == 2 else None
+        df = _defer_folds(hbufs, 6) if lib.hrl_heads_set_bwd_form(0) == 2 else None
         if df is not None:
             _heads_backward_deferred(lib, df, hbufs, N, ws, call)
         else:
@@ -2221,10 +2245,7 @@ class _ConvBNChain(nn.Module):
     def meta_params(self):
         """Advance the BatchNorms' batch counters (as their forward would) and collect the chain's arguments."""
         counters = [b.num_batches_tracked for b in self.bns]
-        if _FOLDS is not None:
-            for c in counters:                     # advanced by the step tail's first launch
-                _FOLDS.add_counter(c)
-        else:
+        if not _defer_counters(counters):          # else advanced by the step tail's first launch
             torch._foreach_add_(counters, 1)       # one launch for all counters
         meta, params = [], []
         for c, b in zip(self.convs, self.bns):

@@ -119,15 +119,15 @@ class StepTail:
         return self.total
 
 
-def split_torus_tower(net):
+def split_torus_tower(net, on=True):
     """Run a torus-conv tower (GeeseNet) as two Functions split after its middle unit (nn.torus_tower), so a
     data-parallel segmented capture can all-reduce the upper half's gradients while the lower half's backward
     replays (hungry_geese.py:48-51: conv0 and 12 blocks -> units [0, 7) and [7, 13)).  Same values as the one
-    Function up to the order of the BatchNorm sums at the split."""
+    Function up to the order of the BatchNorm sums at the split.  on=False removes the split again."""
     from .envs.hungry_geese import TorusConv2d
     torus = [m for m in net.modules() if isinstance(m, TorusConv2d)]
     if len(torus) >= 2:
-        torus[0].tower_split = (len(torus) + 1) // 2
+        torus[0].tower_split = (len(torus) + 1) // 2 if on else None
 
 
 class LearnerStep:
@@ -148,7 +148,8 @@ class LearnerStep:
         self.reducer = None
         if world_size > 1:
             self.reducer = hdist.GradAllReduce(self.grads, group=reduce_group, bucket_bytes=bucket_bytes)
-            split_torus_tower(self.net)
+            if self.graph and segment_backward:
+                split_torus_tower(self.net)   # only a segmented capture uses the cut (eager: one Function)
         if lr is None:
             # train.py:318-321: lr = 3e-8 * batch_size * forward_steps for the batch ONE update sees.
             # Here args['batch_size'] is the per-rank shard and the gradients are SUMmed over the ranks,
@@ -532,6 +533,7 @@ class LearnerStep:
         except RuntimeError as e:
             self.segments = None
             self.segment_error = str(e)
+            split_torus_tower(self.net, False)   # no segmented capture: the tower runs as one Function again
 
     def _plan_flush_segments(self):
         """Recurrent net, data parallel: segment 1 = the live parameters completed by the backward and the first

@@ -174,12 +174,16 @@ int64_t hrl_conv3x3_stats_blocks(int64_t M);
  * both fp32 operands on v_mfma_f32_16x16x32_bf16 (six partial products, fp32 accumulation; error below one fp32
  * rounding per product), 0 the fp32 v_mfma_f32_16x16x4_f32.  Process-wide; returns the previous setting. */
 int hrl_conv3x3_set_split(int on);
-/* Kernel form of hrl_conv3x3_block_backward with an input gradient: form != 0 (the default) the tile-shared,
- * pipelined kernel (8 waves share each 16-row tile: weight gradient and input gradient blocks split over the
- * waves, the next tile staged in a second LDS buffer while the MFMAs run), 0 the per-wave kernel.  The input
- * gradient and the epilogue are the same in both; the weight gradient sums the tiles in a different
- * association.  Process-wide; returns the previous setting. */
+/* Kernel form of hrl_conv3x3_block_backward: 1 (the default) the 8-wave tile-shared, pipelined kernel (the next
+ * tile staged in a second LDS buffer while the MFMAs run); 2 two independent 4-wave workgroups per CU, each
+ * sharing a 16-row tile among its waves (single-buffered LDS images, ABI 25); 0 the per-wave kernel.
+ * Forms 0 and 1 run the per-wave kernel without an input gradient.  The input gradient and the epilogue are the
+ * same in all; the weight gradient sums the tiles in a different association per form.  Process-wide; returns
+ * the previous setting. */
 int hrl_conv3x3_set_block_form(int form);
+/* Rows of epilogue-2 sums (32 x 2 doubles each) hrl_conv3x3_block_backward writes into `part` under the current
+ * block form (ABI 25; form 2 writes more rows than hrl_conv3x3_stats_blocks). */
+int64_t hrl_conv3x3_block_sum_blocks(int64_t M);
 /* The chain's forward conv with BN statistics (hrl_conv3x3_forward_ex, epilogue 1, packed weights, no bias):
  * 2 (default) = the LDS-DMA ring form (every wave computes, x' staged from a raw ring), 1 = the block backward's
  * tile-shared form, 0 = the per-wave conv3x3_kernel (tools/fwd_form_bench.py).  Returns the previous. */
@@ -205,7 +209,7 @@ int hrl_conv3x3_wgrad_ex(const float *x, const float *in_alpha, const float *in_
  *             with the epilogue of hrl_conv3x3_forward_ex and ref = x: 0 none, 2 BN_{i-1}'s backward sums
  *             into part (ep_mean, ep_alpha, ep_beta), 3 gin *= [x > 0].
  * g, y, x, gin: (M, 288) rows; M * 1152 bytes < 4 GiB.  workspace: hrl_conv3x3_workspace_bytes(M) bytes;
- * part: hrl_conv3x3_stats_blocks(M) x 32 x 2 doubles.  Replaces, for the TicTacToe body
+ * part: hrl_conv3x3_block_sum_blocks(M) x 32 x 2 doubles.  Replaces, for the TicTacToe body
  * (tictactoe.py:57-65), the autograd backward of conv -> BatchNorm2d -> ReLU per block.
  */
 /* dweight NULL: the weight gradient is left as per-workgroup partial rows in the workspace (9216 floats each,

@@ -534,7 +534,7 @@ def _dp_rank_main(rank, world, port, out_path, name, graph):
     dist.destroy_process_group()
 
 
-def _simulated_dp(name, dev, steps=2, world=2):
+def _simulated_dp(name, dev, steps=2, world=2, split=True):
     """The data-parallel update without any collective: one replica per shard (its own BatchNorm statistics,
     as under the reference's nn.DataParallel), each computing its shard's gradients with LearnerStep's own
     backward; the SUM of the replicas' gradients is clipped and applied by Adam with the global batch's lr
@@ -551,7 +551,8 @@ def _simulated_dp(name, dev, steps=2, world=2):
     for r in range(world):
         torch.manual_seed(0)
         net = cls()
-        split_torus_tower(net)      # as a data-parallel LearnerStep runs GeeseNet's tower
+        if split:                   # as a data-parallel graph LearnerStep runs GeeseNet's tower
+            split_torus_tower(net)
         st = LearnerStep(net, args, dev, lr=lr)
         st.fold_deferral = False    # the shard's gradient complete in the flat buffer after _grads
         reps.append((net, st))
@@ -591,7 +592,7 @@ def test_two_rank_bn_nets_match_simulated_replicas(cuda, name, graph):
         out = os.path.join(d, 'r0.pt')
         mp.spawn(_dp_rank_main, args=(2, _free_port(), out, name, graph), nprocs=2, join=True)
         res = torch.load(out, weights_only=True)
-    ref, ref_bufs = _simulated_dp(name, cuda)
+    ref, ref_bufs = _simulated_dp(name, cuda, split=graph)   # eager data-parallel steps keep one tower
     p0, p1 = res['params']
     assert torch.equal(p0, p1)
     torch.testing.assert_close(p0, ref, rtol=1e-5, atol=2e-6)
@@ -602,3 +603,80 @@ def test_two_rank_bn_nets_match_simulated_replicas(cuda, name, graph):
         assert res['launched'][-1] > 0, res['launched']   # second step: buckets launched before finish()
         if name == 'Geister':   # deferred weights: the accumulate hook, then mark_ready after the flush
             assert 2 in res['expected'], res['expected']
+
+
+def _schedule_rank_main(rank, world, port, out_path):
+    """One rank of the segmented graph step's replay schedule (LearnerStep.step, the path bench.py --gpus N
+    takes every timed step), with recording stand-ins for the three captured graphs: each stand-in logs its
+    replay and writes this rank's values into its segment's range of the flat gradient buffer, as the real
+    graph's kernels would; the all-reduce calls are the product's (GradAllReduce.all_reduce_ranges over gloo),
+    wrapped to log their issue and their waits."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from handyrl_amd import distributed as hdist
+    from handyrl_amd.trainer import LearnerStep
+    hdist.init_process_group('cpu')
+    batch, args = make_batch_and_args()
+    step = LearnerStep(SmallNet(), args, torch.device('cpu'), world_size=world, loss_fn=oracle_loss)
+    flat = step.grads.flat
+    n = flat.numel()
+    log = []
+
+    class Graph:
+        def __init__(self, name, lo=0, hi=0):
+            self.name, self.lo, self.hi = name, lo, hi
+
+        def replay(self):
+            log.append('replay:' + self.name)
+            if self.hi > self.lo:     # this rank's gradients of the segment: rank + 1 + element index
+                flat[self.lo:self.hi] = torch.arange(self.lo, self.hi, dtype=torch.float32) + (rank + 1)
+
+    cut = n // 3
+    upper, lower = [(cut, n)], [(0, cut)]
+    step.graph = True
+    step.segments = [(upper, []), (lower, [])]
+    step._graph = Graph('upper', cut, n)
+    step._graph_seg2 = Graph('lower', 0, cut)
+    step._graph_update = Graph('update')
+    step._static, step._static_hidden = batch, None
+    step._static_out = {'total': torch.zeros(())}
+    real = step.reducer.all_reduce_ranges
+
+    class Work:
+        def __init__(self, w, tag):
+            self.w, self.tag = w, tag
+
+        def wait(self):
+            log.append('wait:' + self.tag)
+            return self.w.wait()
+
+    def all_reduce_ranges(ranges):
+        tag = 'upper' if ranges == upper else ('lower' if ranges == lower else repr(ranges))
+        log.append('issue:' + tag)
+        return [Work(w, tag) for w in real(ranges)]
+    step.reducer.all_reduce_ranges = all_reduce_ranges
+    for _ in range(2):
+        log.append('step')
+        step.step(batch)
+    ref = torch.arange(n, dtype=torch.float32) * world + sum(r + 1 for r in range(world))
+    if rank == 0:
+        torch.save({'log': log, 'flat': flat.clone(), 'ref': ref}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_segmented_graph_replay_schedule_two_ranks():
+    """The per-step order of the data-parallel graph step (bench.py --gpus N), two gloo ranks on the
+    CPU: upper graph (loss, heads, chain) -> the upper segment's all-reduce issued -> lower graph (stem) replays
+    while it runs -> the lower segment's all-reduce -> both waited for -> update graph (clip, Adam); and each
+    segment's range of the flat buffer is the SUM over the ranks of what that rank's graph wrote (the upper
+    range all-reduced only after the upper graph wrote it, the lower only after the lower one)."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, 'sched.pt')
+        mp.spawn(_schedule_rank_main, args=(2, _free_port(), out), nprocs=2, join=True)
+        res = torch.load(out, weights_only=True)
+    one = ['replay:upper', 'issue:upper', 'replay:lower', 'issue:lower', 'wait:upper', 'wait:lower',
+           'replay:update']
+    assert res['log'] == ['step'] + one + ['step'] + one, res['log']
+    assert torch.equal(res['flat'], res['ref'])

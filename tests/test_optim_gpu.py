@@ -183,12 +183,61 @@ def test_grad_fold_norm_folds_partials(cuda):
     torch.cuda.synchronize(cuda)
     ref = before.double().cpu()
     conv = p1.double().sum(0).view(9, 32, 32).permute(2, 1, 0).reshape(-1)   # (tap, ci, co) -> (co, ci, tap)
-    ref[:9216] = conv
-    ref[9226:9226 + 162] = p0.double().sum(0)[99:261]
-    ref[9416:9425] = p0.double().sum(0)[261:270]
+    # folds ADD into their destinations (another use of the parameter may have added its gradient there)
+    ref[:9216] += conv.cpu()
+    ref[9226:9226 + 162] += p0.double().sum(0)[99:261].cpu()
+    ref[9416:9425] += p0.double().sum(0)[261:270].cpu()
     got = flat.double().cpu()
     assert float((got - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
     assert torch.equal(got[9216:9226], before[9216:9226].double().cpu())
     tot = float(norm_part.sum())
     assert abs(tot - float((got ** 2).sum())) <= 1e-9 * tot
     assert float(step) == 1.0 and [int(c) for c in ctr] == [1, 16, 3]   # each counter by its increment
+
+
+def _twice_stem_net():
+    """The TicTacToe net with its stem applied twice (to the board and to its mirror image): the stem's HIP
+    Function is reached twice, so one use may leave its weight gradient as deferred partials while autograd adds
+    the other use's gradient into the same p.grad during the backward."""
+    import torch.nn.functional as F
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+
+    class TwiceStem(SimpleConv2dModel):
+        def forward(self, x, hidden=None):
+            h = F.relu(self.conv(x)) + F.relu(self.conv(x.flip(-1)))
+            for blk in self.blocks:
+                h = F.relu(blk(h))
+            return {'policy': self.head_p(h), 'value': torch.tanh(self.head_v(h))}
+    return TwiceStem()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', ['shared_stem', 'nine_blocks'])
+def test_deferred_folds_match_unfolded_step(cuda, case):
+    """LearnerStep with the step tail's deferred folds vs the same step with every Function folding its own
+    partials (fold_deferral off): a parameter used twice in the step (the fold adds to what autograd accumulated,
+    ADVICE r5) and a 9-block chain, whose 9 + 6 + 2 folds and 9 BatchNorm counters overflow the tail's tables
+    (16 / 8): the Functions past the limit fold with their own launch, the counters advance by their own add."""
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.synthetic import tictactoe_batch, default_args
+    from handyrl_amd.trainer import LearnerStep
+    B, T = 64, 9
+    args = default_args(T, B)
+    make = _twice_stem_net if case == 'shared_stem' else (lambda: SimpleConv2dModel(layers=9))
+    torch.manual_seed(0)
+    a = make()
+    torch.manual_seed(0)
+    b = make()
+    sa, sb = LearnerStep(a, args, cuda), LearnerStep(b, args, cuda)
+    assert sa.fold_deferral and sa.tail is not None
+    sb.fold_deferral = False
+    for s in range(2):
+        batch = tictactoe_batch(B, T, cuda, seed=7 + s)
+        oa, ob = sa.step(batch), sb.step(batch)
+        ga, gb = float(oa['grad_norm']), float(ob['grad_norm'])
+        assert abs(ga - gb) <= 1e-5 * gb, (s, ga, gb)
+    for (k, va), vb in zip(a.state_dict().items(), b.state_dict().values()):
+        if k.endswith('num_batches_tracked'):
+            assert int(va) == int(vb) == 2, k
+        else:
+            torch.testing.assert_close(va, vb, rtol=1e-5, atol=1e-6, msg=k)

@@ -1,5 +1,5 @@
-"""Time one chain block's backward: the fused hrl_conv3x3_block_backward (the default tile-shared form 1 and
-the per-wave form 0) vs the three launches it replaces.
+"""Time one chain block's backward: the fused hrl_conv3x3_block_backward (the default two-workgroup form 2, the
+tile-shared form 1 and the per-wave form 0) vs the three launches it replaces.
 
     python tools/block_bench.py [--M 131072] [--iters 20]
 HRL_LIB_PATH selects another build of libhrl.so (diagnostic variants).  HIP events on the launch stream.
@@ -20,6 +20,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--M', type=int, default=131072)
     ap.add_argument('--iters', type=int, default=20)
+    ap.add_argument('--epi', type=int, default=2, help='epilogue of the fused launch: 0, 2 (BN sums) or 3 (mask)')
+    ap.add_argument('--forms', default='', help='only these block forms (comma list), e.g. 2,1')
     opts = ap.parse_args()
     dev = torch.device('cuda', 0)
     lib = _native.load()
@@ -35,13 +37,15 @@ def main():
     _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array([w]), 1, P(packed), stream), 'pack')
     ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    part = torch.empty(lib.hrl_conv3x3_stats_blocks(M) * 64, dtype=torch.float64, device=dev)
+    part = torch.empty(max(lib.hrl_conv3x3_stats_blocks(M), lib.hrl_conv3x3_block_sum_blocks(M)) * 64,
+                       dtype=torch.float64, device=dev)
     dw, gin, dy = torch.empty(32, 32, 3, 3, device=dev), torch.empty_like(g), torch.empty_like(g)
 
     def fused():
         _native.check(lib.hrl_conv3x3_block_backward(
-            P(g), P(y), M, *[P(t) for t in c[:6]], P(x), P(c[6]), P(c[7]), P(packed[0, 1]), P(dw), P(gin), 2,
-            P(c[8]), P(c[9]), P(c[10]), P(part), P(ws), ws_bytes, stream), 'block')
+            P(g), P(y), M, *[P(t) for t in c[:6]], P(x), P(c[6]), P(c[7]), P(packed[0, 1]), P(dw), P(gin),
+            opts.epi, P(c[8]), P(c[9]), P(c[10]), P(part) if opts.epi == 2 else None, P(ws), ws_bytes, stream),
+            'block')
 
     def three():
         _native.check(lib.hrl_bn_backward_apply(P(y), P(g), M, 32, 9, P(c[0]), P(c[1]), P(c[2]), P(c[3]), 1,
@@ -52,7 +56,8 @@ def main():
                                                  P(c[8]), P(c[9]), P(c[10]), P(part), P(ws), ws_bytes, stream),
                       'dgrad')
 
-    out = {'M': M, 'lib': os.path.basename(_native.LIB_PATH)}
+    out = {'M': M, 'lib': os.path.basename(_native.LIB_PATH), 'epi': opts.epi}
+    only = {int(f) for f in opts.forms.split(',')} if opts.forms else None
 
     def form(f):
         def run():
@@ -60,8 +65,13 @@ def main():
             fused()
             lib.hrl_conv3x3_set_block_form(prev)
         return run
-    for name, fn in (('fused_us', fused), ('fused_tile_shared_us', form(1)),
-                     ('fused_per_wave_us', form(0)), ('three_launches_us', three)):
+    cases = [('fused_two_wg_us', form(2), 2), ('fused_tile_shared_us', form(1), 1), ('fused_per_wave_us', form(0), 0),
+             ('three_launches_us', three, None)]
+    if only is None:
+        cases = [('fused_us', fused, None)] + cases
+    for name, fn, f in cases:
+        if only is not None and f not in only:
+            continue
         for _ in range(3):
             fn()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

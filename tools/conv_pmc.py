@@ -36,7 +36,8 @@ def main():
     _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array([w]), 1, P(packed), stream), 'pack')
     ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    part = torch.empty(lib.hrl_conv3x3_stats_blocks(M) * 64, dtype=torch.float64, device=dev)
+    part = torch.empty(max(lib.hrl_conv3x3_stats_blocks(M), lib.hrl_conv3x3_block_sum_blocks(M)) * 64,
+                       dtype=torch.float64, device=dev)
     dw, out = torch.empty(32, 32, 3, 3, device=dev), torch.empty_like(g)
     if opts.which == 'fwd':
         lib.hrl_conv3x3_set_fwd_form(opts.form)
