@@ -544,6 +544,47 @@ def secondary_host_rollout(device, E=256):
     return out
 
 
+def secondary_player_rollout(device):
+    """The per-player device generator (rollout.DeviceGenerator's per-player ply, generation.py:35-62): every
+    player's view through one forward per ply, per-player records and state, into a PlayerReplay -- the modes the
+    host generator served before round 6: TicTacToe with observation=True, ParallelTicTacToe (simultaneous
+    moves, parallel_tictactoe.py:20-24) and Geister with observation=True (recurrent state per player and game)."""
+    from handyrl_amd.envs.geister import GeisterNet, GeisterBatch
+    from handyrl_amd.rollout import TicTacToeBatch, ParallelTicTacToeBatch, DeviceGenerator, PlayerReplay
+    from handyrl_amd.nn import accelerate
+    out = {}
+    for name, cls, make_net, E, reps, obs in (('TicTacToe_observation', TicTacToeBatch, SimpleConv2dModel, 16384, 5,
+                                               True),
+                                              ('ParallelTicTacToe', ParallelTicTacToeBatch, SimpleConv2dModel, 16384,
+                                               5, False),
+                                              ('Geister_observation', GeisterBatch, GeisterNet, 2048, 1, True)):
+        torch.manual_seed(0)
+        net = accelerate(make_net().to(device))
+        gen = DeviceGenerator(cls(E, device), net, observation=obs)
+        rep = PlayerReplay(2 * E, cls.MAX_PLIES, cls.OBS_SHAPE, cls.A, cls.P, device, obs_dtype=torch.uint8,
+                           mover=not obs)
+        g = torch.Generator(device=device).manual_seed(0)
+        rep.add(gen.generate(generator=g))   # warm-up (and the ply graph's capture)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        plies = 0
+        for _ in range(reps):
+            ep = gen.generate(generator=g)
+            rep.add(ep)
+            plies += ep['length'].sum()
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t0
+        plies = int(plies)
+        out[name] = {'value': round(plies / dt, 1), 'unit': 'env-steps/s', 'games': E * reps,
+                     'games_per_s': round(E * reps / dt, 1), 'mean_plies': round(plies / (E * reps), 1),
+                     'observation': obs}
+        del gen, rep, net
+        torch.cuda.empty_cache()
+    out['note'] = ('one forward per ply over all P x E (player, game) views; env-steps = plies; the host generator '
+                   'served these modes before (host_rollout)')
+    return out
+
+
 def secondary_geister_rollout(device, E=2048, reps=2):
     """BASELINE.json configs[2]: Geister device self-play, E concurrent games, recurrent GeisterNet inference."""
     from handyrl_amd.envs.geister import GeisterNet, GeisterBatch
@@ -695,6 +736,7 @@ def main():
         gle = secondary_geister_learner(device) if (opts.secondary and world == 1) else None
         gee = secondary_geese_learner(device) if (opts.secondary and world == 1) else None
         hro = secondary_host_rollout(device) if (opts.secondary and world == 1) else None
+        pro = secondary_player_rollout(device) if (opts.secondary and world == 1) else None
         line = {
             'metric': 'learner env-steps/sec at B=4096 T=32 (TicTacToe net, UPGO/VTRACE)',
             'value': round(value, 1),
@@ -735,6 +777,8 @@ def main():
             line['geese_learner'] = gee
         if hro is not None:
             line['host_rollout'] = hro
+        if pro is not None:
+            line['player_rollout'] = pro
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -617,6 +617,47 @@ class GeisterBatch:
         self.turn_count.fill_(-2)
         self.win.fill_(-1)
         self.cnt.zero_()
+        if getattr(self, 'pidx', None) is not None:
+            self.pidx.fill_(-1)
+
+    pidx = None   # (E, 36) piece index (colour*8 + slot) per cell, kept only when piece_order(True) asked for it
+
+    def piece_order(self, on=True):
+        """Keep each cell's piece index (the reference's piece numbering, geister.py:227-234, 380-386), so that
+        legal_rank() can give the reference's legal-action order; off by default (the rules do not need it)."""
+        self.pidx = torch.full((self.E, 36), -1, dtype=torch.long, device=self.device) if on else None
+
+    def legal_rank(self):
+        """(E, 214) sort key of every action in the reference's legal_actions order (geister.py:472-486): the
+        layouts 144..213 ascending; a move by the mover's piece of slot s in absolute direction d at s*4 + d (the
+        pieces by index, each piece's directions in order).  Needs piece_order(True) before reset()."""
+        assert self.pidx is not None, 'legal_rank needs piece_order(True)'
+        a = torch.arange(self.MOVES, device=self.device).view(1, -1)
+        c = self.color.view(-1, 1)
+        a_abs = torch.where(c == 1, self.MOVES - 1 - a, a)
+        cell = (a_abs % 36).expand(self.E, -1)
+        slot = torch.gather(self.pidx, 1, cell) - c * 8
+        key = slot.clamp(min=0) * 4 + a_abs // 36
+        lay = torch.arange(self.A - self.MOVES, device=self.device).view(1, -1).expand(self.E, -1)
+        return torch.cat([key, lay], 1)
+
+    def _track_pieces(self, action, active):
+        """pidx through one step (before the rules move the board): a layout puts the mover's pieces 0..7 on
+        their initial squares, a move carries the piece's index to its target (off the board: gone)."""
+        E, rows, c = self.E, torch.arange(self.E, device=self.device), self.color
+        setting = active & (self.turn_count < 0)
+        moving = active & (self.turn_count >= 0)
+        cells = self.opos[c]
+        cur = torch.gather(self.pidx, 1, cells)
+        new = c.view(-1, 1) * 8 + torch.arange(8, device=self.device).view(1, -1)
+        self.pidx.scatter_(1, cells, torch.where(setting.view(-1, 1), new, cur))
+        a_abs = torch.where(c == 1, self.MOVES - 1 - action, action).clamp(0, self.MOVES - 1)
+        src, dst = a_abs % 36, self.tgt[a_abs // 36, a_abs % 36]
+        piece = self.pidx[rows, src]
+        self.pidx[rows, src] = torch.where(moving, torch.full_like(piece, -1), piece)
+        on = moving & (dst >= 0)
+        dst_s = dst.clamp(min=0)
+        self.pidx[rows, dst_s] = torch.where(on, piece, self.pidx[rows, dst_s])
 
     def turn(self):
         return self.color
@@ -656,6 +697,8 @@ class GeisterBatch:
     def step(self, action, active):
         """Play `action` (E,) for the side to move in every `active` game (geister.py:359-394)."""
         E, dev = self.E, self.device
+        if self.pidx is not None:
+            self._track_pieces(action.to(torch.long), active.to(torch.bool))
         if self._hip():
             from .._native import load, check, ptr, stream_of
             assert action.shape == (E,) and active.shape == (E,)

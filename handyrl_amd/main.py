@@ -12,15 +12,18 @@ written) with the actors and the learner on the GPU:
 
 * ``prepare_env`` / ``make_env`` resolve the env by name or module path
   (environment.py:18-39) and ``env.net()`` gives the model class;
-* generation: an env module with a batched (device) twin (``BATCHED``:
-  TicTacToe, Geister, CIGeister) in the stock layout (turn_based_training,
-  no opponent observation) is played by ``rollout.DeviceGenerator`` into
-  ``rollout.DeviceReplay``; ANY other env -- a user's module, ParallelTicTacToe,
-  the reference's own plugins named by module path, ``observation: True``,
-  solo training -- is played through the plugin API by
-  ``hostgen.HostBatchGenerator`` (host envs, one batched GPU forward per
-  ply, generation.py's semantics) into ``hostgen.MomentReplay``;
-  ``generator: host`` in train_args forces that path for every env;
+* generation: an env module with a batched (device) twin (TicTacToe,
+  ParallelTicTacToe, Geister, CIGeister) is played by
+  ``rollout.DeviceGenerator``: in the stock layout of an alternating env
+  (turn_based_training, no opponent observation) the mover-only ply into
+  ``rollout.DeviceReplay``; with ``observation: True``, solo training or a
+  simultaneous-move env the per-player ply (every player's view, records
+  with a player axis) into ``rollout.PlayerReplay``.  ANY other env -- a
+  user's module, the reference's own plugins named by module path -- is
+  played through the plugin API by ``hostgen.HostBatchGenerator`` (host
+  envs, one batched GPU forward per ply, generation.py's semantics) into
+  ``hostgen.MomentReplay``; ``generator: host`` in train_args forces that
+  path for every env;
 * ``update_episodes`` games per epoch with the current weights (the
   reference's workers hold the latest published model), recency-weighted
   replay of ``maximum_episodes``; training starts once ``minimum_episodes``
@@ -48,7 +51,7 @@ import yaml
 from . import distributed as hdist
 from .environment import make_env, prepare_env
 from .hostgen import HostBatchGenerator, MomentReplay
-from .rollout import DeviceGenerator, DeviceReplay, TicTacToeBatch
+from .rollout import DeviceGenerator, DeviceReplay, ParallelTicTacToeBatch, PlayerReplay, TicTacToeBatch
 from .trainer import Trainer
 
 
@@ -56,7 +59,8 @@ def _batched_envs():
     from .envs.geister import GeisterBatch
     from .envs.ci_geister import CIGeisterBatch
     return {'handyrl_amd.envs.tictactoe': TicTacToeBatch, 'handyrl_amd.envs.geister': GeisterBatch,
-            'handyrl_amd.envs.ci_geister': CIGeisterBatch}
+            'handyrl_amd.envs.ci_geister': CIGeisterBatch,
+            'handyrl_amd.envs.parallel_tictactoe': ParallelTicTacToeBatch}
 
 
 TRAIN_DEFAULTS = {   # config.yaml:9-31
@@ -105,10 +109,13 @@ def train_main(args, device=None, loss_fn=None, model_dir='models', log=print):
     mode = targs.get('generator', 'auto')
     if mode not in ('auto', 'device', 'host'):
         raise ValueError("train_args['generator'] must be auto, device or host, not %r" % (mode,))
-    stock = targs['turn_based_training'] and not targs['observation']
-    if mode == 'device' and (batched is None or not stock):
-        raise ValueError('no batched (device) form of env %r for this training mode' % module)
-    use_device = batched is not None and stock and mode != 'host'
+    # the mover-only ply for the stock mode of an alternating env, the per-player ply (every player's view,
+    # records with a player axis) with observation, for simultaneous envs and for solo training
+    tbt, observe = targs['turn_based_training'], targs['observation']
+    per_player = observe or not tbt or getattr(batched, 'SIMULTANEOUS', False)
+    if mode == 'device' and batched is None:
+        raise ValueError('no batched (device) form of env %r' % module)
+    use_device = batched is not None and mode != 'host'
     seed = int(targs['seed']) + rank
     torch.manual_seed(targs['seed'])            # the same initial weights on every rank
     net = env.net()()
@@ -123,10 +130,16 @@ def train_main(args, device=None, loss_fn=None, model_dir='models', log=print):
     maximum = _per_rank(targs['maximum_episodes'], world)
     rng = torch.Generator(device=device).manual_seed(seed)
     if use_device:
-        gen = DeviceGenerator(batched(games, device), net, gamma=targs['gamma'])
+        gen = DeviceGenerator(batched(games, device), net, gamma=targs['gamma'], observation=observe,
+                              per_player=per_player)
         # binary observation planes live in HBM as uint8 (widened by the gather)
-        replay = DeviceReplay(maximum, batched.MAX_PLIES, batched.OBS_SHAPE, batched.A, batched.P, device,
-                              maximum_episodes=maximum, obs_dtype=torch.uint8)
+        if per_player:
+            replay = PlayerReplay(maximum, batched.MAX_PLIES, batched.OBS_SHAPE, batched.A, batched.P, device,
+                                  maximum_episodes=maximum, obs_dtype=torch.uint8, solo=not tbt,
+                                  mover=tbt and not observe)
+        else:
+            replay = DeviceReplay(maximum, batched.MAX_PLIES, batched.OBS_SHAPE, batched.A, batched.P, device,
+                                  maximum_episodes=maximum, obs_dtype=torch.uint8)
 
         def play():
             ep = gen.generate(generator=rng)

@@ -21,8 +21,18 @@ batcher process rebuilds padded training windows on the CPU (train.py:33-133,
   make_batch layout (train.py:109-133) the learner consumes -- no host copy,
   no pickling.
 
-Scope: turn-based two-player training without opponent observation
-(turn_based_training=True, observation=False), the TicTacToe configuration.
+Training modes.  With turn_based_training=True and observation=False (the
+stock configuration) only the player to move runs inference each ply and the
+episode records one mover per ply.  With ``observation=True`` (every player
+infers every ply, generation.py:35-46) or a simultaneous-move env
+(``SIMULTANEOUS``, e.g. ``ParallelTicTacToeBatch``: every player moves every
+ply, parallel_tictactoe.py:20-24) ``DeviceGenerator`` runs the per-player
+ply instead: one forward over all P x E (player, game) views, per-player
+recurrent state in HBM advanced for the players that inferred, the turn
+players sampled, per-player records with the turn and observation masks;
+``PlayerReplay`` gathers those into make_batch's per-player layout
+(train.py:63-67), one random player per window for solo training
+(turn_based_training=False, train.py:55-56).
 """
 
 import contextlib
@@ -32,7 +42,8 @@ import torch
 
 from .util import map_r, bimap_r
 
-__all__ = ['TicTacToeBatch', 'DeviceGenerator', 'DeviceReplay', 'episodes_to_wire']
+__all__ = ['TicTacToeBatch', 'ParallelTicTacToeBatch', 'DeviceGenerator', 'DeviceReplay', 'PlayerReplay',
+           'episodes_to_wire', 'player_episodes_to_wire', 'reference_uniforms']
 
 
 class TicTacToeBatch:
@@ -102,6 +113,44 @@ class TicTacToeBatch:
         w = self.winner.float()
         return torch.stack([w, -w], dim=1)
 
+    def turns_mask(self):
+        """(E, P) bool: the players to move (turns(), environment.py:107-113): the side to move."""
+        return torch.nn.functional.one_hot(self.turn(), self.P).bool()
+
+
+class ParallelTicTacToeBatch(TicTacToeBatch):
+    """E Parallel Tic-Tac-Toe games (handyrl/envs/parallel_tictactoe.py:13-61): both players choose a move every
+    ply (turns() = both) and one of them, picked uniformly, is played with its own colour.  The reference's turn()
+    returns an exception object, so observation(p) is the non-turn view for both p, and its colour never changes
+    from black: both players see [zeros, white stones, black stones] (tictactoe.py:157-168)."""
+
+    ALTERNATING = False
+    SIMULTANEOUS = True
+
+    def turns_mask(self):
+        return torch.ones(self.E, self.P, dtype=torch.bool, device=self.device)
+
+    def turn(self):
+        return torch.zeros(self.E, dtype=torch.long, device=self.device)
+
+    def observation(self, player):
+        b = self.board
+        planes = torch.stack([torch.zeros_like(b, dtype=torch.bool), b == -1, b == 1], dim=1)
+        return planes.float().view(-1, 3, 3, 3)
+
+    def step_players(self, actions, turns, active, u):
+        """The played player: floor(u * P) of the E uniforms u (random.choice over the action dict's P keys,
+        parallel_tictactoe.py:21); its action with its colour, player 0 black (parallel_tictactoe.py:25-35)."""
+        rows = torch.arange(self.E, device=self.device)
+        sel = torch.clamp((u * self.P).long(), max=self.P - 1)
+        act = torch.where(active, actions[rows, sel], torch.zeros_like(sel))
+        colour = torch.where(sel == 0, 1, -1).to(self.board.dtype)
+        self.board[rows, act] = torch.where(active, colour, self.board[rows, act])
+        sums = self.board.long()[:, self.lines].sum(-1)                   # (E, 8)
+        won = active & (sums == 3 * colour.long().view(-1, 1)).any(-1)
+        self.winner.copy_(torch.where(won, colour, self.winner))
+        self.nmoves.add_(active.int())
+
 
 def _leaves(x):
     """The tensors of a nested list / tuple / dict, in order."""
@@ -115,6 +164,35 @@ def _alloc(spec, lead, device, dtype=torch.float32):
     if isinstance(spec, dict):
         return {k: torch.zeros(*lead, *v, device=device, dtype=dtype) for k, v in spec.items()}
     return torch.zeros(*lead, *spec, device=device, dtype=dtype)
+
+
+def _stack_views(views, batch_first=False):
+    """P views (each a tensor (E, ...) or {name: (E, ...)}) -> (P * E, ...) player-major, or (E, P, ...)."""
+    def stack(xs):
+        return torch.stack(xs, 1) if batch_first else torch.cat(xs, 0)
+    if isinstance(views[0], dict):
+        return {k: stack([v[k] for v in views]) for k in views[0]}
+    return stack(views)
+
+
+def reference_uniforms(seeds, Tm, P, simultaneous=False):
+    """The random-stream values seeded reference games draw (generation.py:53, parallel_tictactoe.py:21): for
+    game k, ``random.seed(seeds[k])`` then per ply each turn player's ``random.choices`` takes one ``random()``
+    (players in order: the mover, ply % P, or every player of a simultaneous env) and a simultaneous env's step
+    one ``random.choice`` over the P players.  Returns u (E, Tm, P) float64 and sel (E, Tm) int64 (None for
+    alternating envs), for ``DeviceGenerator.generate(reference=...)``.  Draws past a game's end are unused."""
+    import random as _random
+    E = len(seeds)
+    u = np.zeros((E, Tm, P), dtype=np.float64)
+    sel = np.zeros((E, Tm), dtype=np.int64) if simultaneous else None
+    for e, seed in enumerate(seeds):
+        r = _random.Random(seed)
+        for t in range(Tm):
+            for p in (range(P) if simultaneous else (t % P,)):
+                u[e, t, p] = r.random()
+            if simultaneous:
+                sel[e, t] = r.choice(list(range(P)))
+    return u, sel
 
 
 def sample_record_torch(st, logits, legal, value, active, player, reward):
@@ -187,20 +265,33 @@ class DeviceGenerator:
     graph replay instead of ≈100 small launches; the discounted-return loop is
     a third graph.  Eager and graph mode run the same ply function on the same
     uniforms (one (Tm, E, A) draw per call), so they give the same episodes.
+
+    ``observation=True`` or a ``SIMULTANEOUS`` env selects the per-player ply
+    (module doc; ``_ply_players``): the episode's records gain a player axis
+    (E, Tm, P, ...) with ``tmask`` / ``omask``; its ply is one graph for every
+    ply.  ``generate(reference=(u, sel))`` samples by the reference's inverse
+    CDF instead of Gumbel-max: u (E, Tm, P) are the ``random()`` values each
+    turn player's ``random.choices`` draws and sel (E, Tm) the simultaneous
+    env's played-player uniforms (``reference_uniforms``), so seeded reference
+    games replay move for move.
     """
 
-    def __init__(self, env_batch, net, gamma=0.8, check_every=16, graph=None):
+    def __init__(self, env_batch, net, gamma=0.8, check_every=16, graph=None, observation=False, per_player=None):
         self.env = env_batch
         self.net = net
         self.gamma = gamma
         self.check_every = check_every
         self.graph = graph
+        self.observation = bool(observation)
+        # per_player=True also for a mover-only alternating game whose batches need per-player records (solo)
+        self.per_player = (self.observation or getattr(env_batch, 'SIMULTANEOUS', False) if per_player is None
+                           else bool(per_player) or self.observation or getattr(env_batch, 'SIMULTANEOUS', False))
         self._st = None
 
     def _use_graph(self):
         dev = torch.device(self.env.device)
         if self.graph is None:
-            return dev.type == 'cuda' and getattr(self.env, 'ALTERNATING', False)
+            return dev.type == 'cuda' and (self.per_player or getattr(self.env, 'ALTERNATING', False))
         return bool(self.graph) and dev.type == 'cuda'
 
     def _state(self):
@@ -224,6 +315,32 @@ class DeviceGenerator:
               't': torch.zeros(1, dtype=torch.long, device=dev),
               'rows': torch.arange(E, device=dev),
               'hidden': None, 'obs_dev': torch.device(dev).type}
+        if self.per_player:
+            # records with a player axis; the uniforms (Tm, E, P, A) for Gumbel-max, (E, Tm, P) / (E, Tm) for the
+            # reference sampler; the state (P, E, ...): the (player, game) rows of one forward are its view
+            st.update(obs=_alloc(env.OBS_SHAPE, (E, Tm, P), dev),
+                      policy=torch.zeros(E, Tm, P, A, device=dev),
+                      amask=torch.full((E, Tm, P, A), 1e32, device=dev),
+                      action=torch.zeros(E, Tm, P, dtype=torch.long, device=dev),
+                      value=torch.zeros(E, Tm, P, device=dev),
+                      tmask=torch.zeros(E, Tm, P, dtype=torch.bool, device=dev),
+                      omask=torch.zeros(E, Tm, P, dtype=torch.bool, device=dev),
+                      U=torch.empty(Tm, E, P, A, device=dev),
+                      Uref=torch.zeros(E, Tm, P, dtype=torch.float64, device=dev),
+                      Usel=torch.empty(Tm, E, device=dev),
+                      reference=torch.zeros(1, dtype=torch.bool, device=dev), rank=False,
+                      players=torch.arange(P, device=dev).view(P, 1).expand(P, E).contiguous(), pmajor=True)
+            st['flat_state'] = False
+            if (self.observation and hasattr(self.net, 'inference_hidden') and hasattr(self.net, 'inference_session')
+                    and torch.device(dev).type == 'cuda'):
+                # every player infers every ply: the net's own stacked layout over the P*E rows, advanced in place
+                # inside its inference session (GeisterNet), leaves (P*E, ...) player-major
+                st['hidden'] = map_r(self.net.inference_hidden(P * E, 1, dev), lambda h: h[0])
+                st['flat_state'] = True
+            elif hasattr(self.net, 'init_hidden'):
+                st['hidden'] = map_r(self.net.init_hidden([P, E]), lambda h: h.to(dev).contiguous())
+            self._st = st
+            return st
         st['pmajor'] = False   # state leaves (E, P, ...) as init_hidden gives them
         if hasattr(self.net, 'inference_hidden') and torch.device(dev).type == 'cuda':
             st['hidden'] = self.net.inference_hidden(E, P, dev)   # leaves (P, E, ...), the net's own layout
@@ -236,7 +353,8 @@ class DeviceGenerator:
     def _reset(self, st, generator, draw=True):
         self.env.reset()
         map_r(st['obs'], lambda b: b.zero_())
-        for k in ('policy', 'action', 'value', 'turn', 'reward', 'ret'):
+        for k in ('policy', 'action', 'value', 'turn', 'reward', 'ret') + (('tmask', 'omask') if self.per_player
+                                                                           else ()):
             st[k].zero_()
         st['amask'].fill_(1e32)
         if st['hidden'] is not None:
@@ -244,11 +362,95 @@ class DeviceGenerator:
         if draw:
             torch.rand(st['U'].shape, out=st['U'], generator=generator, device=st['U'].device)
             st['U'].clamp_(1e-20, 1.0)
+            if self.per_player:
+                torch.rand(st['Usel'].shape, out=st['Usel'], generator=generator, device=st['Usel'].device)
         st['t'].zero_()
+
+    def _ply_players(self, st):
+        """The per-player ply (generation.py:35-62 with observation, or every player a turn player): every
+        (player, game) view in one forward -- the players that infer are the turn players, or all with
+        ``observation`` --, their values / observations recorded and their state advanced, the turn players'
+        policies masked and sampled, then the env steps on the turn players' actions."""
+        env, E, P, A = self.env, self.env.E, self.env.P, self.env.A
+        t = st['t']
+        hidden = st['hidden']
+        # a snapshot: an env's active() may be state its step updates in place (GeisterBatch.live), and the
+        # reward after the step is recorded for the games that were live before it
+        active = (env.active() if hasattr(env, 'active') else ~env.terminal()).clone()
+        live = active.view(E, 1)
+        turns = (env.turns_mask() if hasattr(env, 'turns_mask') else
+                 torch.nn.functional.one_hot(env.turn().long(), P).bool()) & live          # (E, P)
+        infer = live.expand(E, P) if self.observation else turns
+        views = [env.observation(st['players'][p]) for p in range(P)]
+        o = _stack_views(views)                                                           # (P * E, ...)
+        h_in = (None if hidden is None else hidden if st['flat_state'] else
+                map_r(hidden, lambda h: h.view(P * E, *h.shape[2:])))
+        out = self.net(o, h_in)
+        logits = out['policy'].float().view(P, E, A).transpose(0, 1)                   # (E, P, A)
+        value = out['value'].float().reshape(P, E).t()                                  # (E, P)
+        legal = (env.legal_players() if hasattr(env, 'legal_players') else
+                 env.legal().view(E, 1, A).expand(E, P, A))
+        m = torch.where(legal, 0.0, 1e32)                                                 # generation.py:50-51
+        p = logits - m
+        # Gumbel-max over the legal logits (softmax sampling), or the reference's inverse CDF of random.choices:
+        # bisect(cumsum(softmax(p[legal])), u * total), fp64 here (the reference's fp32 sums decide otherwise only
+        # when u falls within their rounding of a boundary)
+        g = st['U'].index_select(0, t).view(E, P, A)
+        a_gumbel = torch.argmax(p - torch.log(-torch.log(g)), dim=-1)
+        # the reference's legal_actions order: ascending labels, or the env's own (legal_rank: Geister's pieces)
+        base = (env.legal_rank().view(E, 1, A) if st['rank'] else
+                torch.arange(A, device=p.device).view(1, 1, A)).expand(E, P, A)
+        order = torch.argsort(torch.where(legal, base, 1 << 30), dim=-1, stable=True)    # legal ones first
+        lo = torch.gather(legal, -1, order)
+        pd = torch.where(lo, torch.gather(p, -1, order).double(), float('-inf'))
+        w = torch.exp(pd - pd.max(-1, keepdim=True).values)
+        cum = torch.cumsum(w / w.sum(-1, keepdim=True), -1)
+        x = st['Uref'].index_select(1, t).view(E, P, 1) * cum[..., -1:]
+        k = ((cum <= x) & lo).sum(-1, keepdim=True)                                      # bisect_right over legal
+        k = torch.minimum(k, lo.sum(-1, keepdim=True) - 1).clamp(min=0)
+        a_ref = torch.gather(order, -1, k).squeeze(-1)                                   # legal entries lead
+        a = torch.where(st['reference'], a_ref, a_gumbel)
+
+        def record(buf, x, mask, fill=0):
+            keep = mask.view(*mask.shape, *([1] * (x.dim() - mask.dim())))
+            buf.index_copy_(1, t, torch.where(keep, x, fill).to(buf.dtype).unsqueeze(1))
+        views_e = _stack_views(views, batch_first=True)                                   # (E, P, ...)
+        bimap_r(st['obs'], views_e, lambda b, v: record(b, v, infer))
+        record(st['value'], value, infer)
+        record(st['policy'], p, turns)
+        record(st['amask'], m, turns, 1e32)
+        record(st['action'], a, turns)
+        record(st['tmask'], turns, turns)
+        record(st['omask'], infer, infer)
+        if hidden is not None and st['flat_state']:
+            # the session advanced every (player, game) row in place -- all of them inferred (observation); a
+            # finished game's rows moved too, but nothing reads them again.  Without the in-place form: a copy
+            dst, src = _leaves(hidden), _leaves(out['hidden'])
+            if not all(d.data_ptr() == x.data_ptr() and d.stride() == x.stride() for d, x in zip(dst, src)):
+                for d, x in zip(dst, src):
+                    d.copy_(x)
+        elif hidden is not None:                                   # only the players that inferred advance
+            keep = infer.t().contiguous()                          # (P, E)
+
+            def advance(h, nh):
+                nh = nh.view(h.shape)
+                h.copy_(torch.where(keep.view(P, E, *([1] * (h.dim() - 2))), nh, h))
+            bimap_r(hidden, out['hidden'], advance)
+        if getattr(env, 'SIMULTANEOUS', False):
+            env.step_players(a, turns, active, st['Usel'].index_select(0, t).view(E))
+        else:
+            rows = torch.arange(E, device=a.device)
+            env.step(a[rows, env.turn().long()], active)
+        if hasattr(env, 'reward'):
+            r = env.reward().to(st['reward'].dtype)
+            st['reward'].index_copy_(1, t, torch.where(live, r, 0).unsqueeze(1))
+        t.add_(1)
 
     def _ply(self, st, mover):
         """One ply for every game at ply index st['t'] (a device scalar, advanced here); ``mover``: the
         player index every live game moves with (ALTERNATING envs), or None."""
+        if self.per_player:
+            return self._ply_players(st)
         env, E = self.env, self.env.E
         t = st['t']
         hidden = st['hidden']
@@ -339,22 +541,40 @@ class DeviceGenerator:
         self._reset(st, None, draw=False)   # the call's uniforms stay as drawn
 
     @torch.no_grad()
-    def generate(self, generator=None):
-        alternating = getattr(self.env, 'ALTERNATING', False)
+    def generate(self, generator=None, reference=None):
+        """One batch of E games; ``reference`` (per-player mode): (u, sel) from ``reference_uniforms``."""
+        alternating = getattr(self.env, 'ALTERNATING', False) and not self.per_player
         st = self._state()
+        if reference is not None and not self.per_player:
+            raise ValueError('the reference sampler is the per-player ply\'s (observation or simultaneous envs)')
         was_training = self.net.training
         self.net.eval()
-        # per-call weight preparation (GeisterNet); its own stacked state is advanced in place by the net
-        session = getattr(self.net, 'inference_session', None)
+        # per-call weight preparation (GeisterNet); its own stacked state is advanced in place by the net (the
+        # per-player ply too when every player infers; otherwise it runs the net's ordinary forward)
+        session = (getattr(self.net, 'inference_session', None)
+                   if (not self.per_player or st.get('flat_state')) else None)
         with session(inplace_state=st['pmajor']) if session is not None else contextlib.nullcontext():
-            out = self._generate(st, generator, alternating)
+            out = self._generate(st, generator, alternating, reference)
         self.net.train(was_training)
         return out
 
-    def _generate(self, st, generator, alternating):
+    def _generate(self, st, generator, alternating, reference=None):
         env = self.env
         Tm, P = env.MAX_PLIES, env.P
+        if self.per_player:
+            # an env whose legal_actions order is not ascending keeps what gives it (Geister: piece indices)
+            st['rank'] = reference is not None and hasattr(env, 'legal_rank')
+            if st['rank'] and getattr(env, 'pidx', None) is None:
+                env.piece_order(True)
+                st['graphs'] = None   # the ply changes: recapture
         self._reset(st, generator)
+        if self.per_player:
+            st['reference'].fill_(reference is not None)
+            if reference is not None:
+                u, sel = reference
+                st['Uref'].copy_(torch.as_tensor(u, dtype=torch.float64))
+                if sel is not None:   # the played player p is floor(Usel * P): the middle of its interval
+                    st['Usel'].copy_(((torch.as_tensor(sel, dtype=torch.float64) + 0.5) / P).t().float())
         graphs = None
         if self._use_graph():
             if st['graphs'] is None:
@@ -375,7 +595,8 @@ class DeviceGenerator:
                 self._returns(st)
         out = {'observation': map_r(st['obs'], lambda b: b.clone())}
         for key, k in (('policy', 'policy'), ('action_mask', 'amask'), ('action', 'action'), ('value', 'value'),
-                       ('turn', 'turn'), ('return', 'ret')):
+                       ('turn', 'turn'), ('return', 'ret')) + ((('tmask', 'tmask'), ('omask', 'omask'))
+                                                            if self.per_player else ()):
             out[key] = st[k].clone()
         out.update(length=env.plies().long(), outcome=env.outcome(), reward=st['reward'].float())
         return out
@@ -480,6 +701,139 @@ class DeviceReplay:
     def sample(self, B, T, generator=None):
         slots, start = self.sample_windows(B, T, generator)
         return self.gather(slots, start, T)
+
+
+class PlayerReplay(DeviceReplay):
+    """DeviceReplay for the per-player episodes (``DeviceGenerator`` with ``observation`` or a simultaneous env):
+    records (N, Tm, P, ...) with the turn and observation masks; ``gather`` forms make_batch's per-player layout
+    (train.py:63-67, 76-83): every player, or one player per window (``players``, solo training, train.py:55-56),
+    zeros / 1e32 / the outcome where a player did not infer or move and past the episode's end.  ``solo``
+    (turn_based_training=False) samples one player per window; ``mover`` (turn_based_training without
+    observation, e.g. a simultaneous env under the stock configuration) takes observation, policy, action and
+    action mask from each ply's first turn player and the rest per player, as make_batch's first branch does
+    (train.py:62-66)."""
+
+    def __init__(self, capacity, max_plies, obs_shape, A, P, device, maximum_episodes=None,
+                 obs_dtype=torch.float32, solo=False, mover=False):
+        self.solo, self.mover = bool(solo), bool(mover)
+        self.N, self.Tm, self.P, self.device = capacity, max_plies, P, device
+        self.maximum_episodes = maximum_episodes or capacity
+        f = dict(device=device)
+        self.obs = _alloc(obs_shape, (capacity, max_plies, P), device, obs_dtype)
+        self.policy = torch.zeros(capacity, max_plies, P, A, **f)
+        self.amask = torch.full((capacity, max_plies, P, A), 1e32, **f)
+        self.action = torch.zeros(capacity, max_plies, P, dtype=torch.long, **f)
+        self.value = torch.zeros(capacity, max_plies, P, **f)
+        self.tmask = torch.zeros(capacity, max_plies, P, dtype=torch.bool, **f)
+        self.omask = torch.zeros(capacity, max_plies, P, dtype=torch.bool, **f)
+        self.reward = torch.zeros(capacity, max_plies, P, **f)
+        self.ret = torch.zeros(capacity, max_plies, P, **f)
+        self.length = torch.ones(capacity, dtype=torch.long, **f)
+        self.outcome = torch.zeros(capacity, P, **f)
+        self.ptr = 0
+        self.count = 0
+
+    def add(self, ep):
+        E = ep['length'].shape[0]
+        slots = (self.ptr + torch.arange(E, device=self.device)) % self.N
+        bimap_r(self.obs, ep['observation'], lambda dst, src: dst.index_copy_(0, slots, src.to(dst.dtype)))
+        for dst, key in ((self.policy, 'policy'), (self.amask, 'action_mask'), (self.action, 'action'),
+                         (self.value, 'value'), (self.tmask, 'tmask'), (self.omask, 'omask'),
+                         (self.reward, 'reward'), (self.ret, 'return'), (self.length, 'length'),
+                         (self.outcome, 'outcome')):
+            dst.index_copy_(0, slots, ep[key].to(dst.dtype))
+        self.ptr = (self.ptr + E) % self.N
+        self.count = min(self.count + E, self.N)
+
+    def gather(self, slots, start, T, players=None, mover=None):
+        """make_batch of the windows [start, start+T) of episodes ``slots`` over every player, or over one
+        player per window (``players`` (B,) long); ``mover`` (default: the replay's): observation, policy, action
+        and action mask of each ply's first turn player."""
+        mover = self.mover if mover is None else mover
+        B, dev = slots.shape[0], self.device
+        t = start.view(-1, 1) + torch.arange(T, device=dev).view(1, -1)      # (B, T)
+        length = self.length[slots].view(-1, 1)
+        valid = t < length
+        tc = torch.minimum(t, length - 1)
+        e = slots.view(-1, 1)
+        pidx = (torch.arange(self.P, device=dev).view(1, 1, -1).expand(B, T, self.P) if players is None
+                else players.view(B, 1, 1).expand(B, T, 1))
+        # make_batch's first branch: m['turn'][0], the lowest-index turn player of the ply
+        midx = torch.argmax(self.tmask[e, tc].long(), dim=-1, keepdim=True) if mover else pidx
+
+        def take(x, ix=pidx):   # (N, Tm, P, ...) -> (B, T, Pn, ...)
+            y = x[e, tc]
+            Pn = ix.shape[2]
+            idx = ix.reshape(B, T, Pn, *([1] * (y.dim() - 3))).expand(B, T, Pn, *y.shape[3:])
+            return torch.gather(y, 2, idx)
+        Pn = pidx.shape[2]
+        vf = valid.float()
+        vp = vf.view(B, T, 1)
+        obs = map_r(self.obs, lambda o: take(o, midx).float() * vp.view(B, T, 1, *([1] * (o.dim() - 3))))
+        pol = take(self.policy, midx) * vp.unsqueeze(-1)
+        amask = torch.where(valid.view(B, T, 1, 1), take(self.amask, midx), torch.full_like(pol, 1e32))
+        act = take(self.action, midx) * valid.long().view(B, T, 1)
+        oc = torch.gather(self.outcome[slots], 1, pidx[:, 0]).view(B, 1, Pn, 1)
+        val = torch.where(valid.view(B, T, 1, 1), take(self.value).unsqueeze(-1), oc.expand(B, T, Pn, 1))
+        rew = take(self.reward) * vp
+        ret = take(self.ret) * vp
+        tm = take(self.tmask).float() * vp
+        om = take(self.omask).float() * vp
+        progress = torch.where(valid, t.float() / length.float(), torch.ones_like(vf))
+        return {
+            'observation': obs,
+            'policy': pol.contiguous(),
+            'value': val.contiguous(),
+            'action': act.unsqueeze(-1).contiguous(),
+            'outcome': oc.contiguous(),
+            'reward': rew.unsqueeze(-1).contiguous(),
+            'return': ret.unsqueeze(-1).contiguous(),
+            'episode_mask': vf.view(B, T, 1, 1).contiguous(),
+            'turn_mask': tm.unsqueeze(-1).contiguous(),
+            'observation_mask': om.unsqueeze(-1).contiguous(),
+            'action_mask': amask.contiguous(),
+            'progress': progress.unsqueeze(-1).contiguous(),
+        }
+
+    def sample(self, B, T, generator=None):
+        """B windows; solo replays: one uniformly chosen player per window (train.py:55-56)."""
+        slots, start = self.sample_windows(B, T, generator)
+        players = torch.randint(self.P, (B,), device=self.device, generator=generator) if self.solo else None
+        return self.gather(slots, start, T, players)
+
+
+def player_episodes_to_wire(ep, compress_steps=4):
+    """Per-player device episodes -> the reference episode format (generation.py:29-86): a player's observation
+    and value where it inferred, its policy / action mask / action where it moved, None elsewhere."""
+    import bz2
+    import pickle
+    cpu = map_r(ep, lambda v: v.cpu().numpy())
+    P = cpu['tmask'].shape[2]
+    has_reward = bool((cpu['reward'] != 0).any())
+    out = []
+    for e in range(cpu['length'].shape[0]):
+        L = int(cpu['length'][e])
+        moments = []
+        for t in range(L):
+            m = {k: {p: None for p in range(P)} for k in ('observation', 'policy', 'action_mask', 'action',
+                                                          'value', 'reward', 'return')}
+            for p in range(P):
+                if cpu['omask'][e, t, p]:
+                    m['observation'][p] = map_r(cpu['observation'], lambda o: o[e, t, p].astype(np.float32))
+                    m['value'][p] = np.array([cpu['value'][e, t, p]], dtype=np.float32)
+                if cpu['tmask'][e, t, p]:
+                    m['policy'][p] = cpu['policy'][e, t, p].astype(np.float32)
+                    m['action_mask'][p] = cpu['action_mask'][e, t, p].astype(np.float32)
+                    m['action'][p] = int(cpu['action'][e, t, p])
+                if has_reward:
+                    m['reward'][p] = float(cpu['reward'][e, t, p])
+                m['return'][p] = float(cpu['return'][e, t, p])
+            m['turn'] = [p for p in range(P) if cpu['tmask'][e, t, p]]
+            moments.append(m)
+        out.append({'args': {}, 'steps': L, 'outcome': {p: float(cpu['outcome'][e, p]) for p in range(P)},
+                    'moment': [bz2.compress(pickle.dumps(moments[i:i + compress_steps]))
+                               for i in range(0, L, compress_steps)]})
+    return out
 
 
 def episodes_to_wire(ep, compress_steps=4):

@@ -65,7 +65,7 @@ def test_train_main_host_generator_cpu(tmp_path, env, obs, tbt):
     host generator plays them (generation.py semantics) into the moment replay; the learner trains on the
     make_batch layout of the mode (oracle loss on the CPU)."""
     args = _small(env)
-    args['train_args'].update(observation=obs, turn_based_training=tbt, epochs=2)
+    args['train_args'].update(observation=obs, turn_based_training=tbt, epochs=2, generator='host')
     logs = []
     model = train_main(args, device=torch.device('cpu'), loss_fn=_oracle_loss, model_dir=str(tmp_path),
                        log=logs.append)
@@ -73,6 +73,34 @@ def test_train_main_host_generator_cpu(tmp_path, env, obs, tbt):
     saved = torch.load(os.path.join(tmp_path, '2.pth'), weights_only=True)
     assert set(saved) == set(model.state_dict())
     for v in saved.values():
+        assert torch.isfinite(v.float()).all()
+
+
+@pytest.mark.parametrize('env,obs,tbt', [('ParallelTicTacToe', False, True), ('ParallelTicTacToe', True, True),
+                                          ('TicTacToe', True, True), ('TicTacToe', False, False),
+                                          ('Geister', True, True)])
+def test_train_main_device_player_modes_cpu(tmp_path, env, obs, tbt):
+    """Batched envs with observation, solo training or simultaneous moves are played by the device generator's
+    per-player ply into the PlayerReplay (no host env in the loop); two epochs train on its batches."""
+    import handyrl_amd.main as hm
+    args = _small(env)
+    args['train_args'].update(observation=obs, turn_based_training=tbt, epochs=2)
+    if env == 'Geister':
+        args['train_args'].update(update_episodes=4, minimum_episodes=4, batch_size=2, forward_steps=4, epochs=1)
+    built = []
+    real = hm.PlayerReplay
+
+    def spy(*a, **k):
+        built.append(k)
+        return real(*a, **k)
+    hm.PlayerReplay = spy
+    try:
+        model = train_main(args, device=torch.device('cpu'), loss_fn=_oracle_loss, model_dir=str(tmp_path),
+                           log=lambda *_: None)
+    finally:
+        hm.PlayerReplay = real
+    assert built and built[0]['solo'] == (not tbt) and built[0]['mover'] == (tbt and not obs)
+    for v in model.state_dict().values():
         assert torch.isfinite(v.float()).all()
 
 
@@ -147,7 +175,22 @@ def test_train_main_two_ranks_agree_on_steps(tmp_path):
 def test_train_main_host_generator_gpu(tmp_path, cuda, env, obs):
     """The host generator path on the GPU: batched HIP / torch inference per ply, HIP learner step."""
     args = _small(env)
-    args['train_args'].update(observation=obs)
+    args['train_args'].update(observation=obs, generator='host')
+    if env == 'Geister':
+        args['train_args'].update(update_episodes=8, minimum_episodes=8, batch_size=4, forward_steps=8, epochs=1)
+    model = train_main(args, device=cuda, model_dir=str(tmp_path), log=lambda *_: None)
+    assert os.path.exists(tmp_path / ('%d.pth' % args['train_args']['epochs']))
+    for v in model.state_dict().values():
+        assert torch.isfinite(v.float()).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('env,obs,tbt', [('ParallelTicTacToe', False, True), ('TicTacToe', True, True),
+                                          ('Geister', True, True)])
+def test_train_main_device_player_modes_gpu(tmp_path, cuda, env, obs, tbt):
+    """The per-player device generator (captured ply graph) and PlayerReplay feeding the HIP learner step."""
+    args = _small(env)
+    args['train_args'].update(observation=obs, turn_based_training=tbt)
     if env == 'Geister':
         args['train_args'].update(update_episodes=8, minimum_episodes=8, batch_size=4, forward_steps=8, epochs=1)
     model = train_main(args, device=cuda, model_dir=str(tmp_path), log=lambda *_: None)
