@@ -328,7 +328,7 @@ class DeviceGenerator:
                       U=torch.empty(Tm, E, P, A, device=dev),
                       Uref=torch.zeros(E, Tm, P, dtype=torch.float64, device=dev),
                       Usel=torch.empty(Tm, E, device=dev),
-                      reference=torch.zeros(1, dtype=torch.bool, device=dev), rank=False,
+                      ref_mode=False, rank=False,
                       players=torch.arange(P, device=dev).view(P, 1).expand(P, E).contiguous(), pmajor=True)
             st['flat_state'] = False
             if (self.observation and hasattr(self.net, 'inference_hidden') and hasattr(self.net, 'inference_session')
@@ -395,21 +395,22 @@ class DeviceGenerator:
         # Gumbel-max over the legal logits (softmax sampling), or the reference's inverse CDF of random.choices:
         # bisect(cumsum(softmax(p[legal])), u * total), fp64 here (the reference's fp32 sums decide otherwise only
         # when u falls within their rounding of a boundary)
-        g = st['U'].index_select(0, t).view(E, P, A)
-        a_gumbel = torch.argmax(p - torch.log(-torch.log(g)), dim=-1)
-        # the reference's legal_actions order: ascending labels, or the env's own (legal_rank: Geister's pieces)
-        base = (env.legal_rank().view(E, 1, A) if st['rank'] else
-                torch.arange(A, device=p.device).view(1, 1, A)).expand(E, P, A)
-        order = torch.argsort(torch.where(legal, base, 1 << 30), dim=-1, stable=True)    # legal ones first
-        lo = torch.gather(legal, -1, order)
-        pd = torch.where(lo, torch.gather(p, -1, order).double(), float('-inf'))
-        w = torch.exp(pd - pd.max(-1, keepdim=True).values)
-        cum = torch.cumsum(w / w.sum(-1, keepdim=True), -1)
-        x = st['Uref'].index_select(1, t).view(E, P, 1) * cum[..., -1:]
-        k = ((cum <= x) & lo).sum(-1, keepdim=True)                                      # bisect_right over legal
-        k = torch.minimum(k, lo.sum(-1, keepdim=True) - 1).clamp(min=0)
-        a_ref = torch.gather(order, -1, k).squeeze(-1)                                   # legal entries lead
-        a = torch.where(st['reference'], a_ref, a_gumbel)
+        if not st['ref_mode']:
+            g = st['U'].index_select(0, t).view(E, P, A)
+            a = torch.argmax(p - torch.log(-torch.log(g)), dim=-1)
+        else:
+            # the reference's legal_actions order: ascending labels, or the env's own (legal_rank: Geister's pieces)
+            base = (env.legal_rank().view(E, 1, A) if st['rank'] else
+                    torch.arange(A, device=p.device).view(1, 1, A)).expand(E, P, A)
+            order = torch.argsort(torch.where(legal, base, 1 << 30), dim=-1, stable=True)    # legal ones first
+            lo = torch.gather(legal, -1, order)
+            pd = torch.where(lo, torch.gather(p, -1, order).double(), float('-inf'))
+            w = torch.exp(pd - pd.max(-1, keepdim=True).values)
+            cum = torch.cumsum(w / w.sum(-1, keepdim=True), -1)
+            x = st['Uref'].index_select(1, t).view(E, P, 1) * cum[..., -1:]
+            k = ((cum <= x) & lo).sum(-1, keepdim=True)                                  # bisect_right over legal
+            k = torch.minimum(k, lo.sum(-1, keepdim=True) - 1).clamp(min=0)
+            a = torch.gather(order, -1, k).squeeze(-1)                                   # legal entries lead
 
         def record(buf, x, mask, fill=0):
             keep = mask.view(*mask.shape, *([1] * (x.dim() - mask.dim())))
@@ -562,14 +563,17 @@ class DeviceGenerator:
         env = self.env
         Tm, P = env.MAX_PLIES, env.P
         if self.per_player:
-            # an env whose legal_actions order is not ascending keeps what gives it (Geister: piece indices)
-            st['rank'] = reference is not None and hasattr(env, 'legal_rank')
+            # the sampler is part of the captured ply: a change of sampler recaptures it; an env whose
+            # legal_actions order is not ascending keeps what gives it (Geister: piece indices)
+            ref_mode = reference is not None
+            if ref_mode != st['ref_mode']:
+                st['ref_mode'], st['graphs'] = ref_mode, None
+            st['rank'] = ref_mode and hasattr(env, 'legal_rank')
             if st['rank'] and getattr(env, 'pidx', None) is None:
                 env.piece_order(True)
-                st['graphs'] = None   # the ply changes: recapture
+                st['graphs'] = None
         self._reset(st, generator)
         if self.per_player:
-            st['reference'].fill_(reference is not None)
             if reference is not None:
                 u, sel = reference
                 st['Uref'].copy_(torch.as_tensor(u, dtype=torch.float64))
