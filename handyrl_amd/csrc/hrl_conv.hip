@@ -1874,6 +1874,13 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
 // there; every output row depends on its own input row only, its store is dropped and its statistics masked.
 namespace fw3 {
 
+// diagnostic variants (FW3_VARIANT; the product is 0): bit 1 = the y stores by lane 0 only (same instruction count,
+// so the counted vmcnt waits stay right; ~no write traffic), bit 2 = no MFMAs
+#ifndef FW3_VARIANT
+#define FW3_VARIANT 0
+#endif
+constexpr int kVariant = FW3_VARIANT;
+
 constexpr int kSlots = 5;                                   // raw-x ring depth
 constexpr int kRawBytes = kTile * kRow * 4;                 // one tile of x (18,432 B, rows contiguous)
 constexpr int kPieces = kRawBytes / 1024;                   // 18 LDS-DMA wave-instructions per tile
@@ -2061,7 +2068,7 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         for (int s = 0; s < kNq; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int p = 0; p < kCells; ++p) {
-            if (!g_uses_p<G>(p)) continue;
+            if (!g_uses_p<G>(p) || (kVariant & 2)) continue;
             uint32_t A[3][4];
 #pragma unroll
             for (int part = 0; part < 3; ++part) {
@@ -2116,6 +2123,9 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
         for (int rr = 0; rr < 4; ++rr) {
             const int row = (lane >> 4) * 4 + rr;
             const int off = (row * kRow + co * kCells + C::kQ[0]) * 4;
+            if constexpr (kVariant & 1) {
+                if (lane != 0) continue;
+            }
             if constexpr (kNq == 3) {
                 u32x3 v;
                 v.x = __float_as_uint(acc[0][rr]);
