@@ -46,9 +46,10 @@ from handyrl_amd.synthetic import tictactoe_batch, default_args  # noqa: E402
 from handyrl_amd.trainer import LearnerStep            # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-SCAN_PMC = 'r03s4_scan_pmc.json'   # PMC passes over the scan kernel the tree ships (unchanged since round 3)
-BLOCK_PMC = 'r04_block_pmc.json'   # the chain block backward (tools/block_pmc.py)
-FWD_PMC = 'r04_fwd_pmc.json'       # the ring forward conv, fwd form 2 (tools/conv_pmc.py fwd 2)
+# PMC passes on the final round-6 tree (tools/gpu_r6i.sh: rocprofv3 FETCH_SIZE / WRITE_SIZE, gfx950-corrected)
+SCAN_PMC = 'r06_scan_pmc.json'     # the scan kernel (tools/scan_pmc.py, tools/scan_pmc_json.py)
+BLOCK_PMC = 'r06_block_pmc.json'   # the chain block backward, form 1 (tools/conv_pmc.py bwd 1, tools/pmc_bytes.py)
+FWD_PMC = 'r06_fwd_pmc.json'       # the ring forward conv, fwd form 2 (tools/conv_pmc.py fwd 2, tools/pmc_bytes.py)
 
 
 def scan_bytes_per_launch(B, T, P=2, Pp=1, rewards=False):
@@ -719,7 +720,7 @@ def main():
             'frac': round(blk_gbs / HBM_PEAK_GBS, 4),
             'traffic': block_traffic(),
             'traffic_source': 'profiles/%s (rocprofv3 FETCH_SIZE/WRITE_SIZE passes over '
-                              'tools/block_bench.py, gfx950-corrected)' % BLOCK_PMC,
+                              'tools/conv_pmc.py bwd 1, gfx950-corrected)' % BLOCK_PMC,
             'bytes_per_launch': blk_bytes,
             'us_per_launch': round(us_blk, 2),
             'launches_timed': n_blk,
