@@ -103,6 +103,15 @@ SIGNATURES = {
                                                   _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, ctypes.c_int, _f32p,
                                                   _f32p, _f32p, ctypes.c_void_p, ctypes.c_void_p, _i64,
                                                   ctypes.c_void_p]),
+    'hrl_conv3x3_forward_bnfold': (ctypes.c_int, [_f32p, _i64, ctypes.c_void_p, _i64, _f32p, _f32p, _f32p, _f32p,
+                                                  ctypes.c_double, ctypes.c_double, _f32p, _f32p, _f32p, _f32p,
+                                                  _f32p, _f32p, ctypes.c_void_p, ctypes.c_void_p, _i64,
+                                                  ctypes.c_void_p]),
+    'hrl_conv3x3_block_backward_bnfold': (ctypes.c_int, [_f32p, _f32p, _i64, _f32p, _f32p, _f32p, _f32p,
+                                                         ctypes.c_void_p, _i64, _f32p, _f32p, _f32p, _f32p,
+                                                         _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, ctypes.c_int,
+                                                         _f32p, _f32p, _f32p, ctypes.c_void_p, ctypes.c_void_p,
+                                                         _i64, ctypes.c_void_p]),
     'hrl_conv3x3_wgrad_ex': (ctypes.c_int, [_f32p, _f32p, _f32p, _f32p, _i64, _f32p, ctypes.c_void_p, _i64,
                                             ctypes.c_void_p]),
     'hrl_hidden_gather': (ctypes.c_int, [ctypes.c_void_p, _f32p, _i64, _i64, ctypes.c_int, ctypes.c_void_p,
@@ -234,7 +243,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
 }
 
-ABI_VERSION = 25
+ABI_VERSION = 26
 
 _lib = None
 

@@ -683,7 +683,105 @@ struct BlockBwdArgs {
     int64_t M;
     unsigned *tickets;                                           // block form 2: per-CU arrival tickets
     int stagger;                                                 // block form 2: s_sleep(32)s of the later arrival
+    // a BatchNorm finalize folded into the prologue (fold_part nullptr: none; bnfold below): mode 0 = the input BN's
+    // forward statistics -> its alpha / beta (the conv's prologue), mode 1 = BN_i's backward sums -> k / mean(dy)
+    const double *fold_part;                                     // partial rows [fold_nblocks][32][2]
+    int fold_nblocks, fold_mode;
+    double fold_count, fold_eps;
+    float fold_momentum;
+    const float *fold_w, *fold_b;                                // mode 0: the BN's weight / bias
+    float *fold_rm, *fold_rv;                                    // mode 0: running statistics (workgroup 0)
+    float *fold_o0, *fold_o1, *fold_o2, *fold_o3;                // mode 0: mean invstd alpha beta; 1: dw db k gm
 };
+
+// ------------------------------------------------------------------ BatchNorm finalize in a consumer's prologue
+// hrl_bn_finalize_stats / _backward (bn_finalize_kernel, one group) as the first step of the kernel that consumes
+// its coefficients, instead of a launch of its own: every 512-thread workgroup folds the fold_nblocks partial rows
+// of all 32 channels in bn_finalize_kernel's exact order -- thread i of its 256 sums rows i, i + 256 (0.0 first),
+// then the fixed tree (i, i + 128), (i, i + 64), (i, i + 32) ... (i, i + 1) -- and computes the channel's
+// coefficients with its float operations; workgroup 0 writes the outputs the separate launch wrote (the running
+// statistics advance once).  Bit-identical to the two launches (tests/test_bn_gpu.py).  Here thread (c, k, j)
+// holds leaves j + 8 m (m < 32): the levels 128 .. 8 are its register tree, 4, 2, 1 a shuffle over its 8 lanes.
+namespace bnfold {
+
+constexpr int kThreadsFold = 512;
+
+__device__ __forceinline__ void fold(const BlockBwdArgs &a, unsigned char *lds, float &c0, float &c1) {
+    double *sums = reinterpret_cast<double *>(lds);                 // [32][2]
+    float *coef = reinterpret_cast<float *>(lds + 64 * 8);          // [2][32]
+    const int tid = threadIdx.x;
+    const int ck = tid >> 3, j = tid & 7, c = ck >> 1, k = ck & 1;
+    const int nb = a.fold_nblocks;
+    const double *pc = a.fold_part + (c * 2 + k);
+    double v[32];
+#pragma unroll
+    for (int m = 0; m < 32; ++m) {
+        const int i = j + 8 * m;
+        const double lo = i < nb ? pc[(int64_t)i * kC * 2] : 0.0;
+        const double hi = i + 256 < nb ? pc[(int64_t)(i + 256) * kC * 2] : 0.0;
+        v[m] = (0.0 + lo) + hi;      // bn_finalize_kernel's s = 0.0; s += part[i]; s += part[i + 256] (+0.0 exact)
+    }
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1)
+#pragma unroll
+        for (int m = 0; m < w; ++m) v[m] += v[m + w];
+    double e = v[0];
+    e += __shfl_down(e, 4, 8);
+    e += __shfl_down(e, 2, 8);
+    e += __shfl_down(e, 1, 8);
+    if (j == 0) sums[ck] = e;
+    __syncthreads();
+    if (tid < kC) {
+        const int ch = tid;
+        const double S0 = sums[ch * 2], S1 = sums[ch * 2 + 1];
+        const double M = a.fold_count;
+        const bool out = blockIdx.x == 0;
+        if (a.fold_mode == 0) {   // bn_finalize_kernel mode 0's float operations
+            const float w = a.fold_w ? a.fold_w[ch] : 1.0f;
+            const double mean = S0 / M;
+            double var = S1 / M - mean * mean;
+            if (var < 0.0) var = 0.0;
+            const float meanf = (float)mean;
+            const float invstd = (float)(1.0 / sqrt(var + a.fold_eps));
+            const float alpha = invstd * w;
+            const float beta = (a.fold_b ? a.fold_b[ch] : 0.0f) - meanf * alpha;
+            coef[ch] = alpha;
+            coef[kC + ch] = beta;
+            if (out) {
+                const float momentum = a.fold_momentum;
+                a.fold_o0[ch] = meanf;
+                a.fold_o1[ch] = invstd;
+                a.fold_o2[ch] = alpha;
+                a.fold_o3[ch] = beta;
+                if (a.fold_rm) a.fold_rm[ch] = momentum * meanf + (1.0f - momentum) * a.fold_rm[ch];
+                if (a.fold_rv) {
+                    const float unbiased = (float)(M > 1.0 ? var * M / (M - 1.0) : var);
+                    a.fold_rv[ch] = momentum * unbiased + (1.0f - momentum) * a.fold_rv[ch];
+                }
+            }
+        } else {                  // mode 1: the BN's saved invstd is bn_invstd
+            const float invstd = a.bn_invstd[ch];
+            const float sum_dy = (float)S0, dot = (float)S1;
+            const float kc = dot * invstd * invstd / (float)M;
+            const float gm = sum_dy / (float)M;
+            coef[ch] = kc;
+            coef[kC + ch] = gm;
+            if (out) {
+                if (a.fold_o0) a.fold_o0[ch] = dot * invstd;
+                if (a.fold_o1) a.fold_o1[ch] = sum_dy;
+                a.fold_o2[ch] = kc;
+                a.fold_o3[ch] = gm;
+            }
+        }
+    }
+    __syncthreads();
+    const int ch = threadIdx.x & 31;
+    c0 = coef[ch];
+    c1 = coef[kC + ch];
+    __syncthreads();   // every lane has its coefficients before the caller's staging reuses these bytes
+}
+
+}  // namespace bnfold
 
 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -1100,7 +1198,10 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
     // BN_i's backward apply for channel ch (bn_bwd_apply_kernel's per-channel values), the prologue's BN_{i-1}
     float mu = 0.f, kk = 0.f, gmn = 0.f, is = 1.f, ww = 1.f, al = 1.f, be = 0.f;
     if constexpr (!kFwd) {
-        mu = a.bn_mean[ch]; kk = a.bn_k[ch]; gmn = a.bn_gm[ch]; is = a.bn_invstd[ch];
+        // BN_i's backward finalize (bnfold) first, while the registers are free (beside tile 0's loads it spilled)
+        if (a.fold_part) bnfold::fold(a, smem, kk, gmn);
+        else { kk = a.bn_k[ch]; gmn = a.bn_gm[ch]; }
+        mu = a.bn_mean[ch]; is = a.bn_invstd[ch];
         ww = a.bn_w ? a.bn_w[ch] : 1.0f;
         al = is * ww;
         be = (a.bn_b ? a.bn_b[ch] : 0.0f) - mu * al;
@@ -1993,8 +2094,10 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
     }
     float pa = 1.f, pb = 0.f;
     if constexpr (PRO) {
-        pa = a.in_alpha[ch];
-        pb = a.in_beta[ch];
+        if (!a.fold_part) {
+            pa = a.in_alpha[ch];
+            pb = a.in_beta[ch];
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the weight and prologue loads, before any DMA is counted
     const uint32_t smem_base = (uint32_t)(uintptr_t)smem;
@@ -2048,6 +2151,11 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
     // prologue: tiles 0 .. kSlots-1 in flight; tile 0 staged
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) dma(j, j);
+    if constexpr (PRO) {
+        // the input BN's finalize (bnfold) while the ring fills; its loads' wait also covers the DMAs issued
+        // before them (the counted waits below then pass at once)
+        if (a.fold_part) bnfold::fold(a, smem, pa, pb);
+    }
     vm_wait<(kSlots - 1) * NP>();                            // tile 0 landed
     bb2::bar_lds();
     stage(0, 0);
@@ -2162,6 +2270,251 @@ __device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, 
 
 }  // namespace fw3
 
+// ------------------------------------------------------------------ the chain's forward conv, y staged in the ring
+// conv3x3_fwd_ls_kernel<PRO> (fwd form 3): fw3's ring, staging and split MFMA sequence (bit-identical y and sums),
+// with y leaving through LDS.  fw3 stores y straight from the accumulators: 8- and 12-byte runs 36 bytes apart per
+// lane, which cost more than the ring's reads (a ping-pong form measured them: profiles/r06_fw4_pingpong.txt).  A
+// tile of y is 18,432 contiguous bytes of HBM and exactly one ring slot, and tile it's slot is free once its x' is
+// staged, so:
+//  * iteration it: the MFMAs of tile it, then y(it) into ring slot it % kSlots as [row][288] fp32 (the HBM image);
+//  * iteration it + 1, after the barrier: wave W reads back its LDS-DMA pieces p = W, W + 8, W + 16 of that slot,
+//    stores them as 1 KiB contiguous buffer stores, then issues tile it + kSlots's LDS-DMA into the same pieces
+//    (only this wave reads or writes them, so no barrier between);
+//  * tile X's LDS-DMA is issued in iteration X - 4 (fw3: X - 5): one ring slot holds the drained tile.
+namespace fw5 {
+
+// diagnostic variants (FW5_VARIANT; the product is 0): bit 1 = the y stores by lane 0 only (same instruction
+// count), bit 2 = y written to LDS with the row groups 16 banks apart (wrong y: the bank-conflict-free write cost)
+#ifndef FW5_VARIANT
+#define FW5_VARIANT 0
+#endif
+constexpr int kVariant = FW5_VARIANT;
+
+constexpr int kSlots = fw3::kSlots;
+constexpr int kRawBytes = fw3::kRawBytes;
+constexpr int kImg0 = fw3::kImg0;
+constexpr int kRaw0 = fw3::kRaw0;
+constexpr int kLdsBytes = fw3::kLdsBytes;
+static_assert(kSlots == 5 && kRawBytes == kTile * kRow * 4, "one ring slot = one tile of y");
+
+template <bool PRO, int W>
+__device__ __forceinline__ void run(const BlockBwdArgs &a, unsigned char *smem, int lane) {
+    constexpr int kCt = W & 1, G = W >> 1;
+    using C = fw3::Cells<G>;
+    constexpr int kNq = C::kN;
+    constexpr int NP = fw3::pieces_of<W>();
+    const int64_t ntiles = (a.M + kTile - 1) / kTile;
+    const int64_t t0 = blockIdx.x;
+    const int64_t step = gridDim.x;
+    const int n_iter = t0 < ntiles ? (int)((ntiles - 1 - t0) / step + 1) : 0;
+    const int ch = lane & 31, hh = lane >> 5;
+    uint4 wh[kTaps], wm[kTaps], wl[kTaps];
+    {
+        const int ci0 = 8 * (lane >> 4), j = lane & 15;
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) {
+            if (!fw3::g_uses_tap<G>(t)) continue;
+            uint32_t hv[4], mv[4], lv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int tc = t * 2 + kCt;
+                const float w0 = a.wpk[(tc * kC + ci0 + 2 * d) * 16 + j];
+                const float w1 = a.wpk[(tc * kC + ci0 + 2 * d + 1) * 16 + j];
+                uint32_t h0, m0, l0, h1, m1, l1;
+                hrl_split::split3(w0, h0, m0, l0);
+                hrl_split::split3(w1, h1, m1, l1);
+                hv[d] = h0 | (h1 << 16);
+                mv[d] = m0 | (m1 << 16);
+                lv[d] = l0 | (l1 << 16);
+            }
+            wh[t] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+            wm[t] = make_uint4(mv[0], mv[1], mv[2], mv[3]);
+            wl[t] = make_uint4(lv[0], lv[1], lv[2], lv[3]);
+        }
+    }
+    float pa = 1.f, pb = 0.f;
+    if constexpr (PRO) {
+        pa = a.in_alpha[ch];
+        pb = a.in_beta[ch];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the weight and prologue loads, before any DMA is counted
+    const uint32_t smem_base = (uint32_t)(uintptr_t)smem;
+    auto rows_of = [&](int it) __attribute__((always_inline)) {
+        const int64_t t = t0 + (int64_t)it * step;
+        return it < n_iter ? (int)min<int64_t>(kTile, a.M - t * kTile) : 0;
+    };
+    auto dma = [&](int it) __attribute__((always_inline)) {   // tile it -> ring slot it % kSlots (this wave's pieces)
+        const int64_t t = t0 + (int64_t)it * step;
+        const int rows = rows_of(it);
+        const u32x4 desc = fw3::wave_desc(a.x + (rows > 0 ? t * kTile * kRow : 0), (uint32_t)rows * kRow * 4);
+        const uint32_t raw = smem_base + kRaw0 + (uint32_t)(it % kSlots) * kRawBytes;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            const int p = W + 8 * j;
+            fw3::dma16(desc, p * 1024 + lane * 16, raw + p * 1024);
+        }
+    };
+    const int c0 = hh ? 4 : 0;
+    const int rho0 = 2 * ((W + (ch >> 2)) & 7);              // bb2 staging wave W's row pair (its diagonal)
+    auto stage = [&](int it) __attribute__((always_inline)) {
+        const float *raw = reinterpret_cast<const float *>(smem + kRaw0 + (it % kSlots) * kRawBytes);
+        unsigned char *xi = smem + kImg0 + (it & 1) * bb2::kImgBytes;
+        uint32_t xp[3][5];
+        float xv[2][5];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const float *src = raw + (rho0 + r) * kRow + ch * kCells + c0;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                float v = src[i];
+                if constexpr (PRO) {   // bn_apply_kernel's float operations
+                    const float u = v * pa + pb;
+                    v = u < 0.f ? 0.f : u;
+                }
+                xv[r][i] = v;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) hrl_split::split_pair(xv[0][i], xv[1][i], xp[0][i], xp[1][i], xp[2][i]);
+        const int half = rho0 >> 3, sub = 2 * (rho0 & 7);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const int o = bb2::img_off(c0 + i, ch, half) + sub;
+#pragma unroll
+            for (int part = 0; part < 3; ++part)
+                *reinterpret_cast<uint32_t *>(xi + part * bb2::kPartBytes + o) = xp[part][i];
+        }
+    };
+    // tile it's y: this wave's pieces of its ring slot -> HBM (1 KiB contiguous per store), then tile it + kSlots's
+    // LDS-DMA into the same pieces (the stores have consumed the reads)
+    auto drain = [&](int it, bool refill) __attribute__((always_inline)) {
+        const int64_t t = t0 + (int64_t)it * step;
+        const int rows = rows_of(it);
+        const __amdgpu_buffer_rsrc_t od = wave_rsrc(a.gin + (rows > 0 ? t * kTile * kRow : 0), (uint32_t)rows * kRow * 4);
+        const unsigned char *raw = smem + kRaw0 + (it % kSlots) * kRawBytes;
+        u32x4 v[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) v[j] = *reinterpret_cast<const u32x4 *>(raw + (W + 8 * j) * 1024 + lane * 16);
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            if constexpr (kVariant & 1) {
+                if (lane != 0) continue;
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(v[j], od, (W + 8 * j) * 1024 + lane * 16, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the pieces are read before the DMA rewrites them
+        if (refill) dma(it + kSlots);
+    };
+    const int co = kCt * 16 + (lane & 15);
+    const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+    const int tr_sub = 8 * (pp & 1);
+    double s1 = 0.0, s2 = 0.0;
+    // prologue: tiles 0 .. kSlots-2 in flight; tile 0 staged
+#pragma unroll
+    for (int j = 0; j < kSlots - 1; ++j) dma(j);
+    fw3::vm_wait<(kSlots - 2) * NP>();                       // tile 0 landed
+    bb2::bar_lds();
+    stage(0);
+    fw3::vm_wait<(kSlots - 3) * NP>();                       // tile 1 landed
+    bb2::bar_lds();
+    for (int it = 0; it < n_iter; ++it) {
+        BB2_STAMP(it, 0);
+        if (it == 0) dma(kSlots - 1);                        // ring slot kSlots-1 is still empty
+        else drain(it - 1, true);                            // y(it-1) out, tile it-1+kSlots in
+        stage(it + 1);                                       // runs past the last tile too (stale rows, unread)
+        BB2_STAMP(it, 1);
+        const unsigned char *img = smem + kImg0 + (it & 1) * bb2::kImgBytes;
+        f32x4 acc[kNq];
+#pragma unroll
+        for (int s = 0; s < kNq; ++s) acc[s] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < kCells; ++p) {
+            if (!fw3::g_uses_p<G>(p)) continue;
+            uint32_t A[3][4];
+#pragma unroll
+            for (int part = 0; part < 3; ++part) {
+#pragma unroll
+                for (int hlf = 0; hlf < 2; ++hlf) {
+                    const int o = part * bb2::kPartBytes + bb2::img_off(p, 8 * g + 4 * hlf + qq, pp >> 1) + tr_sub;
+                    const bb2::v4s r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (bb2::lds_v4s *)((__attribute__((address_space(3))) unsigned char *)(img + o)));
+                    const uint2 u = __builtin_bit_cast(uint2, r);
+                    A[part][2 * hlf] = u.x;
+                    A[part][2 * hlf + 1] = u.y;
+                }
+            }
+            const uint4 Ah = make_uint4(A[0][0], A[0][1], A[0][2], A[0][3]);
+            const uint4 Am = make_uint4(A[1][0], A[1][1], A[1][2], A[1][3]);
+            const uint4 Al = make_uint4(A[2][0], A[2][1], A[2][2], A[2][3]);
+#pragma unroll
+            for (int s = 0; s < kNq; ++s) {
+                const int tap = tap_of(p, C::kQ[s]);
+                if (tap < 0) continue;
+                f32x4 c = acc[s];
+                c = mfma_bf16(Al, wh[tap], c);   // smallest terms first (bb2's order)
+                c = mfma_bf16(Am, wm[tap], c);
+                c = mfma_bf16(Ah, wl[tap], c);
+                c = mfma_bf16(Am, wh[tap], c);
+                c = mfma_bf16(Ah, wm[tap], c);
+                c = mfma_bf16(Ah, wh[tap], c);
+                acc[s] = c;
+            }
+        }
+        BB2_STAMP(it, 2);
+        // the output's BN statistics (fp32 per tile, fp64 across tiles), then y into tile it's ring slot
+        const int rows = rows_of(it);
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int s = 0; s < kNq; ++s) {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int row = g * 4 + rr;
+                const float u = row < rows ? acc[s][rr] : 0.f;
+                t1 += u;
+                t2 += u * u;
+            }
+        }
+        s1 += (double)t1;
+        s2 += (double)t2;
+        {
+            float *yo = reinterpret_cast<float *>(smem + kRaw0 + (it % kSlots) * kRawBytes);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                for (int s = 0; s < kNq; ++s) {
+                    int o = (g * 4 + rr) * kRow + co * kCells + C::kQ[s];
+                    if constexpr (kVariant & 2) o = (o + 16 * g) % (kTile * kRow);
+                    yo[o] = acc[s][rr];
+                }
+        }
+        // tile it+2 landed: younger are this wave's later LDS-DMA pieces and y stores (tile X's DMA is issued in
+        // iteration X-4, after that iteration's stores; the prologue issued tiles 0..3, iteration 0 tile 4)
+        if (it == 0) fw3::vm_wait<2 * NP>();
+        else if (it == 1) fw3::vm_wait<3 * NP>();
+        else fw3::vm_wait<4 * NP>();
+        BB2_STAMP(it, 3);
+        bb2::bar_lds();                                      // y(it) and tile it+1's image staged
+    }
+    if (n_iter > 0) drain(n_iter - 1, false);
+    fw3::vm_wait<0>();
+    // the sums: [wave][lane] -> channel (wave & 1) * 16 + (lane & 15), waves and lane groups in a fixed order
+    __syncthreads();
+    double *dred = reinterpret_cast<double *>(smem);
+    dred[(W * 64 + lane) * 2 + 0] = s1;
+    dred[(W * 64 + lane) * 2 + 1] = s2;
+    __syncthreads();
+    if (W == 0) {
+        const int c = lane >> 1, k = lane & 1, ct = c >> 4, l16 = c & 15;
+        double tot = 0.0;
+        for (int w = ct; w < 8; w += 2)
+            for (int lg = 0; lg < 4; ++lg) tot += dred[(w * 64 + lg * 16 + l16) * 2 + k];
+        a.part[((int64_t)blockIdx.x * kC + c) * 2 + k] = tot;
+    }
+}
+
+}  // namespace fw5
+
+
 template <bool PRO>
 __global__ __launch_bounds__(bb2::kThreads) void conv3x3_fwd_dma_kernel(BlockBwdArgs a) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[fw3::kLdsBytes];
@@ -2176,6 +2529,23 @@ __global__ __launch_bounds__(bb2::kThreads) void conv3x3_fwd_dma_kernel(BlockBwd
     case 5: fw3::run<PRO, 5>(a, smem, lane); break;
     case 6: fw3::run<PRO, 6>(a, smem, lane); break;
     default: fw3::run<PRO, 7>(a, smem, lane); break;
+    }
+}
+
+template <bool PRO>
+__global__ __launch_bounds__(bb2::kThreads) void conv3x3_fwd_ls_kernel(BlockBwdArgs a) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[fw5::kLdsBytes];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    switch (wave) {
+    case 0: fw5::run<PRO, 0>(a, smem, lane); break;
+    case 1: fw5::run<PRO, 1>(a, smem, lane); break;
+    case 2: fw5::run<PRO, 2>(a, smem, lane); break;
+    case 3: fw5::run<PRO, 3>(a, smem, lane); break;
+    case 4: fw5::run<PRO, 4>(a, smem, lane); break;
+    case 5: fw5::run<PRO, 5>(a, smem, lane); break;
+    case 6: fw5::run<PRO, 6>(a, smem, lane); break;
+    default: fw5::run<PRO, 7>(a, smem, lane); break;
     }
 }
 
@@ -2300,8 +2670,8 @@ int g_bb4_stagger = [] {
     const char *e = getenv("HRL_BB4_STAGGER");
     return e ? atoi(e) : 0;
 }();
-// The chain's forward conv (epilogue 1, packed weights, no bias): 2 = the LDS-DMA ring form (fw3, default),
-// 1 = the tile-shared form (bb2, EPI 1), 0 = conv3x3_kernel<PRO, 1>.
+// The chain's forward conv (epilogue 1, packed weights, no bias): 3 = the ring form with y staged through LDS (fw5),
+// 2 = the LDS-DMA ring form (fw3, default), 1 = the tile-shared form (bb2, EPI 1), 0 = conv3x3_kernel<PRO, 1>.
 int g_fwd_form = 2;
 
 // One 4-wave workgroup per CU (LDS: 109 KB forward, 145 KB weight gradient);
@@ -2358,7 +2728,7 @@ int hrl_conv3x3_set_block_form(int form) {
 
 int hrl_conv3x3_set_fwd_form(int form) {
     const int prev = g_fwd_form;
-    g_fwd_form = form < 0 ? 0 : (form > 2 ? 2 : form);
+    g_fwd_form = form < 0 ? 0 : (form > 3 ? 3 : form);
     return prev;
 }
 
@@ -2394,7 +2764,10 @@ int hrl_conv3x3_forward_ex(const float *x, int64_t M, const float *in_alpha, con
         BlockBwdArgs a{};
         a.x = x; a.in_alpha = in_alpha; a.in_beta = in_beta; a.wpk = wpk; a.gin = y; a.part = part; a.M = M;
         const dim3 grid(grid_for(M)), block(bb2::kThreads);
-        if (g_fwd_form == 2) {
+        if (g_fwd_form == 3) {
+            if (in_alpha) hipLaunchKernelGGL((conv3x3_fwd_ls_kernel<true>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((conv3x3_fwd_ls_kernel<false>), grid, block, 0, s, a);
+        } else if (g_fwd_form == 2) {
             if (in_alpha) hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<true>), grid, block, 0, s, a);
             else hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<false>), grid, block, 0, s, a);
         } else if (in_alpha) {
@@ -2532,6 +2905,84 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
 #undef HRL_BLOCK4_LAUNCH
     int rc = status();
     if (rc || !dweight) return rc;   // no dweight: the partials stay for a later fold (hrl_grad_fold_norm)
+    hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, wpart, grid,
+                       dweight);
+    return status();
+}
+
+int hrl_conv3x3_forward_bnfold(const float *x, int64_t M, const double *prev_part, int64_t prev_nblocks,
+                               const float *gamma, const float *beta, float *running_mean, float *running_var,
+                               double momentum, double eps, float *save_mean, float *save_invstd, float *alpha,
+                               float *beta_out, const float *packed, float *y, double *part, void *workspace,
+                               int64_t workspace_bytes, void *stream) {
+    if (M < 1 || !x || !prev_part || prev_nblocks < 1 || !save_mean || !save_invstd || !alpha || !beta_out ||
+        !packed || !y || !part || !workspace)
+        return HRL_EINVAL;
+    if (!aligned16(x) || !aligned16(y) || workspace_bytes < hrl_conv3x3_workspace_bytes(M)) return HRL_EINVAL;
+    if (prev_part == part) return HRL_EINVAL;   // the prologue reads every row the epilogue rewrites
+    if (g_fwd_form != 2 || !g_split || prev_nblocks > 512 || M * kRow * 4 > 0xffffffffLL) {
+        // the other forms: the two launches
+        const int rc = hrl_bn_finalize_stats(prev_part, prev_nblocks, kC, M * kCells, gamma, beta, running_mean,
+                                             running_var, momentum, eps, save_mean, save_invstd, alpha, beta_out,
+                                             stream);
+        if (rc) return rc;
+        return hrl_conv3x3_forward_ex(x, M, alpha, beta_out, packed, nullptr, 2, y, 1, nullptr, nullptr, nullptr,
+                                      nullptr, part, workspace, workspace_bytes, stream);
+    }
+    BlockBwdArgs a{};
+    a.x = x; a.wpk = packed; a.gin = y; a.part = part; a.M = M;
+    a.fold_part = prev_part; a.fold_nblocks = (int)prev_nblocks; a.fold_mode = 0;
+    a.fold_count = (double)(M * kCells); a.fold_eps = eps; a.fold_momentum = (float)momentum;
+    a.fold_w = gamma; a.fold_b = beta; a.fold_rm = running_mean; a.fold_rv = running_var;
+    a.fold_o0 = save_mean; a.fold_o1 = save_invstd; a.fold_o2 = alpha; a.fold_o3 = beta_out;
+    hipLaunchKernelGGL((conv3x3_fwd_dma_kernel<true>), dim3(grid_for(M)), dim3(bb2::kThreads), 0,
+                       static_cast<hipStream_t>(stream), a);
+    return status();
+}
+
+int hrl_conv3x3_block_backward_bnfold(const float *g, const float *y, int64_t M, const float *bn_weight,
+                                      const float *bn_bias, const float *save_mean, const float *save_invstd,
+                                      const double *sums, int64_t sums_nblocks, float *dgamma, float *dbeta,
+                                      float *kcoef, float *gmean, const float *x, const float *in_alpha,
+                                      const float *in_beta, const float *packed_flip, float *dweight, float *gin,
+                                      int epilogue, const float *ep_mean, const float *ep_alpha, const float *ep_beta,
+                                      double *part, void *workspace, int64_t workspace_bytes, void *stream) {
+    if (!sums || sums_nblocks < 1 || !save_invstd || !kcoef || !gmean) return HRL_EINVAL;
+    if (part && sums == part) return HRL_EINVAL;   // the prologue reads every row the epilogue rewrites
+    const bool fused = g_block_form == 1 && gin && sums_nblocks <= 512;
+    if (!fused) {   // the other forms: the two launches
+        const int rc = hrl_bn_finalize_backward(sums, sums_nblocks, kC, M * kCells, bn_weight, save_invstd, dgamma,
+                                                dbeta, kcoef, gmean, stream);
+        if (rc) return rc;
+        return hrl_conv3x3_block_backward(g, y, M, bn_weight, bn_bias, save_mean, save_invstd, kcoef, gmean, x,
+                                          in_alpha, in_beta, packed_flip, dweight, gin, epilogue, ep_mean, ep_alpha,
+                                          ep_beta, part, workspace, workspace_bytes, stream);
+    }
+    if (M < 1 || !g || !y || !save_mean || !x || !workspace) return HRL_EINVAL;
+    if ((in_alpha == nullptr) != (in_beta == nullptr)) return HRL_EINVAL;
+    if (workspace_bytes < hrl_conv3x3_workspace_bytes(M) || M * kRow * 4 > 0xffffffffLL) return HRL_EINVAL;
+    if (!packed_flip || epilogue < 0 || epilogue == 1 || epilogue > 3) return HRL_EINVAL;
+    if (epilogue == 2 && (!ep_mean || !ep_alpha || !ep_beta || !part)) return HRL_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int grid = block_grid_for(M);
+    float *wpart = static_cast<float *>(workspace) + kTaps * 2 * kC * 16 * 2;
+    BlockBwdArgs a{g, y, bn_weight, bn_bias, save_mean, save_invstd, kcoef, gmean, x, in_alpha, in_beta, packed_flip,
+                   ep_mean, ep_alpha, ep_beta, gin, part, wpart, M};
+    a.fold_part = sums; a.fold_nblocks = (int)sums_nblocks; a.fold_mode = 1; a.fold_count = (double)(M * kCells);
+    a.fold_o0 = dgamma; a.fold_o1 = dbeta; a.fold_o2 = kcoef; a.fold_o3 = gmean;
+    const bool pro = in_alpha != nullptr;
+#define HRL_BLOCK2_LAUNCH(PRO, EPI) \
+    hipLaunchKernelGGL((conv3x3_block_bwd2_kernel<PRO, EPI>), dim3(grid), dim3(bb2::kThreads), 0, s, a)
+    if (epilogue == 2) {
+        if (pro) HRL_BLOCK2_LAUNCH(true, 2); else HRL_BLOCK2_LAUNCH(false, 2);
+    } else if (epilogue == 3) {
+        if (pro) HRL_BLOCK2_LAUNCH(true, 3); else HRL_BLOCK2_LAUNCH(false, 3);
+    } else {
+        if (pro) HRL_BLOCK2_LAUNCH(true, 0); else HRL_BLOCK2_LAUNCH(false, 0);
+    }
+#undef HRL_BLOCK2_LAUNCH
+    int rc = status();
+    if (rc || !dweight) return rc;
     hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(kTaps * kC * kC / 64), dim3(256), 0, s, wpart, grid,
                        dweight);
     return status();

@@ -510,7 +510,7 @@ int hrl_debug_set_stamps_targets(void *buf) {
 }
 #endif
 
-int hrl_abi_version(void) { return 25; }
+int hrl_abi_version(void) { return 26; }
 
 int hrl_targets_set_short_form(int form) {
     const int prev = g_short_form;

@@ -1970,6 +1970,11 @@ class _MultiBoardConv(nn.Module):
 
 _UNIT = {}
 
+# The chain's BatchNorm finalizes run in the prologue of the kernel that consumes them (hrl_conv3x3_forward_bnfold,
+# hrl_conv3x3_block_backward_bnfold: five launches fewer per TicTacToe step, bit-identical); False restores the
+# separate hrl_bn_finalize_* launches (tests compare the two).
+FOLD_BN = True
+
 
 def _unit_coefs(dev):
     """(alpha, beta) = (1, 0) per channel: the stem ReLU in front of a chain as an identity BN + ReLU (cached)."""
@@ -1989,7 +1994,10 @@ def _chain_forward(h0, meta, relu_in, params, apply_out=True):
     ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     nblk = lib.hrl_conv3x3_stats_blocks(M)
-    part = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
+    # conv i's statistics rows alternate between two buffers: conv i+1 reads them in its prologue (FOLD_BN) while
+    # its own epilogue writes the other
+    parts = torch.empty(2, nblk * 32 * 2, dtype=torch.float64, device=dev)
+    fold = FOLD_BN
     unit = _unit_coefs(dev) if relu_in else None
     x = h0
     a_prev, b_prev = (unit[0], unit[1]) if relu_in else (None, None)
@@ -2000,16 +2008,28 @@ def _chain_forward(h0, meta, relu_in, params, apply_out=True):
     for k in range(0, len(weights), 8):       # hrl_conv3x3_pack_n takes up to 8 weights per launch
         _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array(weights[k:k + 8]), len(weights[k:k + 8]),
                                              P(packed[k]), stream), 'hrl_conv3x3_pack_n')
+    n = len(meta)
     for i, (rm, rv, momentum, eps) in enumerate(meta):
         w, gamma, beta = params[3 * i:3 * i + 3]
         y = torch.empty_like(h0)
-        _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(a_prev), P(b_prev), P(packed[i, 0]), None, 2, P(y), 1,
-                                                 None, None, None, None, P(part), P(ws), ws_bytes, stream),
-                      'hrl_conv3x3_forward_ex')
+        part = parts[i % 2]
+        if fold and i > 0:
+            # BN_{i-1}'s finalize runs in conv i's prologue and fills coefs[i-1] (hrl_conv3x3_forward_bnfold)
+            prm, prv, pmom, peps = meta[i - 1]
+            pc = coefs[i - 1]
+            _native.check(lib.hrl_conv3x3_forward_bnfold(
+                P(x), M, P(parts[(i - 1) % 2]), nblk, P(params[3 * i - 2]), P(params[3 * i - 1]), P(prm), P(prv),
+                float(pmom), float(peps), P(pc[0]), P(pc[1]), P(pc[2]), P(pc[3]), P(packed[i, 0]), P(y), P(part),
+                P(ws), ws_bytes, stream), 'hrl_conv3x3_forward_bnfold')
+        else:
+            _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(a_prev), P(b_prev), P(packed[i, 0]), None, 2, P(y),
+                                                     1, None, None, None, None, P(part), P(ws), ws_bytes, stream),
+                          'hrl_conv3x3_forward_ex')
         coef = torch.empty(4, 32, dtype=torch.float32, device=dev)   # mean, invstd, alpha, beta
-        _native.check(lib.hrl_bn_finalize_stats(P(part), nblk, 32, M * 9, P(gamma), P(beta), P(rm), P(rv),
-                                                float(momentum), float(eps), P(coef[0]), P(coef[1]),
-                                                P(coef[2]), P(coef[3]), stream), 'hrl_bn_finalize_stats')
+        if not fold or i == n - 1:
+            _native.check(lib.hrl_bn_finalize_stats(P(part), nblk, 32, M * 9, P(gamma), P(beta), P(rm), P(rv),
+                                                    float(momentum), float(eps), P(coef[0]), P(coef[1]),
+                                                    P(coef[2]), P(coef[3]), stream), 'hrl_bn_finalize_stats')
         ys.append(y)
         coefs.append(coef)
         x, a_prev, b_prev = y, coef[2], coef[3]
@@ -2035,7 +2055,9 @@ def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, pa
     bn_ws = torch.empty(bn_ws_bytes, dtype=torch.uint8, device=dev)
     # the block backward's epilogue-2 sum rows (its workgroups) or the input-gradient conv's
     nblk = max(lib.hrl_conv3x3_block_sum_blocks(M), lib.hrl_conv3x3_stats_blocks(M))
-    part = torch.empty(nblk * 32 * 2, dtype=torch.float64, device=dev)
+    # block i writes BN_{i-1}'s sums into parts[i % 2] while (FOLD_BN) its prologue reads BN_i's from the other
+    parts = torch.empty(2, nblk * 32 * 2, dtype=torch.float64, device=dev)
+    fold = FOLD_BN
     g = g.contiguous()
     grads = [None] * (3 * n)
     sums, sums_n = (part_in, nblk_in) if part_in is not None else (None, 0)   # BN_i's backward sums, if formed
@@ -2049,13 +2071,16 @@ def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, pa
         else:
             x, a, b = ys[i - 1], coefs[i - 1][2], coefs[i - 1][3]
         dw = bw[0]
+        part = parts[i % 2]
         if sums is not None:
             # BN_i's backward sums are formed (by the consumer or block i+1's input-gradient epilogue): the block's
-            # BN backward apply, weight gradient and input gradient run as ONE launch (conv3x3_block_bwd_kernel)
+            # BN backward apply, weight gradient and input gradient run as ONE launch (conv3x3_block_bwd_kernel),
+            # with BN_i's finalize in its prologue (FOLD_BN, hrl_conv3x3_block_backward_bnfold)
             kg = torch.empty(2, 32, dtype=torch.float32, device=dev)
-            _native.check(lib.hrl_bn_finalize_backward(P(sums), sums_n, 32, M * 9, P(gamma), P(invstd), P(dgam),
-                                                       P(dbet), P(kg[0]), P(kg[1]), stream),
-                          'hrl_bn_finalize_backward')
+            if not fold:
+                _native.check(lib.hrl_bn_finalize_backward(P(sums), sums_n, 32, M * 9, P(gamma), P(invstd),
+                                                           P(dgam), P(dbet), P(kg[0]), P(kg[1]), stream),
+                              'hrl_bn_finalize_backward')
             gin, epi, ep = None, 0, (None, None, None)
             if i > 0:
                 gin, epi, ep = torch.empty_like(h0), 2, (coefs[i - 1][0], coefs[i - 1][2], coefs[i - 1][3])
@@ -2064,10 +2089,17 @@ def _chain_backward(h0, ys, coefs, unit, params, relu_in, g, need_input_grad, pa
             df = _defer_folds([bw])
             wsb = ws if df is None else torch.empty(ws_bytes, dtype=torch.uint8, device=dev)   # partials live on
             ev = _block_timing_start()
-            _native.check(lib.hrl_conv3x3_block_backward(
-                P(g), P(ys[i]), M, P(gamma), P(beta), P(mean), P(invstd), P(kg[0]), P(kg[1]), P(x), P(a), P(b),
-                P(packed[i, 1]), None if df is not None else P(dw), P(gin), epi, P(ep[0]), P(ep[1]), P(ep[2]),
-                P(part) if i > 0 else None, P(wsb), ws_bytes, stream), 'hrl_conv3x3_block_backward')
+            if fold:
+                _native.check(lib.hrl_conv3x3_block_backward_bnfold(
+                    P(g), P(ys[i]), M, P(gamma), P(beta), P(mean), P(invstd), P(sums), sums_n, P(dgam), P(dbet),
+                    P(kg[0]), P(kg[1]), P(x), P(a), P(b), P(packed[i, 1]), None if df is not None else P(dw), P(gin),
+                    epi, P(ep[0]), P(ep[1]), P(ep[2]), P(part) if i > 0 else None, P(wsb), ws_bytes, stream),
+                    'hrl_conv3x3_block_backward_bnfold')
+            else:
+                _native.check(lib.hrl_conv3x3_block_backward(
+                    P(g), P(ys[i]), M, P(gamma), P(beta), P(mean), P(invstd), P(kg[0]), P(kg[1]), P(x), P(a), P(b),
+                    P(packed[i, 1]), None if df is not None else P(dw), P(gin), epi, P(ep[0]), P(ep[1]), P(ep[2]),
+                    P(part) if i > 0 else None, P(wsb), ws_bytes, stream), 'hrl_conv3x3_block_backward')
             _block_timing_end(ev)
             if df is not None:   # [block][tap][ci][co] partial rows -> dW (co, ci, kh, kw): fold mode 1
                 off = ctypes.c_int64(0)

@@ -224,6 +224,36 @@ int hrl_conv3x3_block_backward(const float *g, const float *y, int64_t M, const 
                                double *part, void *workspace, int64_t workspace_bytes, void *stream);
 
 /*
+ * The BatchNorm finalize folded into the kernel that consumes it (ABI 26): the chain's kernels no longer wait on
+ * a finalize launch of their own between them.
+ *
+ * hrl_conv3x3_forward_bnfold = hrl_bn_finalize_stats(prev_part, prev_nblocks, 32, M*9, gamma, beta, running_mean,
+ *   running_var, momentum, eps, save_mean, save_invstd, alpha, beta_out) followed by hrl_conv3x3_forward_ex(x, M,
+ *   alpha, beta_out, packed, NULL, 2, y, 1, ..., part): the previous conv's BN statistics -> its coefficients ->
+ *   this conv's BN + ReLU prologue, epilogue 1 (this conv's statistics into part).  Under fwd form 2 (default) one
+ *   launch: every workgroup folds the partial rows in bn_finalize_kernel's order (bit-identical coefficients),
+ *   workgroup 0 writes the four outputs and advances the running statistics; other forms run the two launches.
+ *   prev_part != part (the prologue reads every row the epilogue rewrites); prev_nblocks <= 512 for the fused form.
+ * hrl_conv3x3_block_backward_bnfold = hrl_bn_finalize_backward(sums, sums_nblocks, 32, M*9, bn_weight,
+ *   save_invstd, dgamma, dbeta, kcoef, gmean) followed by hrl_conv3x3_block_backward(... kcoef, gmean ...): one
+ *   launch under block form 1 (default) with an input gradient, the two otherwise.  sums != part.
+ * Both replace the finalize between two of the TicTacToe body's convs (tictactoe.py:57-65; BatchNorm2d's
+ * statistics / backward reduction, train.py:383).
+ */
+int hrl_conv3x3_forward_bnfold(const float *x, int64_t M, const double *prev_part, int64_t prev_nblocks,
+                               const float *gamma, const float *beta, float *running_mean, float *running_var,
+                               double momentum, double eps, float *save_mean, float *save_invstd, float *alpha,
+                               float *beta_out, const float *packed, float *y, double *part, void *workspace,
+                               int64_t workspace_bytes, void *stream);
+int hrl_conv3x3_block_backward_bnfold(const float *g, const float *y, int64_t M, const float *bn_weight,
+                                      const float *bn_bias, const float *save_mean, const float *save_invstd,
+                                      const double *sums, int64_t sums_nblocks, float *dgamma, float *dbeta,
+                                      float *kcoef, float *gmean, const float *x, const float *in_alpha,
+                                      const float *in_beta, const float *packed_flip, float *dweight, float *gin,
+                                      int epilogue, const float *ep_mean, const float *ep_alpha, const float *ep_beta,
+                                      double *part, void *workspace, int64_t workspace_bytes, void *stream);
+
+/*
  * Fused ConvLSTM cell gates (GeisterNet DRC, handyrl/envs/geister.py:48-63;
  * replaces the split/sigmoid/tanh/mul/add chain of ConvLSTMCell.forward and
  * its autograd backward).  Gate pre-activations z = zx + zh in channel order

@@ -480,8 +480,9 @@ def test_block_backward_weight_gradient_exact_on_integer_data(cuda, M, pro, form
 @pytest.mark.parametrize('pro', [False, True])
 def test_tile_shared_forward_matches_per_wave_conv(cuda, M, pro):
     """The chain's forward conv with BN statistics (hrl_conv3x3_forward_ex, epilogue 1) in the tile-shared form
-    (the block backward kernel with x' staged in place of dY) and the LDS-DMA ring form (2, conv3x3_fwd_dma_kernel;
-    3 the same with waves 4-7 computing before they stage) vs the per-wave conv3x3_kernel: the output is bit-identical (the same split MFMA order on the same x'), the
+    (the block backward kernel with x' staged in place of dY), the LDS-DMA ring form (2, conv3x3_fwd_dma_kernel) and
+    the ping-pong ring form (3, conv3x3_fwd_pp_kernel: two wave groups alternating MFMAs and staging) vs the
+    per-wave conv3x3_kernel: the output is bit-identical (the same split MFMA order on the same x'), the
     per-channel sums sum(y) and sum(y^2) agree
     with the fp64 sums to fp32 rounding of a different per-tile grouping.  Ragged M = 37 (rows past the batch
     contribute nothing) and M = 20000 (several tiles per workgroup); with and without the BN + ReLU prologue."""
@@ -500,7 +501,7 @@ def test_tile_shared_forward_matches_per_wave_conv(cuda, M, pro):
     nblk = lib.hrl_conv3x3_stats_blocks(M)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
     outs = []
-    for form in (0, 1, 2):
+    for form in (0, 1, 2, 3):
         prev = lib.hrl_conv3x3_set_fwd_form(form)
         y, part = torch.empty_like(x), torch.full((nblk * 64,), float('nan'), dtype=torch.float64, device=cuda)
         try:
@@ -510,13 +511,14 @@ def test_tile_shared_forward_matches_per_wave_conv(cuda, M, pro):
         finally:
             lib.hrl_conv3x3_set_fwd_form(prev)
         outs.append((y, part))
-    (y0, p0), (y1, p1), (y2, p2) = outs
+    (y0, p0), (y1, p1), (y2, p2), (y3, p3) = outs
     assert torch.equal(y1, y0)
     assert torch.equal(y2, y0)
+    assert torch.equal(y3, y0)
     yd = y0.double().view(M, 32, 9)
     ref = torch.stack([yd.sum((0, 2)), (yd * yd).sum((0, 2))], 1)
     scale = torch.stack([yd.abs().sum((0, 2)), (yd * yd).sum((0, 2))], 1)
-    for p in (p0, p1, p2):
+    for p in (p0, p1, p2, p3):
         s = p.view(nblk, 32, 2).sum(0)
         assert bool(torch.isfinite(s).all())
         assert float(((s - ref).abs() / scale).max()) < 1e-6
@@ -613,3 +615,108 @@ def test_heads_backward_forms_agree(cuda, N, bn):
             bref = torch.stack([(dhx * m).sum((0, 2)), (dhx * m * (x - d(mu).view(1, 32, 1))).sum((0, 2))], 1)
             scale = float((dhx.abs() * (1 + x.abs())).sum((0, 2)).max())
             assert float((d(part) - bref).abs().max()) / scale < 1e-6, form
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('M', [37, 20000, 131072])
+@pytest.mark.parametrize('prev_rows', [None, 512])
+def test_finalize_folded_into_the_consumer_is_bit_identical(cuda, M, prev_rows):
+    """hrl_conv3x3_forward_bnfold / hrl_conv3x3_block_backward_bnfold (the BatchNorm finalize in the consumer kernel's
+    prologue, ABI 26) vs hrl_bn_finalize_stats / _backward followed by hrl_conv3x3_forward_ex / block_backward on the
+    same inputs: y, the statistics rows, the coefficients, the running statistics, the input gradient, dgamma and
+    dbeta, the weight gradient -- all bit-identical.  prev_rows None: the producer's own row count
+    (hrl_conv3x3_stats_blocks); 512: as many rows as the fused heads' backward writes (two per folding thread)."""
+    from handyrl_amd import _native
+    lib = _native.load()
+    P = _native.ptr
+    stream = _native.stream_of(cuda)
+    g0 = torch.Generator(device=cuda).manual_seed(M + 3)
+    rnd = lambda *s: torch.randn(*s, device=cuda, generator=g0)   # noqa: E731
+    nblk = lib.hrl_conv3x3_stats_blocks(M)
+    nprev = prev_rows or nblk
+    x, g = rnd(M, 288), rnd(M, 288)
+    w = rnd(32, 32, 3, 3) * 0.1
+    gamma, beta = rnd(32).abs() + 0.5, rnd(32) * 0.2
+    prev = (rnd(nprev, 32, 2).double() * torch.tensor([1.0, 0.0], device=cuda).double()
+            + torch.stack([torch.zeros(32, device=cuda), rnd(32).abs() * 3 + 1], 1).double()) * (M * 9 / nprev)
+    prev = prev.reshape(-1).contiguous()
+    packed = torch.empty(1, 2, 9216, device=cuda)
+    _native.check(lib.hrl_conv3x3_pack_n(_native.ptr_array([w]), 1, P(packed), stream), 'pack')
+    ws_bytes = lib.hrl_conv3x3_workspace_bytes(M)
+    outs = []
+    for fused in (False, True):
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+        rm, rv = torch.full((32,), 0.1, device=cuda), torch.full((32,), 0.9, device=cuda)
+        coef = torch.empty(4, 32, device=cuda)
+        y, part = torch.empty_like(x), torch.zeros(nblk * 64, dtype=torch.float64, device=cuda)
+        if fused:
+            _native.check(lib.hrl_conv3x3_forward_bnfold(P(x), M, P(prev), nprev, P(gamma), P(beta), P(rm), P(rv),
+                                                         0.1, 1e-5, P(coef[0]), P(coef[1]), P(coef[2]), P(coef[3]),
+                                                         P(packed[0, 0]), P(y), P(part), P(ws), ws_bytes, stream),
+                          'fwd fold')
+        else:
+            _native.check(lib.hrl_bn_finalize_stats(P(prev), nprev, 32, M * 9, P(gamma), P(beta), P(rm), P(rv), 0.1,
+                                                    1e-5, P(coef[0]), P(coef[1]), P(coef[2]), P(coef[3]), stream),
+                          'fin')
+            _native.check(lib.hrl_conv3x3_forward_ex(P(x), M, P(coef[2]), P(coef[3]), P(packed[0, 0]), None, 2, P(y),
+                                                     1, None, None, None, None, P(part), P(ws), ws_bytes, stream),
+                          'fwd')
+        # the backward of the same block with BN_i's sums = prev (its rows as the consumer's sums)
+        kg, dgb = torch.empty(2, 32, device=cuda), torch.empty(2, 32, device=cuda)
+        dw, gin = torch.empty(32, 32, 3, 3, device=cuda), torch.empty_like(g)
+        epart = torch.zeros(lib.hrl_conv3x3_block_sum_blocks(M) * 64, dtype=torch.float64, device=cuda)
+        args = (P(g), P(y), M, P(gamma), P(beta), P(coef[0]), P(coef[1]))
+        tail = (P(x), P(coef[2]), P(coef[3]), P(packed[0, 1]), P(dw), P(gin), 2, P(coef[0]), P(coef[2]), P(coef[3]),
+                P(epart), P(ws), ws_bytes, stream)
+        if fused:
+            _native.check(lib.hrl_conv3x3_block_backward_bnfold(*args, P(prev), nprev, P(dgb[0]), P(dgb[1]), P(kg[0]),
+                                                                P(kg[1]), *tail), 'bwd fold')
+        else:
+            _native.check(lib.hrl_bn_finalize_backward(P(prev), nprev, 32, M * 9, P(gamma), P(coef[1]), P(dgb[0]),
+                                                       P(dgb[1]), P(kg[0]), P(kg[1]), stream), 'fin bwd')
+            _native.check(lib.hrl_conv3x3_block_backward(*args, P(kg[0]), P(kg[1]), *tail), 'bwd')
+        torch.cuda.synchronize(cuda)
+        outs.append((y, part, coef, rm, rv, kg, dgb, dw, gin, epart))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert bool(torch.isfinite(outs[1][1]).all()) and bool(torch.isfinite(outs[1][8]).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N', [37, 4096])
+@pytest.mark.parametrize('relu_in', [False, True])
+def test_chain_with_folded_finalizes_is_bit_identical(cuda, N, relu_in):
+    """The TicTacToe body chain (_ConvBNChain -> _chain_forward / _chain_backward) with nn.FOLD_BN on (the finalizes
+    in the consumers' prologues) and off (their own launches): output, input gradient, every parameter gradient and
+    the running statistics bit-identical."""
+    from handyrl_amd import nn as hnn
+    from handyrl_amd.envs.tictactoe import SimpleConv2dModel
+    from handyrl_amd.nn import accelerate, _ConvBNChain
+    torch.manual_seed(1)
+    net = accelerate(SimpleConv2dModel()).to(cuda)
+    convs = [blk.conv for blk in net.blocks]
+    bns = [blk.bn for blk in net.blocks]
+    for b in bns:
+        b.fused_relu = True
+        b.weight.data.uniform_(0.5, 1.5)
+        b.bias.data.uniform_(-0.2, 0.2)
+    chain = _ConvBNChain(convs, bns, relu_in=relu_in)
+    x = torch.randn(N, 32, 3, 3, device=cuda)
+    g = torch.randn(N, 32, 3, 3, device=cuda)
+    params = [p for c, b in zip(convs, bns) for p in (c.weight, b.weight, b.bias)]
+    results = []
+    prev = hnn.FOLD_BN
+    try:
+        for fold in (False, True):
+            hnn.FOLD_BN = fold
+            for b in bns:
+                b.reset_running_stats()
+            xi = x.clone().requires_grad_()
+            y = chain(xi)
+            grads = torch.autograd.grad(y, [xi] + params, g)
+            stats = [t.clone() for b in bns for t in (b.running_mean, b.running_var)]
+            results.append([y.detach()] + list(grads) + stats)
+    finally:
+        hnn.FOLD_BN = prev
+    for a, b in zip(*results):
+        assert torch.equal(a, b)
