@@ -700,19 +700,23 @@ struct BlockBwdArgs {
 // of all 32 channels in bn_finalize_kernel's exact order -- thread i of its 256 sums rows i, i + 256 (0.0 first),
 // then the fixed tree (i, i + 128), (i, i + 64), (i, i + 32) ... (i, i + 1) -- and computes the channel's
 // coefficients with its float operations; workgroup 0 writes the outputs the separate launch wrote (the running
-// statistics advance once).  Bit-identical to the two launches (tests/test_bn_gpu.py).  Here thread (c, k, j)
-// holds leaves j + 8 m (m < 32): the levels 128 .. 8 are its register tree, 4, 2, 1 a shuffle over its 8 lanes.
+// statistics advance once).  Bit-identical to the two launches (tests/test_bn_gpu.py).  Here lane (c, k) of wave j
+// holds leaves j + 8 m (m < 32; one contiguous 512-byte row per wave load): the levels 128 .. 8 are its register
+// tree, 4, 2, 1 run over the eight waves' nodes through LDS.
 namespace bnfold {
 
 constexpr int kThreadsFold = 512;
 
 __device__ __forceinline__ void fold(const BlockBwdArgs &a, unsigned char *lds, float &c0, float &c1) {
     double *sums = reinterpret_cast<double *>(lds);                 // [32][2]
+    double *part8 = reinterpret_cast<double *>(lds + 64 * 8 + 64 * 4);   // [8][64]: the tree's level-8 nodes
     float *coef = reinterpret_cast<float *>(lds + 64 * 8);          // [2][32]
     const int tid = threadIdx.x;
-    const int ck = tid >> 3, j = tid & 7, c = ck >> 1, k = ck & 1;
+    // lane (c, k) = tid & 63 reads one double of every row its wave j = tid >> 6 owns: rows j + 8 m, 512 contiguous
+    // bytes per wave instruction
+    const int ck = tid & 63, j = tid >> 6;
     const int nb = a.fold_nblocks;
-    const double *pc = a.fold_part + (c * 2 + k);
+    const double *pc = a.fold_part + ck;
     double v[32];
 #pragma unroll
     for (int m = 0; m < 32; ++m) {
@@ -725,11 +729,18 @@ __device__ __forceinline__ void fold(const BlockBwdArgs &a, unsigned char *lds, 
     for (int w = 16; w >= 1; w >>= 1)
 #pragma unroll
         for (int m = 0; m < w; ++m) v[m] += v[m + w];
-    double e = v[0];
-    e += __shfl_down(e, 4, 8);
-    e += __shfl_down(e, 2, 8);
-    e += __shfl_down(e, 1, 8);
-    if (j == 0) sums[ck] = e;
+    part8[j * 64 + ck] = v[0];
+    __syncthreads();
+    if (tid < 64) {   // the levels 4, 2, 1 over the eight waves' nodes
+        double e[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) e[q] = part8[q * 64 + ck];
+#pragma unroll
+        for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+            for (int q = 0; q < w; ++q) e[q] += e[q + w];
+        sums[ck] = e[0];
+    }
     __syncthreads();
     if (tid < kC) {
         const int ch = tid;

@@ -1970,10 +1970,11 @@ class _MultiBoardConv(nn.Module):
 
 _UNIT = {}
 
-# The chain's BatchNorm finalizes run in the prologue of the kernel that consumes them (hrl_conv3x3_forward_bnfold,
-# hrl_conv3x3_block_backward_bnfold: five launches fewer per TicTacToe step, bit-identical); False restores the
-# separate hrl_bn_finalize_* launches (tests compare the two).
-FOLD_BN = True
+# True: the chain's BatchNorm finalizes run in the prologue of the kernel that consumes them
+# (hrl_conv3x3_forward_bnfold, hrl_conv3x3_block_backward_bnfold: five launches fewer per TicTacToe step,
+# bit-identical).  Off by default: every workgroup re-reading the 128 KB of partial rows cost more than the five
+# launches it saves (+14..25 us per step, profiles/r06_fold_ab.txt); tests keep both paths equal.
+FOLD_BN = False
 
 
 def _unit_coefs(dev):

@@ -185,8 +185,9 @@ int hrl_conv3x3_set_block_form(int form);
  * block form (ABI 25; form 2 writes more rows than hrl_conv3x3_stats_blocks). */
 int64_t hrl_conv3x3_block_sum_blocks(int64_t M);
 /* The chain's forward conv with BN statistics (hrl_conv3x3_forward_ex, epilogue 1, packed weights, no bias):
- * 2 (default) = the LDS-DMA ring form (every wave computes, x' staged from a raw ring), 1 = the block backward's
- * tile-shared form, 0 = the per-wave conv3x3_kernel (tools/fwd_form_bench.py).  Returns the previous. */
+ * 2 (default) = the LDS-DMA ring form (every wave computes, x' staged from a raw ring), 3 = the same with y staged
+ * through the ring slot into 1 KiB contiguous stores (round 6, bit-identical), 1 = the block backward's tile-shared
+ * form, 0 = the per-wave conv3x3_kernel (tools/fwd_form_bench.py).  Returns the previous. */
 int hrl_conv3x3_set_fwd_form(int form);
 /* Both packed layouts of n <= 8 weights (32, 32, 3, 3) in one launch: packed[(l*2 + f) * 9216], f = 0 forward,
  * 1 input gradient (host array of device pointers).  hrl_conv3x3_forward_ex with flip | 2 takes `weight`

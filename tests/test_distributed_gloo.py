@@ -346,7 +346,7 @@ def test_rccl_graph_step_matches_single_gpu_step(cuda):
 def _segmented_rank_main(rank, world, port, out_path, steps, segment=True, name='TicTacToe'):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK='0')
-    from handyrl_amd.trainer import LearnerStep
+    from handyrl_amd.trainer import LearnerStep, split_torus_tower
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     dist.init_process_group('gloo', rank=rank, world_size=world)
@@ -358,6 +358,8 @@ def _segmented_rank_main(rank, world, port, out_path, steps, segment=True, name=
     args = dict(args, batch_size=B // world)   # per-rank shard; LearnerStep's lr is the global batch's
     torch.manual_seed(0)
     net = cls()
+    if not segment:
+        split_torus_tower(net)   # the reference run: the same split tower (a segmented capture sets it itself)
     step = LearnerStep(net, args, dev, graph=True, world_size=world, segment_backward=segment)
     hidden = _hidden(net, B // world, batch['value'].size(2), dev) if rec else None
     for _ in range(steps):
