@@ -673,61 +673,66 @@ bool dims_ok(int64_t B, int64_t T, int64_t P, int64_t Pp, int64_t A, LossDims &d
 //   value[bt, p]  = o_val[bt, p|0] * omask[bt, p]
 // one launch each way instead of torch's mul / sum / sub / mul (and their backward mul / sum-to-size
 // pairs).  The float operations and the p order are torch's: products rounded, summed from 0 in p order.
+// I: the index type -- 32-bit unsigned whenever every index fits (a 64-bit division by the runtime A / Pq is a
+// long software sequence per element; the results are the same)
+template <typename I>
 __global__ __launch_bounds__(kThreads) void out_mask_fwd_kernel(const float *__restrict__ opol,
                                                                 const float *__restrict__ oval,
                                                                 const float *__restrict__ tmask,
                                                                 const float *__restrict__ omask,
-                                                                const float *__restrict__ amask, int64_t BT, int P,
+                                                                const float *__restrict__ amask, I BT, int P,
                                                                 int Pq, int A, float *__restrict__ pol,
                                                                 float *__restrict__ val) {
-    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    const int64_t npol = BT * A;
+    const I i = (I)blockIdx.x * kThreads + threadIdx.x;
+    const I npol = BT * (I)A;
     if (i < npol) {
-        const int64_t bt = i / A;
-        const int a = (int)(i - bt * A);
+        const I bt = i / (I)A;
+        const int a = (int)(i - bt * (I)A);
         float acc = 0.f;
-        for (int p = 0; p < P; ++p) acc += opol[(bt * Pq + (Pq == 1 ? 0 : p)) * A + a] * tmask[bt * P + p];
+        for (int p = 0; p < P; ++p)
+            acc += opol[(bt * (I)Pq + (I)(Pq == 1 ? 0 : p)) * (I)A + (I)a] * tmask[bt * (I)P + (I)p];
         pol[i] = acc - amask[i];
-    } else if (oval && i < npol + BT * P) {
-        const int64_t j = i - npol;
-        const int64_t bt = j / P;
-        const int p = (int)(j - bt * P);
-        val[j] = oval[bt * Pq + (Pq == 1 ? 0 : p)] * omask[j];
+    } else if (oval && i < npol + BT * (I)P) {
+        const I j = i - npol;
+        const I bt = j / (I)P;
+        const int p = (int)(j - bt * (I)P);
+        val[j] = oval[bt * (I)Pq + (I)(Pq == 1 ? 0 : p)] * omask[j];
     }
 }
 
+template <typename I>
 __global__ __launch_bounds__(kThreads) void out_mask_bwd_kernel(const float *__restrict__ gpol,
                                                                 const float *__restrict__ gval,
                                                                 const float *__restrict__ tmask,
-                                                                const float *__restrict__ omask, int64_t BT, int P,
+                                                                const float *__restrict__ omask, I BT, int P,
                                                                 int Pq, int A, float *__restrict__ gopol,
                                                                 float *__restrict__ goval) {
-    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    const int64_t npol = BT * Pq * A;
+    const I i = (I)blockIdx.x * kThreads + threadIdx.x;
+    const I npol = BT * (I)Pq * (I)A;
     if (i < npol) {
-        const int64_t btq = i / A;
-        const int a = (int)(i - btq * A);
-        const int64_t bt = btq / Pq;
-        const int q = (int)(btq - bt * Pq);
-        const float g = gpol[bt * A + a];
+        const I btq = i / (I)A;
+        const int a = (int)(i - btq * (I)A);
+        const I bt = btq / (I)Pq;
+        const int q = (int)(btq - bt * (I)Pq);
+        const float g = gpol[bt * (I)A + (I)a];
         float acc;
         if (Pq == 1) {
             acc = 0.f;
-            for (int p = 0; p < P; ++p) acc += g * tmask[bt * P + p];
+            for (int p = 0; p < P; ++p) acc += g * tmask[bt * (I)P + (I)p];
         } else {
-            acc = g * tmask[bt * P + q];
+            acc = g * tmask[bt * (I)P + (I)q];
         }
         gopol[i] = acc;
-    } else if (gval && i < npol + BT * Pq) {
-        const int64_t btq = i - npol;
-        const int64_t bt = btq / Pq;
-        const int q = (int)(btq - bt * Pq);
+    } else if (gval && i < npol + BT * (I)Pq) {
+        const I btq = i - npol;
+        const I bt = btq / (I)Pq;
+        const int q = (int)(btq - bt * (I)Pq);
         float acc;
         if (Pq == 1) {
             acc = 0.f;
-            for (int p = 0; p < P; ++p) acc += gval[bt * P + p] * omask[bt * P + p];
+            for (int p = 0; p < P; ++p) acc += gval[bt * (I)P + (I)p] * omask[bt * (I)P + (I)p];
         } else {
-            acc = gval[bt * P + q] * omask[bt * P + q];
+            acc = gval[bt * (I)P + (I)q] * omask[bt * (I)P + (I)q];
         }
         goval[btq] = acc;
     }
@@ -806,9 +811,13 @@ int hrl_output_mask_forward(const float *opol, const float *oval, const float *t
     if (!opol || !tmask || !amask || !pol || (oval && (!omask || !val))) return HRL_EINVAL;
     const int64_t n = BT * A + (oval ? BT * P : 0);
     if (n > ((int64_t)1 << 40)) return HRL_EINVAL;
-    hipLaunchKernelGGL(out_mask_fwd_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                       static_cast<hipStream_t>(stream), opol, oval, tmask, omask, amask, BT, (int)P, (int)Pq,
-                       (int)A, pol, val);
+    const dim3 grid((unsigned)((n + kThreads - 1) / kThreads));
+    if (n + kThreads < ((int64_t)1 << 31))
+        hipLaunchKernelGGL(out_mask_fwd_kernel<uint32_t>, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                           opol, oval, tmask, omask, amask, (uint32_t)BT, (int)P, (int)Pq, (int)A, pol, val);
+    else
+        hipLaunchKernelGGL(out_mask_fwd_kernel<int64_t>, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                           opol, oval, tmask, omask, amask, BT, (int)P, (int)Pq, (int)A, pol, val);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
 }
@@ -820,9 +829,13 @@ int hrl_output_mask_backward(const float *gpol, const float *gval, const float *
     if (!gpol || !tmask || !gopol || (gval && (!omask || !goval))) return HRL_EINVAL;
     const int64_t n = BT * Pq * A + (gval ? BT * Pq : 0);
     if (n > ((int64_t)1 << 40)) return HRL_EINVAL;
-    hipLaunchKernelGGL(out_mask_bwd_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                       static_cast<hipStream_t>(stream), gpol, gval, tmask, omask, BT, (int)P, (int)Pq, (int)A,
-                       gopol, goval);
+    const dim3 grid((unsigned)((n + kThreads - 1) / kThreads));
+    if (n + kThreads < ((int64_t)1 << 31))
+        hipLaunchKernelGGL(out_mask_bwd_kernel<uint32_t>, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                           gpol, gval, tmask, omask, (uint32_t)BT, (int)P, (int)Pq, (int)A, gopol, goval);
+    else
+        hipLaunchKernelGGL(out_mask_bwd_kernel<int64_t>, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                           gpol, gval, tmask, omask, BT, (int)P, (int)Pq, (int)A, gopol, goval);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? HRL_OK : HRL_ELAUNCH_BASE - (int)e;
 }
