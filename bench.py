@@ -746,6 +746,9 @@ def main():
             'steps': opts.steps,
             'warmup': opts.warmup,
             'ms_per_step': round(elapsed / opts.steps * 1e3, 4),
+            'timing_note': ('the first ~30 graph replays after the capture run 5-25% slow while the GPU clock '
+                            'settles, MFMA-bound kernels most (profiles/r06_replay_clock_ramp.txt); fewer warm-up '
+                            'steps put part of that ramp in the timed region'),
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
